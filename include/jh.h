@@ -1,0 +1,196 @@
+/*
+ * jh.h -- C ABI of libjh.so, the MI355X-native Jepsen history checker.
+ *
+ * This is the drop-in boundary for the verification phase of Jepsen
+ * (reference: jepsen "0.1.14-SNAPSHOT", /root/reference/jepsen/project.clj:1).
+ * Each entry point replaces one `jepsen.checker/Checker` reify on the JVM
+ * side; a JNA shim encodes the history once into the
+ * columnar layout below and calls:
+ *
+ *   jh_check_cas_independent  <- (independent/checker (checker/linearizable
+ *                                   {:model (model/cas-register v0)}))
+ *                                 jepsen/src/jepsen/independent.clj:247-298
+ *                                 jepsen/src/jepsen/checker.clj:127-158
+ *   jh_check_cas              <- (checker/linearizable {:model (model/cas-register)})
+ *                                 jepsen/src/jepsen/checker.clj:127-158
+ *   jh_check_counter          <- (checker/counter)  jepsen/src/jepsen/checker.clj:679-734
+ *   jh_check_set              <- (checker/set)      jepsen/src/jepsen/checker.clj:182-233
+ *
+ * Plain pointers and sizes only. The caller owns every buffer; the library
+ * never retains a caller pointer after returning. All entry points are
+ * reentrant: one jh_ctx serialises its device work with a mutex.
+ *
+ * History encoding (one row per history map, in history order; the row
+ * number IS knossos' :index, jepsen/src/jepsen/core.clj:441):
+ *   process  >= 0 for an integer client process; < 0 for anything else
+ *            (:nemesis is -1, other non-integers are interned to -2, -3, ...)
+ *   type     JH_TYPE_INVOKE / OK / FAIL / INFO
+ *   f        JH_F_READ / WRITE / CAS / ADD, anything else interned >= 16
+ *   key      (key v) when :value is an independent tuple (a MapEntry,
+ *            jepsen/src/jepsen/independent.clj:21-29), interned to
+ *            [0, n_keys); -1 when :value is not a tuple.  May be NULL (= all -1).
+ *   value    scalar :value (after unwrapping a tuple); for :cas the `cur`
+ *            element of [cur new]; JH_NIL for nil / absent :value.
+ *            For a set :read, the offset of its elements in `aux`.
+ *   value2   for :cas the `new` element; for a set :read the element count;
+ *            JH_NIL otherwise.
+ */
+#ifndef JH_H
+#define JH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JH_ABI_VERSION 1
+
+/* Return codes. Anything non-zero also writes a NUL-terminated message into
+ * the caller's err buffer; the JNA shim throws ex-info and check-safe turns
+ * it into {:valid? :unknown :error ...} (jepsen/src/jepsen/checker.clj:77-88). */
+#define JH_OK            0
+#define JH_EINVAL        1   /* malformed arguments or history */
+#define JH_EUNSUPPORTED  2   /* input the device path does not handle: shim falls back */
+#define JH_EDEVICE       3   /* HIP error, or no device */
+#define JH_ENOMEM        4   /* device allocation failed */
+
+/* :type */
+#define JH_TYPE_INVOKE 0
+#define JH_TYPE_OK     1
+#define JH_TYPE_FAIL   2
+#define JH_TYPE_INFO   3
+
+/* :f */
+#define JH_F_READ  0
+#define JH_F_WRITE 1
+#define JH_F_CAS   2
+#define JH_F_ADD   3
+
+#define JH_NIL INT64_MIN
+
+/* Verdict codes, ordered like jepsen.checker/valid-priorities
+ * (jepsen/src/jepsen/checker.clj:26-31): true 0 < :unknown 0.5 < false 1. */
+#define JH_VALID    0
+#define JH_UNKNOWN  1
+#define JH_INVALID  2
+
+/* Per-key causes. */
+#define JH_CAUSE_NONE         0
+#define JH_CAUSE_BUDGET       1  /* memo-insert budget exhausted -> :unknown */
+#define JH_CAUSE_WINDOW       2  /* more than JH_MAX_WINDOW concurrent ops   */
+#define JH_CAUSE_DOUBLE_INVOKE 3 /* knossos.history/complete would throw     */
+#define JH_CAUSE_ORPHAN       4  /* :ok/:fail with no open invocation        */
+#define JH_CAUSE_BAD_F        5  /* op :f the cas-register model does not know */
+#define JH_CAUSE_NIL_VALUE    6  /* nil where the checker does arithmetic     */
+#define JH_CAUSE_OVERFLOW     7  /* long overflow (Clojure + throws)          */
+
+#define JH_MAX_WINDOW 64
+
+typedef struct jh_history {
+    int64_t n;                 /* entries */
+    const int64_t *process;
+    const int64_t *type;
+    const int64_t *f;
+    const int64_t *key;        /* may be NULL */
+    const int64_t *value;
+    const int64_t *value2;
+    int64_t n_keys;            /* keys are 0..n_keys-1 */
+    const int64_t *aux;        /* set-read elements, CSR via value/value2; may be NULL */
+    int64_t n_aux;
+    int32_t on_device;         /* 1: every pointer above is a device (HBM) pointer */
+    int32_t reserved;
+} jh_history;
+
+typedef struct jh_lin_opts {
+    int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */
+    int64_t budget;            /* max memo inserts per key before :unknown; <=0: default */
+    int64_t stream;            /* hipStream_t to run on (0 = the ctx stream) */
+} jh_lin_opts;
+
+#define JH_DEFAULT_BUDGET (1 << 20)
+
+typedef struct jh_key_verdict {
+    int32_t valid;             /* JH_VALID / JH_UNKNOWN / JH_INVALID */
+    int32_t cause;             /* JH_CAUSE_* */
+    int64_t fail_entry;        /* invalid: history row of the ok completion of the
+                                  first op no linearization can get past; else -1 */
+    int64_t explored;          /* memo inserts (WGL cache size) for this key */
+} jh_key_verdict;
+
+typedef struct jh_summary {
+    int64_t valid;             /* merge-valid over keys (checker.clj:33-47) */
+    int64_t n_invalid;         /* == (count :failures) (independent.clj:289-295) */
+    int64_t n_unknown;
+    int64_t first_fail_entry;  /* min fail_entry over invalid keys, or -1 */
+    int64_t n_keys;            /* keys checked (keys present in the history) */
+    int64_t explored;          /* sum of memo inserts */
+    int64_t memo_probes;       /* memo slots read by the search (roofline bytes) */
+    double  device_ms;         /* device time of the check (HIP events) */
+    double  dfs_ms;            /* of which the WGL search kernel */
+} jh_summary;
+
+typedef struct jh_ctx jh_ctx;
+
+int  jh_version(void);
+/* Opens a context on HIP device `device`. */
+int  jh_open(int device, jh_ctx **out);
+void jh_close(jh_ctx *ctx);
+
+/* (independent/checker (checker/linearizable {:model (model/cas-register init)})).
+ * out[k] receives the verdict of key k for k in [0, h->n_keys); keys that
+ * occur in no tuple get valid = JH_VALID, explored = -1 (they have no
+ * :results entry, independent.clj:222-232). */
+int jh_check_cas_independent(jh_ctx *ctx, const jh_history *h,
+                             const jh_lin_opts *opts,
+                             jh_key_verdict *out, jh_summary *sum,
+                             char *err, size_t errlen);
+
+/* (checker/linearizable {:model (model/cas-register init)}) on a history
+ * whose values are not tuples (key column ignored). */
+int jh_check_cas(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts,
+                 jh_key_verdict *out, char *err, size_t errlen);
+
+/* Device-resident variant for benchmarking and for callers that keep the
+ * encoded history in HBM: h->on_device must be 1; out_dev is a device array
+ * of n_keys verdicts; sum is host. Runs on opts->stream, synchronises it. */
+int jh_check_cas_independent_device(jh_ctx *ctx, const jh_history *h,
+                                    const jh_lin_opts *opts,
+                                    jh_key_verdict *out_dev, jh_summary *sum,
+                                    char *err, size_t errlen);
+
+/* (checker/counter). reads_out receives 3*n_reads int64 [lower value upper]
+ * triples in history order (the :reads vector); at most reads_cap triples
+ * are written, *n_reads is always the full count. *valid is JH_VALID /
+ * JH_INVALID / JH_UNKNOWN (cause in *cause). *first_err_entry = history row
+ * of the :ok read behind (first errors), or -1. */
+int jh_check_counter(jh_ctx *ctx, const jh_history *h,
+                     int64_t *reads_out, int64_t reads_cap,
+                     int64_t *n_reads, int64_t *n_errors,
+                     int64_t *first_err_entry, int32_t *valid, int32_t *cause,
+                     char *err, size_t errlen);
+
+typedef struct jh_set_result {
+    int32_t valid;             /* JH_VALID / JH_INVALID / JH_UNKNOWN ("Set was never read") */
+    int32_t cause;
+    int64_t attempt_count, acknowledged_count, ok_count,
+            lost_count, recovered_count, unexpected_count;
+    int64_t first_fail_entry;  /* min row of an :ok :add whose element is lost;
+                                  else the final read's row if unexpected; else -1 */
+    int64_t final_read_entry;
+    /* Run-length form of the four result sets (util.clj:536-575): run r of
+     * set s is [runs[s][2r], runs[s][2r+1]] inclusive. Sets: 0 ok, 1 lost,
+     * 2 unexpected, 3 recovered. Caller provides runs_cap pairs per set. */
+    int64_t n_runs[4];
+} jh_set_result;
+
+int jh_check_set(jh_ctx *ctx, const jh_history *h, jh_set_result *res,
+                 int64_t *runs_ok, int64_t *runs_lost, int64_t *runs_unexpected,
+                 int64_t *runs_recovered, int64_t runs_cap,
+                 char *err, size_t errlen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JH_H */

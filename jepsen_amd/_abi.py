@@ -1,0 +1,116 @@
+"""ctypes mirror of include/jh.h (the C ABI of libjh.so).
+
+Kept in one place so the product binding (`_native.py`), the test oracle
+wrapper (`oracle/oracle.py`) and the generator wrapper (`synth.py`) agree on
+every struct layout.
+"""
+import ctypes as C
+
+JH_ABI_VERSION = 1
+
+JH_OK, JH_EINVAL, JH_EUNSUPPORTED, JH_EDEVICE, JH_ENOMEM = 0, 1, 2, 3, 4
+TYPE_INVOKE, TYPE_OK, TYPE_FAIL, TYPE_INFO = 0, 1, 2, 3
+F_READ, F_WRITE, F_CAS, F_ADD = 0, 1, 2, 3
+F_FIRST_INTERNED = 16
+NIL = -(1 << 63)
+
+VALID, UNKNOWN, INVALID = 0, 1, 2
+
+CAUSES = {
+    0: None,
+    1: "budget",
+    2: "window",
+    3: "double-invoke",
+    4: "orphan-completion",
+    5: "unsupported-f",
+    6: "nil-value",
+    7: "overflow",
+}
+
+MAX_WINDOW = 64
+DEFAULT_BUDGET = 1 << 20
+
+_p64 = C.POINTER(C.c_int64)
+
+
+class JhHistory(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64),
+        ("process", _p64),
+        ("type", _p64),
+        ("f", _p64),
+        ("key", _p64),
+        ("value", _p64),
+        ("value2", _p64),
+        ("n_keys", C.c_int64),
+        ("aux", _p64),
+        ("n_aux", C.c_int64),
+        ("on_device", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
+class JhLinOpts(C.Structure):
+    _fields_ = [("init_value", C.c_int64), ("budget", C.c_int64), ("stream", C.c_int64)]
+
+
+class JhKeyVerdict(C.Structure):
+    _fields_ = [("valid", C.c_int32), ("cause", C.c_int32),
+                ("fail_entry", C.c_int64), ("explored", C.c_int64)]
+
+
+class JhSummary(C.Structure):
+    _fields_ = [("valid", C.c_int64), ("n_invalid", C.c_int64), ("n_unknown", C.c_int64),
+                ("first_fail_entry", C.c_int64), ("n_keys", C.c_int64),
+                ("explored", C.c_int64), ("memo_probes", C.c_int64),
+                ("device_ms", C.c_double), ("dfs_ms", C.c_double)]
+
+
+class JhSetResult(C.Structure):
+    _fields_ = [("valid", C.c_int32), ("cause", C.c_int32),
+                ("attempt_count", C.c_int64), ("acknowledged_count", C.c_int64),
+                ("ok_count", C.c_int64), ("lost_count", C.c_int64),
+                ("recovered_count", C.c_int64), ("unexpected_count", C.c_int64),
+                ("first_fail_entry", C.c_int64), ("final_read_entry", C.c_int64),
+                ("n_runs", C.c_int64 * 4)]
+
+
+# numpy structured dtype with the same layout as jh_key_verdict
+try:
+    import numpy as _np
+    VERDICT_DTYPE = _np.dtype([("valid", _np.int32), ("cause", _np.int32),
+                               ("fail_entry", _np.int64), ("explored", _np.int64)])
+except Exception:  # pragma: no cover
+    VERDICT_DTYPE = None
+
+
+def ptr64(a):
+    """int64* for a C-contiguous numpy int64 array (or None)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(_p64)
+
+
+def make_history(cols, on_device=False):
+    """Build a JhHistory from an object with numpy (or device-pointer) columns.
+
+    `cols` must have attributes n, process, type, f, key, value, value2,
+    n_keys, aux (may be None)."""
+    h = JhHistory()
+    h.n = int(cols.n)
+    if on_device:
+        def dp(x):
+            return C.cast(C.c_void_p(int(x)), _p64) if x else None
+        h.process, h.type, h.f = dp(cols.process), dp(cols.type), dp(cols.f)
+        h.key, h.value, h.value2 = dp(cols.key), dp(cols.value), dp(cols.value2)
+        h.aux = dp(getattr(cols, "aux", 0))
+        h.on_device = 1
+    else:
+        h.process, h.type, h.f = ptr64(cols.process), ptr64(cols.type), ptr64(cols.f)
+        h.key, h.value, h.value2 = ptr64(cols.key), ptr64(cols.value), ptr64(cols.value2)
+        h.aux = ptr64(cols.aux) if getattr(cols, "aux", None) is not None else None
+        h.on_device = 0
+    h.n_keys = int(cols.n_keys)
+    aux = getattr(cols, "aux", None)
+    h.n_aux = int(len(aux)) if (aux is not None and not on_device) else int(getattr(cols, "n_aux", 0))
+    return h

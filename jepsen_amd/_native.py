@@ -1,0 +1,172 @@
+"""ctypes binding of libjh.so (include/jh.h). The product path: there is no
+CPU fallback. If the library or a GPU is missing, every call raises.
+"""
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+from . import _abi as A
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libjh.so")
+_lib = None
+_lock = threading.Lock()
+
+
+class JhError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libjh error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+def lib():
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"{LIB_PATH} is missing: run `python -m jepsen_amd.build` "
+                                   "(the HIP extension is required; there is no CPU fallback)")
+            L = C.CDLL(LIB_PATH)
+            H = C.POINTER(A.JhHistory)
+            L.jh_version.restype = C.c_int
+            L.jh_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+            L.jh_close.argtypes = [C.c_void_p]
+            L.jh_close.restype = None
+            L.jh_check_cas_independent.argtypes = [C.c_void_p, H, C.POINTER(A.JhLinOpts),
+                                                   C.POINTER(A.JhKeyVerdict), C.POINTER(A.JhSummary),
+                                                   C.c_char_p, C.c_size_t]
+            L.jh_check_cas_independent_device.argtypes = L.jh_check_cas_independent.argtypes
+            L.jh_check_cas.argtypes = [C.c_void_p, H, C.POINTER(A.JhLinOpts),
+                                       C.POINTER(A.JhKeyVerdict), C.c_char_p, C.c_size_t]
+            p64 = C.POINTER(C.c_int64)
+            L.jh_check_counter.argtypes = [C.c_void_p, H, p64, C.c_int64, p64, p64, p64,
+                                           C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                           C.c_char_p, C.c_size_t]
+            L.jh_check_set.argtypes = [C.c_void_p, H, C.POINTER(A.JhSetResult), p64, p64, p64, p64,
+                                       C.c_int64, C.c_char_p, C.c_size_t]
+            if L.jh_version() != A.JH_ABI_VERSION:
+                raise RuntimeError("libjh.so ABI version mismatch")
+            _lib = L
+    return _lib
+
+
+EXPORTED_SYMBOLS = ["jh_version", "jh_open", "jh_close", "jh_check_cas_independent",
+                    "jh_check_cas", "jh_check_cas_independent_device", "jh_check_counter",
+                    "jh_check_set"]
+
+
+def _raise(rc, err):
+    if rc != A.JH_OK:
+        raise JhError(rc, err.value.decode(errors="replace"))
+
+
+def _opts(init, budget, stream=0):
+    return A.JhLinOpts(A.NIL if init is None else int(init), int(budget or 0), int(stream))
+
+
+class Context:
+    """One jh_ctx on one HIP device (jh_open / jh_close)."""
+
+    def __init__(self, device=0):
+        L = lib()
+        h = C.c_void_p()
+        rc = L.jh_open(int(device), C.byref(h))
+        if rc != A.JH_OK:
+            raise JhError(rc, f"jh_open({device}) failed (no usable HIP device?)")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().jh_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- linearizability ---------------------------------------------------
+    def check_cas_independent(self, cols, init=None, budget=None):
+        """Returns (verdicts: structured array [n_keys] of VERDICT_DTYPE, JhSummary)."""
+        h = A.make_history(cols)
+        out = np.zeros(max(cols.n_keys, 1), dtype=A.VERDICT_DTYPE)
+        s = A.JhSummary()
+        err = C.create_string_buffer(1024)
+        rc = lib().jh_check_cas_independent(self._h, C.byref(h), C.byref(_opts(init, budget)),
+                                            out.ctypes.data_as(C.POINTER(A.JhKeyVerdict)),
+                                            C.byref(s), err, len(err))
+        _raise(rc, err)
+        return out[:cols.n_keys], s
+
+    def check_cas_independent_device(self, dcols, verdicts_dev_ptr, init=None, budget=None,
+                                     stream=0):
+        """dcols: object whose column attributes are device pointers (ints)."""
+        h = A.make_history(dcols, on_device=True)
+        s = A.JhSummary()
+        err = C.create_string_buffer(1024)
+        rc = lib().jh_check_cas_independent_device(
+            self._h, C.byref(h), C.byref(_opts(init, budget, stream)),
+            C.cast(C.c_void_p(int(verdicts_dev_ptr)), C.POINTER(A.JhKeyVerdict)),
+            C.byref(s), err, len(err))
+        _raise(rc, err)
+        return s
+
+    def check_cas(self, cols, init=None, budget=None):
+        h = A.make_history(cols)
+        v = A.JhKeyVerdict()
+        err = C.create_string_buffer(1024)
+        rc = lib().jh_check_cas(self._h, C.byref(h), C.byref(_opts(init, budget)), C.byref(v),
+                                err, len(err))
+        _raise(rc, err)
+        return v.valid, v.cause, v.fail_entry, v.explored
+
+    # -- counter / set -----------------------------------------------------
+    def check_counter(self, cols, reads_cap=None):
+        h = A.make_history(cols)
+        cap = cols.n if reads_cap is None else reads_cap
+        reads = np.zeros(3 * max(cap, 1), np.int64)
+        nr, ne, fe = C.c_int64(), C.c_int64(), C.c_int64()
+        valid, cause = C.c_int32(), C.c_int32()
+        err = C.create_string_buffer(1024)
+        rc = lib().jh_check_counter(self._h, C.byref(h), A.ptr64(reads), cap, C.byref(nr),
+                                    C.byref(ne), C.byref(fe), C.byref(valid), C.byref(cause),
+                                    err, len(err))
+        _raise(rc, err)
+        k = min(nr.value, cap)
+        return {"valid": valid.value, "cause": cause.value, "reads": reads[:3 * k].reshape(-1, 3),
+                "n_reads": nr.value, "n_errors": ne.value, "first_err_entry": fe.value}
+
+    def check_set(self, cols, runs_cap=None):
+        h = A.make_history(cols)
+        cap = (cols.n + len(cols.aux) + 2) if runs_cap is None else runs_cap
+        runs = [np.zeros(2 * max(cap, 1), np.int64) for _ in range(4)]
+        r = A.JhSetResult()
+        err = C.create_string_buffer(1024)
+        rc = lib().jh_check_set(self._h, C.byref(h), C.byref(r), *[A.ptr64(x) for x in runs], cap,
+                                err, len(err))
+        _raise(rc, err)
+        out = {name: getattr(r, name) for name, _ in A.JhSetResult._fields_ if name != "n_runs"}
+        out["runs"] = [runs[i][:2 * min(r.n_runs[i], cap)].reshape(-1, 2) for i in range(4)]
+        out["n_runs"] = list(r.n_runs)
+        return out
+
+
+_default = {}
+
+
+def default_context(device=None):
+    """Process-wide context per device (LOCAL_RANK by default)."""
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", "0"))
+    with _lock:
+        ctx = _default.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        with _lock:
+            _default[device] = ctx
+    return ctx

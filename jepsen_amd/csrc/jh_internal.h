@@ -1,0 +1,120 @@
+// jh_internal.h -- shared internals of libjh.so (HIP, gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+#include <string>
+#include "../../include/jh.h"
+
+#define JH_WAVE 64
+
+// ---------------------------------------------------------------------------
+// error plumbing: every entry point returns a JH_* code and fills err.
+struct JhError {
+    int code = JH_OK;
+    std::string msg;
+};
+
+#define HIP_TRY(expr)                                                                 \
+    do {                                                                              \
+        hipError_t _e = (expr);                                                       \
+        if (_e != hipSuccess) {                                                       \
+            throw_hip(_e, #expr, __FILE__, __LINE__);                                 \
+        }                                                                             \
+    } while (0)
+
+struct JhException {
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] inline void throw_hip(hipError_t e, const char *expr, const char *file, int line) {
+    char buf[512];
+    snprintf(buf, sizeof buf, "HIP error %s (%d) at %s:%d: %s", hipGetErrorString(e), (int)e,
+             file, line, expr);
+    throw JhException{e == hipErrorOutOfMemory ? JH_ENOMEM : JH_EDEVICE, buf};
+}
+[[noreturn]] inline void throw_jh(int code, const std::string &msg) { throw JhException{code, msg}; }
+
+// ---------------------------------------------------------------------------
+// Device workspace: named, grow-only buffers owned by the context. Entry
+// points never allocate in the steady state (same-size calls reuse).
+struct Buf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+struct jh_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::vector<Buf> bufs;
+    hipEvent_t ev[8] = {};
+    uint32_t gen_base = 0;        // memo generation tags (see jh_lin.hip)
+    int n_cu = 256;
+    void *pinned = nullptr;       // small pinned staging for scalars
+    size_t pinned_bytes = 0;
+
+    template <class T>
+    T *ws(int slot, size_t count, bool zero = false) {
+        if ((int)bufs.size() <= slot) bufs.resize(slot + 1);
+        size_t need = count * sizeof(T);
+        if (need == 0) need = 16;
+        Buf &b = bufs[slot];
+        if (b.bytes < need) {
+            if (b.p) HIP_TRY(hipFree(b.p));
+            b.p = nullptr;
+            size_t alloc = need + need / 8;
+            HIP_TRY(hipMalloc(&b.p, alloc));
+            b.bytes = alloc;
+            if (zero) HIP_TRY(hipMemsetAsync(b.p, 0, alloc, stream));
+        }
+        return (T *)b.p;
+    }
+    bool ws_fresh(int slot) const { return (int)bufs.size() <= slot || bufs[slot].p == nullptr; }
+};
+
+// workspace slot ids (one namespace for the whole library)
+enum WsSlot {
+    WS_COL_PROCESS = 0, WS_COL_TYPE, WS_COL_F, WS_COL_KEY, WS_COL_VALUE, WS_COL_VALUE2, WS_COL_AUX,
+    WS_KEYS_A, WS_KEYS_B, WS_ROWS_A, WS_ROWS_B, WS_SORT_TMP, WS_SEG_OFF, WS_REC, WS_PAIR,
+    WS_VIOL, WS_RANK, WS_MISC, WS_VERDICT, WS_QUEUE, WS_DEFER, WS_MEMO, WS_STACK, WS_SCRATCH,
+    WS_MEMO_DEEP, WS_STACK_DEEP, WS_SCRATCH_DEEP, WS_SUMMARY, WS_STATS,
+    WS_C_PAIR, WS_C_LAST, WS_C_LO, WS_C_HI, WS_C_OUT, WS_C_FLAG, WS_C_TMP, WS_C_IDX,
+    WS_S_BITS, WS_S_RUNS, WS_S_TMP, WS_S_CNT,
+    WS_BFS_SET, WS_BFS_Q, WS_BFS_META,
+    WS_COUNT
+};
+
+// row-level helpers shared by kernels
+__device__ __forceinline__ uint64_t jh_mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33; return x;
+}
+
+inline int grid_for(int64_t n, int block, int cap = 65536) {
+    int64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+// Copies a host jh_history to device workspace columns (or passes device
+// pointers through). Returns a device-pointer view.
+jh_history stage_history(jh_ctx *ctx, const jh_history *h, bool need_key, bool need_aux);
+
+// linearizability (jh_lin.hip)
+void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts *opts,
+                           bool keyed, jh_key_verdict *out_dev, jh_summary *sum,
+                           hipStream_t stream);
+// counter (jh_counter.hip)
+void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_t reads_cap,
+                   int64_t *n_reads, int64_t *n_errors, int64_t *first_err, int32_t *valid,
+                   int32_t *cause, hipStream_t stream);
+// set (jh_set.hip)
+void set_check(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, int64_t *runs[4],
+               int64_t runs_cap, hipStream_t stream);

@@ -1,0 +1,257 @@
+// jh_set.hip -- checker/set on MI355X.
+//
+// Replaces (checker/set), jepsen/src/jepsen/checker.clj:182-233:
+//   attempts = #{:value of every :invoke :add}     (:190-194)
+//   adds     = #{:value of every :ok :add}         (:195-199)
+//   final-read = :value of the LAST :ok :read      (:200-204)
+//   ok = R n attempts, unexpected = R - attempts, lost = adds - R,
+//   recovered = ok - adds                          (:210-223)
+// plus counts and util/integer-interval-set-str strings (util.clj:536-575),
+// which the library returns as sorted runs [lo hi] for the host to format.
+//
+// Elements live in [vmin, vmax]; each of the three sets is a bitmap over that
+// span (atomicOr of 32-bit words), every set operation is a word-wise
+// boolean, and runs fall out of the bit boundaries of each word.
+#include "jh_internal.h"
+#include <hipcub/hipcub.hpp>
+
+namespace {
+constexpr int T_INVOKE = 0, T_OK = 1;
+
+struct SetMeta {
+    long long vmin, vmax;
+    long long final_row;
+    int nil_attempt, nil_add;
+    long long cnt[6];          // attempt, ack, ok, lost, recovered, unexpected
+    unsigned long long first_lost_row;
+};
+
+__global__ void k_set_scan(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
+                           const int64_t *__restrict__ val, int64_t n, SetMeta *m) {
+    long long lo = LLONG_MAX, hi = LLONG_MIN, fr = -1;
+    int na = 0, nd = 0;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t ty = type[r], ff = f[r];
+        if (ff == JH_F_ADD && (ty == T_INVOKE || ty == T_OK)) {
+            const int64_t v = val[r];
+            if (v == JH_NIL) { if (ty == T_INVOKE) na = 1; else nd = 1; }
+            else { lo = min(lo, (long long)v); hi = max(hi, (long long)v); }
+        } else if (ff == JH_F_READ && ty == T_OK) fr = max(fr, (long long)r);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o)); hi = max(hi, __shfl_xor(hi, o));
+        fr = max(fr, __shfl_xor(fr, o));
+        na |= __shfl_xor(na, o); nd |= __shfl_xor(nd, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&m->vmin, lo); atomicMax(&m->vmax, hi); atomicMax(&m->final_row, fr);
+        if (na) atomicOr(&m->nil_attempt, 1);
+        if (nd) atomicOr(&m->nil_add, 1);
+    }
+}
+
+__global__ void k_set_range(const int64_t *__restrict__ aux, int64_t off, int64_t cnt, SetMeta *m) {
+    long long lo = LLONG_MAX, hi = LLONG_MIN;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cnt;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const long long v = aux[off + i];
+        lo = min(lo, v); hi = max(hi, v);
+    }
+    for (int o = 32; o > 0; o >>= 1) { lo = min(lo, __shfl_xor(lo, o)); hi = max(hi, __shfl_xor(hi, o)); }
+    if ((threadIdx.x & 63) == 0) { atomicMin(&m->vmin, lo); atomicMax(&m->vmax, hi); }
+}
+
+__global__ void k_set_mark_rows(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
+                                const int64_t *__restrict__ val, int64_t n, long long vmin,
+                                uint32_t *__restrict__ A, uint32_t *__restrict__ D) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        if (f[r] != JH_F_ADD) continue;
+        const int64_t ty = type[r];
+        if (ty != T_INVOKE && ty != T_OK) continue;
+        const uint64_t b = (uint64_t)(val[r] - vmin);
+        atomicOr(&(ty == T_INVOKE ? A : D)[b >> 5], 1u << (b & 31));
+    }
+}
+
+__global__ void k_set_mark_read(const int64_t *__restrict__ aux, int64_t off, int64_t cnt,
+                                long long vmin, uint32_t *__restrict__ R) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cnt;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t b = (uint64_t)(aux[off + i] - vmin);
+        atomicOr(&R[b >> 5], 1u << (b & 31));
+    }
+}
+
+__device__ __forceinline__ void set_words(const uint32_t *A, const uint32_t *D, const uint32_t *R,
+                                          int64_t w, int64_t nw, uint32_t out[4]) {
+    const uint32_t a = A[w], d = D[w], r = R[w];
+    const uint32_t ok = r & a;
+    out[0] = ok;          // ok
+    out[1] = d & ~r;      // lost
+    out[2] = r & ~a;      // unexpected
+    out[3] = ok & ~d;     // recovered
+}
+
+// per word: population counts and run-start counts of the four result sets
+__global__ void k_set_count(const uint32_t *__restrict__ A, const uint32_t *__restrict__ D,
+                            const uint32_t *__restrict__ R, int64_t nw,
+                            uint32_t *__restrict__ starts /* 4 x nw */, SetMeta *m) {
+    long long c[6] = {0, 0, 0, 0, 0, 0};
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw;
+         w += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t x[4], px[4] = {0, 0, 0, 0};
+        set_words(A, D, R, w, nw, x);
+        if (w > 0) set_words(A, D, R, w - 1, nw, px);
+        c[0] += __popc(A[w]); c[1] += __popc(D[w]);
+        c[2] += __popc(x[0]); c[3] += __popc(x[1]); c[4] += __popc(x[3]); c[5] += __popc(x[2]);
+        for (int s = 0; s < 4; s++) {
+            const uint32_t st = x[s] & ~((x[s] << 1) | (px[s] >> 31));
+            starts[s * nw + w] = __popc(st);
+        }
+    }
+    for (int i = 0; i < 6; i++) {
+        long long v = c[i];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd((unsigned long long *)&m->cnt[i], (unsigned long long)v);
+    }
+}
+
+__global__ void k_set_emit(const uint32_t *__restrict__ A, const uint32_t *__restrict__ D,
+                           const uint32_t *__restrict__ R, int64_t nw, long long vmin,
+                           const uint32_t *__restrict__ spos /* 4 x nw exclusive scans */,
+                           int64_t *__restrict__ runs /* 4 x 2 x cap */, int64_t cap) {
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw;
+         w += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t x[4], px[4] = {0, 0, 0, 0}, nx[4] = {0, 0, 0, 0};
+        set_words(A, D, R, w, nw, x);
+        if (w > 0) set_words(A, D, R, w - 1, nw, px);
+        if (w + 1 < nw) set_words(A, D, R, w + 1, nw, nx);
+        for (int s = 0; s < 4; s++) {
+            // a run starting in this word is numbered by the scan; its end is
+            // the next end bit at or after the start, possibly in later words
+            uint32_t st = x[s] & ~((x[s] << 1) | (px[s] >> 31));
+            int64_t k = spos[s * nw + w];
+            while (st) {
+                const int b = __ffs(st) - 1;
+                st &= st - 1;
+                if (k < cap) {
+                    int64_t *o = runs + (int64_t)s * 2 * cap;
+                    o[2 * k] = vmin + w * 32 + b;
+                    // scan forward for the end of this run
+                    int64_t ww = w;
+                    uint32_t cur = x[s] >> b;
+                    int bb = b;
+                    for (;;) {
+                        const uint32_t inv = ~cur;
+                        const int len = inv ? __ffs(inv) - 1 : 32 - bb;
+                        if (bb + len < 32 || ww + 1 >= nw) { o[2 * k + 1] = vmin + ww * 32 + bb + len - 1; break; }
+                        // run reaches the word boundary: continue into the next word
+                        ww++;
+                        uint32_t y[4];
+                        set_words(A, D, R, ww, nw, y);
+                        cur = y[s]; bb = 0;
+                        if (!(cur & 1)) { o[2 * k + 1] = vmin + ww * 32 - 1; break; }
+                    }
+                }
+                k++;
+            }
+        }
+    }
+}
+
+__global__ void k_set_first_lost(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
+                                 const int64_t *__restrict__ val, int64_t n, long long vmin,
+                                 const uint32_t *__restrict__ D, const uint32_t *__restrict__ R,
+                                 SetMeta *m) {
+    unsigned long long best = ~0ULL;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        if (f[r] != JH_F_ADD || type[r] != T_OK) continue;
+        const uint64_t b = (uint64_t)(val[r] - vmin);
+        const uint32_t bit = 1u << (b & 31);
+        if ((D[b >> 5] & bit) && !(R[b >> 5] & bit)) best = min(best, (unsigned long long)r);
+    }
+    for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o));
+    if ((threadIdx.x & 63) == 0 && best != ~0ULL) atomicMin(&m->first_lost_row, best);
+}
+}  // namespace
+
+void set_check(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, int64_t *runs_out[4],
+               int64_t runs_cap, hipStream_t st) {
+    memset(res, 0, sizeof(*res));
+    res->first_fail_entry = -1; res->final_read_entry = -1;
+    const int64_t n = dh->n;
+    SetMeta *m = ctx->ws<SetMeta>(WS_S_CNT, 1);
+    SetMeta mi;
+    memset(&mi, 0, sizeof mi);
+    mi.vmin = LLONG_MAX; mi.vmax = LLONG_MIN; mi.final_row = -1; mi.first_lost_row = ~0ULL;
+    HIP_TRY(hipMemcpyAsync(m, &mi, sizeof mi, hipMemcpyHostToDevice, st));
+    if (n > 0) k_set_scan<<<grid_for(n, 256, 4096), 256, 0, st>>>(dh->type, dh->f, dh->value, n, m);
+    SetMeta mh;
+    HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    res->final_read_entry = mh.final_row;
+    if (mh.final_row < 0) { res->valid = JH_UNKNOWN; res->cause = JH_CAUSE_NIL_VALUE; return; }
+    int64_t rd[2];
+    HIP_TRY(hipMemcpyAsync(rd, dh->value + mh.final_row, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(rd + 1, dh->value2 + mh.final_row, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (rd[0] == JH_NIL) { res->valid = JH_UNKNOWN; res->cause = JH_CAUSE_NIL_VALUE; return; }
+    if (mh.nil_attempt || mh.nil_add)
+        throw_jh(JH_EUNSUPPORTED, "nil set elements (integer-interval-set-str prints those in hash order)");
+    if (!dh->aux && rd[1] > 0) throw_jh(JH_EINVAL, "set read without an aux element array");
+    const int64_t off = rd[0], cnt = rd[1];
+    if (cnt > 0)
+        k_set_range<<<grid_for(cnt, 256, 4096), 256, 0, st>>>(dh->aux, off, cnt, m);
+    HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    long long vmin = mh.vmin, vmax = mh.vmax;
+    if (vmin > vmax) { vmin = 0; vmax = 0; }
+    const unsigned long long span = (unsigned long long)(vmax - vmin) + 1;
+    if (span > (1ULL << 34)) throw_jh(JH_EUNSUPPORTED, "set elements span more than 2^34");
+    const int64_t nw = (int64_t)((span + 31) / 32);
+    uint32_t *bits = ctx->ws<uint32_t>(WS_S_BITS, 3 * nw);
+    uint32_t *A = bits, *D = bits + nw, *R = bits + 2 * nw;
+    HIP_TRY(hipMemsetAsync(bits, 0, sizeof(uint32_t) * 3 * nw, st));
+    if (n > 0) k_set_mark_rows<<<grid_for(n, 256), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, A, D);
+    if (cnt > 0) k_set_mark_read<<<grid_for(cnt, 256), 256, 0, st>>>(dh->aux, off, cnt, vmin, R);
+    uint32_t *starts = ctx->ws<uint32_t>(WS_S_RUNS, 8 * nw + 8);
+    uint32_t *spos = starts + 4 * nw;
+    k_set_count<<<grid_for(nw, 256), 256, 0, st>>>(A, D, R, nw, starts, m);
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, starts, spos, (int)nw, st));
+    void *tmp = ctx->ws<char>(WS_S_TMP, tb);
+    for (int s = 0; s < 4; s++)   // per-set run numbering starts at 0
+        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, starts + s * nw, spos + s * nw, (int)nw, st));
+    uint32_t lastpos[4], lastc[4];
+    for (int s = 0; s < 4; s++) {
+        HIP_TRY(hipMemcpyAsync(&lastpos[s], spos + s * nw + nw - 1, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&lastc[s], starts + s * nw + nw - 1, 4, hipMemcpyDeviceToHost, st));
+    }
+    if (n > 0)
+        k_set_first_lost<<<grid_for(n, 256), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, D, R, m);
+    HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    int64_t nruns[4];
+    for (int s = 0; s < 4; s++) nruns[s] = (int64_t)lastpos[s] + lastc[s];
+    const int64_t cap = runs_cap;
+    int64_t *runs = ctx->ws<int64_t>(WS_C_OUT, 8 * std::max<int64_t>(cap, 1));
+    k_set_emit<<<grid_for(nw, 256), 256, 0, st>>>(A, D, R, nw, vmin, spos, runs, cap);
+    res->attempt_count = mh.cnt[0]; res->acknowledged_count = mh.cnt[1];
+    res->ok_count = mh.cnt[2]; res->lost_count = mh.cnt[3];
+    res->recovered_count = mh.cnt[4]; res->unexpected_count = mh.cnt[5];
+    res->valid = (mh.cnt[3] == 0 && mh.cnt[5] == 0) ? JH_VALID : JH_INVALID;
+    if (mh.cnt[3]) res->first_fail_entry = mh.first_lost_row == ~0ULL ? -1 : (int64_t)mh.first_lost_row;
+    else if (mh.cnt[5]) res->first_fail_entry = mh.final_row;
+    for (int s = 0; s < 4; s++) res->n_runs[s] = nruns[s];
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int s = 0; s < 4; s++) {
+        const int64_t k = std::min<int64_t>(nruns[s], cap);
+        if (k > 0 && runs_out[s])
+            HIP_TRY(hipMemcpyAsync(runs_out[s], runs + (int64_t)s * 2 * cap, sizeof(int64_t) * 2 * k,
+                                   hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+}

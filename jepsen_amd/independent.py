@@ -1,0 +1,104 @@
+"""jepsen.independent on MI355X (jepsen/src/jepsen/independent.clj).
+
+`checker(inner)` lifts a checker over [k v] tuples. When the inner checker
+is (or composes) a cas-register `linearizable`, the whole history is encoded
+once and ALL keys are checked by one libjh call (splitter + per-key WGL on
+the GPU); any other composed checkers still run per key on their own.
+"""
+from . import _abi as A
+from . import history as H
+from .checker import (Checker, Compose, Linearizable, check_safe, lin_result, merge_valid,
+                      _init_state, _ctx)
+
+DIR = "independent"
+tuple_ = H.tuple_
+is_tuple = H.is_tuple
+
+
+def history_keys(history):
+    """independent.clj:222-232 (in first-appearance order)."""
+    seen = {}
+    for op in history:
+        v = op.get("value")
+        if is_tuple(v) and v.key not in seen:
+            seen[v.key] = True
+    return list(seen)
+
+
+def subhistory(k, history):
+    """independent.clj:234-245: un-keyed ops plus the ops of key k, unwrapped."""
+    out = []
+    for op in history:
+        v = op.get("value")
+        if not is_tuple(v):
+            out.append(op)
+        elif v.key == k:
+            o = dict(op)
+            o["value"] = v.val
+            out.append(o)
+    return out
+
+
+def _lin_member(inner):
+    if isinstance(inner, Linearizable) and inner.supported():
+        return None, inner
+    if isinstance(inner, Compose):
+        for name, c in inner.checker_map.items():
+            if isinstance(c, Linearizable) and c.supported():
+                return name, c
+    return None, None
+
+
+class IndependentChecker(Checker):
+    """independent.clj:247-298."""
+
+    def __init__(self, inner):
+        self.inner = inner
+
+    def _results_map(self, results):
+        failures = [k for k, r in results.items() if not r.get("valid?")]
+        return {"valid?": merge_valid(r.get("valid?") for r in results.values()),
+                "results": results,
+                "failures": failures}
+
+    def check(self, test, history, opts):
+        history = list(history)
+        name, lin = _lin_member(self.inner)
+        if lin is not None:
+            cols = H.encode(history, keyed=True)
+            unkeyed_client = any(int(p) >= 0 and int(k) < 0 for p, k in zip(cols.process, cols.key))
+            if cols.n_keys and not unkeyed_client:
+                verdicts, _ = _ctx().check_cas_independent(
+                    cols, init=_init_state(lin.model, cols), budget=lin.budget)
+                lin_res = {}
+                for kid, key in enumerate(cols.keys):
+                    v = verdicts[kid]
+                    if int(v["explored"]) < 0:
+                        continue
+                    lin_res[key] = lin_result(int(v["valid"]), int(v["cause"]), int(v["fail_entry"]),
+                                              int(v["explored"]), cols)
+                if name is None:
+                    return self._results_map(lin_res)
+                results = {}
+                for key, lr in lin_res.items():
+                    sub = subhistory(key, history)
+                    r = {}
+                    for nm, c in self.inner.checker_map.items():
+                        r[nm] = lr if nm == name else check_safe(
+                            c, test, sub, {"subdirectory": [DIR, key], "history-key": key})
+                    r["valid?"] = merge_valid(x.get("valid?") if isinstance(x, dict) else None
+                                              for x in r.values())
+                    results[key] = r
+                return self._results_map(results)
+        # generic path: every key through the inner checker (per-key device
+        # calls for a linearizable inner)
+        results = {}
+        for key in history_keys(history):
+            sub = subhistory(key, history)
+            results[key] = check_safe(self.inner, test, sub,
+                                      {"subdirectory": [DIR, key], "history-key": key})
+        return self._results_map(results)
+
+
+def checker(inner):
+    return IndependentChecker(inner)

@@ -1,0 +1,118 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes wrapper around oracle/liboracle.so.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, and only as the checker / CPU baseline. The product
+path (jepsen_amd + libjh.so) never imports it.
+
+See jh_oracle.h for what the oracle restates and how it is pinned.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from jepsen_amd import _abi as A
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+def build(quiet=True):
+    subprocess.run(["make", "-C", _HERE], check=True,
+                   stdout=subprocess.DEVNULL if quiet else None)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        H = C.POINTER(A.JhHistory)
+        V = C.POINTER(A.JhKeyVerdict)
+        p64 = C.POINTER(C.c_int64)
+        L.orc_check_cas.argtypes = [H, C.c_int64, C.c_int64, V]
+        L.orc_check_cas_independent.argtypes = [H, C.c_int64, C.c_int64, C.c_int, C.c_int, V,
+                                                C.POINTER(A.JhSummary)]
+        L.orc_check_cas_independent_range.argtypes = [H, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                                                      C.c_int64, C.c_int64, V]
+        L.orc_check_counter.argtypes = [H, p64, C.c_int64, p64, p64, p64,
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        L.orc_check_set.argtypes = [H, C.POINTER(A.JhSetResult), p64, p64, p64, p64, C.c_int64]
+        L.orc_interval_str.argtypes = [p64, C.c_int64, C.c_char_p, C.c_int64]
+        L.orc_interval_str.restype = C.c_int64
+        L.orc_lin_selftest_key.argtypes = [H, C.c_int64, C.c_int64, p64]
+        _lib = L
+    return _lib
+
+
+def check_cas(cols, init=A.NIL, budget=A.DEFAULT_BUDGET):
+    h = cols.as_jh()
+    v = A.JhKeyVerdict()
+    lib().orc_check_cas(C.byref(h), init, budget, C.byref(v))
+    return v.valid, v.cause, v.fail_entry, v.explored
+
+
+def check_cas_independent(cols, init=A.NIL, budget=A.DEFAULT_BUDGET, mode=0, threads=1):
+    """Returns (verdicts structured array [n_keys], summary)."""
+    h = cols.as_jh()
+    out = np.zeros(max(cols.n_keys, 1), dtype=A.VERDICT_DTYPE)
+    s = A.JhSummary()
+    lib().orc_check_cas_independent(C.byref(h), init, budget, mode, threads,
+                                    out.ctypes.data_as(C.POINTER(A.JhKeyVerdict)), C.byref(s))
+    return out[:cols.n_keys], s
+
+
+def check_cas_independent_range(cols, k0, k1, init=A.NIL, budget=A.DEFAULT_BUDGET, mode=0,
+                                threads=1):
+    h = cols.as_jh()
+    out = np.zeros(max(k1 - k0, 1), dtype=A.VERDICT_DTYPE)
+    lib().orc_check_cas_independent_range(C.byref(h), init, budget, mode, threads, k0, k1,
+                                          out.ctypes.data_as(C.POINTER(A.JhKeyVerdict)))
+    return out[:k1 - k0]
+
+
+def key_selftest(cols, init=A.NIL, budget=A.DEFAULT_BUDGET):
+    """Runs the three CPU formulations on a whole (single-key) history.
+
+    Returns dict with canonical/list/bruteforce verdicts and explored counts."""
+    h = cols.as_jh()
+    res = np.zeros(8, np.int64)
+    lib().orc_lin_selftest_key(C.byref(h), init, budget, A.ptr64(res))
+    return {"status": int(res[0]), "canonical": int(res[1]), "canonical_explored": int(res[2]),
+            "list": int(res[3]), "list_explored": int(res[4]), "bruteforce": int(res[5]),
+            "n_ops": int(res[6]), "max_window": int(res[7])}
+
+
+def check_counter(cols, reads_cap=None):
+    h = cols.as_jh()
+    cap = cols.n if reads_cap is None else reads_cap
+    reads = np.zeros(3 * max(cap, 1), np.int64)
+    nr, ne, fe = C.c_int64(), C.c_int64(), C.c_int64()
+    valid, cause = C.c_int32(), C.c_int32()
+    lib().orc_check_counter(C.byref(h), A.ptr64(reads), cap, C.byref(nr), C.byref(ne),
+                            C.byref(fe), C.byref(valid), C.byref(cause))
+    k = min(nr.value, cap)
+    return {"valid": valid.value, "cause": cause.value, "reads": reads[:3 * k].reshape(-1, 3),
+            "n_reads": nr.value, "n_errors": ne.value, "first_err_entry": fe.value}
+
+
+def check_set(cols, runs_cap=None):
+    h = cols.as_jh()
+    cap = (cols.n + len(cols.aux) + 2) if runs_cap is None else runs_cap
+    runs = [np.zeros(2 * max(cap, 1), np.int64) for _ in range(4)]
+    r = A.JhSetResult()
+    lib().orc_check_set(C.byref(h), C.byref(r), *[A.ptr64(x) for x in runs], cap)
+    out = {name: getattr(r, name) for name, _ in A.JhSetResult._fields_ if name != "n_runs"}
+    out["runs"] = [runs[i][:2 * min(r.n_runs[i], cap)].reshape(-1, 2) for i in range(4)]
+    out["n_runs"] = list(r.n_runs)
+    return out
+
+
+def interval_str(values):
+    a = np.asarray(sorted(set(int(x) for x in values)), np.int64)
+    buf = C.create_string_buffer(64 + 24 * max(len(a), 1))
+    lib().orc_interval_str(A.ptr64(a) if len(a) else None, len(a), buf, len(buf))
+    return buf.value.decode()

@@ -1,0 +1,108 @@
+"""Parity of the device counter and set checkers with the oracle and with the
+reference's known answers (checker_test.clj:90-166)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, load_npz_cols
+from jepsen_amd import _abi as A
+from jepsen_amd import checker
+from jepsen_amd import history as H
+from jepsen_amd import synth
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("case", json.load(open(os.path.join(GOLD, "counter.json")))["cases"],
+                         ids=lambda c: c["name"])
+def test_counter_known_answers_device(ctx, case):
+    r = checker.check(checker.counter(), None, case["history"], {})
+    assert r == case["expected"]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_counter_random(ctx, seed):
+    cols = synth.counter(n_ops=200000, n_procs=10 + seed, read_every=11, p_fail=0.05, p_info=0.02,
+                         n_bad_reads=3 * seed, seed=seed)
+    g = ctx.check_counter(cols)
+    c = oracle.check_counter(cols)
+    assert g["valid"] == c["valid"] and g["cause"] == c["cause"]
+    assert g["n_reads"] == c["n_reads"] and g["n_errors"] == c["n_errors"]
+    assert g["first_err_entry"] == c["first_err_entry"]
+    assert (g["reads"] == c["reads"]).all()
+
+
+def test_counter_golden(ctx):
+    cols, z = load_npz_cols("synthetic_counter.npz")
+    g = ctx.check_counter(cols)
+    assert (g["reads"] == z["reads"]).all() and g["valid"] == int(z["valid"])
+    assert g["first_err_entry"] == int(z["first_err_entry"])
+
+
+def test_counter_c2_scale(ctx):
+    """C2 counter: 100M entries, add:read 100:1 -- device result must be
+    self-consistent (reads non-decreasing bounds) and the valid variant valid."""
+    cols = synth.counter(n_ops=50_000_000, n_procs=10, read_every=101, p_fail=0.05, p_info=0.01,
+                         n_bad_reads=0, seed=2)
+    g = ctx.check_counter(cols, reads_cap=1 << 22)
+    assert g["valid"] == A.VALID and g["n_errors"] == 0
+    r = g["reads"]
+    assert (r[:, 0] <= r[:, 1]).all() and (r[:, 1] <= r[:, 2]).all()
+
+
+def test_counter_errors(ctx):
+    inv = lambda p, f, v: {"process": p, "type": "invoke", "f": f, "value": v}
+    ok = lambda p, f, v: {"process": p, "type": "ok", "f": f, "value": v}
+    for h in ([inv(0, "add", 1), inv(0, "add", 1)], [ok(0, "add", 1)],
+              [inv(0, "add", None), ok(0, "add", None)],
+              [inv(0, "read", None), ok(0, "read", None)]):
+        cols = H.encode(h, keyed=False)
+        g = ctx.check_counter(cols)
+        c = oracle.check_counter(cols)
+        assert (g["valid"], g["cause"]) == (c["valid"], c["cause"]) and g["valid"] == A.UNKNOWN
+
+
+def _set_same(g, c):
+    for k in ("valid", "cause", "attempt_count", "acknowledged_count", "ok_count", "lost_count",
+              "recovered_count", "unexpected_count", "first_fail_entry", "final_read_entry"):
+        assert g[k] == c[k], k
+    for i in range(4):
+        assert g["n_runs"][i] == c["n_runs"][i]
+        assert (g["runs"][i] == c["runs"][i]).all(), i
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_set_random(ctx, seed):
+    cols = synth.set_history(n_adds=300000, n_procs=10, p_fail=0.05, p_info=0.03,
+                             n_lost=seed * 7, n_unexpected=seed, seed=seed)
+    _set_same(ctx.check_set(cols), oracle.check_set(cols))
+
+
+def test_set_golden_and_map(ctx):
+    cols, z = load_npz_cols("synthetic_set.npz")
+    g = ctx.check_set(cols)
+    assert g["valid"] == int(z["valid"]) and g["first_fail_entry"] == int(z["first_fail_entry"])
+    assert (g["runs"][1] == z["runs_lost"]).all()
+    r = checker.SetChecker().check(None, cols, {})
+    assert r["lost-count"] == int(z["counts"][3])
+    assert r["lost"] == checker._runs_str(z["runs_lost"].tolist())
+
+
+def test_set_edge_cases(ctx):
+    inv = lambda p, f, v: {"process": p, "type": "invoke", "f": f, "value": v}
+    ok = lambda p, f, v: {"process": p, "type": "ok", "f": f, "value": v}
+    # never read
+    r = checker.check(checker.set(), None, [inv(0, "add", 1), ok(0, "add", 1)], {})
+    assert r == {"valid?": "unknown", "error": "Set was never read"}
+    # reads: the LAST ok read counts; elements in any order
+    h = [inv(0, "add", 1), ok(0, "add", 1), inv(0, "add", 2), ok(0, "add", 2),
+         inv(1, "read", None), ok(1, "read", [5]),
+         inv(1, "read", None), ok(1, "read", [2, 1, 9])]
+    r = checker.check(checker.set(), None, h, {})
+    assert r["valid?"] is False and r["unexpected"] == "#{9}" and r["ok"] == "#{1..2}"
+    assert r["lost"] == "#{}" and r["recovered-count"] == 0
+    cols = H.encode(h, keyed=False)
+    _set_same(ctx.check_set(cols), oracle.check_set(cols))

@@ -1,0 +1,137 @@
+"""Parity of the device linearizability path (libjh.so, through the C ABI)
+with the CPU oracle: verdict, cause, first failing row and WGL cache size
+must be bit-identical on every key."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, load_npz_cols
+from jepsen_amd import _abi as A
+from jepsen_amd import history as H
+from jepsen_amd import synth
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(gpu, cpu):
+    for f in ("valid", "cause", "fail_entry", "explored"):
+        bad = np.nonzero(gpu[f] != cpu[f])[0]
+        assert len(bad) == 0, (f, bad[:10], gpu[bad[:5]], cpu[bad[:5]])
+
+
+def test_perf_test_history(ctx):
+    d = json.load(open(os.path.join(GOLD, "perf_test.json")))
+    cols = H.encode(d["history"], keyed=False)
+    g = ctx.check_cas(cols, init=0)
+    c = oracle.check_cas(cols, init=0)
+    assert g[0] == A.VALID and tuple(g) == tuple(c)
+    g = ctx.check_cas(cols, init=None)
+    c = oracle.check_cas(cols, init=A.NIL)
+    assert g[0] == A.INVALID and tuple(g) == tuple(c)
+
+
+@pytest.mark.parametrize("name", ["cas_small", "cas_tiny", "cas_init0", "cas_crashy"])
+def test_golden_vectors(ctx, name):
+    man = {m["name"]: m for m in json.load(open(os.path.join(GOLD, "manifest.json")))["synthetic"]}
+    cols, z = load_npz_cols(f"synthetic_{name}.npz")
+    v, s = ctx.check_cas_independent(cols, init=man[name]["init"])
+    exp = np.zeros(cols.n_keys, A.VERDICT_DTYPE)
+    for f in ("valid", "cause", "fail_entry", "explored"):
+        exp[f] = z[f]
+    _same(v, exp)
+    assert s.n_invalid == man[name]["n_invalid"]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5])
+def test_random_histories(ctx, seed):
+    cols, _ = synth.cas_register(n_keys=500, ops_per_key=120, threads_per_key=8, readers=3,
+                                 groups=8, p_info=0.05, p_invalid=0.05, seed=1000 + seed)
+    g, gs = ctx.check_cas_independent(cols)
+    c, cs = oracle.check_cas_independent(cols, threads=8)
+    _same(g, c)
+    assert (gs.valid, gs.n_invalid, gs.n_unknown, gs.first_fail_entry, gs.explored) == \
+           (cs.valid, cs.n_invalid, cs.n_unknown, cs.first_fail_entry, cs.explored)
+
+
+def test_budget_and_deferral(ctx):
+    """Keys past the quick budget go to the deep pass; keys past the full
+    budget are :unknown with explored == budget, exactly like the oracle."""
+    cols, _ = synth.cas_register(n_keys=300, ops_per_key=300, p_invalid=0.2, seed=77)
+    for budget in (100, 3000, 50000):
+        g, _ = ctx.check_cas_independent(cols, budget=budget)
+        c, _ = oracle.check_cas_independent(cols, budget=budget, threads=8)
+        _same(g, c)
+
+
+def test_c3_scale_properties(ctx):
+    """BASELINE config C3 (10k keys x ~1k entries): every key the generator
+    did not fault is valid, and the device equals the oracle on every key."""
+    cols, truth = synth.cas_register(seed=3)
+    g, gs = ctx.check_cas_independent(cols)
+    assert not ((g["valid"] == A.INVALID) & (truth == 0)).any()
+    assert gs.n_keys == cols.n_keys
+    c, cs = oracle.check_cas_independent(cols, threads=16)
+    _same(g, c)
+
+
+def test_single_key_c1(ctx):
+    """C1: one key, 5 processes, 10k entries (plain history, no tuples)."""
+    cols, _ = synth.cas_register(n_keys=1, ops_per_key=5000, threads_per_key=5, readers=2,
+                                 groups=1, p_info=0.01, p_invalid=0.0, seed=1, keyed=False,
+                                 process_limit=10 ** 6)
+    g = ctx.check_cas(cols)
+    c = oracle.check_cas(cols)
+    assert tuple(g) == tuple(c) and g[0] == A.VALID
+
+
+def test_edge_cases(ctx):
+    inv = lambda p, f, v: {"process": p, "type": "invoke", "f": f, "value": v}
+    ok = lambda p, f, v: {"process": p, "type": "ok", "f": f, "value": v}
+    info = lambda p, f, v: {"process": p, "type": "info", "f": f, "value": v}
+    fail = lambda p, f, v: {"process": p, "type": "fail", "f": f, "value": v}
+    cases = [
+        [],
+        [{"process": "nemesis", "type": "info", "f": "start"}],
+        [inv(0, "write", 1), inv(0, "write", 2)],
+        [inv(0, "write", 1), info(0, "write", 1), inv(0, "write", 2)],
+        [ok(0, "write", 1)],
+        [inv(0, "incr", 1), ok(0, "incr", 1)],
+        [inv(0, "incr", 1), fail(0, "incr", 1)],
+        [inv(0, "write", 3), info(0, "write", 3), inv(1, "read", None), ok(1, "read", 3)],
+        [inv(0, "cas", [None, 2]), ok(0, "cas", [None, 2]), inv(1, "read", None), ok(1, "read", 2)],
+        [inv(0, "write", 1), ok(0, "write", 1), inv(0, "write", 2), ok(0, "write", 2),
+         inv(1, "read", None), ok(1, "read", 1)],
+        [inv(0, "read", None), ok(0, "read", None)],
+        [inv(0, "write", -7), ok(0, "write", -7), inv(1, "read", None), ok(1, "read", -7)],
+    ]
+    for i, h in enumerate(cases):
+        cols = H.encode(h, keyed=False)
+        for init in (None, 0):
+            g = ctx.check_cas(cols, init=init)
+            c = oracle.check_cas(cols, init=A.NIL if init is None else init)
+            assert tuple(g) == tuple(c), (i, init, g, c)
+
+
+def test_keys_without_client_ops_and_unkeyed(ctx):
+    """A key seen only on a nemesis entry still gets a (valid, empty) result;
+    a client op whose value is not a tuple belongs to EVERY key
+    (independent.clj:234-245) -- the device path reports EUNSUPPORTED and the
+    host falls back to per-key calls."""
+    from jepsen_amd import checker, independent, model
+    t = independent.tuple_
+    h = [{"process": 0, "type": "invoke", "f": "write", "value": t("a", 1)},
+         {"process": 0, "type": "ok", "f": "write", "value": t("a", 1)},
+         {"process": "nemesis", "type": "info", "f": "start", "value": t("b", None)}]
+    r = checker.check(independent.checker(checker.linearizable({"model": model.cas_register()})),
+                      {}, h, {})
+    assert r["valid?"] is True and set(r["results"]) == {"a", "b"}
+    h2 = h + [{"process": 1, "type": "invoke", "f": "read", "value": None},
+              {"process": 1, "type": "ok", "f": "read", "value": 1}]
+    r = checker.check(independent.checker(checker.linearizable({"model": model.cas_register()})),
+                      {}, h2, {})
+    # key "a": write 1 then read 1 -> valid; key "b": read 1 from nil -> invalid
+    assert r["results"]["a"]["valid?"] is True and r["results"]["b"]["valid?"] is False
+    assert r["failures"] == ["b"]

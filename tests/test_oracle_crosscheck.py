@@ -1,0 +1,120 @@
+"""Independent CPU formulations of linearizability must agree (no GPU).
+
+canonical WGL (what libjh.so implements) == knossos-style linked-list WGL
+(verdict AND cache size) == brute-force linearization search (verdict), and
+for invalid keys the WGL cache equals the full reachable configuration set."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from jepsen_amd import _abi as A
+from jepsen_amd import history as H
+from jepsen_amd import synth
+from oracle import oracle
+
+
+def _sub(cols, k):
+    sel = np.nonzero((cols.key == k) | (cols.key < 0))[0]
+    return H.Columns(n=len(sel), process=cols.process[sel].copy(), type=cols.type[sel].copy(),
+                     f=cols.f[sel].copy(), key=np.full(len(sel), -1, np.int64),
+                     value=cols.value[sel].copy(), value2=cols.value2[sel].copy(), n_keys=0,
+                     aux=cols.aux)
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_three_formulations_agree_tiny(built, seed):
+    cols, _ = synth.cas_register(n_keys=600, ops_per_key=7, threads_per_key=4, readers=1, groups=5,
+                                 p_info=0.15, p_invalid=0.3, nemesis_every=7, seed=seed)
+    counts = {A.VALID: 0, A.INVALID: 0}
+    for k in range(cols.n_keys):
+        r = oracle.key_selftest(_sub(cols, k))
+        assert r["status"] == 0
+        assert r["canonical"] == r["list"], r
+        assert r["canonical_explored"] == r["list_explored"], r
+        assert r["bruteforce"] in (r["canonical"], -1), r
+        counts[r["canonical"]] += 1
+    assert counts[A.INVALID] > 10 and counts[A.VALID] > 10
+
+
+def test_init_value_variants(built):
+    cols, _ = synth.cas_register(n_keys=300, ops_per_key=8, threads_per_key=3, readers=1,
+                                 groups=3, p_info=0.1, p_invalid=0.2, seed=21, init_nil=False)
+    for k in range(cols.n_keys):
+        for init in (0, A.NIL, 3):
+            r = oracle.key_selftest(_sub(cols, k), init=init)
+            assert r["canonical"] == r["list"] and r["canonical_explored"] == r["list_explored"]
+            assert r["bruteforce"] in (r["canonical"], -1)
+
+
+def test_invalid_keys_explore_whole_reachable_set(built):
+    cols, _ = synth.cas_register(n_keys=150, ops_per_key=60, threads_per_key=6, readers=2,
+                                 groups=3, p_info=0.05, p_invalid=0.3, seed=31)
+    L = oracle.lib()
+    L.orc_key_stats.argtypes = [C.POINTER(A.JhHistory), C.c_int64, C.c_int64, C.c_int64,
+                                C.c_int64, C.c_int64, C.POINTER(C.c_int64)]
+    h = cols.as_jh()
+    res = np.zeros(6 * cols.n_keys, np.int64)
+    L.orc_key_stats(C.byref(h), A.NIL, A.DEFAULT_BUDGET, 1 << 22, 0, cols.n_keys, A.ptr64(res))
+    r = res.reshape(-1, 6)
+    assert (r[:, 0] == r[:, 2]).all()                 # same verdict
+    inv = r[:, 0] == A.INVALID
+    assert inv.sum() > 5
+    assert (r[inv, 1] == r[inv, 3]).all()             # explored == |reachable|
+
+
+def test_faithful_split_equals_bucketed(built):
+    """independent.clj:234-245's O(K*N) subhistory == the O(N) bucketed split."""
+    cols, _ = synth.cas_register(n_keys=120, ops_per_key=50, seed=41, nemesis_every=30)
+    a, sa = oracle.check_cas_independent(cols, mode=0)
+    b, sb = oracle.check_cas_independent(cols, mode=1, threads=4)
+    assert (a == b).all()
+    assert sa.valid == sb.valid and sa.n_invalid == sb.n_invalid
+
+
+def test_budget_gives_unknown(built):
+    cols, _ = synth.cas_register(n_keys=50, ops_per_key=200, seed=51, p_invalid=0.2)
+    v, _ = oracle.check_cas_independent(cols, budget=50)
+    assert (v["valid"] == A.UNKNOWN).any()
+    unk = v["valid"] == A.UNKNOWN
+    assert (v["explored"][unk] == 50).all() and (v["cause"][unk] == 1).all()
+    # raising the budget resolves them, and never flips a resolved verdict
+    w, _ = oracle.check_cas_independent(cols)
+    res = v["valid"] != A.UNKNOWN
+    assert (w["valid"][res] == v["valid"][res]).all()
+
+
+def test_history_completion_errors(built):
+    def enc(ops):
+        return H.encode(ops, keyed=False)
+    inv = lambda p, f, v: {"process": p, "type": "invoke", "f": f, "value": v}
+    ok = lambda p, f, v: {"process": p, "type": "ok", "f": f, "value": v}
+    info = lambda p, f, v: {"process": p, "type": "info", "f": f, "value": v}
+    # double invoke (knossos.history/complete throws -> :unknown)
+    v = oracle.check_cas(enc([inv(0, "write", 1), inv(0, "write", 2)]))
+    assert v[0] == A.UNKNOWN and A.CAUSES[v[1]] == "double-invoke"
+    # an :info does not close the process: invoking again is a double invoke
+    v = oracle.check_cas(enc([inv(0, "write", 1), info(0, "write", 1), inv(0, "write", 2)]))
+    assert v[0] == A.UNKNOWN and A.CAUSES[v[1]] == "double-invoke"
+    # completion without invocation
+    v = oracle.check_cas(enc([ok(0, "write", 1)]))
+    assert v[0] == A.UNKNOWN and A.CAUSES[v[1]] == "orphan-completion"
+    # unknown :f on a non-failed op
+    v = oracle.check_cas(enc([inv(0, "incr", 1), ok(0, "incr", 1)]))
+    assert v[0] == A.UNKNOWN and A.CAUSES[v[1]] == "unsupported-f"
+    # nemesis entries are ignored; empty history is valid
+    v = oracle.check_cas(enc([{"process": "nemesis", "type": "info", "f": "start"}]))
+    assert v[0] == A.VALID
+    v = oracle.check_cas(enc([]))
+    assert v[0] == A.VALID and v[3] == 0
+    # a crashed write may or may not have happened
+    v = oracle.check_cas(enc([inv(0, "write", 3), info(0, "write", 3), inv(1, "read", None),
+                              ok(1, "read", 3), inv(2, "read", None), ok(2, "read", 3)]))
+    assert v[0] == A.VALID
+    v = oracle.check_cas(enc([inv(0, "write", 3), info(0, "write", 3), inv(1, "read", None),
+                              ok(1, "read", None)]))
+    assert v[0] == A.VALID
+    # a stale read after a completed write is not
+    v = oracle.check_cas(enc([inv(0, "write", 1), ok(0, "write", 1), inv(0, "write", 2),
+                              ok(0, "write", 2), inv(1, "read", None), ok(1, "read", 1)]))
+    assert v[0] == A.INVALID and v[2] == 5

@@ -256,6 +256,210 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// Per-key tables, built by ONE wave (lanes 0..63) into LDS (or this wave's
+// global scratch when they do not fit):
+//   ops[j]   the key's ops in call order: completed values, return rank rr
+//            (-1 crashed) and a = # ok returns before the invocation
+//   W, woff  the window table: W(t) = ops called before the t-th ok return
+//            and not yet returned there, in call order (<= 64 per t)
+// knossos.history/complete is applied here from the pairing (k_pair):
+// failed ops and crashed/nil reads are dropped (sound; see jh_oracle.c).
+// Returns true if a search is needed; otherwise v is the key's verdict.
+struct KeySrc {
+    const Rec *rec;
+    const int32_t *pair;
+    const uint32_t *off;
+    const uint32_t *rows;
+    const unsigned long long *viol;
+    int32_t *rank;
+    int32_t *flags;
+};
+struct KeyTables {
+    Op *ops;
+    int32_t *woff;
+    uint16_t *W;
+    int n_ops, n_ok;
+    uint32_t s0, s1;
+};
+
+__device__ bool build_key_tables(const KeySrc &S, int key, int lane, char *lds, int lds_bytes,
+                                 char *gscr, uint64_t scr_bytes, KeyTables &T, jh_key_verdict &v) {
+    const uint32_t s0 = S.off[key], s1 = S.off[key + 1];
+    v.valid = JH_VALID; v.cause = 0; v.fail_entry = -1; v.explored = 0;
+    if (s0 == s1) {                          // key absent: no :results entry
+        v.explored = -1;
+        return false;
+    }
+    const unsigned long long vi = S.viol[key];
+    if (vi != VIOL_NONE) {
+        v.valid = JH_UNKNOWN; v.cause = (int)(vi & 15);
+        return false;
+    }
+
+    // ---- pass 1: ranks of kept invocations and of ok returns -----------
+    int n_ops = 0, n_ok = 0, n_crash = 0, badf = 0;
+    long long sum_a_ok = 0, sum_a_crash = 0;
+    for (uint32_t base = s0; base < s1; base += 64) {
+        const uint32_t p = base + lane;
+        const bool valid = p < s1;
+        Rec x = valid ? S.rec[p] : Rec{-1, 0, 0, 0, 0, 0};
+        const int q = valid ? S.pair[p] : -1;
+        Rec y = q >= 0 ? S.rec[q] : Rec{-1, 0, 0, 0, 0, 0};
+        // as an invocation
+        const bool inv = x.proc >= 0 && x.type == T_INVOKE;
+        const bool c_ok = inv && q >= 0 && y.type == T_OK;
+        const bool c_fail = inv && q >= 0 && y.type == T_FAIL;
+        int v1c = x.v1;
+        if (c_ok && x.v1 == 0 && (x.f != F_CAS || x.v2 == 0)) v1c = y.v1;
+        const bool kept = inv && !c_fail && !(x.f == F_READ && (!c_ok || v1c == 0));
+        // as an ok return whose invocation is kept
+        bool ret = false;
+        if (x.proc >= 0 && x.type == T_OK && q >= 0) {
+            int iv1 = y.v1;
+            if (iv1 == 0 && (y.f != F_CAS || y.v2 == 0)) iv1 = x.v1;
+            ret = !(y.f == F_READ && iv1 == 0);
+        }
+        const uint64_t bi = ballot(kept), br = ballot(ret);
+        const int my_op = n_ops + mbcnt(bi);
+        const int a = n_ok + mbcnt(br);
+        if (valid) S.rank[p] = kept ? my_op : (ret ? -(a + 2) : -1);
+        badf |= (int)(ballot(kept && x.f > F_CAS) != 0);
+        const bool crash = kept && !c_ok;
+        n_crash += __popcll(ballot(crash));
+        long long sa_ok = (kept && c_ok) ? a : 0, sa_cr = crash ? a : 0;
+        for (int o = 32; o > 0; o >>= 1) {
+            sa_ok += __shfl_xor(sa_ok, o);
+            sa_cr += __shfl_xor(sa_cr, o);
+        }
+        sum_a_ok += sa_ok; sum_a_crash += sa_cr;
+        n_ops += __popcll(bi);
+        n_ok += __popcll(br);
+    }
+    if (badf) {
+        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_BAD_F;
+        return false;
+    }
+    if (n_ok == 0) {
+        return false;
+    }
+    const long long sumW = (long long)n_ok * (n_ok + 1) / 2 - sum_a_ok +
+                           (long long)n_crash * n_ok - sum_a_crash;
+    if (sumW > 64LL * n_ok) {                // the average window is wider than 64
+        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
+        return false;
+    }
+    if (n_ops > 65535 || n_ok >= (int)T_MASK) {
+        if (lane == 0) atomicOr(S.flags, 1);
+        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
+        return false;
+    }
+    // ---- table placement: LDS if it fits, else this wave's global scratch
+    const uint64_t b_ops = (uint64_t)n_ops * sizeof(Op);
+    const uint64_t b_off = ((uint64_t)(n_ok + 1) * 4 + 15) & ~15ULL;
+    const uint64_t b_w = ((uint64_t)sumW * 2 + 128 + 15) & ~15ULL;   // +64 entries slack
+    const uint64_t total = b_ops + b_off + b_w;
+    char *tb;
+    if (total <= (uint64_t)lds_bytes) tb = lds;
+    else if (total <= scr_bytes) tb = gscr;
+    else {
+        if (lane == 0) atomicOr(S.flags, 2);
+        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
+        return false;
+    }
+    Op *ops = (Op *)tb;
+    int32_t *woff = (int32_t *)(tb + b_ops);
+    uint16_t *W = (uint16_t *)(tb + b_ops + b_off);
+
+    // ---- pass 2: op records in call order --------------------------------
+    {
+        int nops = 0, nok = 0;
+        for (uint32_t base = s0; base < s1; base += 64) {
+            const uint32_t p = base + lane;
+            const bool valid = p < s1;
+            const int rk = valid ? S.rank[p] : -1;
+            const bool kept = rk >= 0, ret = rk <= -2;
+            const uint64_t bi = ballot(kept), br = ballot(ret);
+            if (kept) {
+                Rec x = S.rec[p];
+                const int q = S.pair[p];
+                int rr = -1, v1c = x.v1, v2c = x.v2;
+                if (q >= 0) {
+                    Rec y = S.rec[q];
+                    if (y.type == T_OK) {
+                        rr = -(S.rank[q] + 2);
+                        if (x.f == F_CAS) { if (x.v1 == 0 && x.v2 == 0) { v1c = y.v1; v2c = y.v2; } }
+                        else if (x.v1 == 0) v1c = y.v1;
+                    }
+                }
+                const int a = nok + mbcnt(br);
+                Op o; o.v1 = v1c; o.v2 = v2c; o.rr = rr; o.fa = x.f | (a << 2);
+                ops[rk] = o;
+            }
+            nops += __popcll(bi);
+            nok += __popcll(br);
+        }
+    }
+    wave_sync();
+
+    // ---- window table W(t): W(t) = W(t-1) - {RET[t-1]} + {ops with a == t}
+    int too_wide = 0;
+    {
+        int w = 0, nxt = 0, offt = 0;
+        for (int t = 0; t < n_ok; t++) {
+            int prev = 0;
+            bool keep = false;
+            if (t > 0 && lane < w) {
+                prev = W[offt - w + lane];
+                keep = ops[prev].rr != t - 1;
+            }
+            const uint64_t bk = ballot(keep);
+            const int nk = __popcll(bk);
+            if (keep) W[offt + mbcnt(bk)] = (uint16_t)prev;
+            // append ops whose invocation precedes the t-th ok return
+            int added = 0;
+            for (;;) {
+                const int j = nxt + lane;
+                const bool in = j < n_ops && (ops[j].fa >> 2) <= t;
+                const uint64_t ba = ballot(in);
+                const int c = __popcll(ba);     // a is non-decreasing: a prefix
+                if (in && nk + added + lane < 64) W[offt + nk + added + lane] = (uint16_t)j;
+                added += c; nxt += c;
+                if (c < 64) break;
+            }
+            w = nk + added;
+            if (w > 64) { too_wide = 1; break; }
+            if (lane == 0) woff[t] = offt;
+            offt += w;
+            wave_sync();
+        }
+        if (lane == 0) woff[n_ok] = offt;
+    }
+    wave_sync();
+    if (too_wide) {
+        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
+        return false;
+    }
+
+    T.ops = ops; T.woff = woff; T.W = W; T.n_ops = n_ops; T.n_ok = n_ok; T.s0 = s0; T.s1 = s1;
+    return true;
+}
+
+// history row of the ok completion of RET[t] (the first op no configuration
+// gets past, for an invalid key)
+__device__ long long ret_row(const KeySrc &S, const KeyTables &T, uint32_t t, int lane) {
+    const int want = -((int)t + 2);
+    for (uint32_t base = T.s0; base < T.s1; base += 64) {
+        const uint32_t p = base + lane;
+        const bool hit = p < T.s1 && S.rank[p] == want;
+        const uint64_t b = ballot(hit);
+        if (b) {
+            const int l = __builtin_ctzll(b);
+            return (long long)S.rows[readlane((int)p, l)];
+        }
+    }
+    return -1;
+}
+
 __global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int lane = threadIdx.x;
@@ -265,6 +469,7 @@ __global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
     char *gscr = A.scratch + (size_t)blockIdx.x * A.scratch_bytes;
     const uint32_t cap_mask = A.memo_cap - 1;
     unsigned long long my_probes = 0;
+    const KeySrc src{A.rec, A.pair, A.off, A.rows, A.viol, A.rank, A.flags};
 
     for (;;) {
         int idx = 0;
@@ -272,171 +477,16 @@ __global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
         idx = readlane(idx, 0);
         if (idx >= A.n_list) break;
         const int key = A.list[idx];
-        const uint32_t s0 = A.off[key], s1 = A.off[key + 1];
         jh_key_verdict v;
-        v.valid = JH_VALID; v.cause = 0; v.fail_entry = -1; v.explored = 0;
-        if (s0 == s1) {                          // key absent: no :results entry
-            v.explored = -1;
+        KeyTables T;
+        if (!build_key_tables(src, key, lane, lds, LDS_BYTES, gscr, A.scratch_bytes, T, v)) {
             if (lane == 0) A.out[key] = v;
             continue;
         }
-        const unsigned long long vi = A.viol[key];
-        if (vi != VIOL_NONE) {
-            v.valid = JH_UNKNOWN; v.cause = (int)(vi & 15);
-            if (lane == 0) A.out[key] = v;
-            continue;
-        }
-
-        // ---- pass 1: ranks of kept invocations and of ok returns -----------
-        int n_ops = 0, n_ok = 0, n_crash = 0, badf = 0;
-        long long sum_a_ok = 0, sum_a_crash = 0;
-        for (uint32_t base = s0; base < s1; base += 64) {
-            const uint32_t p = base + lane;
-            const bool valid = p < s1;
-            Rec x = valid ? A.rec[p] : Rec{-1, 0, 0, 0, 0, 0};
-            const int q = valid ? A.pair[p] : -1;
-            Rec y = q >= 0 ? A.rec[q] : Rec{-1, 0, 0, 0, 0, 0};
-            // as an invocation
-            const bool inv = x.proc >= 0 && x.type == T_INVOKE;
-            const bool c_ok = inv && q >= 0 && y.type == T_OK;
-            const bool c_fail = inv && q >= 0 && y.type == T_FAIL;
-            int v1c = x.v1;
-            if (c_ok && x.v1 == 0 && (x.f != F_CAS || x.v2 == 0)) v1c = y.v1;
-            const bool kept = inv && !c_fail && !(x.f == F_READ && (!c_ok || v1c == 0));
-            // as an ok return whose invocation is kept
-            bool ret = false;
-            if (x.proc >= 0 && x.type == T_OK && q >= 0) {
-                int iv1 = y.v1;
-                if (iv1 == 0 && (y.f != F_CAS || y.v2 == 0)) iv1 = x.v1;
-                ret = !(y.f == F_READ && iv1 == 0);
-            }
-            const uint64_t bi = ballot(kept), br = ballot(ret);
-            const int my_op = n_ops + mbcnt(bi);
-            const int a = n_ok + mbcnt(br);
-            if (valid) A.rank[p] = kept ? my_op : (ret ? -(a + 2) : -1);
-            badf |= (int)(ballot(kept && x.f > F_CAS) != 0);
-            const bool crash = kept && !c_ok;
-            n_crash += __popcll(ballot(crash));
-            long long sa_ok = (kept && c_ok) ? a : 0, sa_cr = crash ? a : 0;
-            for (int o = 32; o > 0; o >>= 1) {
-                sa_ok += __shfl_xor(sa_ok, o);
-                sa_cr += __shfl_xor(sa_cr, o);
-            }
-            sum_a_ok += sa_ok; sum_a_crash += sa_cr;
-            n_ops += __popcll(bi);
-            n_ok += __popcll(br);
-        }
-        if (badf) {
-            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_BAD_F;
-            if (lane == 0) A.out[key] = v;
-            continue;
-        }
-        if (n_ok == 0) {
-            if (lane == 0) A.out[key] = v;
-            continue;
-        }
-        const long long sumW = (long long)n_ok * (n_ok + 1) / 2 - sum_a_ok +
-                               (long long)n_crash * n_ok - sum_a_crash;
-        if (sumW > 64LL * n_ok) {                // the average window is wider than 64
-            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-            if (lane == 0) A.out[key] = v;
-            continue;
-        }
-        if (n_ops > 65535 || n_ok >= (int)T_MASK) {
-            if (lane == 0) atomicOr(A.flags, 1);
-            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-            if (lane == 0) A.out[key] = v;
-            continue;
-        }
-        // ---- table placement: LDS if it fits, else this wave's global scratch
-        const uint64_t b_ops = (uint64_t)n_ops * sizeof(Op);
-        const uint64_t b_off = ((uint64_t)(n_ok + 1) * 4 + 15) & ~15ULL;
-        const uint64_t b_w = ((uint64_t)sumW * 2 + 128 + 15) & ~15ULL;   // +64 entries slack
-        const uint64_t total = b_ops + b_off + b_w;
-        char *tb;
-        if (total <= (uint64_t)LDS_BYTES) tb = lds;
-        else if (total <= A.scratch_bytes) tb = gscr;
-        else {
-            if (lane == 0) atomicOr(A.flags, 2);
-            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-            if (lane == 0) A.out[key] = v;
-            continue;
-        }
-        Op *ops = (Op *)tb;
-        int32_t *woff = (int32_t *)(tb + b_ops);
-        uint16_t *W = (uint16_t *)(tb + b_ops + b_off);
-
-        // ---- pass 2: op records in call order --------------------------------
-        {
-            int nops = 0, nok = 0;
-            for (uint32_t base = s0; base < s1; base += 64) {
-                const uint32_t p = base + lane;
-                const bool valid = p < s1;
-                const int rk = valid ? A.rank[p] : -1;
-                const bool kept = rk >= 0, ret = rk <= -2;
-                const uint64_t bi = ballot(kept), br = ballot(ret);
-                if (kept) {
-                    Rec x = A.rec[p];
-                    const int q = A.pair[p];
-                    int rr = -1, v1c = x.v1, v2c = x.v2;
-                    if (q >= 0) {
-                        Rec y = A.rec[q];
-                        if (y.type == T_OK) {
-                            rr = -(A.rank[q] + 2);
-                            if (x.f == F_CAS) { if (x.v1 == 0 && x.v2 == 0) { v1c = y.v1; v2c = y.v2; } }
-                            else if (x.v1 == 0) v1c = y.v1;
-                        }
-                    }
-                    const int a = nok + mbcnt(br);
-                    Op o; o.v1 = v1c; o.v2 = v2c; o.rr = rr; o.fa = x.f | (a << 2);
-                    ops[rk] = o;
-                }
-                nops += __popcll(bi);
-                nok += __popcll(br);
-            }
-        }
-        wave_sync();
-
-        // ---- window table W(t): W(t) = W(t-1) - {RET[t-1]} + {ops with a == t}
-        int too_wide = 0;
-        {
-            int w = 0, nxt = 0, offt = 0;
-            for (int t = 0; t < n_ok; t++) {
-                int prev = 0;
-                bool keep = false;
-                if (t > 0 && lane < w) {
-                    prev = W[offt - w + lane];
-                    keep = ops[prev].rr != t - 1;
-                }
-                const uint64_t bk = ballot(keep);
-                const int nk = __popcll(bk);
-                if (keep) W[offt + mbcnt(bk)] = (uint16_t)prev;
-                // append ops whose invocation precedes the t-th ok return
-                int added = 0;
-                for (;;) {
-                    const int j = nxt + lane;
-                    const bool in = j < n_ops && (ops[j].fa >> 2) <= t;
-                    const uint64_t ba = ballot(in);
-                    const int c = __popcll(ba);     // a is non-decreasing: a prefix
-                    if (in && nk + added + lane < 64) W[offt + nk + added + lane] = (uint16_t)j;
-                    added += c; nxt += c;
-                    if (c < 64) break;
-                }
-                w = nk + added;
-                if (w > 64) { too_wide = 1; break; }
-                if (lane == 0) woff[t] = offt;
-                offt += w;
-                wave_sync();
-            }
-            if (lane == 0) woff[n_ok] = offt;
-        }
-        wave_sync();
-        if (too_wide) {
-            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-            if (lane == 0) A.out[key] = v;
-            continue;
-        }
-
+        const int n_ok = T.n_ok;
+        const Op *ops = T.ops;
+        const int32_t *woff = T.woff;
+        const uint16_t *W = T.W;
         // ---- WGL search in canonical coordinates ------------------------------
         const uint32_t gen = (A.gen_base + (uint32_t)key + 1) & ((1u << GEN_BITS) - 1);
         const uint64_t gen_hi = (uint64_t)gen << 40;
@@ -554,26 +604,169 @@ __global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
         v.valid = verdict;
         v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
         v.explored = inserts;
-        if (verdict == JH_INVALID) {
-            // row of the ok completion of RET[tmax]
-            const int want = -((int)tmax + 2);
-            long long row = -1;
-            for (uint32_t base = s0; base < s1; base += 64) {
-                const uint32_t p = base + lane;
-                const bool hit = p < s1 && A.rank[p] == want;
-                const uint64_t b = ballot(hit);
-                if (b) {
-                    const int l = __builtin_ctzll(b);
-                    row = (long long)A.rows[readlane((int)p, l)];
-                    break;
-                }
-            }
-            v.fail_entry = row;
-        }
+        if (verdict == JH_INVALID) v.fail_entry = ret_row(src, T, tmax, lane);
         if (lane == 0) A.out[key] = v;
     }
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
+}
+
+// ---------------------------------------------------------------------------
+// Heavy keys: parallel breadth-first enumeration of the reachable
+// configuration graph by a whole workgroup. For a key with no terminal
+// configuration (invalid) WGL's cache ends up holding exactly this set, so
+// verdict, explored count and the furthest return rank (fail_entry) are
+// identical to the sequential search. A key where a terminal configuration
+// is reachable (valid) or the set outgrows the budget is handed to the
+// sequential search (only it defines where :unknown starts for those).
+constexpr int BFS_THREADS = 512;
+constexpr int BFS_LDS_BYTES = 49152;
+constexpr uint64_t BFS_EMPTY = ~0ULL;
+
+struct BfsArgs {
+    KeySrc src;
+    const int32_t *list;
+    int32_t n_list;
+    int32_t *queue;
+    jh_key_verdict *out;
+    int32_t *unres_list;
+    int32_t *unres_count;
+    uint64_t *set;          // per workgroup: set_cap slots
+    uint32_t set_cap;       // power of two
+    uint64_t *q;            // per workgroup: 2 x q_cap configurations
+    uint32_t q_cap;
+    char *scratch;          // per workgroup table space
+    uint64_t scratch_bytes;
+    int64_t budget;
+    int32_t init_state;
+    int32_t states_ok;      // every interned state < 2^12
+};
+
+__device__ __forceinline__ uint64_t bfs_pack(uint32_t t, uint32_t s, uint32_t m) {
+    return ((uint64_t)t << 44) | ((uint64_t)s << 32) | m;
+}
+
+__global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    __shared__ KeyTables sT;
+    __shared__ jh_key_verdict sv;
+    __shared__ int s_key, s_need, s_maxw, s_status;
+    __shared__ unsigned s_ncur, s_nnext, s_tmax;
+    __shared__ unsigned long long s_count;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    uint64_t *set = A.set + (size_t)blockIdx.x * A.set_cap;
+    uint64_t *qa = A.q + (size_t)blockIdx.x * 2 * A.q_cap;
+    char *gscr = A.scratch + (size_t)blockIdx.x * A.scratch_bytes;
+    const uint32_t cmask = A.set_cap - 1;
+    for (;;) {
+        if (tid == 0) {
+            const int idx = atomicAdd(A.queue, 1);
+            s_key = idx < A.n_list ? A.list[idx] : -1;
+        }
+        __syncthreads();
+        const int key = s_key;
+        if (key < 0) break;
+        if (wid == 0) {
+            KeyTables T;
+            jh_key_verdict v;
+            const bool need = build_key_tables(A.src, key, lane, lds, BFS_LDS_BYTES, gscr,
+                                               A.scratch_bytes, T, v);
+            if (lane == 0) { sT = T; sv = v; s_need = need; s_maxw = 0; s_status = 0; }
+        }
+        __syncthreads();
+        if (!s_need) {
+            if (tid == 0) A.out[key] = sv;
+            __syncthreads();
+            continue;
+        }
+        const KeyTables T = sT;
+        for (int t = tid; t < T.n_ok; t += BFS_THREADS) atomicMax(&s_maxw, T.woff[t + 1] - T.woff[t]);
+        __syncthreads();
+        if (s_maxw > 32 || !A.states_ok || T.n_ok >= (1 << 20) - 2) {
+            if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
+            __syncthreads();
+            continue;
+        }
+        for (uint32_t i = tid; i < A.set_cap; i += BFS_THREADS) set[i] = BFS_EMPTY;
+        if (tid == 0) {
+            qa[0] = bfs_pack(0, (uint32_t)A.init_state, 0);
+            s_ncur = 1; s_nnext = 0; s_tmax = 0; s_count = 0;
+        }
+        __syncthreads();
+        uint64_t *cur = qa, *nxt = qa + A.q_cap;
+        for (;;) {
+            const unsigned ncur = s_ncur;
+            for (unsigned i = tid; i < ncur; i += BFS_THREADS) {
+                const uint64_t c = cur[i];
+                const uint32_t t = (uint32_t)(c >> 44), s = (uint32_t)(c >> 32) & 0xFFF;
+                const uint32_t mask = (uint32_t)c;
+                const int wo = T.woff[t], w = T.woff[t + 1] - wo;
+                for (int j = 0; j < w; j++) {
+                    if ((mask >> j) & 1) continue;
+                    const Op o = T.ops[T.W[wo + j]];
+                    int s2;
+                    if (!cas_step(o.fa & 3, o.v1, o.v2, (int)s, &s2)) continue;
+                    uint32_t u = t, nm = mask | (1u << j);
+                    if (o.rr == (int)t) {
+                        const uint32_t lin = nm;
+                        u = t + 1;
+                        while (u < (uint32_t)T.n_ok) {
+                            bool hit = false;
+                            for (int m = 0; m < w && !hit; m++)
+                                hit = ((lin >> m) & 1) && T.ops[T.W[wo + m]].rr == (int)u;
+                            if (!hit) break;
+                            u++;
+                        }
+                        nm = 0;
+                        if (u < (uint32_t)T.n_ok) {
+                            int b = 0;
+                            for (int m = 0; m < w; m++) {
+                                const int rr = T.ops[T.W[wo + m]].rr;
+                                if (rr < 0 || rr >= (int)u) {
+                                    if ((lin >> m) & 1) nm |= 1u << b;
+                                    b++;
+                                }
+                            }
+                        }
+                    }
+                    const uint64_t ck = bfs_pack(u, (uint32_t)s2, nm);
+                    uint32_t h = (uint32_t)jh_mix64(ck) & cmask;
+                    bool ins = false;
+                    for (uint32_t probe = 0; probe <= cmask; probe++) {
+                        const unsigned long long prev =
+                            atomicCAS((unsigned long long *)&set[h], BFS_EMPTY, ck);
+                        if (prev == BFS_EMPTY) { ins = true; break; }
+                        if (prev == ck) break;
+                        h = (h + 1) & cmask;
+                    }
+                    if (!ins) continue;
+                    const unsigned long long n = atomicAdd(&s_count, 1ULL);
+                    if ((long long)n >= A.budget) atomicOr(&s_status, 2);
+                    if (u == (uint32_t)T.n_ok) atomicOr(&s_status, 1);
+                    atomicMax(&s_tmax, u);
+                    const unsigned pos = atomicAdd(&s_nnext, 1u);
+                    if (pos < A.q_cap) nxt[pos] = ck; else atomicOr(&s_status, 2);
+                }
+            }
+            __syncthreads();
+            const int st = s_status;
+            const unsigned nn = s_nnext;
+            __syncthreads();
+            if (st || nn == 0) break;
+            if (tid == 0) { s_ncur = nn; s_nnext = 0; }
+            uint64_t *tmp = cur; cur = nxt; nxt = tmp;
+            __syncthreads();
+        }
+        if (s_status) {
+            if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
+        } else if (wid == 0) {
+            jh_key_verdict v;
+            v.valid = JH_INVALID; v.cause = 0; v.explored = (int64_t)s_count;
+            v.fail_entry = ret_row(A.src, T, s_tmax, lane);
+            if (lane == 0) A.out[key] = v;
+        }
+        __syncthreads();
+    }
 }
 
 __global__ void k_summary(const jh_key_verdict *__restrict__ v, int64_t K, long long *sum) {
@@ -688,7 +881,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
 
     // phase 1: every key, quick budget, persistent grid
     const uint32_t memo_cap1 = 1u << 16;
-    const int64_t quick = std::min<int64_t>(budget, memo_cap1 / 4);
+    int64_t quick = std::min<int64_t>(budget, memo_cap1 / 4);
+    if (const char *e = getenv("JH_QUICK_BUDGET")) quick = std::max<int64_t>(1, std::min<int64_t>(quick, atoll(e)));
     const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * 8);
     uint64_t *memo = ctx->ws<uint64_t>(WS_MEMO, (size_t)waves1 * memo_cap1 * 2, /*zero=*/true);
     if (clear_memo) HIP_TRY(hipMemsetAsync(memo, 0, ctx->bufs[WS_MEMO].bytes, st));
@@ -717,18 +911,48 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const int n_defer = qh[1];
+    HIP_TRY(hipEventRecord(ctx->ev[4], st));
+    int n_unres = 0;
     if (n_defer > 0) {
-        // phase 2: deferred keys with the full budget and a memo sized for it
+        // phase 2: heavy keys, one workgroup each, parallel reachable-set BFS
+        uint32_t set_cap = 1u << 12;
+        while ((int64_t)set_cap < 2 * budget && set_cap < (1u << 30)) set_cap <<= 1;
+        const uint32_t q_cap = (uint32_t)std::min<int64_t>(budget + 64, (int64_t)1 << 30);
+        const int wg2 = std::min(n_defer, 128);
+        uint64_t *bset = ctx->ws<uint64_t>(WS_BFS_SET, (size_t)wg2 * set_cap);
+        uint64_t *bq = ctx->ws<uint64_t>(WS_BFS_Q, (size_t)wg2 * 2 * q_cap);
+        char *bscr = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)wg2 * scr_bytes);
+        int32_t *unres = ctx->ws<int32_t>(WS_BFS_META, n_defer + 1);
+        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(q + 3, 0, sizeof(int32_t), st));
+        BfsArgs c{};
+        c.src = KeySrc{rec, pair, off, rB, viol, rank, q + 2};
+        c.list = defer; c.n_list = n_defer; c.queue = q; c.out = out_dev;
+        c.unres_list = unres; c.unres_count = q + 3;
+        c.set = bset; c.set_cap = set_cap; c.q = bq; c.q_cap = q_cap;
+        c.scratch = bscr; c.scratch_bytes = scr_bytes; c.budget = budget;
+        c.init_state = init_state; c.states_ok = (vmax - vmin + 2) < 4096 ? 1 : 0;
+        k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        n_unres = qh[3];
+    }
+    HIP_TRY(hipEventRecord(ctx->ev[5], st));
+    if (n_unres > 0) {
+        // phase 3: keys BFS could not settle (a terminal configuration is
+        // reachable, or the set outgrew the budget): the sequential search
+        // with the full budget defines their verdict and explored count
         uint32_t cap2 = 1u << 16;
         while ((int64_t)cap2 < 2 * budget && cap2 < (1u << 30)) cap2 <<= 1;
-        const int waves2 = std::min(n_defer, 64);
+        const int waves2 = std::min(n_unres, 64);
         uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2);
         Frame *stack2 = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap);
-        char *scr2 = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes);
+        char *scr2 = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)std::max(waves2, 1) * scr_bytes);
         HIP_TRY(hipMemsetAsync(memo2, 0, (size_t)waves2 * cap2 * 16, st));
         HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
         DfsArgs b = a;
-        b.list = defer; b.n_list = n_defer; b.memo = memo2; b.memo_cap = cap2;
+        b.list = ctx->ws<int32_t>(WS_BFS_META, 1); b.n_list = n_unres; b.memo = memo2; b.memo_cap = cap2;
         b.stack = stack2; b.scratch = scr2; b.budget = budget; b.defer = 0;
         b.gen_base = ctx->gen_base + (uint32_t)K + 1;
         k_lin_dfs<<<waves2, 64, LDS_BYTES, st>>>(b);
@@ -758,5 +982,16 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]));
         HIP_TRY(hipEventElapsedTime(&ms_dfs, ctx->ev[1], ctx->ev[2]));
         sum->device_ms = ms; sum->dfs_ms = ms_dfs;
+        if (getenv("JH_DEBUG")) {
+            float a = 0, b = 0, c = 0;
+            HIP_TRY(hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]));
+            HIP_TRY(hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[4]));
+            HIP_TRY(hipEventElapsedTime(&c, ctx->ev[4], ctx->ev[2]));
+            float d = 0;
+            HIP_TRY(hipEventElapsedTime(&d, ctx->ev[5], ctx->ev[2]));
+            HIP_TRY(hipEventElapsedTime(&c, ctx->ev[4], ctx->ev[5]));
+            fprintf(stderr, "[jh] keys=%lld prep=%.3f ms phase1=%.3f ms (waves %d) deferred=%d bfs=%.3f ms unresolved=%d deep=%.3f ms\n",
+                    (long long)K, a, b, waves1, n_defer, c, n_unres, d);
+        }
     }
 }

@@ -1,0 +1,74 @@
+"""Multi-rank sharding of the independent checker, world_size 2 on gloo
+(CPU). The per-rank checker here is the oracle; on GPUs it is libjh on each
+rank's device and the all-reduce runs on RCCL (bench.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from jepsen_amd import _abi as A
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from jepsen_amd import shard, synth
+        from oracle import oracle
+        cols, _ = synth.cas_register(n_keys=240, ops_per_key=80, p_invalid=0.1, seed=9)
+
+        def check_fn(sub, init, budget):
+            return oracle.check_cas_independent(sub)
+
+        mine, v, g = shard.check_cas_independent_sharded(cols, rank, world, check_fn)
+        q.put((rank, mine.tolist(), v.tolist(), g))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_equals_single(built, world):
+    from jepsen_amd import shard, synth
+    from oracle import oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cols, _ = synth.cas_register(n_keys=240, ops_per_key=80, p_invalid=0.1, seed=9)
+    full, s = oracle.check_cas_independent(cols)
+    seen = set()
+    for rank, mine, v, g in res:
+        v = np.array([tuple(x) for x in v], dtype=A.VERDICT_DTYPE)
+        for i, k in enumerate(mine):
+            assert tuple(v[i]) == tuple(full[k]), (rank, k)
+            seen.add(k)
+        # every rank sees the same global summary, equal to the unsharded one
+        assert g["valid"] == s.valid and g["n_invalid"] == s.n_invalid
+        assert g["n_unknown"] == s.n_unknown and g["n_keys"] == s.n_keys
+        assert g["explored"] == s.explored and g["first_fail_entry"] == s.first_fail_entry
+    assert seen == set(range(cols.n_keys))
+
+
+def test_lpt_balances():
+    from jepsen_amd import shard
+    costs = np.array([9, 8, 7, 6, 5, 4, 3, 2, 1, 1], np.int64)
+    owner = shard.assign_keys(costs, 3)
+    loads = np.bincount(owner, weights=costs, minlength=3)
+    assert loads.max() - loads.min() <= 2

@@ -66,6 +66,20 @@ def test_budget_and_deferral(ctx):
         _same(g, c)
 
 
+@pytest.mark.parametrize("quick", ["1", "40", "700"])
+def test_heavy_key_paths(ctx, quick, monkeypatch):
+    """Force keys through the deferral -> workgroup BFS -> sequential DFS
+    cascade with a tiny quick budget: results must not change."""
+    cols, _ = synth.cas_register(n_keys=400, ops_per_key=150, p_invalid=0.2, p_info=0.05, seed=88)
+    c, _ = oracle.check_cas_independent(cols, threads=8)
+    monkeypatch.setenv("JH_QUICK_BUDGET", quick)
+    g, _ = ctx.check_cas_independent(cols)
+    _same(g, c)
+    g, _ = ctx.check_cas_independent(cols, budget=2000)
+    c, _ = oracle.check_cas_independent(cols, budget=2000, threads=8)
+    _same(g, c)
+
+
 def test_c3_scale_properties(ctx):
     """BASELINE config C3 (10k keys x ~1k entries): every key the generator
     did not fault is valid, and the device equals the oracle on every key."""

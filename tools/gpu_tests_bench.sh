@@ -1,0 +1,5 @@
+# GPU parity tests then the bench with phase timings
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -x -q -k "not c2_scale" > gpurun_out/gpu_tests.log 2>&1 && \
+JH_DEBUG=1 timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu > gpurun_out/bench.log 2>&1

@@ -30,7 +30,11 @@ namespace {
 constexpr int F_READ = 0, F_WRITE = 1, F_CAS = 2, F_OTHER = 4;
 constexpr int T_INVOKE = 0, T_OK = 1, T_FAIL = 2, T_INFO = 3;
 constexpr uint64_t VIOL_NONE = ~0ULL;
-constexpr int LDS_BYTES = 20480;          // per-wave table budget (8 waves/CU)
+constexpr int LDS_TBL = 15360;            // per-wave op/window tables
+constexpr int MEMO_SLOTS = 2048;          // per-wave LDS memo (hot layers t >= theta)
+constexpr int MEMO_EVICT = 1024;          // evict at load factor 1/2
+constexpr int RING = 64;                  // per-wave LDS stack ring (frames)
+constexpr int LDS_BYTES = LDS_TBL + MEMO_SLOTS * 8 + RING * 16;   // 32 KB -> 5 waves/CU
 constexpr int STATE_BITS = 20, T_BITS = 20, GEN_BITS = 24;
 constexpr uint32_t STATE_MASK = (1u << STATE_BITS) - 1, T_MASK = (1u << T_BITS) - 1;
 
@@ -223,6 +227,8 @@ struct DfsArgs {
     uint32_t gen_base;
     int32_t *flags;             // [0] |= 1: key too large for this build
     unsigned long long *probes; // total memo probes (roofline accounting)
+    int32_t states8;            // every interned state < 256 (LDS memo packing)
+    unsigned long long *dbg;    // JH_DEBUG=2: per-wave cycle accounting (8 words)
 };
 
 __device__ __forceinline__ uint64_t ballot(bool b) { return __ballot(b); }
@@ -256,15 +262,19 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// Per-key tables, built by ONE wave (lanes 0..63) into LDS (or this wave's
-// global scratch when they do not fit):
+// Per-key tables, built by ONE wave (lanes 0..63) into LDS when they fit,
+// else into the wave's global scratch. Everything that touches them is
+// templated on the location so LDS tables compile to ds_* and scratch to
+// global_* instructions (a runtime-chosen pointer would be a flat access,
+// which waits for every outstanding global store of the wave).
 //   ops[j]   the key's ops in call order: completed values, return rank rr
 //            (-1 crashed) and a = # ok returns before the invocation
 //   W, woff  the window table: W(t) = ops called before the t-th ok return
 //            and not yet returned there, in call order (<= 64 per t)
 // knossos.history/complete is applied here from the pairing (k_pair):
 // failed ops and crashed/nil reads are dropped (sound; see jh_oracle.c).
-// Returns true if a search is needed; otherwise v is the key's verdict.
+extern __shared__ __attribute__((aligned(16))) char jh_lds[];
+
 struct KeySrc {
     const Rec *rec;
     const int32_t *pair;
@@ -274,18 +284,32 @@ struct KeySrc {
     int32_t *rank;
     int32_t *flags;
 };
-struct KeyTables {
-    Op *ops;
-    int32_t *woff;
-    uint16_t *W;
+struct KeyInfo {
     int n_ops, n_ok;
+    long long sumW;
     uint32_t s0, s1;
 };
 
-__device__ bool build_key_tables(const KeySrc &S, int key, int lane, char *lds, int lds_bytes,
-                                 char *gscr, uint64_t scr_bytes, KeyTables &T, jh_key_verdict &v) {
-    const uint32_t s0 = S.off[key], s1 = S.off[key + 1];
+__device__ __forceinline__ uint64_t tbl_ops_bytes(const KeyInfo &K) { return (uint64_t)K.n_ops * sizeof(Op); }
+__device__ __forceinline__ uint64_t tbl_off_bytes(const KeyInfo &K) { return ((uint64_t)(K.n_ok + 1) * 4 + 15) & ~15ULL; }
+__device__ __forceinline__ uint64_t tbl_w_bytes(const KeyInfo &K) { return ((uint64_t)K.sumW * 2 + 128 + 15) & ~15ULL; }
+__device__ __forceinline__ uint64_t tbl_bytes(const KeyInfo &K) {
+    return tbl_ops_bytes(K) + tbl_off_bytes(K) + tbl_w_bytes(K);
+}
+
+// table base: the dynamic LDS region at lds_off, or the global scratch
+template <bool L>
+__device__ __forceinline__ char *tbl_base(uint32_t lds_off, char *gscr) {
+    if constexpr (L) return jh_lds + lds_off;
+    else return gscr;
+}
+
+// Pass 1: ranks of kept invocations and of ok returns (into S.rank), op and
+// window sizes. Returns true if the key needs a search; otherwise v is final.
+__device__ bool key_pass1(const KeySrc &S, int key, int lane, KeyInfo &K, jh_key_verdict &v) {
     v.valid = JH_VALID; v.cause = 0; v.fail_entry = -1; v.explored = 0;
+    const uint32_t s0 = S.off[key], s1 = S.off[key + 1];
+    K.s0 = s0; K.s1 = s1;
     if (s0 == s1) {                          // key absent: no :results entry
         v.explored = -1;
         return false;
@@ -295,8 +319,6 @@ __device__ bool build_key_tables(const KeySrc &S, int key, int lane, char *lds, 
         v.valid = JH_UNKNOWN; v.cause = (int)(vi & 15);
         return false;
     }
-
-    // ---- pass 1: ranks of kept invocations and of ok returns -----------
     int n_ops = 0, n_ok = 0, n_crash = 0, badf = 0;
     long long sum_a_ok = 0, sum_a_crash = 0;
     for (uint32_t base = s0; base < s1; base += 64) {
@@ -335,16 +357,14 @@ __device__ bool build_key_tables(const KeySrc &S, int key, int lane, char *lds, 
         n_ops += __popcll(bi);
         n_ok += __popcll(br);
     }
+    K.n_ops = n_ops; K.n_ok = n_ok;
     if (badf) {
         v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_BAD_F;
         return false;
     }
-    if (n_ok == 0) {
-        return false;
-    }
-    const long long sumW = (long long)n_ok * (n_ok + 1) / 2 - sum_a_ok +
-                           (long long)n_crash * n_ok - sum_a_crash;
-    if (sumW > 64LL * n_ok) {                // the average window is wider than 64
+    if (n_ok == 0) return false;
+    K.sumW = (long long)n_ok * (n_ok + 1) / 2 - sum_a_ok + (long long)n_crash * n_ok - sum_a_crash;
+    if (K.sumW > 64LL * n_ok) {                // the average window is wider than 64
         v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
         return false;
     }
@@ -353,32 +373,25 @@ __device__ bool build_key_tables(const KeySrc &S, int key, int lane, char *lds, 
         v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
         return false;
     }
-    // ---- table placement: LDS if it fits, else this wave's global scratch
-    const uint64_t b_ops = (uint64_t)n_ops * sizeof(Op);
-    const uint64_t b_off = ((uint64_t)(n_ok + 1) * 4 + 15) & ~15ULL;
-    const uint64_t b_w = ((uint64_t)sumW * 2 + 128 + 15) & ~15ULL;   // +64 entries slack
-    const uint64_t total = b_ops + b_off + b_w;
-    char *tb;
-    if (total <= (uint64_t)lds_bytes) tb = lds;
-    else if (total <= scr_bytes) tb = gscr;
-    else {
-        if (lane == 0) atomicOr(S.flags, 2);
-        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-        return false;
-    }
-    Op *ops = (Op *)tb;
-    int32_t *woff = (int32_t *)(tb + b_ops);
-    uint16_t *W = (uint16_t *)(tb + b_ops + b_off);
+    return true;
+}
 
-    // ---- pass 2: op records in call order --------------------------------
+// Pass 2 + window sweep into the table at `tb`. Returns the widest window
+// (> 64: the key is :unknown with cause window, as in the oracle).
+template <bool L>
+__device__ int key_fill(const KeySrc &S, const KeyInfo &K, int lane, char *tb) {
+    Op *ops = (Op *)tb;
+    int32_t *woff = (int32_t *)(tb + tbl_ops_bytes(K));
+    uint16_t *W = (uint16_t *)(tb + tbl_ops_bytes(K) + tbl_off_bytes(K));
+    const int n_ops = K.n_ops, n_ok = K.n_ok;
     {
-        int nops = 0, nok = 0;
-        for (uint32_t base = s0; base < s1; base += 64) {
+        int nok = 0;
+        for (uint32_t base = K.s0; base < K.s1; base += 64) {
             const uint32_t p = base + lane;
-            const bool valid = p < s1;
+            const bool valid = p < K.s1;
             const int rk = valid ? S.rank[p] : -1;
             const bool kept = rk >= 0, ret = rk <= -2;
-            const uint64_t bi = ballot(kept), br = ballot(ret);
+            const uint64_t br = ballot(ret);
             if (kept) {
                 Rec x = S.rec[p];
                 const int q = S.pair[p];
@@ -395,62 +408,53 @@ __device__ bool build_key_tables(const KeySrc &S, int key, int lane, char *lds, 
                 Op o; o.v1 = v1c; o.v2 = v2c; o.rr = rr; o.fa = x.f | (a << 2);
                 ops[rk] = o;
             }
-            nops += __popcll(bi);
             nok += __popcll(br);
         }
     }
     wave_sync();
-
-    // ---- window table W(t): W(t) = W(t-1) - {RET[t-1]} + {ops with a == t}
-    int too_wide = 0;
-    {
-        int w = 0, nxt = 0, offt = 0;
-        for (int t = 0; t < n_ok; t++) {
-            int prev = 0;
-            bool keep = false;
-            if (t > 0 && lane < w) {
-                prev = W[offt - w + lane];
-                keep = ops[prev].rr != t - 1;
-            }
-            const uint64_t bk = ballot(keep);
-            const int nk = __popcll(bk);
-            if (keep) W[offt + mbcnt(bk)] = (uint16_t)prev;
-            // append ops whose invocation precedes the t-th ok return
-            int added = 0;
-            for (;;) {
-                const int j = nxt + lane;
-                const bool in = j < n_ops && (ops[j].fa >> 2) <= t;
-                const uint64_t ba = ballot(in);
-                const int c = __popcll(ba);     // a is non-decreasing: a prefix
-                if (in && nk + added + lane < 64) W[offt + nk + added + lane] = (uint16_t)j;
-                added += c; nxt += c;
-                if (c < 64) break;
-            }
-            w = nk + added;
-            if (w > 64) { too_wide = 1; break; }
-            if (lane == 0) woff[t] = offt;
-            offt += w;
-            wave_sync();
+    // W(t) = W(t-1) - {RET[t-1]} + {ops with a == t}
+    int maxw = 0;
+    int w = 0, nxt = 0, offt = 0;
+    for (int t = 0; t < n_ok; t++) {
+        int prev = 0;
+        bool keep = false;
+        if (t > 0 && lane < w) {
+            prev = W[offt - w + lane];
+            keep = ops[prev].rr != t - 1;
         }
-        if (lane == 0) woff[n_ok] = offt;
+        const uint64_t bk = ballot(keep);
+        const int nk = __popcll(bk);
+        if (keep) W[offt + mbcnt(bk)] = (uint16_t)prev;
+        // append ops whose invocation precedes the t-th ok return
+        int added = 0;
+        for (;;) {
+            const int j = nxt + lane;
+            const bool in = j < n_ops && (ops[j].fa >> 2) <= t;
+            const uint64_t ba = ballot(in);
+            const int c = __popcll(ba);     // a is non-decreasing: a prefix
+            if (in && nk + added + lane < 64) W[offt + nk + added + lane] = (uint16_t)j;
+            added += c; nxt += c;
+            if (c < 64) break;
+        }
+        w = nk + added;
+        maxw = max(maxw, w);
+        if (w > 64) break;
+        if (lane == 0) woff[t] = offt;
+        offt += w;
+        wave_sync();
     }
+    if (lane == 0) woff[n_ok] = offt;
     wave_sync();
-    if (too_wide) {
-        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-        return false;
-    }
-
-    T.ops = ops; T.woff = woff; T.W = W; T.n_ops = n_ops; T.n_ok = n_ok; T.s0 = s0; T.s1 = s1;
-    return true;
+    return maxw;
 }
 
 // history row of the ok completion of RET[t] (the first op no configuration
 // gets past, for an invalid key)
-__device__ long long ret_row(const KeySrc &S, const KeyTables &T, uint32_t t, int lane) {
+__device__ long long ret_row(const KeySrc &S, const KeyInfo &K, uint32_t t, int lane) {
     const int want = -((int)t + 2);
-    for (uint32_t base = T.s0; base < T.s1; base += 64) {
+    for (uint32_t base = K.s0; base < K.s1; base += 64) {
         const uint32_t p = base + lane;
-        const bool hit = p < T.s1 && S.rank[p] == want;
+        const bool hit = p < K.s1 && S.rank[p] == want;
         const uint64_t b = ballot(hit);
         if (b) {
             const int l = __builtin_ctzll(b);
@@ -460,153 +464,353 @@ __device__ long long ret_row(const KeySrc &S, const KeyTables &T, uint32_t t, in
     return -1;
 }
 
-__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    const int lane = threadIdx.x;
+// ---------------------------------------------------------------------------
+// The WGL depth-first search for one key (one wave), templated on where the
+// tables live. Returns the verdict; sets inserts / tmax.
+//
+// Memo: every configuration with t >= theta lives in the LDS table (8-byte
+// keys t:16|state:8|mask:40); every one with t < theta in this wave's
+// gen-tagged HBM table. When LDS reaches half load the layers below the
+// current t move to HBM in one bulk pass; a lookup goes to LDS or HBM by the
+// child's t alone, so the set stays exact. Stack: an LDS ring of the top
+// RING frames, written through to HBM.
+// LDS memo slot of an 8-byte key: one 32-bit multiply-xorshift
+__device__ __forceinline__ uint32_t lds_hash(uint64_t k) {
+    uint32_t h = (uint32_t)k * 0x9E3779B1u ^ (uint32_t)(k >> 32) * 0x85EBCA77u;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    return (h >> 13) & (MEMO_SLOTS - 1);
+}
+
+// Evict the LDS memo's layers below t_new into this wave's HBM table
+// (out of line: it runs once per MEMO_EVICT inserts and must not bloat the
+// search loop). Entries are staged through global scratch, the LDS table is
+// rebuilt with the kept layers. Returns the new LDS entry count and sets
+// theta (0xFFFFFFFF = one layer alone is too wide: HBM only from now on).
+__device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint64_t *memo, uint64_t *stage,
+                                            uint32_t cap_mask, uint32_t gen, uint32_t t_new, int lane) {
+    const uint64_t gen_hi = (uint64_t)gen << 40;
+    int kept = 0;
+#pragma unroll 1
+    for (int r = 0; r < MEMO_SLOTS / 64; r++) {
+        const uint64_t x = lmemo[lane + 64 * r];
+        stage[lane + 64 * r] = x;
+        kept += __popcll(ballot(x != 0 && (uint32_t)(x >> 48) >= t_new));
+    }
+    uint32_t th2 = t_new;
+    if (kept > MEMO_EVICT / 2) { th2 = 0xFFFFFFFFu; kept = 0; }
+    wave_sync();
+#pragma unroll 1
+    for (int r = 0; r < MEMO_SLOTS / 64; r++) lmemo[lane + 64 * r] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    wave_sync();
+#pragma unroll 1
+    for (int r = 0; r < MEMO_SLOTS / 64; r++) {
+        const uint64_t x = stage[lane + 64 * r];
+        if (x == 0) continue;
+        const uint32_t xt = (uint32_t)(x >> 48);
+        if (xt < th2) {
+            const uint32_t cs = (uint32_t)(x >> 40) & 0xFF;
+            const uint64_t cm = x & ((1ULL << 40) - 1);
+            uint32_t h = (uint32_t)memo_hash(xt, cs, cm) & cap_mask;
+            const uint64_t w1 = gen_hi | ((uint64_t)xt << 20) | cs;
+            for (;;) {
+                const uint64_t e1 = __hip_atomic_load(&memo[2 * (size_t)h + 1], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+                if ((e1 >> 40) != gen) {
+                    unsigned long long exp = e1;
+                    if (__hip_atomic_compare_exchange_strong((unsigned long long *)&memo[2 * (size_t)h + 1],
+                                                             &exp, (unsigned long long)w1,
+                                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT)) {
+                        __hip_atomic_store(&memo[2 * (size_t)h], cm, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    continue;
+                }
+                h = (h + 1) & cap_mask;
+            }
+        } else {
+            uint32_t h = lds_hash(x);
+            for (;;) {
+                unsigned long long z = 0;
+                if (__hip_atomic_compare_exchange_strong((unsigned long long *)&lmemo[h], &z,
+                                                         (unsigned long long)x, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                    break;
+                h = (h + 1) & (MEMO_SLOTS - 1);
+            }
+        }
+    }
+    // every HBM write of this wave is visible to its later probes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    wave_sync();
+    return ((uint64_t)th2 << 32) | (uint32_t)kept;
+}
+
+// Probe this wave's HBM table (a lane whose child lies below theta; rare:
+// only after an eviction and a backtrack below the evicted layers).
+// Returns slot | absent << 32.
+__device__ __forceinline__ uint64_t hbm_probe(const uint64_t *memo, uint32_t cap_mask, uint32_t gen,
+                                              uint32_t ct, uint32_t cs, uint64_t cm,
+                                              unsigned long long &probes) {
+    const uint64_t w1want = ((uint64_t)gen << 40) | ((uint64_t)ct << 20) | cs;
+    uint32_t h = (uint32_t)memo_hash(ct, cs, cm) & cap_mask;
+    for (;;) {
+        const uint64_t e1 = __hip_atomic_load(&memo[2 * (size_t)h + 1], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        probes++;
+        if ((e1 >> 40) != gen) return (1ULL << 32) | h;
+        if (e1 == w1want) {
+            const uint64_t e0 = __hip_atomic_load(&memo[2 * (size_t)h], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            if (e0 == cm) return h;
+        }
+        h = (h + 1) & cap_mask;
+    }
+}
+
+// The RET member (the op whose return defines t) is being lifted: advance t
+// past every ok return whose op is already linearized and compact the mask
+// onto W(t'). Wave-wide (all lanes), uniform result.
+__device__ __forceinline__ void ret_lift(uint64_t lin, uint32_t t, int n_ok, int w, int o_rr,
+                                         int lane, uint32_t &u_out, uint64_t &nm_out) {
+    uint32_t u = t + 1;
+    while (u < (uint32_t)n_ok && ballot(((lin >> lane) & 1) && o_rr == (int)u)) u++;
+    uint64_t nm = 0;
+    if (u < (uint32_t)n_ok) {
+        const uint64_t keep = ballot(lane < w && (o_rr < 0 || o_rr >= (int)u));
+        uint64_t bits = lin & keep;
+        while (bits) {
+            const int b = __builtin_ctzll(bits);
+            bits &= bits - 1;
+            nm |= 1ULL << __popcll(keep & ((1ULL << b) - 1));
+        }
+    }
+    u_out = u;
+    nm_out = nm;
+}
+
+template <bool L>
+__device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int maxw, int key, int lane,
+                          uint64_t *memo, Frame *stack, uint64_t *stage, long long &inserts,
+                          uint32_t &tmax_out, unsigned long long &my_probes) {
+    const Op *ops = (const Op *)tb;
+    const int32_t *woff = (const int32_t *)(tb + tbl_ops_bytes(K));
+    const uint16_t *W = (const uint16_t *)(tb + tbl_ops_bytes(K) + tbl_off_bytes(K));
+    const int n_ok = K.n_ok;
     const uint64_t lane_bit = 1ULL << lane;
+    const uint32_t cap_mask = A.memo_cap - 1;
+    const uint32_t gen = (A.gen_base + (uint32_t)key + 1) & ((1u << GEN_BITS) - 1);
+    const uint64_t gen_hi = (uint64_t)gen << 40;
+    uint64_t *lmemo = (uint64_t *)(jh_lds + LDS_TBL);
+    Frame *ring = (Frame *)(jh_lds + LDS_TBL + MEMO_SLOTS * 8);
+    const bool lds_ok = A.states8 && maxw <= 40 && n_ok < 65535;
+    uint32_t theta = lds_ok ? 0u : 0xFFFFFFFFu;
+    int lcount = 0;
+    for (int i = lane; i < MEMO_SLOTS; i += 64) lmemo[i] = 0;
+    uint32_t t = 0, tmax = 0, depth = 0, ring_lo = 0;
+    uint64_t mask = 0;
+    int s = A.init_state, start = 0;
+    int verdict = -1;
+    long long ins = 0;
+    unsigned long long n_steps = 0, n_evict = 0, n_reload = 0;
+    // lane-resident window member
+    int w = 0, o_f = 0, o_v1 = 0, o_v2 = 0, o_rr = -1;
+#define LOAD_WINDOW(tt)                                                        \
+    do {                                                                       \
+        const int wo_ = woff[tt];                                              \
+        w = woff[(tt) + 1] - wo_;                                              \
+        const Op o_ = ops[W[wo_ + min(lane, max(w - 1, 0))]];                  \
+        const bool in_ = lane < w;                                             \
+        o_f = in_ ? (o_.fa & 3) : 3; o_v1 = o_.v1; o_v2 = o_.v2;               \
+        o_rr = in_ ? o_.rr : -1;                                               \
+    } while (0)
+    wave_sync();
+    LOAD_WINDOW(0);
+    while (true) {
+        n_steps++;
+        // candidates: un-linearized members at or after `start` the model
+        // allows (o_f == 3 marks lanes outside the window)
+        const bool legal = o_f == F_WRITE || (o_f == F_CAS && s == o_v1) ||
+                           (o_f == F_READ && (o_v1 == 0 || o_v1 == s));
+        const int s2 = o_f == F_WRITE ? o_v1 : (o_f == F_CAS ? o_v2 : s);
+        const bool cand = legal && lane >= start && !(mask & lane_bit);
+        uint32_t ct = t;
+        uint64_t cm = mask | lane_bit;
+        const uint64_t bret = ballot(cand && o_rr == (int)t);
+        if (bret) {
+            uint32_t u;
+            uint64_t nm;
+            ret_lift(mask | bret, t, n_ok, w, o_rr, lane, u, nm);
+            if (o_rr == (int)t) { ct = u; cm = nm; }
+        }
+        // memo probes, all candidates at once (= the sequential scan, since
+        // nothing is inserted until the first new child is chosen)
+        const uint64_t lkey = ((uint64_t)ct << 48) | ((uint64_t)(uint32_t)s2 << 40) | cm;
+        const bool go_lds = cand && ct >= theta;
+        bool absent = false;
+        uint32_t slot = lds_hash(lkey);
+        if (go_lds) {
+            uint64_t e = lmemo[slot];
+            while (e != 0 && e != lkey) {
+                slot = (slot + 1) & (MEMO_SLOTS - 1);
+                e = lmemo[slot];
+            }
+            absent = e == 0;
+        }
+        const bool go_hbm = cand && ct < theta;
+        if (ballot(go_hbm) && go_hbm) {
+            const uint64_t r = hbm_probe(memo, cap_mask, gen, ct, (uint32_t)s2, cm, my_probes);
+            slot = (uint32_t)r;
+            absent = (r >> 32) != 0;
+        }
+        const uint64_t bn = ballot(absent);
+        if (bn) {
+            if (ins >= A.budget) { verdict = JH_UNKNOWN; break; }
+            const int i = __builtin_ctzll(bn);
+            const bool to_lds = (ballot(go_lds) >> i) & 1;
+            if (lane == i) {
+                if (to_lds) lmemo[slot] = lkey;
+                else {
+                    __hip_atomic_store(&memo[2 * (size_t)slot], cm, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&memo[2 * (size_t)slot + 1],
+                                       gen_hi | ((uint64_t)ct << 20) | (uint32_t)s2,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            ins++;
+            // push the parent onto the LDS ring (written through to HBM)
+            if (lane == 0) {
+                Frame fr; fr.mask = mask; fr.t_i = (t << 6) | (uint32_t)i; fr.s = s;
+                ring[depth & (RING - 1)] = fr;
+                stack[depth] = fr;
+            }
+            depth++;
+            if (depth - ring_lo > RING) ring_lo = depth - RING;
+            const uint32_t nt = (uint32_t)readlane((int)ct, i);
+            mask = ((uint64_t)(uint32_t)readlane((int)(uint32_t)(cm >> 32), i) << 32) |
+                   (uint32_t)readlane((int)(uint32_t)cm, i);
+            s = readlane(s2, i);
+            start = 0;
+            if (to_lds) {
+                if (++lcount >= MEMO_EVICT) {
+                    n_evict++;
+                    const uint64_t r = memo_evict(lmemo, memo, stage, cap_mask, gen, nt, lane);
+                    lcount = (int)(uint32_t)r;
+                    theta = (uint32_t)(r >> 32);
+                }
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
+            if (nt != t) {
+                t = nt;
+                tmax = max(tmax, t);
+                if (t == (uint32_t)n_ok) { verdict = JH_VALID; break; }
+                LOAD_WINDOW(t);
+                n_reload++;
+            }
+        } else {
+            if (depth == 0) { verdict = JH_INVALID; break; }
+            depth--;
+            Frame fr;
+            if (depth >= ring_lo) fr = ring[depth & (RING - 1)];
+            else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                fr = stack[depth];
+                ring_lo = depth;
+            }
+            const uint32_t pt = fr.t_i >> 6;
+            mask = fr.mask; s = fr.s; start = (int)(fr.t_i & 63) + 1;
+            if (pt != t) { t = pt; LOAD_WINDOW(t); n_reload++; }
+        }
+        if (depth >= A.stack_cap) { verdict = JH_UNKNOWN; if (lane == 0) atomicOr(A.flags, 4); break; }
+    }
+#undef LOAD_WINDOW
+    inserts = ins;
+    tmax_out = tmax;
+    if (A.dbg && lane == 0) {
+        unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
+        d[4] += n_steps; d[5] += (unsigned long long)ins; d[6] += n_evict; d[7] += n_reload;
+    }
+    return verdict;
+}
+
+template <bool L>
+__device__ void dfs_key(const DfsArgs &A, const KeySrc &src, const KeyInfo &K, char *gscr, int key,
+                        int lane, uint64_t *memo, Frame *stack, unsigned long long &my_probes) {
+    char *tb = tbl_base<L>(0, gscr);
+    jh_key_verdict v;
+    v.valid = JH_VALID; v.cause = 0; v.fail_entry = -1; v.explored = 0;
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+    const int maxw = key_fill<L>(src, K, lane, tb);
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    if (A.dbg && lane == 0) { A.dbg[16 * (size_t)blockIdx.x + 1] += c1 - c0; A.dbg[16 * (size_t)blockIdx.x + 8] += L ? 1 : 0; }
+    if (maxw > 64) {
+        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
+        if (lane == 0) A.out[key] = v;
+        return;
+    }
+    long long inserts = 0;
+    uint32_t tmax = 0;
+    uint64_t *stage = (uint64_t *)(gscr + A.scratch_bytes - MEMO_SLOTS * 8);
+    const int verdict = dfs_search<L>(A, K, tb, maxw, key, lane, memo, stack, stage, inserts, tmax, my_probes);
+    if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 2] += __builtin_amdgcn_s_memtime() - c1;
+    if (verdict == JH_UNKNOWN && A.defer && inserts >= A.budget) {
+        if (lane == 0) {
+            const int d = atomicAdd(A.defer_count, 1);
+            A.defer_list[d] = key;
+        }
+        return;
+    }
+    v.valid = verdict;
+    v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
+    v.explored = inserts;
+    if (verdict == JH_INVALID) v.fail_entry = ret_row(src, K, tmax, lane);
+    if (lane == 0) A.out[key] = v;
+}
+
+__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
+    const int lane = threadIdx.x;
     uint64_t *memo = A.memo + (size_t)blockIdx.x * A.memo_cap * 2;
     Frame *stack = A.stack + (size_t)blockIdx.x * A.stack_cap;
     char *gscr = A.scratch + (size_t)blockIdx.x * A.scratch_bytes;
-    const uint32_t cap_mask = A.memo_cap - 1;
     unsigned long long my_probes = 0;
     const KeySrc src{A.rec, A.pair, A.off, A.rows, A.viol, A.rank, A.flags};
-
+    const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
     for (;;) {
         int idx = 0;
         if (lane == 0) idx = atomicAdd(A.queue, 1);
         idx = readlane(idx, 0);
         if (idx >= A.n_list) break;
         const int key = A.list[idx];
+        KeyInfo K;
         jh_key_verdict v;
-        KeyTables T;
-        if (!build_key_tables(src, key, lane, lds, LDS_BYTES, gscr, A.scratch_bytes, T, v)) {
+        const unsigned long long p0 = __builtin_amdgcn_s_memtime();
+        const bool needed = key_pass1(src, key, lane, K, v);
+        if (A.dbg && lane == 0) { A.dbg[16 * (size_t)blockIdx.x + 0] += __builtin_amdgcn_s_memtime() - p0; A.dbg[16 * (size_t)blockIdx.x + 3] += 1; }
+        if (!needed) {
             if (lane == 0) A.out[key] = v;
             continue;
         }
-        const int n_ok = T.n_ok;
-        const Op *ops = T.ops;
-        const int32_t *woff = T.woff;
-        const uint16_t *W = T.W;
-        // ---- WGL search in canonical coordinates ------------------------------
-        const uint32_t gen = (A.gen_base + (uint32_t)key + 1) & ((1u << GEN_BITS) - 1);
-        const uint64_t gen_hi = (uint64_t)gen << 40;
-        uint32_t t = 0, tmax = 0, depth = 0;
-        uint64_t mask = 0;
-        int s = A.init_state, start = 0;
-        long long inserts = 0;
-        int verdict = -1;
-        // lane-resident window member
-        int w = 0, o_f = 0, o_v1 = 0, o_v2 = 0, o_rr = -1;
-        auto load_window = [&](uint32_t tt) {
-            const int wo = woff[tt];
-            w = woff[tt + 1] - wo;
-            if (lane < w) {
-                const Op o = ops[W[wo + lane]];
-                o_f = o.fa & 3; o_v1 = o.v1; o_v2 = o.v2; o_rr = o.rr;
-            } else { o_f = 0; o_v1 = 0; o_v2 = 0; o_rr = -1; }
-        };
-        load_window(0);
-        while (verdict < 0) {
-            // candidates: un-linearized members at or after `start` the model allows
-            int s2 = 0;
-            const bool cand = lane < w && lane >= start && !((mask >> lane) & 1) &&
-                              cas_step(o_f, o_v1, o_v2, s, &s2);
-            const uint64_t bc = ballot(cand);
-            uint32_t ct = t;
-            uint64_t cm = mask | lane_bit;
-            // the member whose return defines R advances t and compacts the mask
-            const uint64_t bret = ballot(cand && o_rr == (int)t);
-            if (bret) {
-                const uint64_t lin = mask | bret;
-                uint32_t u = t + 1;
-                while (u < (uint32_t)n_ok && ballot(((lin >> lane) & 1) && o_rr == (int)u)) u++;
-                uint64_t nm = 0;
-                if (u < (uint32_t)n_ok) {
-                    const uint64_t keep = ballot(lane < w && (o_rr < 0 || o_rr >= (int)u));
-                    uint64_t bits = lin & keep;
-                    while (bits) {
-                        const int b = __builtin_ctzll(bits);
-                        bits &= bits - 1;
-                        nm |= 1ULL << __popcll(keep & ((1ULL << b) - 1));
-                    }
-                }
-                if (o_rr == (int)t) { ct = u; cm = nm; }
-            }
-            // memo probes, all candidates at once (= the sequential scan, since
-            // nothing is inserted until the first new child is chosen)
-            bool absent = false;
-            uint32_t slot = 0;
-            if (cand) {
-                uint32_t h = (uint32_t)memo_hash(ct, (uint32_t)s2, cm) & cap_mask;
-                const uint64_t w1want = gen_hi | ((uint64_t)ct << 20) | (uint32_t)s2;
-                for (;;) {
-                    const uint64_t e1 = __hip_atomic_load(&memo[2 * (size_t)h + 1], __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_WORKGROUP);
-                    my_probes++;
-                    if ((e1 >> 40) != gen) { absent = true; slot = h; break; }
-                    if (e1 == w1want) {
-                        const uint64_t e0 = __hip_atomic_load(&memo[2 * (size_t)h], __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (e0 == cm) break;
-                    }
-                    h = (h + 1) & cap_mask;
-                }
-            }
-            const uint64_t bn = ballot(absent);
-            if (bn) {
-                if (inserts >= A.budget) { verdict = JH_UNKNOWN; break; }
-                const int i = __builtin_ctzll(bn);
-                if (lane == i) {
-                    __hip_atomic_store(&memo[2 * (size_t)slot], cm, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_store(&memo[2 * (size_t)slot + 1],
-                                       gen_hi | ((uint64_t)ct << 20) | (uint32_t)s2,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-                inserts++;
-                if (lane == 0) {
-                    Frame fr; fr.mask = mask; fr.t_i = (t << 6) | (uint32_t)i; fr.s = s;
-                    stack[depth] = fr;
-                }
-                depth++;
-                const uint32_t nt = (uint32_t)readlane((int)ct, i);
-                const uint64_t nm = ((uint64_t)(uint32_t)readlane((int)(uint32_t)(cm >> 32), i) << 32) |
-                                    (uint32_t)readlane((int)(uint32_t)cm, i);
-                s = readlane(s2, i);
-                mask = nm;
-                start = 0;
-                if (nt != t) {
-                    t = nt;
-                    if (t > tmax) tmax = t;
-                    if (t == (uint32_t)n_ok) { verdict = JH_VALID; break; }
-                    load_window(t);
-                }
-                // make the insert visible to this wave's next probes
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            } else {
-                if (depth == 0) { verdict = JH_INVALID; break; }
-                depth--;
-                const Frame fr = stack[depth];
-                const uint32_t pt = fr.t_i >> 6;
-                mask = fr.mask; s = fr.s; start = (int)(fr.t_i & 63) + 1;
-                if (pt != t) { t = pt; load_window(t); }
-            }
-            if (depth >= A.stack_cap) { verdict = JH_UNKNOWN; if (lane == 0) atomicOr(A.flags, 4); break; }
+        const uint64_t need = tbl_bytes(K);
+        if (need <= (uint64_t)LDS_TBL) {
+            dfs_key<true>(A, src, K, gscr, key, lane, memo, stack, my_probes);
+        } else if (need + MEMO_SLOTS * 8 <= A.scratch_bytes) {
+            dfs_key<false>(A, src, K, gscr, key, lane, memo, stack, my_probes);
+        } else {
+            if (lane == 0) atomicOr(A.flags, 2);
+            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
+            if (lane == 0) A.out[key] = v;
         }
-        if (verdict == JH_UNKNOWN && A.defer && inserts >= A.budget) {
-            if (lane == 0) {
-                const int d = atomicAdd(A.defer_count, 1);
-                A.defer_list[d] = key;
-            }
-            continue;
-        }
-        v.valid = verdict;
-        v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
-        v.explored = inserts;
-        if (verdict == JH_INVALID) v.fail_entry = ret_row(src, T, tmax, lane);
-        if (lane == 0) A.out[key] = v;
     }
+    if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 9] = __builtin_amdgcn_s_memtime() - t_begin;
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
 }
@@ -620,10 +824,13 @@ __global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
 // is reachable (valid) or the set outgrows the budget is handed to the
 // sequential search (only it defines where :unknown starts for those).
 constexpr int BFS_THREADS = 512;
-constexpr int BFS_LDS_BYTES = 49152;
+constexpr int BFS_HDR = 256;                       // shared scalars, start of dynamic LDS
+constexpr int BFS_TBL = 49152;
+constexpr int BFS_LDS_BYTES = BFS_HDR + BFS_TBL;
 constexpr uint64_t BFS_EMPTY = ~0ULL;
 
 struct BfsArgs {
+    unsigned long long *dbg;  // JH_DEBUG=2: per-workgroup accounting (8 words)
     KeySrc src;
     const int32_t *list;
     int32_t n_list;
@@ -642,130 +849,170 @@ struct BfsArgs {
     int32_t states_ok;      // every interned state < 2^12
 };
 
+struct BfsShared {
+    KeyInfo K;
+    jh_key_verdict v;
+    int key, need, maxw, status;
+    unsigned ncur, nnext, tmax;
+    unsigned long long count;
+};
+
 __device__ __forceinline__ uint64_t bfs_pack(uint32_t t, uint32_t s, uint32_t m) {
     return ((uint64_t)t << 44) | ((uint64_t)s << 32) | m;
 }
 
+template <bool L>
+__device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, uint64_t *set,
+                        uint64_t *qa) {
+    const int lane = tid & 63, wid = tid >> 6;
+    const uint32_t cmask = A.set_cap - 1;
+    char *tb = tbl_base<L>(BFS_HDR, gscr);
+    const KeyInfo K = sh.K;
+    const int key = sh.key;
+    if (wid == 0) {
+        const int mw = key_fill<L>(A.src, K, lane, tb);
+        if (lane == 0) sh.maxw = mw;
+    }
+    __syncthreads();
+    const Op *ops = (const Op *)tb;
+    const int32_t *woff = (const int32_t *)(tb + tbl_ops_bytes(K));
+    const uint16_t *W = (const uint16_t *)(tb + tbl_ops_bytes(K) + tbl_off_bytes(K));
+    const int n_ok = K.n_ok;
+    if (sh.maxw > 64) {
+        if (tid == 0) {
+            jh_key_verdict v;
+            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW; v.fail_entry = -1; v.explored = 0;
+            A.out[key] = v;
+        }
+        __syncthreads();
+        return;
+    }
+    if (sh.maxw > 32 || !A.states_ok || n_ok >= (1 << 20) - 2) {
+        if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
+        __syncthreads();
+        return;
+    }
+    for (uint32_t i = tid; i < A.set_cap; i += BFS_THREADS) set[i] = BFS_EMPTY;
+    if (tid == 0) {
+        qa[0] = bfs_pack(0, (uint32_t)A.init_state, 0);
+        sh.ncur = 1; sh.nnext = 0; sh.tmax = 0; sh.count = 0; sh.status = 0;
+    }
+    __syncthreads();
+    uint64_t *cur = qa, *nxt = qa + A.q_cap;
+    const unsigned long long b0 = __builtin_amdgcn_s_memtime();
+    unsigned long long levels = 0, items = 0;
+    for (;;) {
+        const unsigned ncur = sh.ncur;
+        levels++; items += ncur;
+        for (unsigned i = tid; i < ncur; i += BFS_THREADS) {
+          const uint64_t c = cur[i];
+          const uint32_t t = (uint32_t)(c >> 44), s = (uint32_t)(c >> 32) & 0xFFF;
+          const uint32_t mask = (uint32_t)c;
+          const int wo = woff[t], w = woff[t + 1] - wo;
+          for (int j = 0; j < w; j++) {
+            if ((mask >> j) & 1) continue;
+            const Op o = ops[W[wo + j]];
+            int s2;
+            if (!cas_step(o.fa & 3, o.v1, o.v2, (int)s, &s2)) continue;
+            uint32_t u = t, nm = mask | (1u << j);
+            if (o.rr == (int)t) {
+                const uint32_t lin = nm;
+                u = t + 1;
+                while (u < (uint32_t)n_ok) {
+                    bool hit = false;
+                    for (int m = 0; m < w && !hit; m++)
+                        hit = ((lin >> m) & 1) && ops[W[wo + m]].rr == (int)u;
+                    if (!hit) break;
+                    u++;
+                }
+                nm = 0;
+                if (u < (uint32_t)n_ok) {
+                    int b = 0;
+                    for (int m = 0; m < w; m++) {
+                        const int rr = ops[W[wo + m]].rr;
+                        if (rr < 0 || rr >= (int)u) {
+                            if ((lin >> m) & 1) nm |= 1u << b;
+                            b++;
+                        }
+                    }
+                }
+            }
+            const uint64_t ck = bfs_pack(u, (uint32_t)s2, nm);
+            uint32_t h = (uint32_t)jh_mix64(ck) & cmask;
+            bool ins = false;
+            for (uint32_t probe = 0; probe <= cmask; probe++) {
+                const unsigned long long prev =
+                    atomicCAS((unsigned long long *)&set[h], BFS_EMPTY, ck);
+                if (prev == BFS_EMPTY) { ins = true; break; }
+                if (prev == ck) break;
+                h = (h + 1) & cmask;
+            }
+            if (!ins) continue;
+            const unsigned long long n = atomicAdd(&sh.count, 1ULL);
+            if ((long long)n >= A.budget) atomicOr(&sh.status, 2);
+            if (u == (uint32_t)n_ok) atomicOr(&sh.status, 1);
+            atomicMax(&sh.tmax, u);
+            const unsigned pos = atomicAdd(&sh.nnext, 1u);
+            if (pos < A.q_cap) nxt[pos] = ck; else atomicOr(&sh.status, 2);
+          }
+        }
+        __syncthreads();
+        const int st = sh.status;
+        const unsigned nn = sh.nnext;
+        __syncthreads();
+        if (st || nn == 0) break;
+        if (tid == 0) { sh.ncur = nn; sh.nnext = 0; }
+        uint64_t *tmp = cur; cur = nxt; nxt = tmp;
+        __syncthreads();
+    }
+    if (A.dbg && tid == 0) {
+        unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
+        d[0] += __builtin_amdgcn_s_memtime() - b0; d[1] += levels; d[2] += items; d[3] += sh.count; d[4] += 1;
+    }
+    if (sh.status) {
+        if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
+    } else if (wid == 0) {
+        jh_key_verdict v;
+        v.valid = JH_INVALID; v.cause = 0; v.explored = (int64_t)sh.count;
+        v.fail_entry = ret_row(A.src, K, sh.tmax, lane);
+        if (lane == 0) A.out[key] = v;
+    }
+    __syncthreads();
+}
+
 __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    __shared__ KeyTables sT;
-    __shared__ jh_key_verdict sv;
-    __shared__ int s_key, s_need, s_maxw, s_status;
-    __shared__ unsigned s_ncur, s_nnext, s_tmax;
-    __shared__ unsigned long long s_count;
+    BfsShared &sh = *(BfsShared *)jh_lds;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     uint64_t *set = A.set + (size_t)blockIdx.x * A.set_cap;
     uint64_t *qa = A.q + (size_t)blockIdx.x * 2 * A.q_cap;
     char *gscr = A.scratch + (size_t)blockIdx.x * A.scratch_bytes;
-    const uint32_t cmask = A.set_cap - 1;
     for (;;) {
         if (tid == 0) {
             const int idx = atomicAdd(A.queue, 1);
-            s_key = idx < A.n_list ? A.list[idx] : -1;
+            sh.key = idx < A.n_list ? A.list[idx] : -1;
         }
         __syncthreads();
-        const int key = s_key;
+        const int key = sh.key;
         if (key < 0) break;
         if (wid == 0) {
-            KeyTables T;
+            KeyInfo K;
             jh_key_verdict v;
-            const bool need = build_key_tables(A.src, key, lane, lds, BFS_LDS_BYTES, gscr,
-                                               A.scratch_bytes, T, v);
-            if (lane == 0) { sT = T; sv = v; s_need = need; s_maxw = 0; s_status = 0; }
+            const bool need = key_pass1(A.src, key, lane, K, v);
+            if (lane == 0) { sh.K = K; sh.v = v; sh.need = need; }
         }
         __syncthreads();
-        if (!s_need) {
-            if (tid == 0) A.out[key] = sv;
+        if (!sh.need) {
+            if (tid == 0) A.out[key] = sh.v;
             __syncthreads();
             continue;
         }
-        const KeyTables T = sT;
-        for (int t = tid; t < T.n_ok; t += BFS_THREADS) atomicMax(&s_maxw, T.woff[t + 1] - T.woff[t]);
-        __syncthreads();
-        if (s_maxw > 32 || !A.states_ok || T.n_ok >= (1 << 20) - 2) {
+        const uint64_t need = tbl_bytes(sh.K);
+        if (need <= (uint64_t)BFS_TBL) bfs_key<true>(A, sh, gscr, tid, set, qa);
+        else if (need <= A.scratch_bytes) bfs_key<false>(A, sh, gscr, tid, set, qa);
+        else {
             if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
             __syncthreads();
-            continue;
         }
-        for (uint32_t i = tid; i < A.set_cap; i += BFS_THREADS) set[i] = BFS_EMPTY;
-        if (tid == 0) {
-            qa[0] = bfs_pack(0, (uint32_t)A.init_state, 0);
-            s_ncur = 1; s_nnext = 0; s_tmax = 0; s_count = 0;
-        }
-        __syncthreads();
-        uint64_t *cur = qa, *nxt = qa + A.q_cap;
-        for (;;) {
-            const unsigned ncur = s_ncur;
-            for (unsigned i = tid; i < ncur; i += BFS_THREADS) {
-                const uint64_t c = cur[i];
-                const uint32_t t = (uint32_t)(c >> 44), s = (uint32_t)(c >> 32) & 0xFFF;
-                const uint32_t mask = (uint32_t)c;
-                const int wo = T.woff[t], w = T.woff[t + 1] - wo;
-                for (int j = 0; j < w; j++) {
-                    if ((mask >> j) & 1) continue;
-                    const Op o = T.ops[T.W[wo + j]];
-                    int s2;
-                    if (!cas_step(o.fa & 3, o.v1, o.v2, (int)s, &s2)) continue;
-                    uint32_t u = t, nm = mask | (1u << j);
-                    if (o.rr == (int)t) {
-                        const uint32_t lin = nm;
-                        u = t + 1;
-                        while (u < (uint32_t)T.n_ok) {
-                            bool hit = false;
-                            for (int m = 0; m < w && !hit; m++)
-                                hit = ((lin >> m) & 1) && T.ops[T.W[wo + m]].rr == (int)u;
-                            if (!hit) break;
-                            u++;
-                        }
-                        nm = 0;
-                        if (u < (uint32_t)T.n_ok) {
-                            int b = 0;
-                            for (int m = 0; m < w; m++) {
-                                const int rr = T.ops[T.W[wo + m]].rr;
-                                if (rr < 0 || rr >= (int)u) {
-                                    if ((lin >> m) & 1) nm |= 1u << b;
-                                    b++;
-                                }
-                            }
-                        }
-                    }
-                    const uint64_t ck = bfs_pack(u, (uint32_t)s2, nm);
-                    uint32_t h = (uint32_t)jh_mix64(ck) & cmask;
-                    bool ins = false;
-                    for (uint32_t probe = 0; probe <= cmask; probe++) {
-                        const unsigned long long prev =
-                            atomicCAS((unsigned long long *)&set[h], BFS_EMPTY, ck);
-                        if (prev == BFS_EMPTY) { ins = true; break; }
-                        if (prev == ck) break;
-                        h = (h + 1) & cmask;
-                    }
-                    if (!ins) continue;
-                    const unsigned long long n = atomicAdd(&s_count, 1ULL);
-                    if ((long long)n >= A.budget) atomicOr(&s_status, 2);
-                    if (u == (uint32_t)T.n_ok) atomicOr(&s_status, 1);
-                    atomicMax(&s_tmax, u);
-                    const unsigned pos = atomicAdd(&s_nnext, 1u);
-                    if (pos < A.q_cap) nxt[pos] = ck; else atomicOr(&s_status, 2);
-                }
-            }
-            __syncthreads();
-            const int st = s_status;
-            const unsigned nn = s_nnext;
-            __syncthreads();
-            if (st || nn == 0) break;
-            if (tid == 0) { s_ncur = nn; s_nnext = 0; }
-            uint64_t *tmp = cur; cur = nxt; nxt = tmp;
-            __syncthreads();
-        }
-        if (s_status) {
-            if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
-        } else if (wid == 0) {
-            jh_key_verdict v;
-            v.valid = JH_INVALID; v.cause = 0; v.explored = (int64_t)s_count;
-            v.fail_entry = ret_row(A.src, T, s_tmax, lane);
-            if (lane == 0) A.out[key] = v;
-        }
-        __syncthreads();
     }
 }
 
@@ -888,7 +1135,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     if (clear_memo) HIP_TRY(hipMemsetAsync(memo, 0, ctx->bufs[WS_MEMO].bytes, st));
     const uint32_t stack_cap = (uint32_t)smax + 2;
     Frame *stack = ctx->ws<Frame>(WS_STACK, (size_t)waves1 * stack_cap);
-    const uint64_t scr_bytes = (((uint64_t)smax * 84 + 4096) + 255) & ~255ULL;
+    const uint64_t scr_bytes = (((uint64_t)smax * 84 + 4096 + MEMO_SLOTS * 8) + 255) & ~255ULL;
     char *scr = ctx->ws<char>(WS_SCRATCH, (size_t)waves1 * scr_bytes);
     int32_t *q = ctx->ws<int32_t>(WS_QUEUE, 8);
     int32_t *list = ctx->ws<int32_t>(WS_STATS, K);
@@ -904,6 +1151,15 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     a.memo = memo; a.memo_cap = memo_cap1; a.stack = stack; a.stack_cap = stack_cap;
     a.scratch = scr; a.scratch_bytes = scr_bytes; a.budget = quick; a.defer = quick < budget ? 1 : 0;
     a.init_state = init_state; a.gen_base = ctx->gen_base; a.flags = q + 2; a.probes = probes;
+    a.states8 = (vmax - vmin + 2) <= 256 ? 1 : 0;
+    const char *dbgenv = getenv("JH_DEBUG");
+    const bool dbg2 = dbgenv && atoi(dbgenv) >= 2;
+    unsigned long long *dbg = nullptr;
+    if (dbg2) {
+        dbg = ctx->ws<unsigned long long>(WS_STATS + 40, (size_t)(waves1 + 256) * 16);
+        HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 256) * 16, st));
+        a.dbg = dbg;
+    }
     HIP_TRY(hipEventRecord(ctx->ev[1], st));
     k_lin_dfs<<<waves1, 64, LDS_BYTES, st>>>(a);
     HIP_TRY(hipGetLastError());
@@ -911,6 +1167,17 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const int n_defer = qh[1];
+    if (dbg2) {
+        std::vector<unsigned long long> h((size_t)waves1 * 16);
+        HIP_TRY(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+        unsigned long long tot[16] = {0}, mx9 = 0;
+        for (int w = 0; w < waves1; w++) { for (int k = 0; k < 16; k++) tot[k] += h[16 * w + k]; mx9 = std::max(mx9, h[16 * w + 9]); }
+        fprintf(stderr, "[jh-dfs] waves=%d keys=%llu pass1=%.0f fill=%.0f search=%.0f cyc/key | steps=%llu inserts=%llu evict=%llu reload=%llu | cyc/step=%.0f | lds-tables=%llu | wave-busy avg=%.0f max=%llu cyc\n",
+                waves1, tot[3], (double)tot[0] / std::max(1ULL, tot[3]), (double)tot[1] / std::max(1ULL, tot[3]),
+                (double)tot[2] / std::max(1ULL, tot[3]), tot[4], tot[5], tot[6], tot[7],
+                (double)tot[2] / std::max(1ULL, tot[4]), tot[8], (double)tot[9] / waves1, mx9);
+        HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 256) * 16, st));
+    }
     HIP_TRY(hipEventRecord(ctx->ev[4], st));
     int n_unres = 0;
     if (n_defer > 0) {
@@ -932,11 +1199,21 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         c.set = bset; c.set_cap = set_cap; c.q = bq; c.q_cap = q_cap;
         c.scratch = bscr; c.scratch_bytes = scr_bytes; c.budget = budget;
         c.init_state = init_state; c.states_ok = (vmax - vmin + 2) < 4096 ? 1 : 0;
+        c.dbg = dbg;
         k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         n_unres = qh[3];
+        if (dbg2) {
+            std::vector<unsigned long long> h((size_t)wg2 * 16);
+            HIP_TRY(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+            for (int w = 0; w < wg2; w++)
+                if (h[16 * w + 4])
+                    fprintf(stderr, "[jh-bfs] wg %d keys=%llu cycles=%llu levels=%llu configs=%llu inserted=%llu cyc/level=%.0f\n",
+                            w, h[16 * w + 4], h[16 * w], h[16 * w + 1], h[16 * w + 2], h[16 * w + 3],
+                            (double)h[16 * w] / std::max(1ULL, h[16 * w + 1]));
+        }
     }
     HIP_TRY(hipEventRecord(ctx->ev[5], st));
     if (n_unres > 0) {

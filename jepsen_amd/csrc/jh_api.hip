@@ -76,6 +76,7 @@ int jh_open(int device, jh_ctx **out) {
     try {
         HIP_TRY(hipSetDevice(device));
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
         for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -97,6 +98,7 @@ void jh_close(jh_ctx *ctx) {
         for (auto &b : ctx->bufs) if (b.p) (void)hipFree(b.p);
         for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+        if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     }
     delete ctx;
 }

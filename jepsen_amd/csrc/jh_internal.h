@@ -51,6 +51,7 @@ struct Buf {
 struct jh_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t aux = nullptr;     // second stream for racing searches (jh_lin.hip)
     std::mutex mu;
     std::vector<Buf> bufs;
     hipEvent_t ev[8] = {};
@@ -71,7 +72,10 @@ struct jh_ctx {
             size_t alloc = need + need / 8;
             HIP_TRY(hipMalloc(&b.p, alloc));
             b.bytes = alloc;
-            if (zero) HIP_TRY(hipMemsetAsync(b.p, 0, alloc, stream));
+            if (zero) {
+                HIP_TRY(hipMemsetAsync(b.p, 0, alloc, stream));
+                HIP_TRY(hipStreamSynchronize(stream));   // callers may run on another stream
+            }
         }
         return (T *)b.p;
     }
@@ -86,7 +90,7 @@ enum WsSlot {
     WS_MEMO_DEEP, WS_STACK_DEEP, WS_SCRATCH_DEEP, WS_SUMMARY, WS_STATS,
     WS_C_PAIR, WS_C_LAST, WS_C_LO, WS_C_HI, WS_C_OUT, WS_C_FLAG, WS_C_TMP, WS_C_IDX,
     WS_S_BITS, WS_S_RUNS, WS_S_TMP, WS_S_CNT,
-    WS_BFS_SET, WS_BFS_Q, WS_BFS_META,
+    WS_BFS_SET, WS_BFS_Q, WS_BFS_META, WS_CLAIM, WS_SCRATCH_BFS, WS_DEBUG,
     WS_COUNT
 };
 

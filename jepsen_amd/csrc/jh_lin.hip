@@ -30,11 +30,11 @@ namespace {
 constexpr int F_READ = 0, F_WRITE = 1, F_CAS = 2, F_OTHER = 4;
 constexpr int T_INVOKE = 0, T_OK = 1, T_FAIL = 2, T_INFO = 3;
 constexpr uint64_t VIOL_NONE = ~0ULL;
-constexpr int LDS_TBL = 15360;            // per-wave op/window tables
-constexpr int MEMO_SLOTS = 2048;          // per-wave LDS memo (hot layers t >= theta)
-constexpr int MEMO_EVICT = 1024;          // evict at load factor 1/2
+constexpr int LDS_TBL = 5120;             // per-wave compact op + delta tables
+constexpr int MEMO_SLOTS = 1024;          // per-wave LDS memo (hot layers t >= theta)
+constexpr int MEMO_EVICT = 512;           // evict at load factor 1/2
 constexpr int RING = 64;                  // per-wave LDS stack ring (frames)
-constexpr int LDS_BYTES = LDS_TBL + MEMO_SLOTS * 8 + RING * 16;   // 32 KB -> 5 waves/CU
+constexpr int LDS_BYTES = LDS_TBL + MEMO_SLOTS * 8 + RING * 16;   // 14 KB -> 11 waves/CU
 constexpr int STATE_BITS = 20, T_BITS = 20, GEN_BITS = 24;
 constexpr uint32_t STATE_MASK = (1u << STATE_BITS) - 1, T_MASK = (1u << T_BITS) - 1;
 
@@ -229,7 +229,16 @@ struct DfsArgs {
     unsigned long long *probes; // total memo probes (roofline accounting)
     int32_t states8;            // every interned state < 256 (LDS memo packing)
     unsigned long long *dbg;    // JH_DEBUG=2: per-wave cycle accounting (8 words)
+    int32_t *claim;             // race with k_lin_bfs: per-key first-writer flag (or null)
 };
+
+constexpr int JH_CANCELLED = 3; // internal: the other search settled the key first
+
+// write a key's verdict; in a race only the first finisher writes
+__device__ __forceinline__ void emit_verdict(jh_key_verdict *out, int32_t *claim, int key,
+                                             const jh_key_verdict &v) {
+    if (!claim || atomicCAS(&claim[key], 0, 1) == 0) out[key] = v;
+}
 
 __device__ __forceinline__ uint64_t ballot(bool b) { return __ballot(b); }
 __device__ __forceinline__ int mbcnt(uint64_t m) {
@@ -465,15 +474,105 @@ __device__ long long ret_row(const KeySrc &S, const KeyInfo &K, uint32_t t, int 
 }
 
 // ---------------------------------------------------------------------------
-// The WGL depth-first search for one key (one wave), templated on where the
-// tables live. Returns the verdict; sets inserts / tmax.
+// The WGL depth-first search, one key per wave.
 //
-// Memo: every configuration with t >= theta lives in the LDS table (8-byte
-// keys t:16|state:8|mask:40); every one with t < theta in this wave's
-// gen-tagged HBM table. When LDS reaches half load the layers below the
-// current t move to HBM in one bulk pass; a lookup goes to LDS or HBM by the
-// child's t alone, so the set stays exact. Stack: an LDS ring of the top
-// RING frames, written through to HBM.
+// Compact per-key tables (the search needs no explicit window table):
+//   OpC ops[j]   8 bytes: v1 | v2 << 16 ; f | a << 2 | (rr + 1) << 16
+//   delta[t]     ret_op | r_t << 16 | c_t << 22
+// where r_t is the position of RET[t] (the op whose ok return defines t) in
+// W(t), and c_t the number of ops appended to the window on entering layer t
+// (c_0 = |W(0)|). Since W(t+1) = W(t) - {RET[t]} + the next c_{t+1} ops in
+// call order, the window lives in lane registers (lane i = member i) and
+// moves between layers with lane shuffles. Lifting RET[t] removes bit r_t
+// from the mask and keeps removing while the next layer's RET op is already
+// linearized: the canonical compaction of orc_wgl_canonical
+// (oracle/jh_oracle.c) done on the mask directly.
+//
+// Memo: every configuration with t >= theta lives in the wave's LDS table
+// (8-byte keys t:16|state:8|mask:40); every one with t < theta in the wave's
+// gen-tagged HBM table. When the LDS table reaches half load, the layers
+// farthest below the current one move to HBM in one bulk pass; a lookup goes
+// to LDS or HBM by the child's t alone, so the memo stays an exact set.
+// Stack: an LDS ring of the top RING frames, written through to HBM.
+struct OpC {
+    uint32_t vv;      // v1 | v2 << 16 (interned states, < 2^16)
+    uint32_t fa;      // f | a << 2 | (rr + 1) << 16   (a < 2^14, rr + 1 < 2^16)
+};
+constexpr int COMPACT_MAX_OK = 16000;
+
+__device__ __forceinline__ uint64_t tblc_ops_bytes(const KeyInfo &K) { return ((uint64_t)K.n_ops * 8 + 15) & ~15ULL; }
+__device__ __forceinline__ uint64_t tblc_bytes(const KeyInfo &K) {
+    return tblc_ops_bytes(K) + (((uint64_t)K.n_ok * 4 + 15) & ~15ULL);
+}
+
+// Pass 2 + delta sweep. Returns the widest window (> 64: :unknown, window).
+template <bool L>
+__device__ int key_fill_c(const KeySrc &S, const KeyInfo &K, int lane, char *tb) {
+    OpC *ops = (OpC *)tb;
+    uint32_t *delta = (uint32_t *)(tb + tblc_ops_bytes(K));
+    const int n_ops = K.n_ops, n_ok = K.n_ok;
+    {
+        int nok = 0;
+        for (uint32_t base = K.s0; base < K.s1; base += 64) {
+            const uint32_t p = base + lane;
+            const bool valid = p < K.s1;
+            const int rk = valid ? S.rank[p] : -1;
+            const bool kept = rk >= 0, ret = rk <= -2;
+            const uint64_t br = ballot(ret);
+            if (kept) {
+                Rec x = S.rec[p];
+                const int q = S.pair[p];
+                int rr = -1, v1c = x.v1, v2c = x.v2;
+                if (q >= 0) {
+                    Rec y = S.rec[q];
+                    if (y.type == T_OK) {
+                        rr = -(S.rank[q] + 2);
+                        if (x.f == F_CAS) { if (x.v1 == 0 && x.v2 == 0) { v1c = y.v1; v2c = y.v2; } }
+                        else if (x.v1 == 0) v1c = y.v1;
+                    }
+                }
+                const int a = nok + mbcnt(br);
+                OpC o;
+                o.vv = (uint32_t)v1c | ((uint32_t)v2c << 16);
+                o.fa = (uint32_t)x.f | ((uint32_t)a << 2) | ((uint32_t)(rr + 1) << 16);
+                ops[rk] = o;
+            }
+            nok += __popcll(br);
+        }
+    }
+    wave_sync();
+    // Sweep the layers with the window as lane-resident op indices.
+    int maxw = 0, w = 0, nxt = 0, m = 0, r_prev = 0;
+    for (int t = 0; t < n_ok; t++) {
+        if (t > 0) {                               // drop RET[t-1]
+            const int src = lane + (lane >= r_prev ? 1 : 0);
+            m = __shfl(m, src & 63);
+            w--;
+        }
+        int c = 0;
+        for (;;) {                                 // append ops invoked before R_t
+            const int j = nxt + lane;
+            const bool in = j < n_ops && (int)((ops[j].fa >> 2) & 0x3FFF) <= t;
+            const int k = __popcll(ballot(in));    // a is non-decreasing: a prefix
+            const int dst = lane - (w + c);
+            if (dst >= 0 && dst < k) m = nxt + dst;
+            c += k; nxt += k;
+            if (k < 64) break;
+        }
+        w += c;
+        maxw = max(maxw, w);
+        if (w > 64 || c > 1023) { maxw = max(maxw, 65); break; }
+        const bool is_ret = lane < w && (int)(ops[m].fa >> 16) == t + 1;
+        const uint64_t br = ballot(is_ret);
+        const int r = br ? __builtin_ctzll(br) : 0;
+        const int ret_op = readlane(m, r);
+        if (lane == 0) delta[t] = (uint32_t)ret_op | ((uint32_t)r << 16) | ((uint32_t)c << 22);
+        r_prev = r;
+    }
+    wave_sync();
+    return maxw;
+}
+
 // LDS memo slot of an 8-byte key: one 32-bit multiply-xorshift
 __device__ __forceinline__ uint32_t lds_hash(uint64_t k) {
     uint32_t h = (uint32_t)k * 0x9E3779B1u ^ (uint32_t)(k >> 32) * 0x85EBCA77u;
@@ -482,23 +581,45 @@ __device__ __forceinline__ uint32_t lds_hash(uint64_t k) {
     return (h >> 13) & (MEMO_SLOTS - 1);
 }
 
-// Evict the LDS memo's layers below t_new into this wave's HBM table
-// (out of line: it runs once per MEMO_EVICT inserts and must not bloat the
-// search loop). Entries are staged through global scratch, the LDS table is
-// rebuilt with the kept layers. Returns the new LDS entry count and sets
-// theta (0xFFFFFFFF = one layer alone is too wide: HBM only from now on).
+// Evict LDS memo layers into this wave's HBM table (out of line: it runs
+// once per MEMO_EVICT inserts). theta is chosen so that the layers kept in
+// LDS (t >= theta, at most a few below the current layer t_cur) fill at most
+// half of what triggered the eviction; 0xFFFFFFFF = the current layer alone
+// is too wide: HBM only from now on. Entries are staged through global
+// scratch and the LDS table is rebuilt. Returns theta << 32 | kept.
 __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint64_t *memo, uint64_t *stage,
-                                            uint32_t cap_mask, uint32_t gen, uint32_t t_new, int lane) {
+                                            uint32_t cap_mask, uint32_t gen, uint32_t t_cur,
+                                            int lane) {
     const uint64_t gen_hi = (uint64_t)gen << 40;
-    int kept = 0;
+    // histogram of entries by distance below t_cur (entries at or above it: bin 0)
+    int bins = 0;                                  // lane b < 16 holds bin b
 #pragma unroll 1
     for (int r = 0; r < MEMO_SLOTS / 64; r++) {
         const uint64_t x = lmemo[lane + 64 * r];
         stage[lane + 64 * r] = x;
-        kept += __popcll(ballot(x != 0 && (uint32_t)(x >> 48) >= t_new));
+        const uint32_t xt = (uint32_t)(x >> 48);
+        const int d = x == 0 ? 99 : (xt >= t_cur ? 0 : (int)min(t_cur - xt, 15u));
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            const int cnt = __popcll(ballot(d == b));
+            if (lane == b) bins += cnt;
+        }
     }
-    uint32_t th2 = t_new;
-    if (kept > MEMO_EVICT / 2) { th2 = 0xFFFFFFFFu; kept = 0; }
+    // theta = t_cur - d*, d* the largest distance keeping <= MEMO_EVICT/2
+    int acc = 0, dstar = -1;
+#pragma unroll 1
+    for (int b = 0; b < 16; b++) {
+        acc += readlane(bins, b);
+        if (acc > MEMO_EVICT / 2) break;
+        dstar = b;
+    }
+    uint32_t th2;
+    int kept = 0;
+    if (dstar < 0) th2 = 0xFFFFFFFFu;
+    else {
+        th2 = t_cur > (uint32_t)dstar ? t_cur - (uint32_t)dstar : 0u;
+        if (dstar == 15) th2 = t_cur - min(t_cur, 15u);
+    }
     wave_sync();
 #pragma unroll 1
     for (int r = 0; r < MEMO_SLOTS / 64; r++) lmemo[lane + 64 * r] = 0;
@@ -533,6 +654,7 @@ __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint64_t *memo, uin
                 h = (h + 1) & cap_mask;
             }
         } else {
+            kept++;
             uint32_t h = lds_hash(x);
             for (;;) {
                 unsigned long long z = 0;
@@ -544,6 +666,7 @@ __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint64_t *memo, uin
             }
         }
     }
+    for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o);
     // every HBM write of this wave is visible to its later probes
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -573,43 +696,25 @@ __device__ __forceinline__ uint64_t hbm_probe(const uint64_t *memo, uint32_t cap
     }
 }
 
-// The RET member (the op whose return defines t) is being lifted: advance t
-// past every ok return whose op is already linearized and compact the mask
-// onto W(t'). Wave-wide (all lanes), uniform result.
-__device__ __forceinline__ void ret_lift(uint64_t lin, uint32_t t, int n_ok, int w, int o_rr,
-                                         int lane, uint32_t &u_out, uint64_t &nm_out) {
-    uint32_t u = t + 1;
-    while (u < (uint32_t)n_ok && ballot(((lin >> lane) & 1) && o_rr == (int)u)) u++;
-    uint64_t nm = 0;
-    if (u < (uint32_t)n_ok) {
-        const uint64_t keep = ballot(lane < w && (o_rr < 0 || o_rr >= (int)u));
-        uint64_t bits = lin & keep;
-        while (bits) {
-            const int b = __builtin_ctzll(bits);
-            bits &= bits - 1;
-            nm |= 1ULL << __popcll(keep & ((1ULL << b) - 1));
-        }
-    }
-    u_out = u;
-    nm_out = nm;
+__device__ __forceinline__ uint64_t drop_bit(uint64_t m, uint32_t r) {
+    const uint64_t lo = (1ULL << r) - 1;
+    return (m & lo) | ((m >> 1) & ~lo);
 }
 
 template <bool L>
-__device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int maxw, int key, int lane,
-                          uint64_t *memo, Frame *stack, uint64_t *stage, long long &inserts,
-                          uint32_t &tmax_out, unsigned long long &my_probes) {
-    const Op *ops = (const Op *)tb;
-    const int32_t *woff = (const int32_t *)(tb + tbl_ops_bytes(K));
-    const uint16_t *W = (const uint16_t *)(tb + tbl_ops_bytes(K) + tbl_off_bytes(K));
-    const int n_ok = K.n_ok;
+__device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key, int lane,
+                          uint64_t *memo, Frame *stack, uint64_t *stage, bool lds_memo,
+                          long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes) {
+    const OpC *ops = (const OpC *)tb;
+    const uint32_t *delta = (const uint32_t *)(tb + tblc_ops_bytes(K));
+    const uint32_t n_ok = (uint32_t)K.n_ok;
     const uint64_t lane_bit = 1ULL << lane;
     const uint32_t cap_mask = A.memo_cap - 1;
     const uint32_t gen = (A.gen_base + (uint32_t)key + 1) & ((1u << GEN_BITS) - 1);
     const uint64_t gen_hi = (uint64_t)gen << 40;
     uint64_t *lmemo = (uint64_t *)(jh_lds + LDS_TBL);
     Frame *ring = (Frame *)(jh_lds + LDS_TBL + MEMO_SLOTS * 8);
-    const bool lds_ok = A.states8 && maxw <= 40 && n_ok < 65535;
-    uint32_t theta = lds_ok ? 0u : 0xFFFFFFFFu;
+    uint32_t theta = lds_memo ? 0u : 0xFFFFFFFFu;
     int lcount = 0;
     for (int i = lane; i < MEMO_SLOTS; i += 64) lmemo[i] = 0;
     uint32_t t = 0, tmax = 0, depth = 0, ring_lo = 0;
@@ -618,35 +723,40 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int maxw
     int verdict = -1;
     long long ins = 0;
     unsigned long long n_steps = 0, n_evict = 0, n_reload = 0;
-    // lane-resident window member
-    int w = 0, o_f = 0, o_v1 = 0, o_v2 = 0, o_rr = -1;
-#define LOAD_WINDOW(tt)                                                        \
-    do {                                                                       \
-        const int wo_ = woff[tt];                                              \
-        w = woff[(tt) + 1] - wo_;                                              \
-        const Op o_ = ops[W[wo_ + min(lane, max(w - 1, 0))]];                  \
-        const bool in_ = lane < w;                                             \
-        o_f = in_ ? (o_.fa & 3) : 3; o_v1 = o_.v1; o_v2 = o_.v2;               \
-        o_rr = in_ ? o_.rr : -1;                                               \
-    } while (0)
+    // the window of layer t in lane registers: f (3 = no member), v1|v2
+    int w = (int)(delta[0] >> 22), P = w;
+    uint32_t r = (delta[0] >> 16) & 63;            // position of RET[t]
+    int lf = 3;
+    uint32_t lv = 0;
+    if (lane < w) { const OpC o = ops[lane]; lf = (int)(o.fa & 3); lv = o.vv; }
     wave_sync();
-    LOAD_WINDOW(0);
     while (true) {
         n_steps++;
-        // candidates: un-linearized members at or after `start` the model
-        // allows (o_f == 3 marks lanes outside the window)
-        const bool legal = o_f == F_WRITE || (o_f == F_CAS && s == o_v1) ||
-                           (o_f == F_READ && (o_v1 == 0 || o_v1 == s));
-        const int s2 = o_f == F_WRITE ? o_v1 : (o_f == F_CAS ? o_v2 : s);
+        if (A.claim && (n_steps & 1023) == 0) {
+            int c = 0;
+            if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (readlane(c, 0)) { verdict = JH_CANCELLED; break; }
+        }
+        // candidates: un-linearized members at or after `start` the model allows
+        const int v1 = (int)(lv & 0xFFFF), v2 = (int)(lv >> 16);
+        const bool legal = lf == F_WRITE || (lf == F_CAS && s == v1) ||
+                           (lf == F_READ && (v1 == 0 || v1 == s));
+        const int s2 = lf == F_WRITE ? v1 : (lf == F_CAS ? v2 : s);
         const bool cand = legal && lane >= start && !(mask & lane_bit);
         uint32_t ct = t;
         uint64_t cm = mask | lane_bit;
-        const uint64_t bret = ballot(cand && o_rr == (int)t);
-        if (bret) {
-            uint32_t u;
-            uint64_t nm;
-            ret_lift(mask | bret, t, n_ok, w, o_rr, lane, u, nm);
-            if (o_rr == (int)t) { ct = u; cm = nm; }
+        if ((ballot(cand) >> r) & 1) {
+            // lifting RET[t]: drop returned members, advance past linearized RETs
+            uint64_t nm = mask | (1ULL << r);
+            uint32_t u = t, ru = r;
+            for (;;) {
+                nm = drop_bit(nm, ru);
+                u++;
+                if (u >= n_ok) { nm = 0; break; }
+                ru = (delta[u] >> 16) & 63;
+                if (!((nm >> ru) & 1)) break;
+            }
+            if (lane == (int)r) { ct = u; cm = nm; }
         }
         // memo probes, all candidates at once (= the sequential scan, since
         // nothing is inserted until the first new child is chosen)
@@ -664,9 +774,9 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int maxw
         }
         const bool go_hbm = cand && ct < theta;
         if (ballot(go_hbm) && go_hbm) {
-            const uint64_t r = hbm_probe(memo, cap_mask, gen, ct, (uint32_t)s2, cm, my_probes);
-            slot = (uint32_t)r;
-            absent = (r >> 32) != 0;
+            const uint64_t rr = hbm_probe(memo, cap_mask, gen, ct, (uint32_t)s2, cm, my_probes);
+            slot = (uint32_t)rr;
+            absent = (rr >> 32) != 0;
         }
         const uint64_t bn = ballot(absent);
         if (bn) {
@@ -700,19 +810,32 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int maxw
             if (to_lds) {
                 if (++lcount >= MEMO_EVICT) {
                     n_evict++;
-                    const uint64_t r = memo_evict(lmemo, memo, stage, cap_mask, gen, nt, lane);
-                    lcount = (int)(uint32_t)r;
-                    theta = (uint32_t)(r >> 32);
+                    const uint64_t er = memo_evict(lmemo, memo, stage, cap_mask, gen, nt, lane);
+                    lcount = (int)(uint32_t)er;
+                    theta = (uint32_t)(er >> 32);
                 }
             } else {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             }
             if (nt != t) {
+                if (nt >= n_ok) { t = nt; tmax = max(tmax, t); verdict = JH_VALID; break; }
+                // move the window forward layer by layer
+                for (uint32_t u = t; u < nt; u++) {
+                    const uint32_t ru = u == t ? r : (delta[u] >> 16) & 63;
+                    const int src = lane + (lane >= (int)ru ? 1 : 0);
+                    lf = __shfl(lf, src & 63);
+                    lv = (uint32_t)__shfl((int)lv, src & 63);
+                    w--;
+                    const int c = (int)(delta[u + 1] >> 22);
+                    const int dst = lane - w;
+                    if (dst >= 0 && dst < c) { const OpC o = ops[P + dst]; lf = (int)(o.fa & 3); lv = o.vv; }
+                    if (lane >= w + c) lf = 3;
+                    w += c; P += c;
+                }
                 t = nt;
                 tmax = max(tmax, t);
-                if (t == (uint32_t)n_ok) { verdict = JH_VALID; break; }
-                LOAD_WINDOW(t);
+                r = (delta[t] >> 16) & 63;
                 n_reload++;
             }
         } else {
@@ -728,11 +851,27 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int maxw
             }
             const uint32_t pt = fr.t_i >> 6;
             mask = fr.mask; s = fr.s; start = (int)(fr.t_i & 63) + 1;
-            if (pt != t) { t = pt; LOAD_WINDOW(t); n_reload++; }
+            if (pt != t) {
+                // move the window back: drop appended ops, re-insert RETs
+                for (uint32_t u = t; u > pt; u--) {
+                    const int c = (int)(delta[u] >> 22);
+                    w -= c; P -= c;
+                    if (lane >= w) lf = 3;
+                    const uint32_t d = delta[u - 1];
+                    const int ru = (int)((d >> 16) & 63);
+                    const int src = lane - (lane > ru ? 1 : 0);
+                    lf = __shfl(lf, src & 63);
+                    lv = (uint32_t)__shfl((int)lv, src & 63);
+                    if (lane == ru) { const OpC o = ops[d & 0xFFFF]; lf = (int)(o.fa & 3); lv = o.vv; }
+                    w++;
+                }
+                t = pt;
+                r = (delta[t] >> 16) & 63;
+                n_reload++;
+            }
         }
         if (depth >= A.stack_cap) { verdict = JH_UNKNOWN; if (lane == 0) atomicOr(A.flags, 4); break; }
     }
-#undef LOAD_WINDOW
     inserts = ins;
     tmax_out = tmax;
     if (A.dbg && lane == 0) {
@@ -749,19 +888,23 @@ __device__ void dfs_key(const DfsArgs &A, const KeySrc &src, const KeyInfo &K, c
     jh_key_verdict v;
     v.valid = JH_VALID; v.cause = 0; v.fail_entry = -1; v.explored = 0;
     const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-    const int maxw = key_fill<L>(src, K, lane, tb);
+    const int maxw = key_fill_c<L>(src, K, lane, tb);
     const unsigned long long c1 = __builtin_amdgcn_s_memtime();
     if (A.dbg && lane == 0) { A.dbg[16 * (size_t)blockIdx.x + 1] += c1 - c0; A.dbg[16 * (size_t)blockIdx.x + 8] += L ? 1 : 0; }
     if (maxw > 64) {
         v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-        if (lane == 0) A.out[key] = v;
+        if (lane == 0) emit_verdict(A.out, A.claim, key, v);
         return;
     }
     long long inserts = 0;
     uint32_t tmax = 0;
     uint64_t *stage = (uint64_t *)(gscr + A.scratch_bytes - MEMO_SLOTS * 8);
-    const int verdict = dfs_search<L>(A, K, tb, maxw, key, lane, memo, stack, stage, inserts, tmax, my_probes);
+    // the LDS memo packs states in 8 bits and masks in 40: else HBM table only
+    const bool lds_memo = A.states8 && maxw <= 40;
+    const int verdict = dfs_search<L>(A, K, tb, key, lane, memo, stack, stage, lds_memo, inserts,
+                                      tmax, my_probes);
     if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 2] += __builtin_amdgcn_s_memtime() - c1;
+    if (verdict == JH_CANCELLED) return;
     if (verdict == JH_UNKNOWN && A.defer && inserts >= A.budget) {
         if (lane == 0) {
             const int d = atomicAdd(A.defer_count, 1);
@@ -773,7 +916,7 @@ __device__ void dfs_key(const DfsArgs &A, const KeySrc &src, const KeyInfo &K, c
     v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
     v.explored = inserts;
     if (verdict == JH_INVALID) v.fail_entry = ret_row(src, K, tmax, lane);
-    if (lane == 0) A.out[key] = v;
+    if (lane == 0) emit_verdict(A.out, A.claim, key, v);
 }
 
 __global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
@@ -796,10 +939,17 @@ __global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
         const bool needed = key_pass1(src, key, lane, K, v);
         if (A.dbg && lane == 0) { A.dbg[16 * (size_t)blockIdx.x + 0] += __builtin_amdgcn_s_memtime() - p0; A.dbg[16 * (size_t)blockIdx.x + 3] += 1; }
         if (!needed) {
-            if (lane == 0) A.out[key] = v;
+            if (lane == 0) emit_verdict(A.out, A.claim, key, v);
             continue;
         }
-        const uint64_t need = tbl_bytes(K);
+        if (K.n_ok >= COMPACT_MAX_OK) {
+            // beyond the compact encoding (a < 2^14): not on this build's path
+            if (lane == 0) atomicOr(A.flags, 1);
+            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
+            if (lane == 0) emit_verdict(A.out, A.claim, key, v);
+            continue;
+        }
+        const uint64_t need = tblc_bytes(K);
         if (need <= (uint64_t)LDS_TBL) {
             dfs_key<true>(A, src, K, gscr, key, lane, memo, stack, my_probes);
         } else if (need + MEMO_SLOTS * 8 <= A.scratch_bytes) {
@@ -807,7 +957,7 @@ __global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
         } else {
             if (lane == 0) atomicOr(A.flags, 2);
             v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-            if (lane == 0) A.out[key] = v;
+            if (lane == 0) emit_verdict(A.out, A.claim, key, v);
         }
     }
     if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 9] = __builtin_amdgcn_s_memtime() - t_begin;
@@ -824,13 +974,14 @@ __global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
 // is reachable (valid) or the set outgrows the budget is handed to the
 // sequential search (only it defines where :unknown starts for those).
 constexpr int BFS_THREADS = 512;
-constexpr int BFS_HDR = 256;                       // shared scalars, start of dynamic LDS
-constexpr int BFS_TBL = 49152;
-constexpr int BFS_LDS_BYTES = BFS_HDR + BFS_TBL;
+constexpr int BFS_HDR = 1024;                      // shared scalars + the layer's window
+constexpr int BFS_TBL = 28672;                     // W-format tables (ops, woff, W) + r[]
+constexpr int LSET = 8192;                         // layer set slots (8 B keys)
+constexpr int BFS_LDS_BYTES = BFS_HDR + BFS_TBL + LSET * 8;   // ~94 KB: one workgroup per CU
 constexpr uint64_t BFS_EMPTY = ~0ULL;
 
 struct BfsArgs {
-    unsigned long long *dbg;  // JH_DEBUG=2: per-workgroup accounting (8 words)
+    unsigned long long *dbg;  // JH_DEBUG=2: per-workgroup accounting (16 words)
     KeySrc src;
     const int32_t *list;
     int32_t n_list;
@@ -838,34 +989,59 @@ struct BfsArgs {
     jh_key_verdict *out;
     int32_t *unres_list;
     int32_t *unres_count;
-    uint64_t *set;          // per workgroup: set_cap slots
-    uint32_t set_cap;       // power of two
-    uint64_t *q;            // per workgroup: 2 x q_cap configurations
+    uint64_t *gset;         // per workgroup: gset_cap slots, layers too wide for LDS
+    uint32_t gset_cap;      // power of two
+    uint64_t *pend;         // per workgroup: 2 x q_cap pending cross-layer configurations
+    uint64_t *front;        // per workgroup: 2 x q_cap frontier configurations
     uint32_t q_cap;
     char *scratch;          // per workgroup table space
     uint64_t scratch_bytes;
     int64_t budget;
     int32_t init_state;
     int32_t states_ok;      // every interned state < 2^12
+    int32_t *claim;         // race with the sequential search (see emit_verdict)
 };
 
 struct BfsShared {
     KeyInfo K;
     jh_key_verdict v;
-    int key, need, maxw, status;
-    unsigned ncur, nnext, tmax;
+    int key, need, maxw, status, mode, gclear, ovf;
+    unsigned npend, npend2, nfront, nnext, tmax, lcount, r;
     unsigned long long count;
+    uint32_t win_vv[64];    // the current layer's window: v1 | v2 << 16
+    uint32_t win_f[64];     // f, or 3 for no member
 };
 
+static_assert(sizeof(BfsShared) <= BFS_HDR, "BFS header");
+
+// a configuration of the pending list / global set: t:20 | s:12 | mask:32
 __device__ __forceinline__ uint64_t bfs_pack(uint32_t t, uint32_t s, uint32_t m) {
     return ((uint64_t)t << 44) | ((uint64_t)s << 32) | m;
 }
+__device__ __forceinline__ uint32_t lset_hash(uint64_t k) {
+    uint32_t h = (uint32_t)k * 0x9E3779B1u ^ (uint32_t)(k >> 32) * 0x85EBCA77u;
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    return (h >> 11) & (LSET - 1);
+}
 
+// Heavy keys, one workgroup each: the reachable configuration set layer by
+// layer. Layer t = configurations whose earliest un-linearized ok return is
+// the t-th; every edge either stays in the layer (lift a non-returning
+// member) or goes to a later layer (lift the returning member RET[t]). So
+// layer t is the closure, under same-layer lifts, of the configurations the
+// earlier layers sent to it: processed in t order, each layer's set is
+// exact and lives in an LDS hash (LDS atomics), and only cross-layer edges
+// go through HBM (a pending list, deduplicated when their layer is formed).
+// For a key with no terminal configuration (invalid) WGL's cache ends up
+// holding exactly this set, so verdict, explored count and the furthest
+// layer (fail_entry) equal the sequential search's. A key where a terminal
+// configuration is reachable (valid) or the set outgrows the budget is left
+// to the sequential search, which alone defines :unknown for those.
 template <bool L>
-__device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, uint64_t *set,
-                        uint64_t *qa) {
+__device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, uint64_t *gset,
+                        uint64_t *pend, uint64_t *front) {
     const int lane = tid & 63, wid = tid >> 6;
-    const uint32_t cmask = A.set_cap - 1;
     char *tb = tbl_base<L>(BFS_HDR, gscr);
     const KeyInfo K = sh.K;
     const int key = sh.key;
@@ -877,105 +1053,203 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
     const Op *ops = (const Op *)tb;
     const int32_t *woff = (const int32_t *)(tb + tbl_ops_bytes(K));
     const uint16_t *W = (const uint16_t *)(tb + tbl_ops_bytes(K) + tbl_off_bytes(K));
-    const int n_ok = K.n_ok;
+    uint8_t *rpos = (uint8_t *)(tb + tbl_bytes(K));           // r[t], after the tables
+    const uint32_t n_ok = (uint32_t)K.n_ok;
+    uint64_t *lset = (uint64_t *)(jh_lds + BFS_HDR + BFS_TBL);
+    const uint32_t gmask = A.gset_cap - 1;
     if (sh.maxw > 64) {
         if (tid == 0) {
             jh_key_verdict v;
             v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW; v.fail_entry = -1; v.explored = 0;
-            A.out[key] = v;
+            emit_verdict(A.out, A.claim, key, v);
         }
         __syncthreads();
         return;
     }
-    if (sh.maxw > 32 || !A.states_ok || n_ok >= (1 << 20) - 2) {
+    if (sh.maxw > 32 || !A.states_ok || n_ok >= (1u << 20) - 2) {
         if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
         __syncthreads();
         return;
     }
-    for (uint32_t i = tid; i < A.set_cap; i += BFS_THREADS) set[i] = BFS_EMPTY;
+    // position of RET[t] in W(t), for every layer
+    for (uint32_t t = tid; t < n_ok; t += BFS_THREADS) {
+        const int wo = woff[t], w = woff[t + 1] - wo;
+        int r = 0;
+        for (int m = 0; m < w; m++)
+            if (ops[W[wo + m]].rr == (int)t) { r = m; break; }
+        rpos[t] = (uint8_t)r;
+    }
     if (tid == 0) {
-        qa[0] = bfs_pack(0, (uint32_t)A.init_state, 0);
-        sh.ncur = 1; sh.nnext = 0; sh.tmax = 0; sh.count = 0; sh.status = 0;
+        pend[0] = bfs_pack(0, (uint32_t)A.init_state, 0);
+        sh.npend = 1; sh.tmax = 0; sh.count = 0; sh.status = 0; sh.gclear = 0;
     }
     __syncthreads();
-    uint64_t *cur = qa, *nxt = qa + A.q_cap;
     const unsigned long long b0 = __builtin_amdgcn_s_memtime();
-    unsigned long long levels = 0, items = 0;
-    for (;;) {
-        const unsigned ncur = sh.ncur;
-        levels++; items += ncur;
-        for (unsigned i = tid; i < ncur; i += BFS_THREADS) {
-          const uint64_t c = cur[i];
-          const uint32_t t = (uint32_t)(c >> 44), s = (uint32_t)(c >> 32) & 0xFFF;
-          const uint32_t mask = (uint32_t)c;
-          const int wo = woff[t], w = woff[t + 1] - wo;
-          for (int j = 0; j < w; j++) {
-            if ((mask >> j) & 1) continue;
-            const Op o = ops[W[wo + j]];
-            int s2;
-            if (!cas_step(o.fa & 3, o.v1, o.v2, (int)s, &s2)) continue;
-            uint32_t u = t, nm = mask | (1u << j);
-            if (o.rr == (int)t) {
-                const uint32_t lin = nm;
-                u = t + 1;
-                while (u < (uint32_t)n_ok) {
-                    bool hit = false;
-                    for (int m = 0; m < w && !hit; m++)
-                        hit = ((lin >> m) & 1) && ops[W[wo + m]].rr == (int)u;
-                    if (!hit) break;
-                    u++;
+    unsigned long long rounds = 0;
+    uint64_t *pcur = pend, *pnxt = pend + A.q_cap;
+    uint64_t *fcur = front, *fnxt = front + A.q_cap;
+    for (uint32_t t = 0; t < n_ok; t++) {
+        // ---- form layer t: dedupe its entries from the pending list ---------
+        for (int i = tid; i < LSET; i += BFS_THREADS) lset[i] = 0;
+        const int wo = woff[t], w = woff[t + 1] - wo;
+        if (tid < 64) {
+            if (tid < w) {
+                const Op o = ops[W[wo + tid]];
+                sh.win_vv[tid] = (uint32_t)o.v1 | ((uint32_t)o.v2 << 16);
+                sh.win_f[tid] = (uint32_t)(o.fa & 3);
+            } else sh.win_f[tid] = 3;
+        }
+        if (tid == 0) {
+            sh.nfront = 0; sh.lcount = 0; sh.mode = 0; sh.ovf = 0; sh.r = rpos[t];
+            // the sequential search settled this key first
+            if (A.claim && __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                sh.status |= 4;
+        }
+        __syncthreads();
+        const unsigned np = sh.npend;
+        // a layer too wide for the LDS set moves to the global set (t-tagged keys)
+        auto migrate = [&]() {
+            if (!sh.gclear) {
+                for (uint32_t i = tid; i < A.gset_cap; i += BFS_THREADS) gset[i] = BFS_EMPTY;
+                __syncthreads();
+                if (tid == 0) sh.gclear = 1;
+            }
+            for (int i = tid; i < LSET; i += BFS_THREADS) {
+                const uint64_t k = lset[i];
+                if (!k) continue;
+                const uint64_t g = bfs_pack(t, (uint32_t)((k - 1) >> 32) & 0xFFF, (uint32_t)(k - 1));
+                uint32_t h = (uint32_t)jh_mix64(g) & gmask;
+                while (atomicCAS((unsigned long long *)&gset[h], BFS_EMPTY, g) != BFS_EMPTY)
+                    h = (h + 1) & gmask;
+            }
+            __syncthreads();
+            if (tid == 0) { sh.mode = 1; sh.ovf = 0; }
+            __syncthreads();
+        };
+        // insert (s, mask) of layer t; returns true if new
+        auto insert = [&](uint32_t cs, uint32_t cm) -> bool {
+            if (sh.status & 2) return false;
+            if (sh.mode == 0) {
+                // keep the LDS set under 3/4 load (+ at most one insert per thread in flight)
+                if (sh.lcount >= LSET * 3 / 4) { sh.ovf = 1; return false; }
+                const uint64_t k = (((uint64_t)cs << 32) | cm) + 1;
+                uint32_t h = lset_hash(k);
+                for (;;) {
+                    const unsigned long long prev = atomicCAS((unsigned long long *)&lset[h], 0ULL, k);
+                    if (prev == 0) break;
+                    if (prev == k) return false;
+                    h = (h + 1) & (LSET - 1);
                 }
-                nm = 0;
-                if (u < (uint32_t)n_ok) {
-                    int b = 0;
-                    for (int m = 0; m < w; m++) {
-                        const int rr = ops[W[wo + m]].rr;
-                        if (rr < 0 || rr >= (int)u) {
-                            if ((lin >> m) & 1) nm |= 1u << b;
-                            b++;
+                atomicAdd(&sh.lcount, 1u);
+            } else {
+                const uint64_t k = bfs_pack(t, cs, cm);
+                uint32_t h = (uint32_t)jh_mix64(k) & gmask;
+                for (uint32_t probe = 0;; probe++) {
+                    if (probe > gmask) { atomicOr(&sh.status, 2); return false; }
+                    const unsigned long long prev = atomicCAS((unsigned long long *)&gset[h], BFS_EMPTY, k);
+                    if (prev == BFS_EMPTY) break;
+                    if (prev == k) return false;
+                    h = (h + 1) & gmask;
+                }
+            }
+            const unsigned long long n = atomicAdd(&sh.count, 1ULL);
+            if ((long long)n >= A.budget + 1) atomicOr(&sh.status, 2);
+            return true;
+        };
+        // An insert refused for LDS load (ovf) re-runs the pass against the
+        // global set: configurations already inserted stay (and are already on
+        // the frontier), the rest are inserted now.
+        for (;;) {
+        if (tid == 0) sh.npend2 = 0;
+        __syncthreads();
+        for (unsigned i = tid; i < np; i += BFS_THREADS) {
+            const uint64_t e = pcur[i];
+            const uint32_t u = (uint32_t)(e >> 44);
+            if (u == t) {
+                const uint32_t cs = (uint32_t)(e >> 32) & 0xFFF, cm = (uint32_t)e;
+                if (insert(cs, cm)) {
+                    const unsigned pos = atomicAdd(&sh.nfront, 1u);
+                    if (pos < A.q_cap) fcur[pos] = ((uint64_t)cs << 32) | cm; else atomicOr(&sh.status, 2);
+                }
+            } else {
+                const unsigned pos = atomicAdd(&sh.npend2, 1u);
+                pnxt[pos] = e;
+            }
+        }
+        __syncthreads();
+        if (!sh.ovf) break;
+        migrate();
+        }
+        { uint64_t *tp = pcur; pcur = pnxt; pnxt = tp; }
+        if (tid == 0) { sh.npend = sh.npend2; if (sh.nfront) sh.tmax = t; }
+        __syncthreads();
+        // ---- close layer t under same-layer lifts ---------------------------
+        if (sh.status) break;
+        const uint32_t r = sh.r;
+        while (sh.nfront > 0 && !sh.status) {
+            rounds++;
+            const unsigned nf = sh.nfront;
+            if (tid == 0) sh.nnext = 0;
+            __syncthreads();
+            for (;;) {
+            for (unsigned i = tid; i < nf; i += BFS_THREADS) {
+                const uint64_t c = fcur[i];
+                const uint32_t s = (uint32_t)(c >> 32), mask = (uint32_t)c;
+                for (int j = 0; j < w; j++) {
+                    if ((mask >> j) & 1) continue;
+                    const uint32_t f = sh.win_f[j], vv = sh.win_vv[j];
+                    const int v1 = (int)(vv & 0xFFFF), v2 = (int)(vv >> 16);
+                    int s2;
+                    if (!cas_step((int)f, v1, v2, (int)s, &s2)) continue;
+                    if ((uint32_t)j == r) {
+                        // cross-layer edge: drop RET members until one is not linearized
+                        uint64_t nm = mask | (1u << j);
+                        uint32_t u = t, ru = r;
+                        for (;;) {
+                            nm = drop_bit(nm, ru);
+                            u++;
+                            if (u >= n_ok) break;
+                            ru = rpos[u];
+                            if (!((nm >> ru) & 1)) break;
+                        }
+                        if (u >= n_ok) { atomicOr(&sh.status, 1); continue; }
+                        const unsigned pos = atomicAdd(&sh.npend, 1u);
+                        if (pos < A.q_cap) pcur[pos] = bfs_pack(u, (uint32_t)s2, (uint32_t)nm);
+                        else atomicOr(&sh.status, 2);
+                    } else {
+                        const uint32_t cm = mask | (1u << j);
+                        if (insert((uint32_t)s2, cm)) {
+                            const unsigned pos = atomicAdd(&sh.nnext, 1u);
+                            if (pos < A.q_cap) fnxt[pos] = ((uint64_t)(uint32_t)s2 << 32) | cm;
+                            else atomicOr(&sh.status, 2);
                         }
                     }
                 }
             }
-            const uint64_t ck = bfs_pack(u, (uint32_t)s2, nm);
-            uint32_t h = (uint32_t)jh_mix64(ck) & cmask;
-            bool ins = false;
-            for (uint32_t probe = 0; probe <= cmask; probe++) {
-                const unsigned long long prev =
-                    atomicCAS((unsigned long long *)&set[h], BFS_EMPTY, ck);
-                if (prev == BFS_EMPTY) { ins = true; break; }
-                if (prev == ck) break;
-                h = (h + 1) & cmask;
+            __syncthreads();
+            if (sh.ovf) { migrate(); continue; }
+            break;
             }
-            if (!ins) continue;
-            const unsigned long long n = atomicAdd(&sh.count, 1ULL);
-            if ((long long)n >= A.budget) atomicOr(&sh.status, 2);
-            if (u == (uint32_t)n_ok) atomicOr(&sh.status, 1);
-            atomicMax(&sh.tmax, u);
-            const unsigned pos = atomicAdd(&sh.nnext, 1u);
-            if (pos < A.q_cap) nxt[pos] = ck; else atomicOr(&sh.status, 2);
-          }
+            { uint64_t *tp = fcur; fcur = fnxt; fnxt = tp; }
+            if (sh.mode == 0 && sh.lcount > LSET / 2 && !sh.status) migrate();
+            if (tid == 0) sh.nfront = sh.nnext;
+            __syncthreads();
         }
-        __syncthreads();
-        const int st = sh.status;
-        const unsigned nn = sh.nnext;
-        __syncthreads();
-        if (st || nn == 0) break;
-        if (tid == 0) { sh.ncur = nn; sh.nnext = 0; }
-        uint64_t *tmp = cur; cur = nxt; nxt = tmp;
-        __syncthreads();
+        if (sh.status) break;
     }
+    __syncthreads();
     if (A.dbg && tid == 0) {
         unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
-        d[0] += __builtin_amdgcn_s_memtime() - b0; d[1] += levels; d[2] += items; d[3] += sh.count; d[4] += 1;
+        d[0] += __builtin_amdgcn_s_memtime() - b0; d[1] += rounds; d[3] += sh.count; d[4] += 1;
     }
     if (sh.status) {
         if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
     } else if (wid == 0) {
         jh_key_verdict v;
-        v.valid = JH_INVALID; v.cause = 0; v.explored = (int64_t)sh.count;
+        v.valid = JH_INVALID; v.cause = 0;
+        v.explored = (int64_t)sh.count - 1;           // the initial configuration is not cached
         v.fail_entry = ret_row(A.src, K, sh.tmax, lane);
-        if (lane == 0) A.out[key] = v;
+        if (lane == 0) emit_verdict(A.out, A.claim, key, v);
     }
     __syncthreads();
 }
@@ -983,8 +1257,9 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
 __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A) {
     BfsShared &sh = *(BfsShared *)jh_lds;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    uint64_t *set = A.set + (size_t)blockIdx.x * A.set_cap;
-    uint64_t *qa = A.q + (size_t)blockIdx.x * 2 * A.q_cap;
+    uint64_t *gset = A.gset + (size_t)blockIdx.x * A.gset_cap;
+    uint64_t *pend = A.pend + (size_t)blockIdx.x * 2 * A.q_cap;
+    uint64_t *front = A.front + (size_t)blockIdx.x * 2 * A.q_cap;
     char *gscr = A.scratch + (size_t)blockIdx.x * A.scratch_bytes;
     for (;;) {
         if (tid == 0) {
@@ -1002,13 +1277,13 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A) {
         }
         __syncthreads();
         if (!sh.need) {
-            if (tid == 0) A.out[key] = sh.v;
+            if (tid == 0) emit_verdict(A.out, A.claim, key, sh.v);
             __syncthreads();
             continue;
         }
-        const uint64_t need = tbl_bytes(sh.K);
-        if (need <= (uint64_t)BFS_TBL) bfs_key<true>(A, sh, gscr, tid, set, qa);
-        else if (need <= A.scratch_bytes) bfs_key<false>(A, sh, gscr, tid, set, qa);
+        const uint64_t need = tbl_bytes(sh.K) + (uint64_t)sh.K.n_ok + 16;
+        if (need <= (uint64_t)BFS_TBL) bfs_key<true>(A, sh, gscr, tid, gset, pend, front);
+        else if (need <= A.scratch_bytes) bfs_key<false>(A, sh, gscr, tid, gset, pend, front);
         else {
             if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
             __syncthreads();
@@ -1130,7 +1405,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const uint32_t memo_cap1 = 1u << 16;
     int64_t quick = std::min<int64_t>(budget, memo_cap1 / 4);
     if (const char *e = getenv("JH_QUICK_BUDGET")) quick = std::max<int64_t>(1, std::min<int64_t>(quick, atoll(e)));
-    const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * 8);
+    const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * (163840 / LDS_BYTES));
     uint64_t *memo = ctx->ws<uint64_t>(WS_MEMO, (size_t)waves1 * memo_cap1 * 2, /*zero=*/true);
     if (clear_memo) HIP_TRY(hipMemsetAsync(memo, 0, ctx->bufs[WS_MEMO].bytes, st));
     const uint32_t stack_cap = (uint32_t)smax + 2;
@@ -1156,7 +1431,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const bool dbg2 = dbgenv && atoi(dbgenv) >= 2;
     unsigned long long *dbg = nullptr;
     if (dbg2) {
-        dbg = ctx->ws<unsigned long long>(WS_STATS + 40, (size_t)(waves1 + 256) * 16);
+        dbg = ctx->ws<unsigned long long>(WS_DEBUG, (size_t)(waves1 + 256) * 16);
         HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 256) * 16, st));
         a.dbg = dbg;
     }
@@ -1181,59 +1456,82 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     HIP_TRY(hipEventRecord(ctx->ev[4], st));
     int n_unres = 0;
     if (n_defer > 0) {
-        // phase 2: heavy keys, one workgroup each, parallel reachable-set BFS
+        // Heavy keys: two exact searches race per key and the first to settle
+        // it writes its verdict (emit_verdict), the other abandons it.
+        //  - the workgroup BFS (stream st) settles keys with no reachable
+        //    terminal configuration (invalid) within the budget;
+        //  - the sequential search with the full budget (aux stream) settles
+        //    every key, and alone decides valid / :unknown.
+        int32_t *claim = ctx->ws<int32_t>(WS_CLAIM, K);
+        HIP_TRY(hipMemsetAsync(claim, 0, (size_t)K * sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(q + 3, 0, sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(q + 6, 0, sizeof(int32_t), st));
+        HIP_TRY(hipEventRecord(ctx->ev[6], st));
+
         uint32_t set_cap = 1u << 12;
         while ((int64_t)set_cap < 2 * budget && set_cap < (1u << 30)) set_cap <<= 1;
         const uint32_t q_cap = (uint32_t)std::min<int64_t>(budget + 64, (int64_t)1 << 30);
         const int wg2 = std::min(n_defer, 128);
         uint64_t *bset = ctx->ws<uint64_t>(WS_BFS_SET, (size_t)wg2 * set_cap);
-        uint64_t *bq = ctx->ws<uint64_t>(WS_BFS_Q, (size_t)wg2 * 2 * q_cap);
-        char *bscr = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)wg2 * scr_bytes);
+        uint64_t *bq = ctx->ws<uint64_t>(WS_BFS_Q, (size_t)wg2 * 4 * q_cap);
+        char *bscr = ctx->ws<char>(WS_SCRATCH_BFS, (size_t)wg2 * scr_bytes);
         int32_t *unres = ctx->ws<int32_t>(WS_BFS_META, n_defer + 1);
-        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
-        HIP_TRY(hipMemsetAsync(q + 3, 0, sizeof(int32_t), st));
         BfsArgs c{};
         c.src = KeySrc{rec, pair, off, rB, viol, rank, q + 2};
         c.list = defer; c.n_list = n_defer; c.queue = q; c.out = out_dev;
         c.unres_list = unres; c.unres_count = q + 3;
-        c.set = bset; c.set_cap = set_cap; c.q = bq; c.q_cap = q_cap;
+        c.gset = bset; c.gset_cap = set_cap; c.pend = bq; c.front = bq + (size_t)wg2 * 2 * q_cap;
+        c.q_cap = q_cap;
         c.scratch = bscr; c.scratch_bytes = scr_bytes; c.budget = budget;
         c.init_state = init_state; c.states_ok = (vmax - vmin + 2) < 4096 ? 1 : 0;
-        c.dbg = dbg;
+        c.dbg = dbg; c.claim = claim;
+        static bool lds_attr = false;
+        if (!lds_attr) {
+            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_bfs, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        BFS_LDS_BYTES));
+            lds_attr = true;
+        }
+
+        uint32_t cap2 = 1u << 16;
+        while ((int64_t)cap2 < 2 * budget && cap2 < (1u << 30)) cap2 <<= 1;
+        const int waves2 = std::min(n_defer, 128);
+        // generation-tagged: zeroed once when allocated (and on wrap), not per call
+        const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;
+        uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
+        if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
+        Frame *stack2 = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap);
+        char *scr2 = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes);
+        DfsArgs b = a;
+        b.list = defer; b.n_list = n_defer; b.queue = q + 6; b.defer = 0;
+        b.memo = memo2; b.memo_cap = cap2; b.stack = stack2; b.scratch = scr2; b.budget = budget;
+        b.gen_base = ctx->gen_base + (uint32_t)K + 1;
+        b.dbg = nullptr; b.claim = claim;
+
+        // fork: the BFS on st, the sequential search on the aux stream
+        HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
         k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        n_unres = qh[3];
+        HIP_TRY(hipEventRecord(ctx->ev[5], st));
+        k_lin_dfs<<<waves2, 64, LDS_BYTES, ctx->aux>>>(b);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
+        HIP_TRY(hipStreamWaitEvent(st, ctx->ev[7], 0));
         if (dbg2) {
+            HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            n_unres = qh[3];
             std::vector<unsigned long long> h((size_t)wg2 * 16);
             HIP_TRY(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
             for (int w = 0; w < wg2; w++)
                 if (h[16 * w + 4])
-                    fprintf(stderr, "[jh-bfs] wg %d keys=%llu cycles=%llu levels=%llu configs=%llu inserted=%llu cyc/level=%.0f\n",
-                            w, h[16 * w + 4], h[16 * w], h[16 * w + 1], h[16 * w + 2], h[16 * w + 3],
+                    fprintf(stderr, "[jh-bfs] wg %d keys=%llu cycles=%llu rounds=%llu configs=%llu cyc/round=%.0f\n",
+                            w, h[16 * w + 4], h[16 * w], h[16 * w + 1], h[16 * w + 3],
                             (double)h[16 * w] / std::max(1ULL, h[16 * w + 1]));
         }
-    }
-    HIP_TRY(hipEventRecord(ctx->ev[5], st));
-    if (n_unres > 0) {
-        // phase 3: keys BFS could not settle (a terminal configuration is
-        // reachable, or the set outgrew the budget): the sequential search
-        // with the full budget defines their verdict and explored count
-        uint32_t cap2 = 1u << 16;
-        while ((int64_t)cap2 < 2 * budget && cap2 < (1u << 30)) cap2 <<= 1;
-        const int waves2 = std::min(n_unres, 64);
-        uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2);
-        Frame *stack2 = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap);
-        char *scr2 = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)std::max(waves2, 1) * scr_bytes);
-        HIP_TRY(hipMemsetAsync(memo2, 0, (size_t)waves2 * cap2 * 16, st));
-        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
-        DfsArgs b = a;
-        b.list = ctx->ws<int32_t>(WS_BFS_META, 1); b.n_list = n_unres; b.memo = memo2; b.memo_cap = cap2;
-        b.stack = stack2; b.scratch = scr2; b.budget = budget; b.defer = 0;
-        b.gen_base = ctx->gen_base + (uint32_t)K + 1;
-        k_lin_dfs<<<waves2, 64, LDS_BYTES, st>>>(b);
-        HIP_TRY(hipGetLastError());
+    } else {
+        HIP_TRY(hipEventRecord(ctx->ev[5], st));
+        HIP_TRY(hipEventRecord(ctx->ev[7], st));
     }
     HIP_TRY(hipEventRecord(ctx->ev[2], st));
     ctx->gen_base += gen_span;
@@ -1265,9 +1563,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             HIP_TRY(hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[4]));
             HIP_TRY(hipEventElapsedTime(&c, ctx->ev[4], ctx->ev[2]));
             float d = 0;
-            HIP_TRY(hipEventElapsedTime(&d, ctx->ev[5], ctx->ev[2]));
+            HIP_TRY(hipEventElapsedTime(&d, ctx->ev[4], ctx->ev[7]));
             HIP_TRY(hipEventElapsedTime(&c, ctx->ev[4], ctx->ev[5]));
-            fprintf(stderr, "[jh] keys=%lld prep=%.3f ms phase1=%.3f ms (waves %d) deferred=%d bfs=%.3f ms unresolved=%d deep=%.3f ms\n",
+            fprintf(stderr, "[jh] keys=%lld prep=%.3f ms phase1=%.3f ms (waves %d) deferred=%d bfs=%.3f ms (gave up %d) seq=%.3f ms\n",
                     (long long)K, a, b, waves1, n_defer, c, n_unres, d);
         }
     }

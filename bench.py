@@ -35,7 +35,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--keys", type=int, default=10000)
     ap.add_argument("--ops-per-key", type=int, default=500)
-    ap.add_argument("--cpu-sample-keys", type=int, default=1000)
+    ap.add_argument("--cpu-sample-keys", type=int, default=10000,
+                    help="keys of the rank-0 history timed on the CPU (default: the whole C3 workload)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     return ap.parse_args()
@@ -162,7 +163,7 @@ def main():
                        "p_invalid": 0.01, "budget": A.DEFAULT_BUDGET,
                        "explored_per_step": int(s.explored), "invalid_keys": int(s.n_invalid),
                        "unknown_keys": int(s.n_unknown), "device_ms": float(np.mean(dev_ms))},
-            "roofline": {"bound": "hbm", "kernel": "k_lin_dfs", "achieved": achieved,
+            "roofline": {"bound": "hbm", "kernel": "k_lin_dfs (phase 1: every key, quick budget)", "achieved": achieved,
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                          "traffic": None, "kernel_ms": dfs_avg * 1e3,
                          "alg_bytes": alg_bytes},

@@ -126,9 +126,9 @@ typedef struct jh_summary {
     int64_t first_fail_entry;  /* min fail_entry over invalid keys, or -1 */
     int64_t n_keys;            /* keys checked (keys present in the history) */
     int64_t explored;          /* sum of memo inserts */
-    int64_t memo_probes;       /* memo slots read by the search (roofline bytes) */
+    int64_t memo_probes;       /* memo slots read by the phase-1 search kernel k_lin_dfs (roofline bytes) */
     double  device_ms;         /* device time of the check (HIP events) */
-    double  dfs_ms;            /* of which the WGL search kernel */
+    double  dfs_ms;            /* of which the phase-1 search kernel k_lin_dfs (all keys, quick budget) */
 } jh_summary;
 
 typedef struct jh_ctx jh_ctx;

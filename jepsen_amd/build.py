@@ -22,6 +22,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 HIPFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
             "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+HIPFLAGS += os.environ.get("JH_HIPFLAGS", "").split()   # e.g. -DJH_STEP_PROF (profiling builds)
 
 
 def _newer(target, deps):

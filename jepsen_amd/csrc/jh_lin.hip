@@ -34,7 +34,15 @@ constexpr int LDS_TBL = 5120;             // per-wave compact op + delta tables
 constexpr int MEMO_SLOTS = 1024;          // per-wave LDS memo (hot layers t >= theta)
 constexpr int MEMO_EVICT = 512;           // evict at load factor 1/2
 constexpr int RING = 64;                  // per-wave LDS stack ring (frames)
-constexpr int LDS_BYTES = LDS_TBL + MEMO_SLOTS * 8 + RING * 16;   // 14 KB -> 11 waves/CU
+#ifdef JH_STEP_PROF
+#define PROF_MARK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(acc, a, b) acc += (b) - (a)
+#else
+#define PROF_MARK(v)
+#define PROF_ADD(acc, a, b)
+#endif
+constexpr int BLOOM_BITS = 32768;           // per-wave LDS Bloom filter over the key's memo
+constexpr int LDS_BYTES = LDS_TBL + MEMO_SLOTS * 8 + RING * 16 + BLOOM_BITS / 8;   // 18.5 KB -> 8 waves/CU
 constexpr int STATE_BITS = 20, T_BITS = 20, GEN_BITS = 24;
 constexpr uint32_t STATE_MASK = (1u << STATE_BITS) - 1, T_MASK = (1u << T_BITS) - 1;
 
@@ -252,6 +260,10 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
     return ((uint64_t)hi << 32) | lo;
 }
 __device__ __forceinline__ int readlane(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+// whole-wave lane shifts on the VALU (DPP), no LDS round trip:
+// lane i <- lane i+1 (lane 63 keeps its value) / lane i <- lane i-1 (lane 0 keeps)
+__device__ __forceinline__ int wave_shl1(int x) { return __builtin_amdgcn_update_dpp(x, x, 0x130, 0xF, 0xF, false); }
+__device__ __forceinline__ int wave_shr1(int x) { return __builtin_amdgcn_update_dpp(x, x, 0x138, 0xF, 0xF, false); }
 
 __device__ __forceinline__ uint64_t memo_hash(uint32_t t, uint32_t s, uint64_t m) {
     return jh_mix64(m * 0x9E3779B97F4A7C15ULL ^ jh_mix64(((uint64_t)t << 32) | s));
@@ -493,7 +505,7 @@ __device__ long long ret_row(const KeySrc &S, const KeyInfo &K, uint32_t t, int 
 // gen-tagged HBM table. When the LDS table reaches half load, the layers
 // farthest below the current one move to HBM in one bulk pass; a lookup goes
 // to LDS or HBM by the child's t alone, so the memo stays an exact set.
-// Stack: an LDS ring of the top RING frames, written through to HBM.
+// Stack: an LDS ring of the top RING frames; overflow spills to HBM in halves.
 struct OpC {
     uint32_t vv;      // v1 | v2 << 16 (interned states, < 2^16)
     uint32_t fa;      // f | a << 2 | (rr + 1) << 16   (a < 2^14, rr + 1 < 2^16)
@@ -581,6 +593,25 @@ __device__ __forceinline__ uint32_t lds_hash(uint64_t k) {
     return (h >> 13) & (MEMO_SLOTS - 1);
 }
 
+// Bloom filter bit positions of a configuration (any injective-enough
+// packing will do: a collision only costs an HBM probe, never a wrong answer)
+__device__ __forceinline__ uint32_t bloom_hash(uint64_t k) {
+    uint32_t h = (uint32_t)k * 0x85EBCA77u ^ (uint32_t)(k >> 32) * 0xC2B2AE3Du;
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    return h;
+}
+__device__ __forceinline__ bool bloom_test(const uint32_t *bloom, uint32_t h) {
+    const uint32_t p1 = h & (BLOOM_BITS - 1), p2 = (h >> 17) & (BLOOM_BITS - 1);
+    return ((bloom[p1 >> 5] >> (p1 & 31)) & (bloom[p2 >> 5] >> (p2 & 31)) & 1u) != 0;
+}
+__device__ __forceinline__ void bloom_set(uint32_t *bloom, uint32_t h) {
+    const uint32_t p1 = h & (BLOOM_BITS - 1), p2 = (h >> 17) & (BLOOM_BITS - 1);
+    atomicOr(&bloom[p1 >> 5], 1u << (p1 & 31));
+    atomicOr(&bloom[p2 >> 5], 1u << (p2 & 31));
+}
+
 // Evict LDS memo layers into this wave's HBM table (out of line: it runs
 // once per MEMO_EVICT inserts). theta is chosen so that the layers kept in
 // LDS (t >= theta, at most a few below the current layer t_cur) fill at most
@@ -589,7 +620,7 @@ __device__ __forceinline__ uint32_t lds_hash(uint64_t k) {
 // scratch and the LDS table is rebuilt. Returns theta << 32 | kept.
 __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint64_t *memo, uint64_t *stage,
                                             uint32_t cap_mask, uint32_t gen, uint32_t t_cur,
-                                            int lane) {
+                                            uint32_t theta_old, int lane) {
     const uint64_t gen_hi = (uint64_t)gen << 40;
     // histogram of entries by distance below t_cur (entries at or above it: bin 0)
     int bins = 0;                                  // lane b < 16 holds bin b
@@ -620,6 +651,8 @@ __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint64_t *memo, uin
         th2 = t_cur > (uint32_t)dstar ? t_cur - (uint32_t)dstar : 0u;
         if (dstar == 15) th2 = t_cur - min(t_cur, 15u);
     }
+    // theta never moves down: layers below the old theta may sit in HBM
+    th2 = max(th2, theta_old);
     wave_sync();
 #pragma unroll 1
     for (int r = 0; r < MEMO_SLOTS / 64; r++) lmemo[lane + 64 * r] = 0;
@@ -714,24 +747,30 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
     const uint64_t gen_hi = (uint64_t)gen << 40;
     uint64_t *lmemo = (uint64_t *)(jh_lds + LDS_TBL);
     Frame *ring = (Frame *)(jh_lds + LDS_TBL + MEMO_SLOTS * 8);
+    uint32_t *bloom = (uint32_t *)(jh_lds + LDS_TBL + MEMO_SLOTS * 8 + RING * 16);
     uint32_t theta = lds_memo ? 0u : 0xFFFFFFFFu;
     int lcount = 0;
     for (int i = lane; i < MEMO_SLOTS; i += 64) lmemo[i] = 0;
+    for (int i = lane; i < BLOOM_BITS / 32; i += 64) bloom[i] = 0;
     uint32_t t = 0, tmax = 0, depth = 0, ring_lo = 0;
     uint64_t mask = 0;
     int s = A.init_state, start = 0;
     int verdict = -1;
-    long long ins = 0;
-    unsigned long long n_steps = 0, n_evict = 0, n_reload = 0;
+    uint32_t ins = 0;
+    const uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
+    uint32_t n_steps = 0, n_evict = 0, n_reload = 0;
     // the window of layer t in lane registers: f (3 = no member), v1|v2
-    int w = (int)(delta[0] >> 22), P = w;
-    uint32_t r = (delta[0] >> 16) & 63;            // position of RET[t]
+#define DELTA(u) delta[(u)]
+    int w = (int)(DELTA(0) >> 22), P = w;
+    uint32_t r = (DELTA(0) >> 16) & 63;             // position of RET[t]
     int lf = 3;
     uint32_t lv = 0;
     if (lane < w) { const OpC o = ops[lane]; lf = (int)(o.fa & 3); lv = o.vv; }
     wave_sync();
+    unsigned long long pc_lift = 0, pc_probe = 0, pc_ins = 0, pc_fwd = 0, pc_pop = 0;
     while (true) {
         n_steps++;
+        PROF_MARK(q0);
         if (A.claim && (n_steps & 1023) == 0) {
             int c = 0;
             if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -753,64 +792,89 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
                 nm = drop_bit(nm, ru);
                 u++;
                 if (u >= n_ok) { nm = 0; break; }
-                ru = (delta[u] >> 16) & 63;
+                ru = (DELTA(u) >> 16) & 63;
                 if (!((nm >> ru) & 1)) break;
             }
             if (lane == (int)r) { ct = u; cm = nm; }
         }
         // memo probes, all candidates at once (= the sequential scan, since
         // nothing is inserted until the first new child is chosen)
+        PROF_MARK(q1);
+        PROF_ADD(pc_lift, q0, q1);
         const uint64_t lkey = ((uint64_t)ct << 48) | ((uint64_t)(uint32_t)s2 << 40) | cm;
-        const bool go_lds = cand && ct >= theta;
-        bool absent = false;
-        uint32_t slot = lds_hash(lkey);
-        if (go_lds) {
-            uint64_t e = lmemo[slot];
+        // LDS memo (lds_memo mode): every recent insert, and every entry of
+        // layers >= theta; older entries may have moved to the HBM table.
+        bool absent = false, probed = false;
+        uint32_t lslot = lds_hash(lkey), hslot = 0;
+        bool go_hbm = cand;
+        if (lds_memo && cand) {
+            uint64_t e = lmemo[lslot];
             while (e != 0 && e != lkey) {
-                slot = (slot + 1) & (MEMO_SLOTS - 1);
-                e = lmemo[slot];
+                lslot = (lslot + 1) & (MEMO_SLOTS - 1);
+                e = lmemo[lslot];
             }
-            absent = e == 0;
+            go_hbm = e == 0 && ct < theta;
+            absent = e == 0 && ct >= theta;
         }
-        const bool go_hbm = cand && ct < theta;
+        // HBM-side entries: the Bloom filter of everything inserted for this
+        // key rules most absent children out without an HBM round trip, and
+        // only candidates before the first surely-absent one matter
+        if (ballot(go_hbm)) {
+            if (go_hbm && !bloom_test(bloom, bloom_hash(lkey))) { go_hbm = false; absent = true; }
+            const uint64_t sure = ballot(absent);
+            if (sure) go_hbm = go_hbm && lane < __builtin_ctzll(sure);
+        }
         if (ballot(go_hbm) && go_hbm) {
             const uint64_t rr = hbm_probe(memo, cap_mask, gen, ct, (uint32_t)s2, cm, my_probes);
-            slot = (uint32_t)rr;
+            hslot = (uint32_t)rr;
             absent = (rr >> 32) != 0;
+            probed = true;
         }
         const uint64_t bn = ballot(absent);
+        PROF_MARK(q2);
+        PROF_ADD(pc_probe, q1, q2);
         if (bn) {
-            if (ins >= A.budget) { verdict = JH_UNKNOWN; break; }
+            if (ins >= budget) { verdict = JH_UNKNOWN; break; }
             const int i = __builtin_ctzll(bn);
-            const bool to_lds = (ballot(go_lds) >> i) & 1;
+            // lds_memo: new entries always go to LDS (evicted by layer later);
+            // else straight to the HBM table at the end of the child's chain
+            const bool to_lds = lds_memo;
+            if (!to_lds && !((ballot(probed) >> i) & 1) && lane == i)
+                hslot = (uint32_t)hbm_probe(memo, cap_mask, gen, ct, (uint32_t)s2, cm, my_probes);
             if (lane == i) {
-                if (to_lds) lmemo[slot] = lkey;
+                bloom_set(bloom, bloom_hash(lkey));
+                if (to_lds) lmemo[lslot] = lkey;
                 else {
-                    __hip_atomic_store(&memo[2 * (size_t)slot], cm, __ATOMIC_RELAXED,
+                    __hip_atomic_store(&memo[2 * (size_t)hslot], cm, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&memo[2 * (size_t)slot + 1],
+                    __hip_atomic_store(&memo[2 * (size_t)hslot + 1],
                                        gen_hi | ((uint64_t)ct << 20) | (uint32_t)s2,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             ins++;
-            // push the parent onto the LDS ring (written through to HBM)
+            // push the parent onto the LDS ring; a full ring spills its
+            // oldest half to the HBM stack in one coalesced store
+            if (depth - ring_lo == RING) {
+                if (lane < RING / 2) stack[ring_lo + lane] = ring[(ring_lo + lane) & (RING - 1)];
+                ring_lo += RING / 2;
+            }
             if (lane == 0) {
                 Frame fr; fr.mask = mask; fr.t_i = (t << 6) | (uint32_t)i; fr.s = s;
                 ring[depth & (RING - 1)] = fr;
-                stack[depth] = fr;
             }
             depth++;
-            if (depth - ring_lo > RING) ring_lo = depth - RING;
             const uint32_t nt = (uint32_t)readlane((int)ct, i);
             mask = ((uint64_t)(uint32_t)readlane((int)(uint32_t)(cm >> 32), i) << 32) |
                    (uint32_t)readlane((int)(uint32_t)cm, i);
             s = readlane(s2, i);
             start = 0;
+            PROF_MARK(q3);
+            PROF_ADD(pc_ins, q2, q3);
             if (to_lds) {
                 if (++lcount >= MEMO_EVICT) {
                     n_evict++;
-                    const uint64_t er = memo_evict(lmemo, memo, stage, cap_mask, gen, nt, lane);
+                    const uint64_t er = memo_evict(lmemo, memo, stage, cap_mask, gen, nt, theta, lane);
                     lcount = (int)(uint32_t)er;
                     theta = (uint32_t)(er >> 32);
                 }
@@ -822,12 +886,13 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
                 if (nt >= n_ok) { t = nt; tmax = max(tmax, t); verdict = JH_VALID; break; }
                 // move the window forward layer by layer
                 for (uint32_t u = t; u < nt; u++) {
-                    const uint32_t ru = u == t ? r : (delta[u] >> 16) & 63;
-                    const int src = lane + (lane >= (int)ru ? 1 : 0);
-                    lf = __shfl(lf, src & 63);
-                    lv = (uint32_t)__shfl((int)lv, src & 63);
+                    const uint32_t ru = u == t ? r : (DELTA(u) >> 16) & 63;
+                    {
+                        const int sf = wave_shl1(lf), sv = wave_shl1((int)lv);
+                        if (lane >= (int)ru) { lf = sf; lv = (uint32_t)sv; }
+                    }
                     w--;
-                    const int c = (int)(delta[u + 1] >> 22);
+                    const int c = (int)(DELTA(u + 1) >> 22);
                     const int dst = lane - w;
                     if (dst >= 0 && dst < c) { const OpC o = ops[P + dst]; lf = (int)(o.fa & 3); lv = o.vv; }
                     if (lane >= w + c) lf = 3;
@@ -835,43 +900,56 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
                 }
                 t = nt;
                 tmax = max(tmax, t);
-                r = (delta[t] >> 16) & 63;
+                r = (DELTA(t) >> 16) & 63;
                 n_reload++;
             }
+            PROF_MARK(q4);
+            PROF_ADD(pc_fwd, q3, q4);
         } else {
             if (depth == 0) { verdict = JH_INVALID; break; }
             depth--;
-            Frame fr;
-            if (depth >= ring_lo) fr = ring[depth & (RING - 1)];
-            else {
+            if (depth < ring_lo) {
+                // ring empty: refill the half below from the HBM stack
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                fr = stack[depth];
-                ring_lo = depth;
+                const uint32_t lo = depth + 1 >= RING / 2 ? depth + 1 - RING / 2 : 0;
+                if (lane < (int)(depth + 1 - lo)) ring[(lo + lane) & (RING - 1)] = stack[lo + lane];
+                ring_lo = lo;
+                wave_sync();
             }
+            const Frame fr = ring[depth & (RING - 1)];
             const uint32_t pt = fr.t_i >> 6;
             mask = fr.mask; s = fr.s; start = (int)(fr.t_i & 63) + 1;
             if (pt != t) {
                 // move the window back: drop appended ops, re-insert RETs
                 for (uint32_t u = t; u > pt; u--) {
-                    const int c = (int)(delta[u] >> 22);
+                    const int c = (int)(DELTA(u) >> 22);
                     w -= c; P -= c;
                     if (lane >= w) lf = 3;
-                    const uint32_t d = delta[u - 1];
+                    const uint32_t d = DELTA(u - 1);
                     const int ru = (int)((d >> 16) & 63);
-                    const int src = lane - (lane > ru ? 1 : 0);
-                    lf = __shfl(lf, src & 63);
-                    lv = (uint32_t)__shfl((int)lv, src & 63);
+                    {
+                        const int sf = wave_shr1(lf), sv = wave_shr1((int)lv);
+                        if (lane > ru) { lf = sf; lv = (uint32_t)sv; }
+                    }
                     if (lane == ru) { const OpC o = ops[d & 0xFFFF]; lf = (int)(o.fa & 3); lv = o.vv; }
                     w++;
                 }
                 t = pt;
-                r = (delta[t] >> 16) & 63;
+                r = (DELTA(t) >> 16) & 63;
                 n_reload++;
             }
+            PROF_MARK(q5);
+            PROF_ADD(pc_pop, q2, q5);
         }
         if (depth >= A.stack_cap) { verdict = JH_UNKNOWN; if (lane == 0) atomicOr(A.flags, 4); break; }
     }
+#ifdef JH_STEP_PROF
+    if (A.dbg && lane == 0) {
+        unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
+        d[10] += pc_lift; d[11] += pc_probe; d[12] += pc_ins; d[13] += pc_fwd; d[14] += pc_pop;
+    }
+#endif
     inserts = ins;
     tmax_out = tmax;
     if (A.dbg && lane == 0) {
@@ -919,7 +997,7 @@ __device__ void dfs_key(const DfsArgs &A, const KeySrc &src, const KeyInfo &K, c
     if (lane == 0) emit_verdict(A.out, A.claim, key, v);
 }
 
-__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
+__device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     const int lane = threadIdx.x;
     uint64_t *memo = A.memo + (size_t)blockIdx.x * A.memo_cap * 2;
     Frame *stack = A.stack + (size_t)blockIdx.x * A.stack_cap;
@@ -961,9 +1039,15 @@ __global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
         }
     }
     if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 9] = __builtin_amdgcn_s_memtime() - t_begin;
+    if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 15] = my_probes;
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
 }
+
+// phase 1: every key under the quick budget
+__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) { lin_dfs_waves(A); }
+// heavy keys: the full-budget sequential search racing k_lin_bfs
+__global__ void __launch_bounds__(64) k_lin_seq(DfsArgs A) { lin_dfs_waves(A); }
 
 // ---------------------------------------------------------------------------
 // Heavy keys: parallel breadth-first enumeration of the reachable
@@ -1412,11 +1496,11 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     Frame *stack = ctx->ws<Frame>(WS_STACK, (size_t)waves1 * stack_cap);
     const uint64_t scr_bytes = (((uint64_t)smax * 84 + 4096 + MEMO_SLOTS * 8) + 255) & ~255ULL;
     char *scr = ctx->ws<char>(WS_SCRATCH, (size_t)waves1 * scr_bytes);
-    int32_t *q = ctx->ws<int32_t>(WS_QUEUE, 8);
+    int32_t *q = ctx->ws<int32_t>(WS_QUEUE, 16);
     int32_t *list = ctx->ws<int32_t>(WS_STATS, K);
     int32_t *defer = ctx->ws<int32_t>(WS_DEFER, K + 1);
     unsigned long long *probes = (unsigned long long *)(q + 4);
-    HIP_TRY(hipMemsetAsync(q, 0, 8 * sizeof(int32_t), st));
+    HIP_TRY(hipMemsetAsync(q, 0, 16 * sizeof(int32_t), st));
     k_iota<<<grid_for(K, 256), 256, 0, st>>>(list, K);
 
     DfsArgs a{};
@@ -1431,14 +1515,15 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const bool dbg2 = dbgenv && atoi(dbgenv) >= 2;
     unsigned long long *dbg = nullptr;
     if (dbg2) {
-        dbg = ctx->ws<unsigned long long>(WS_DEBUG, (size_t)(waves1 + 256) * 16);
-        HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 256) * 16, st));
+        dbg = ctx->ws<unsigned long long>(WS_DEBUG, (size_t)(waves1 + 512) * 16);
+        HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 512) * 16, st));
         a.dbg = dbg;
     }
     HIP_TRY(hipEventRecord(ctx->ev[1], st));
     k_lin_dfs<<<waves1, 64, LDS_BYTES, st>>>(a);
     HIP_TRY(hipGetLastError());
-    int32_t qh[8];
+    HIP_TRY(hipEventRecord(ctx->ev[4], st));
+    int32_t qh[16];
     HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const int n_defer = qh[1];
@@ -1451,9 +1536,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 waves1, tot[3], (double)tot[0] / std::max(1ULL, tot[3]), (double)tot[1] / std::max(1ULL, tot[3]),
                 (double)tot[2] / std::max(1ULL, tot[3]), tot[4], tot[5], tot[6], tot[7],
                 (double)tot[2] / std::max(1ULL, tot[4]), tot[8], (double)tot[9] / waves1, mx9);
-        HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 256) * 16, st));
+        HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 512) * 16, st));
     }
-    HIP_TRY(hipEventRecord(ctx->ev[4], st));
     int n_unres = 0;
     if (n_defer > 0) {
         // Heavy keys: two exact searches race per key and the first to settle
@@ -1506,14 +1590,15 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         b.list = defer; b.n_list = n_defer; b.queue = q + 6; b.defer = 0;
         b.memo = memo2; b.memo_cap = cap2; b.stack = stack2; b.scratch = scr2; b.budget = budget;
         b.gen_base = ctx->gen_base + (uint32_t)K + 1;
-        b.dbg = nullptr; b.claim = claim;
+        b.dbg = dbg ? dbg + 16 * 256 : nullptr; b.claim = claim;
+        b.probes = (unsigned long long *)(q + 8);
 
         // fork: the BFS on st, the sequential search on the aux stream
         HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
         k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        k_lin_dfs<<<waves2, 64, LDS_BYTES, ctx->aux>>>(b);
+        k_lin_seq<<<waves2, 64, LDS_BYTES, ctx->aux>>>(b);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
         HIP_TRY(hipStreamWaitEvent(st, ctx->ev[7], 0));
@@ -1528,6 +1613,16 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                     fprintf(stderr, "[jh-bfs] wg %d keys=%llu cycles=%llu rounds=%llu configs=%llu cyc/round=%.0f\n",
                             w, h[16 * w + 4], h[16 * w], h[16 * w + 1], h[16 * w + 3],
                             (double)h[16 * w] / std::max(1ULL, h[16 * w + 1]));
+            std::vector<unsigned long long> g((size_t)waves2 * 16);
+            HIP_TRY(hipMemcpy(g.data(), dbg + 16 * 256, g.size() * 8, hipMemcpyDeviceToHost));
+            for (int w = 0; w < waves2; w++)
+                if (g[16 * w + 4] > 0)
+                    fprintf(stderr, "[jh-seq] wave %d keys=%llu steps=%llu inserts=%llu evict=%llu reload=%llu search=%llu cyc/step=%.0f busy=%llu hbm-probes=%llu | lift %.0f probe %.0f ins %.0f fwd %.0f pop %.0f cyc/step\n",
+                            w, g[16 * w + 3], g[16 * w + 4], g[16 * w + 5], g[16 * w + 6], g[16 * w + 7], g[16 * w + 2],
+                            (double)g[16 * w + 2] / std::max(1ULL, g[16 * w + 4]), g[16 * w + 9], g[16 * w + 15],
+                            (double)g[16 * w + 10] / std::max(1ULL, g[16 * w + 4]), (double)g[16 * w + 11] / std::max(1ULL, g[16 * w + 4]),
+                            (double)g[16 * w + 12] / std::max(1ULL, g[16 * w + 4]), (double)g[16 * w + 13] / std::max(1ULL, g[16 * w + 4]),
+                            (double)g[16 * w + 14] / std::max(1ULL, g[16 * w + 4]));
         }
     } else {
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
@@ -1555,7 +1650,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         sum->memo_probes = (int64_t)(((uint64_t)(uint32_t)qh[5] << 32) | (uint32_t)qh[4]);
         float ms = 0, ms_dfs = 0;
         HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]));
-        HIP_TRY(hipEventElapsedTime(&ms_dfs, ctx->ev[1], ctx->ev[2]));
+        HIP_TRY(hipEventElapsedTime(&ms_dfs, ctx->ev[1], ctx->ev[4]));
         sum->device_ms = ms; sum->dfs_ms = ms_dfs;
         if (getenv("JH_DEBUG")) {
             float a = 0, b = 0, c = 0;

@@ -1,4 +1,4 @@
-# bench with in-kernel cycle accounting (JH_DEBUG=2)
+# bench with in-kernel cycle accounting only
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 JH_DEBUG=2 timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu --no-parity > gpurun_out/bench_dbg.log 2>&1

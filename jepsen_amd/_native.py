@@ -10,7 +10,7 @@ import numpy as np
 from . import _abi as A
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libjh.so")
+LIB_PATH = os.environ.get("JH_LIB") or os.path.join(_HERE, "libjh.so")   # JH_LIB: A/B builds (tools/)
 _lib = None
 _lock = threading.Lock()
 

@@ -30,10 +30,10 @@ namespace {
 constexpr int F_READ = 0, F_WRITE = 1, F_CAS = 2, F_OTHER = 4;
 constexpr int T_INVOKE = 0, T_OK = 1, T_FAIL = 2, T_INFO = 3;
 constexpr uint64_t VIOL_NONE = ~0ULL;
-constexpr int LDS_TBL = 5120;             // per-wave compact op + delta tables
-constexpr int MEMO_SLOTS = 1024;          // per-wave LDS memo (hot layers t >= theta)
-constexpr int MEMO_EVICT = 512;           // evict at load factor 1/2
-constexpr int RING = 64;                  // per-wave LDS stack ring (frames)
+#ifndef JH_LDS_TBL
+#define JH_LDS_TBL 0
+#endif
+constexpr int LDS_TBL = JH_LDS_TBL;       // per-wave op + layer tables in LDS (0: global, L2-resident)
 #ifdef JH_STEP_PROF
 #define PROF_MARK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(acc, a, b) acc += (b) - (a)
@@ -41,8 +41,26 @@ constexpr int RING = 64;                  // per-wave LDS stack ring (frames)
 #define PROF_MARK(v)
 #define PROF_ADD(acc, a, b)
 #endif
-constexpr int BLOOM_BITS = 32768;           // per-wave LDS Bloom filter over the key's memo
-constexpr int LDS_BYTES = LDS_TBL + MEMO_SLOTS * 8 + RING * 16 + BLOOM_BITS / 8;   // 18.5 KB -> 8 waves/CU
+#ifdef JH_DFS_STATS
+#define DFS_STAT(x) x
+#else
+#define DFS_STAT(x)
+#endif
+// Per-wave LDS of the DFS: [tables LDS_TBL][memo BKT x 4 x 8 B][Bloom][bucket fill bytes]
+template <int LG_BKT, int LG_BLOOM>
+struct MemoCfg {
+    static constexpr int LG = LG_BKT;
+    static constexpr int BKT = 1 << LG_BKT;           // 4-slot buckets (hot layers t >= theta)
+    static constexpr int SLOTS = BKT * 4;
+    static constexpr int EVICT = SLOTS * 5 / 8;        // evict at load factor 5/8
+    static constexpr int BLOOM = 1 << LG_BLOOM;       // bits, over the HBM-resident entries
+    static constexpr int OFF_MEMO = LDS_TBL;
+    static constexpr int OFF_BLOOM = OFF_MEMO + SLOTS * 8;
+    static constexpr int OFF_CNT = OFF_BLOOM + BLOOM / 8;
+    static constexpr int LDS = OFF_CNT + BKT;
+};
+using MemoQ = MemoCfg<8, 14>;    // phase 1: 8 KB memo + 2 KB Bloom = 10.25 KB -> 15 waves/CU
+using MemoH = MemoCfg<12, 16>;   // heavy keys: 128 KB memo + 8 KB Bloom = 140 KB -> 1 wave/CU
 constexpr int STATE_BITS = 20, T_BITS = 20, GEN_BITS = 24;
 constexpr uint32_t STATE_MASK = (1u << STATE_BITS) - 1, T_MASK = (1u << T_BITS) - 1;
 
@@ -63,8 +81,10 @@ struct Op {
 
 struct Frame {        // DFS stack frame: the parent configuration + taken candidate
     uint64_t mask;
+    uint64_t rest;    // candidates after i whose child was not known present at the push
     uint32_t t_i;     // t << 6 | i
     int32_t s;
+    uint32_t pad[2];
 };
 
 struct RangeOut {
@@ -488,40 +508,57 @@ __device__ long long ret_row(const KeySrc &S, const KeyInfo &K, uint32_t t, int 
 // ---------------------------------------------------------------------------
 // The WGL depth-first search, one key per wave.
 //
-// Compact per-key tables (the search needs no explicit window table):
-//   OpC ops[j]   8 bytes: v1 | v2 << 16 ; f | a << 2 | (rr + 1) << 16
-//   delta[t]     ret_op | r_t << 16 | c_t << 22
-// where r_t is the position of RET[t] (the op whose ok return defines t) in
-// W(t), and c_t the number of ops appended to the window on entering layer t
-// (c_0 = |W(0)|). Since W(t+1) = W(t) - {RET[t]} + the next c_{t+1} ops in
-// call order, the window lives in lane registers (lane i = member i) and
-// moves between layers with lane shuffles. Lifting RET[t] removes bit r_t
-// from the mask and keeps removing while the next layer's RET op is already
-// linearized: the canonical compaction of orc_wgl_canonical
-// (oracle/jh_oracle.c) done on the mask directly.
+// One wave alone issues roughly one instruction every 4 cycles, so a DFS
+// step costs what its instruction count says; everything below is shaped to
+// keep the common step short (no per-step divergence, scalar bookkeeping,
+// one LDS round trip).
 //
-// Memo: every configuration with t >= theta lives in the wave's LDS table
-// (8-byte keys t:16|state:8|mask:40); every one with t < theta in the wave's
-// gen-tagged HBM table. When the LDS table reaches half load, the layers
-// farthest below the current one move to HBM in one bulk pass; a lookup goes
-// to LDS or HBM by the child's t alone, so the memo stays an exact set.
-// Stack: an LDS ring of the top RING frames; overflow spills to HBM in halves.
+// Compact per-key tables, both read only in 64-entry windows:
+//   OpC ops[j]   rq = req | nv << 16 (req: the state the op needs, RQ_ANY for
+//                a write; nv: the state after it), fa = f | a << 2 | (rr+1) << 16
+//   Lay lay[t]   rq of RET[t] ; r_t | c_t << 6
+// where RET[t] is the op whose ok return defines layer t, r_t its position
+// in the window W(t), and c_t the number of ops appended to the window on
+// entering layer t (c_0 = |W(0)|). W(t+1) = W(t) - {RET[t]} + the next
+// c_{t+1} ops in call order, so the window lives in lane registers (lane i =
+// member i) and moves between layers with DPP lane shifts plus lane writes
+// from two register-resident prefetch windows: the next ops in call order
+// (ops[pb + lane]) and the layer table (lay[tb0 + lane]). Lifting RET[t]
+// removes bit r_t from the mask and keeps removing while the next layer's RET
+// op is already linearized: the canonical compaction of orc_wgl_canonical
+// (oracle/jh_oracle.c) done on the mask directly. The DFS stack's top 64
+// frames live in VGPRs (lane = depth mod 64) and spill to HBM in halves.
+//
+// Memo, LEAN mode (window <= 40, states < 256): 8-byte keys
+// 1:1|t:15|state:8|mask:40 in an LDS table of 4-slot buckets, each key in
+// either of its two buckets (a byte per bucket counts its filled slots).
+// Every configuration with t >= theta lives there; when the table reaches
+// MEMO_EVICT entries the layers farthest below the current one move to the
+// wave's gen-tagged HBM table and theta rises. A child below theta that is not
+// in LDS is looked up in a Bloom filter of the HBM-resident entries and then
+// in HBM. WIDE mode (any window <= 64, states < 0xFFFE): every configuration
+// in the HBM table, behind a Bloom filter of all inserts.
 struct OpC {
-    uint32_t vv;      // v1 | v2 << 16 (interned states, < 2^16)
+    uint32_t rq;      // req | nv << 16
     uint32_t fa;      // f | a << 2 | (rr + 1) << 16   (a < 2^14, rr + 1 < 2^16)
 };
+struct Lay {
+    uint32_t rq;      // RET[t]'s req | nv << 16
+    uint32_t hi;      // r_t | c_t << 6
+};
+constexpr uint32_t RQ_ANY = 0xFFFF, RQ_EMPTY = 0xFFFE;
 constexpr int COMPACT_MAX_OK = 16000;
 
 __device__ __forceinline__ uint64_t tblc_ops_bytes(const KeyInfo &K) { return ((uint64_t)K.n_ops * 8 + 15) & ~15ULL; }
 __device__ __forceinline__ uint64_t tblc_bytes(const KeyInfo &K) {
-    return tblc_ops_bytes(K) + (((uint64_t)K.n_ok * 4 + 15) & ~15ULL);
+    return tblc_ops_bytes(K) + (((uint64_t)K.n_ok * 8 + 15) & ~15ULL);
 }
 
-// Pass 2 + delta sweep. Returns the widest window (> 64: :unknown, window).
+// Pass 2 + layer sweep. Returns the widest window (> 64: :unknown, window).
 template <bool L>
 __device__ int key_fill_c(const KeySrc &S, const KeyInfo &K, int lane, char *tb) {
     OpC *ops = (OpC *)tb;
-    uint32_t *delta = (uint32_t *)(tb + tblc_ops_bytes(K));
+    Lay *lay = (Lay *)(tb + tblc_ops_bytes(K));
     const int n_ops = K.n_ops, n_ok = K.n_ok;
     {
         int nok = 0;
@@ -545,7 +582,10 @@ __device__ int key_fill_c(const KeySrc &S, const KeyInfo &K, int lane, char *tb)
                 }
                 const int a = nok + mbcnt(br);
                 OpC o;
-                o.vv = (uint32_t)v1c | ((uint32_t)v2c << 16);
+                // cas-register step (doc/tutorial/04-checker.md:58-72) as (needs, becomes)
+                o.rq = x.f == F_READ ? ((uint32_t)v1c | ((uint32_t)v1c << 16))
+                     : x.f == F_WRITE ? (RQ_ANY | ((uint32_t)v1c << 16))
+                     : ((uint32_t)v1c | ((uint32_t)v2c << 16));
                 o.fa = (uint32_t)x.f | ((uint32_t)a << 2) | ((uint32_t)(rr + 1) << 16);
                 ops[rk] = o;
             }
@@ -553,82 +593,152 @@ __device__ int key_fill_c(const KeySrc &S, const KeyInfo &K, int lane, char *tb)
         }
     }
     wave_sync();
-    // Sweep the layers with the window as lane-resident op indices.
-    int maxw = 0, w = 0, nxt = 0, m = 0, r_prev = 0;
+    // Sweep the layers with the window as lane-resident ops (fa, rq).
+    int maxw = 0, w = 0, nxt = 0, r_prev = 0;
+    uint32_t mfa = 0, mrq = 0;
     for (int t = 0; t < n_ok; t++) {
         if (t > 0) {                               // drop RET[t-1]
-            const int src = lane + (lane >= r_prev ? 1 : 0);
-            m = __shfl(m, src & 63);
+            const int src = (lane + (lane >= r_prev ? 1 : 0)) & 63;
+            mfa = (uint32_t)__shfl((int)mfa, src); mrq = (uint32_t)__shfl((int)mrq, src);
             w--;
         }
         int c = 0;
         for (;;) {                                 // append ops invoked before R_t
             const int j = nxt + lane;
-            const bool in = j < n_ops && (int)((ops[j].fa >> 2) & 0x3FFF) <= t;
+            OpC oj = {0, 0xFFFFFFFCu};
+            if (j < n_ops) oj = ops[j];
+            const bool in = j < n_ops && (int)((oj.fa >> 2) & 0x3FFF) <= t;
             const int k = __popcll(ballot(in));    // a is non-decreasing: a prefix
+            const int src = (lane - (w + c)) & 63;
+            const uint32_t fam = (uint32_t)__shfl((int)oj.fa, src), rqm = (uint32_t)__shfl((int)oj.rq, src);
             const int dst = lane - (w + c);
-            if (dst >= 0 && dst < k) m = nxt + dst;
+            if (dst >= 0 && dst < k) { mfa = fam; mrq = rqm; }
             c += k; nxt += k;
             if (k < 64) break;
         }
         w += c;
         maxw = max(maxw, w);
-        if (w > 64 || c > 1023) { maxw = max(maxw, 65); break; }
-        const bool is_ret = lane < w && (int)(ops[m].fa >> 16) == t + 1;
+        if (w > 64) { maxw = max(maxw, 65); break; }
+        const bool is_ret = lane < w && (int)(mfa >> 16) == t + 1;
         const uint64_t br = ballot(is_ret);
         const int r = br ? __builtin_ctzll(br) : 0;
-        const int ret_op = readlane(m, r);
-        if (lane == 0) delta[t] = (uint32_t)ret_op | ((uint32_t)r << 16) | ((uint32_t)c << 22);
+        if (lane == r) {
+            Lay e;
+            e.rq = mrq;
+            e.hi = (uint32_t)r | ((uint32_t)c << 6);
+            lay[t] = e;
+        }
         r_prev = r;
     }
     wave_sync();
     return maxw;
 }
 
-// LDS memo slot of an 8-byte key: one 32-bit multiply-xorshift
-__device__ __forceinline__ uint32_t lds_hash(uint64_t k) {
-    uint32_t h = (uint32_t)k * 0x9E3779B1u ^ (uint32_t)(k >> 32) * 0x85EBCA77u;
-    h ^= h >> 15;
-    h *= 0x2C1B3C6Du;
-    return (h >> 13) & (MEMO_SLOTS - 1);
-}
-
-// Bloom filter bit positions of a configuration (any injective-enough
-// packing will do: a collision only costs an HBM probe, never a wrong answer)
-__device__ __forceinline__ uint32_t bloom_hash(uint64_t k) {
-    uint32_t h = (uint32_t)k * 0x85EBCA77u ^ (uint32_t)(k >> 32) * 0xC2B2AE3Du;
-    h ^= h >> 16;
-    h *= 0x7FEB352Du;
-    h ^= h >> 15;
-    return h;
-}
-__device__ __forceinline__ bool bloom_test(const uint32_t *bloom, uint32_t h) {
-    const uint32_t p1 = h & (BLOOM_BITS - 1), p2 = (h >> 17) & (BLOOM_BITS - 1);
+// Bloom filter (positions from the HBM table's own 64-bit hash): a false
+// positive only costs an HBM probe, never a wrong answer
+template <class M>
+__device__ __forceinline__ bool bloom_test2(const uint32_t *bloom, uint32_t p1, uint32_t p2) {
+    p1 &= M::BLOOM - 1; p2 &= M::BLOOM - 1;
     return ((bloom[p1 >> 5] >> (p1 & 31)) & (bloom[p2 >> 5] >> (p2 & 31)) & 1u) != 0;
 }
-__device__ __forceinline__ void bloom_set(uint32_t *bloom, uint32_t h) {
-    const uint32_t p1 = h & (BLOOM_BITS - 1), p2 = (h >> 17) & (BLOOM_BITS - 1);
+template <class M>
+__device__ __forceinline__ void bloom_set2(uint32_t *bloom, uint32_t p1, uint32_t p2) {
+    p1 &= M::BLOOM - 1; p2 &= M::BLOOM - 1;
     atomicOr(&bloom[p1 >> 5], 1u << (p1 & 31));
     atomicOr(&bloom[p2 >> 5], 1u << (p2 & 31));
 }
+// WIDE mode: positions from the HBM table's own 64-bit hash
+template <class M>
+__device__ __forceinline__ bool bloom_test(const uint32_t *bloom, uint64_t h) {
+    return bloom_test2<M>(bloom, (uint32_t)(h >> 20), (uint32_t)(h >> 44));
+}
+template <class M>
+__device__ __forceinline__ void bloom_set(uint32_t *bloom, uint64_t h) {
+    bloom_set2<M>(bloom, (uint32_t)(h >> 20), (uint32_t)(h >> 44));
+}
+
+// insert a configuration absent from this wave's HBM table (CAS on the first
+// slot of its chain whose generation tag is stale)
+__device__ __forceinline__ void hbm_insert(uint64_t *memo, uint32_t cap_mask, uint32_t gen,
+                                           uint32_t ct, uint32_t cs, uint64_t cm) {
+    uint32_t h = (uint32_t)memo_hash(ct, cs, cm) & cap_mask;
+    const uint64_t w1 = ((uint64_t)gen << 40) | ((uint64_t)ct << 20) | cs;
+    for (;;) {
+        const uint64_t e1 = __hip_atomic_load(&memo[2 * (size_t)h + 1], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((e1 >> 40) != gen) {
+            unsigned long long exp = e1;
+            if (__hip_atomic_compare_exchange_strong((unsigned long long *)&memo[2 * (size_t)h + 1],
+                                                     &exp, (unsigned long long)w1,
+                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                __hip_atomic_store(&memo[2 * (size_t)h], cm, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                return;
+            }
+            continue;
+        }
+        h = (h + 1) & cap_mask;
+    }
+}
+
+// Probe this wave's HBM table. Returns slot | absent << 32.
+__device__ __forceinline__ uint64_t hbm_probe(const uint64_t *memo, uint32_t cap_mask, uint32_t gen,
+                                              uint32_t ct, uint32_t cs, uint64_t cm,
+                                              unsigned long long &probes) {
+    const uint64_t w1want = ((uint64_t)gen << 40) | ((uint64_t)ct << 20) | cs;
+    uint32_t h = (uint32_t)memo_hash(ct, cs, cm) & cap_mask;
+    for (;;) {
+        const uint64_t e1 = __hip_atomic_load(&memo[2 * (size_t)h + 1], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+        probes++;
+        if ((e1 >> 40) != gen) return (1ULL << 32) | h;
+        if (e1 == w1want) {
+            const uint64_t e0 = __hip_atomic_load(&memo[2 * (size_t)h], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (e0 == cm) return h;
+        }
+        h = (h + 1) & cap_mask;
+    }
+}
+
+// LEAN key fields
+__device__ __forceinline__ uint32_t lk_t(uint64_t k) { return (uint32_t)(k >> 48) & 0x7FFF; }
+__device__ __forceinline__ uint32_t lk_s(uint64_t k) { return (uint32_t)(k >> 40) & 0xFF; }
+__device__ __forceinline__ uint64_t lk_m(uint64_t k) { return k & ((1ULL << 40) - 1); }
+// two independent 32-bit hashes of a LEAN key: the top bits pick its two
+// buckets, folded low bits its two Bloom positions
+__device__ __forceinline__ void lk_hash(uint32_t klo, uint32_t khi, uint32_t &h1, uint32_t &h2) {
+    h1 = klo * 0x9E3779B1u ^ khi * 0x85EBCA77u;
+    h2 = klo * 0xC2B2AE3Du ^ khi * 0x27D4EB2Fu;
+}
+template <class M>
+__device__ __forceinline__ void lk_bkts(uint32_t h1, uint32_t h2, uint32_t &b1, uint32_t &b2) {
+    b1 = h1 >> (32 - M::LG);
+    b2 = h2 >> (32 - M::LG);
+}
+__device__ __forceinline__ uint32_t lk_bl(uint32_t h) { return h ^ (h >> 15); }
 
 // Evict LDS memo layers into this wave's HBM table (out of line: it runs
 // once per MEMO_EVICT inserts). theta is chosen so that the layers kept in
 // LDS (t >= theta, at most a few below the current layer t_cur) fill at most
 // half of what triggered the eviction; 0xFFFFFFFF = the current layer alone
-// is too wide: HBM only from now on. Entries are staged through global
-// scratch and the LDS table is rebuilt. Returns theta << 32 | kept.
-__device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint64_t *memo, uint64_t *stage,
+// is too wide: HBM for everything below it from now on. Entries are staged
+// through global scratch and the LDS table is rebuilt; an entry that finds
+// both of its buckets full goes to HBM too and theta rises above its layer.
+// Every entry written to HBM enters the Bloom filter. Returns theta << 32 | kept.
+template <class M>
+__device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint32_t *bcnt, uint32_t *bloom,
+                                            uint64_t *memo, uint64_t *stage,
                                             uint32_t cap_mask, uint32_t gen, uint32_t t_cur,
                                             uint32_t theta_old, int lane) {
-    const uint64_t gen_hi = (uint64_t)gen << 40;
     // histogram of entries by distance below t_cur (entries at or above it: bin 0)
     int bins = 0;                                  // lane b < 16 holds bin b
 #pragma unroll 1
-    for (int r = 0; r < MEMO_SLOTS / 64; r++) {
+    for (int r = 0; r < M::SLOTS / 64; r++) {
         const uint64_t x = lmemo[lane + 64 * r];
         stage[lane + 64 * r] = x;
-        const uint32_t xt = (uint32_t)(x >> 48);
+        const uint32_t xt = lk_t(x);
         const int d = x == 0 ? 99 : (xt >= t_cur ? 0 : (int)min(t_cur - xt, 15u));
 #pragma unroll
         for (int b = 0; b < 16; b++) {
@@ -641,12 +751,11 @@ __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint64_t *memo, uin
 #pragma unroll 1
     for (int b = 0; b < 16; b++) {
         acc += readlane(bins, b);
-        if (acc > MEMO_EVICT / 2) break;
+        if (acc > M::EVICT / 2) break;
         dstar = b;
     }
     uint32_t th2;
-    int kept = 0;
-    if (dstar < 0) th2 = 0xFFFFFFFFu;
+    if (dstar < 0) th2 = t_cur + 1;              // the current layer alone is too wide
     else {
         th2 = t_cur > (uint32_t)dstar ? t_cur - (uint32_t)dstar : 0u;
         if (dstar == 15) th2 = t_cur - min(t_cur, 15u);
@@ -655,78 +764,55 @@ __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint64_t *memo, uin
     th2 = max(th2, theta_old);
     wave_sync();
 #pragma unroll 1
-    for (int r = 0; r < MEMO_SLOTS / 64; r++) lmemo[lane + 64 * r] = 0;
+    for (int r = 0; r < M::SLOTS / 64; r++) lmemo[lane + 64 * r] = 0;
+    for (int i = lane; i < M::BKT / 4; i += 64) bcnt[i] = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     wave_sync();
+    int kept = 0;
+    uint32_t th_min = 0;
 #pragma unroll 1
-    for (int r = 0; r < MEMO_SLOTS / 64; r++) {
+    for (int r = 0; r < M::SLOTS / 64; r++) {
         const uint64_t x = stage[lane + 64 * r];
         if (x == 0) continue;
-        const uint32_t xt = (uint32_t)(x >> 48);
-        if (xt < th2) {
-            const uint32_t cs = (uint32_t)(x >> 40) & 0xFF;
-            const uint64_t cm = x & ((1ULL << 40) - 1);
-            uint32_t h = (uint32_t)memo_hash(xt, cs, cm) & cap_mask;
-            const uint64_t w1 = gen_hi | ((uint64_t)xt << 20) | cs;
-            for (;;) {
-                const uint64_t e1 = __hip_atomic_load(&memo[2 * (size_t)h + 1], __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-                if ((e1 >> 40) != gen) {
-                    unsigned long long exp = e1;
-                    if (__hip_atomic_compare_exchange_strong((unsigned long long *)&memo[2 * (size_t)h + 1],
-                                                             &exp, (unsigned long long)w1,
-                                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT)) {
-                        __hip_atomic_store(&memo[2 * (size_t)h], cm, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    continue;
-                }
-                h = (h + 1) & cap_mask;
+        const uint32_t xt = lk_t(x);
+        bool to_hbm = xt < th2;
+        if (!to_hbm) {
+            uint32_t h1, h2, b1, b2;
+            lk_hash((uint32_t)x, (uint32_t)(x >> 32), h1, h2);
+            lk_bkts<M>(h1, h2, b1, b2);
+            bool placed = false;
+            for (int j = 0; j < 2 && !placed; j++) {
+                const uint32_t b = j ? b2 : b1;
+                const uint32_t sh = 8 * (b & 3);
+                const uint32_t old = (atomicAdd(&bcnt[b >> 2], 1u << sh) >> sh) & 0xFF;
+                if (old < 4) { lmemo[4 * b + old] = x; placed = true; }
+                else atomicSub(&bcnt[b >> 2], 1u << sh);
             }
-        } else {
-            kept++;
-            uint32_t h = lds_hash(x);
-            for (;;) {
-                unsigned long long z = 0;
-                if (__hip_atomic_compare_exchange_strong((unsigned long long *)&lmemo[h], &z,
-                                                         (unsigned long long)x, __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-                    break;
-                h = (h + 1) & (MEMO_SLOTS - 1);
-            }
+            if (placed) kept++;
+            else { to_hbm = true; th_min = max(th_min, xt + 1); }
+        }
+        if (to_hbm) {
+            const uint32_t cs = lk_s(x);
+            const uint64_t cm = lk_m(x);
+            hbm_insert(memo, cap_mask, gen, xt, cs, cm);
+            uint32_t h1, h2;
+            lk_hash((uint32_t)x, (uint32_t)(x >> 32), h1, h2);
+            bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
         }
     }
-    for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o);
-    // every HBM write of this wave is visible to its later probes
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (int o = 32; o > 0; o >>= 1) {
+        kept += __shfl_xor(kept, o);
+        th_min = max(th_min, (uint32_t)__shfl_xor((int)th_min, o));
+    }
+    th2 = max(th2, th_min);
+    // every HBM write of this wave is visible to its later probes (the
+    // table is private to the wave: workgroup scope, served by this CU's
+    // caches, no L2 write-back)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     wave_sync();
     return ((uint64_t)th2 << 32) | (uint32_t)kept;
-}
-
-// Probe this wave's HBM table (a lane whose child lies below theta; rare:
-// only after an eviction and a backtrack below the evicted layers).
-// Returns slot | absent << 32.
-__device__ __forceinline__ uint64_t hbm_probe(const uint64_t *memo, uint32_t cap_mask, uint32_t gen,
-                                              uint32_t ct, uint32_t cs, uint64_t cm,
-                                              unsigned long long &probes) {
-    const uint64_t w1want = ((uint64_t)gen << 40) | ((uint64_t)ct << 20) | cs;
-    uint32_t h = (uint32_t)memo_hash(ct, cs, cm) & cap_mask;
-    for (;;) {
-        const uint64_t e1 = __hip_atomic_load(&memo[2 * (size_t)h + 1], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-        probes++;
-        if ((e1 >> 40) != gen) return (1ULL << 32) | h;
-        if (e1 == w1want) {
-            const uint64_t e0 = __hip_atomic_load(&memo[2 * (size_t)h], __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-            if (e0 == cm) return h;
-        }
-        h = (h + 1) & cap_mask;
-    }
 }
 
 __device__ __forceinline__ uint64_t drop_bit(uint64_t m, uint32_t r) {
@@ -734,232 +820,327 @@ __device__ __forceinline__ uint64_t drop_bit(uint64_t m, uint32_t r) {
     return (m & lo) | ((m >> 1) & ~lo);
 }
 
-template <bool L>
+template <bool L, bool LEAN, class M>
 __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key, int lane,
-                          uint64_t *memo, Frame *stack, uint64_t *stage, bool lds_memo,
+                          uint64_t *memo, Frame *stack, uint64_t *stage,
                           long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes) {
     const OpC *ops = (const OpC *)tb;
-    const uint32_t *delta = (const uint32_t *)(tb + tblc_ops_bytes(K));
+    const Lay *lay = (const Lay *)(tb + tblc_ops_bytes(K));
     const uint32_t n_ok = (uint32_t)K.n_ok;
-    const uint64_t lane_bit = 1ULL << lane;
+    const int n_ops = K.n_ops;
     const uint32_t cap_mask = A.memo_cap - 1;
     const uint32_t gen = (A.gen_base + (uint32_t)key + 1) & ((1u << GEN_BITS) - 1);
     const uint64_t gen_hi = (uint64_t)gen << 40;
-    uint64_t *lmemo = (uint64_t *)(jh_lds + LDS_TBL);
-    Frame *ring = (Frame *)(jh_lds + LDS_TBL + MEMO_SLOTS * 8);
-    uint32_t *bloom = (uint32_t *)(jh_lds + LDS_TBL + MEMO_SLOTS * 8 + RING * 16);
-    uint32_t theta = lds_memo ? 0u : 0xFFFFFFFFu;
+    uint64_t *lmemo = (uint64_t *)(jh_lds + M::OFF_MEMO);
+    uint32_t *bloom = (uint32_t *)(jh_lds + M::OFF_BLOOM);
+    uint32_t *bcnt = (uint32_t *)(jh_lds + M::OFF_CNT);
+    const uint8_t *bcnt8 = (const uint8_t *)bcnt;
+    if constexpr (LEAN) {
+        for (int i = lane; i < M::SLOTS; i += 64) lmemo[i] = 0;
+        for (int i = lane; i < M::BKT / 4; i += 64) bcnt[i] = 0;
+    }
+    for (int i = lane; i < M::BLOOM / 32; i += 64) bloom[i] = 0;
+    const uint32_t lb_lo = lane < 32 ? 1u << lane : 0u, lb_hi = lane >= 32 ? 1u << (lane - 32) : 0u;
+    uint32_t theta = 0;
     int lcount = 0;
-    for (int i = lane; i < MEMO_SLOTS; i += 64) lmemo[i] = 0;
-    for (int i = lane; i < BLOOM_BITS / 32; i += 64) bloom[i] = 0;
+
+    // layer-table window: lane j holds lay[tb0 + j]
+    uint32_t tb0 = 0, drq = 0, dhi = 0;
+    auto load_lay = [&](uint32_t base) {
+        tb0 = base;
+        const uint32_t u = base + (uint32_t)lane;
+        if (u < n_ok) { const Lay e = lay[u]; drq = e.rq; dhi = e.hi; }
+    };
+    auto lay_hi = [&](uint32_t u) -> uint32_t {
+        if (u - tb0 >= 64u) load_lay(u >= 32 ? u - 32 : 0);
+        return (uint32_t)readlane((int)dhi, (int)(u - tb0));
+    };
+    // next-ops window: lane j holds ops[pb + j]
+    int pb = 0;
+    uint32_t urq = RQ_EMPTY;
+    auto load_up = [&](int base) {
+        pb = base;
+        const int j = base + lane;
+        urq = j < n_ops ? ops[j].rq : RQ_EMPTY;
+    };
+    // DFS stack: frames [ring_lo, depth) in lane registers, lane = index mod 64
+    uint32_t fm_lo = 0, fm_hi = 0, f_ti = 0, f_s = 0, fr_lo = 0, fr_hi = 0;
+
+    load_lay(0);
     uint32_t t = 0, tmax = 0, depth = 0, ring_lo = 0;
     uint64_t mask = 0;
-    int s = A.init_state, start = 0;
+    uint32_t s = (uint32_t)A.init_state;
+    uint64_t cand = 0;
+    bool fresh = true;
+    unsigned long long pc_lift = 0, pc_probe = 0, pc_ins = 0, pc_fwd = 0, pc_pop = 0, pc_cand = 0, pc_key = 0, pc_lds = 0;          // cand = the legal un-linearized members (else: a popped frame's rest)
     int verdict = -1;
     uint32_t ins = 0;
     const uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
-    uint32_t n_steps = 0, n_evict = 0, n_reload = 0;
-    // the window of layer t in lane registers: f (3 = no member), v1|v2
-#define DELTA(u) delta[(u)]
-    int w = (int)(DELTA(0) >> 22), P = w;
-    uint32_t r = (DELTA(0) >> 16) & 63;             // position of RET[t]
-    int lf = 3;
-    uint32_t lv = 0;
-    if (lane < w) { const OpC o = ops[lane]; lf = (int)(o.fa & 3); lv = o.vv; }
+    uint32_t n_steps = 0, n_evict = 0, n_reload = 0, n_slow = 0;
+    // the window of layer t in lane registers
+    int w = (int)(lay_hi(0) >> 6), P = w;
+    uint32_t r = lay_hi(0) & 63;                    // position of RET[t]
+    uint32_t wrq = lane < w ? ops[lane].rq : RQ_EMPTY;
+    load_up(P);
     wave_sync();
-    unsigned long long pc_lift = 0, pc_probe = 0, pc_ins = 0, pc_fwd = 0, pc_pop = 0;
     while (true) {
-        n_steps++;
+        DFS_STAT(n_steps++);
         PROF_MARK(q0);
-        if (A.claim && (n_steps & 1023) == 0) {
-            int c = 0;
-            if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (readlane(c, 0)) { verdict = JH_CANCELLED; break; }
-        }
-        // candidates: un-linearized members at or after `start` the model allows
-        const int v1 = (int)(lv & 0xFFFF), v2 = (int)(lv >> 16);
-        const bool legal = lf == F_WRITE || (lf == F_CAS && s == v1) ||
-                           (lf == F_READ && (v1 == 0 || v1 == s));
-        const int s2 = lf == F_WRITE ? v1 : (lf == F_CAS ? v2 : s);
-        const bool cand = legal && lane >= start && !(mask & lane_bit);
+        // candidates: un-linearized members the model allows; after a pop,
+        // the frame's rest (children seen absent after the taken one: the
+        // memo only grows, so nothing else can be absent now)
+        const uint32_t req = wrq & 0xFFFF, nv = wrq >> 16;
+        if (fresh) cand = (ballot(req == s) | ballot(req == RQ_ANY)) & ~mask;
+        PROF_MARK(qa); PROF_ADD(pc_cand, q0, qa);
+        fresh = true;
+        uint64_t absent = 0;
+        // the RET child (lane r), computed on the scalar unit
+        uint32_t u_r = t;
+        uint64_t nm_r = 0;
+        uint32_t klo = 0, khi = 0, b1 = 0, b2 = 0, n1 = 0, n2 = 0, h1 = 0, h2 = 0;
         uint32_t ct = t;
-        uint64_t cm = mask | lane_bit;
-        if ((ballot(cand) >> r) & 1) {
-            // lifting RET[t]: drop returned members, advance past linearized RETs
-            uint64_t nm = mask | (1ULL << r);
-            uint32_t u = t, ru = r;
-            for (;;) {
-                nm = drop_bit(nm, ru);
-                u++;
-                if (u >= n_ok) { nm = 0; break; }
-                ru = (DELTA(u) >> 16) & 63;
-                if (!((nm >> ru) & 1)) break;
-            }
-            if (lane == (int)r) { ct = u; cm = nm; }
-        }
-        // memo probes, all candidates at once (= the sequential scan, since
-        // nothing is inserted until the first new child is chosen)
-        PROF_MARK(q1);
-        PROF_ADD(pc_lift, q0, q1);
-        const uint64_t lkey = ((uint64_t)ct << 48) | ((uint64_t)(uint32_t)s2 << 40) | cm;
-        // LDS memo (lds_memo mode): every recent insert, and every entry of
-        // layers >= theta; older entries may have moved to the HBM table.
-        bool absent = false, probed = false;
-        uint32_t lslot = lds_hash(lkey), hslot = 0;
-        bool go_hbm = cand;
-        if (lds_memo && cand) {
-            uint64_t e = lmemo[lslot];
-            while (e != 0 && e != lkey) {
-                lslot = (lslot + 1) & (MEMO_SLOTS - 1);
-                e = lmemo[lslot];
-            }
-            go_hbm = e == 0 && ct < theta;
-            absent = e == 0 && ct >= theta;
-        }
-        // HBM-side entries: the Bloom filter of everything inserted for this
-        // key rules most absent children out without an HBM round trip, and
-        // only candidates before the first surely-absent one matter
-        if (ballot(go_hbm)) {
-            if (go_hbm && !bloom_test(bloom, bloom_hash(lkey))) { go_hbm = false; absent = true; }
-            const uint64_t sure = ballot(absent);
-            if (sure) go_hbm = go_hbm && lane < __builtin_ctzll(sure);
-        }
-        if (ballot(go_hbm) && go_hbm) {
-            const uint64_t rr = hbm_probe(memo, cap_mask, gen, ct, (uint32_t)s2, cm, my_probes);
-            hslot = (uint32_t)rr;
-            absent = (rr >> 32) != 0;
-            probed = true;
-        }
-        const uint64_t bn = ballot(absent);
-        PROF_MARK(q2);
-        PROF_ADD(pc_probe, q1, q2);
-        if (bn) {
-            if (ins >= budget) { verdict = JH_UNKNOWN; break; }
-            const int i = __builtin_ctzll(bn);
-            // lds_memo: new entries always go to LDS (evicted by layer later);
-            // else straight to the HBM table at the end of the child's chain
-            const bool to_lds = lds_memo;
-            if (!to_lds && !((ballot(probed) >> i) & 1) && lane == i)
-                hslot = (uint32_t)hbm_probe(memo, cap_mask, gen, ct, (uint32_t)s2, cm, my_probes);
-            if (lane == i) {
-                bloom_set(bloom, bloom_hash(lkey));
-                if (to_lds) lmemo[lslot] = lkey;
-                else {
-                    __hip_atomic_store(&memo[2 * (size_t)hslot], cm, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&memo[2 * (size_t)hslot + 1],
-                                       gen_hi | ((uint64_t)ct << 20) | (uint32_t)s2,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t cm = 0;
+        bool probed = false;
+        uint32_t hslot = 0;
+        if (cand) {
+            if ((cand >> r) & 1) {
+                uint64_t nm = mask | (1ULL << r);
+                uint32_t u = t, ru = r;
+                for (;;) {
+                    nm = drop_bit(nm, ru);
+                    u++;
+                    if (u >= n_ok) { nm = 0; break; }
+                    ru = lay_hi(u) & 63;
+                    if (!((nm >> ru) & 1)) break;
                 }
+                u_r = u; nm_r = nm;
             }
-            ins++;
-            // push the parent onto the LDS ring; a full ring spills its
-            // oldest half to the HBM stack in one coalesced store
-            if (depth - ring_lo == RING) {
-                if (lane < RING / 2) stack[ring_lo + lane] = ring[(ring_lo + lane) & (RING - 1)];
-                ring_lo += RING / 2;
-            }
-            if (lane == 0) {
-                Frame fr; fr.mask = mask; fr.t_i = (t << 6) | (uint32_t)i; fr.s = s;
-                ring[depth & (RING - 1)] = fr;
-            }
-            depth++;
-            const uint32_t nt = (uint32_t)readlane((int)ct, i);
-            mask = ((uint64_t)(uint32_t)readlane((int)(uint32_t)(cm >> 32), i) << 32) |
-                   (uint32_t)readlane((int)(uint32_t)cm, i);
-            s = readlane(s2, i);
-            start = 0;
-            PROF_MARK(q3);
-            PROF_ADD(pc_ins, q2, q3);
-            if (to_lds) {
-                if (++lcount >= MEMO_EVICT) {
-                    n_evict++;
-                    const uint64_t er = memo_evict(lmemo, memo, stage, cap_mask, gen, nt, theta, lane);
-                    lcount = (int)(uint32_t)er;
-                    theta = (uint32_t)(er >> 32);
+            PROF_MARK(q1a); PROF_ADD(pc_lift, q0, q1a);
+            const bool is_r = lane == (int)r;
+            if constexpr (LEAN) {
+                // 8-byte child keys, all lanes at once, then one LDS round trip
+                klo = is_r ? (uint32_t)nm_r : ((uint32_t)mask | lb_lo);
+                khi = (is_r ? ((uint32_t)(nm_r >> 32) | (u_r << 16))
+                            : ((uint32_t)(mask >> 32) | lb_hi | (t << 16))) | (nv << 8) | 0x80000000u;
+                lk_hash(klo, khi, h1, h2);
+                lk_bkts<M>(h1, h2, b1, b2);
+                PROF_MARK(qc); PROF_ADD(pc_key, q1a, qc);
+                const uint64_t k = ((uint64_t)khi << 32) | klo;
+                bool hit = false;
+                if ((cand >> lane) & 1) {          // candidate lanes only: fewer bank conflicts
+                    const ulonglong2 *B = (const ulonglong2 *)lmemo;
+                    const ulonglong2 x0 = B[2 * b1], x1 = B[2 * b1 + 1];
+                    const ulonglong2 y0 = B[2 * b2], y1 = B[2 * b2 + 1];
+                    n1 = bcnt8[b1]; n2 = bcnt8[b2];
+                    // bitwise, not short-circuit: no branches between the four reads
+                    hit = (x0.x == k) | (x0.y == k) | (x1.x == k) | (x1.y == k) |
+                          (y0.x == k) | (y0.y == k) | (y1.x == k) | (y1.y == k);
+                }
+                absent = cand & ~ballot(hit);
+                PROF_MARK(qd); PROF_ADD(pc_lds, qc, qd);
+                if (t < theta && absent) {
+                    DFS_STAT(n_slow++);
+                    // children below theta may sit in HBM: Bloom, then HBM for
+                    // the lanes before the first surely-absent one
+                    uint64_t low = absent;
+                    if (u_r >= theta) low &= ~(1ULL << r);
+                    const uint32_t kt = khi >> 16 & 0x7FFF, ks = (khi >> 8) & 0xFF;
+                    const uint64_t km = k & ((1ULL << 40) - 1);
+                    const bool maybe = ((low >> lane) & 1) && bloom_test2<M>(bloom, lk_bl(h1), lk_bl(h2));
+                    const uint64_t bm = ballot(maybe);
+                    const uint64_t sure = absent & ~bm;
+                    const uint64_t lim = sure ? ((1ULL << __builtin_ctzll(sure)) - 1) : ~0ULL;
+                    bool found = false;
+                    if (((bm & lim) >> lane) & 1) {
+                        found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
+                    }
+                    absent &= ~ballot(found);
                 }
             } else {
+                ct = is_r ? u_r : t;
+                cm = is_r ? nm_r : (mask | (1ULL << lane));
+                const bool c_l = (cand >> lane) & 1;
+                const uint64_t hh = memo_hash(ct, nv, cm);
+                const bool maybe = c_l && bloom_test<M>(bloom, hh);
+                const uint64_t bm = ballot(maybe);
+                const uint64_t sure = cand & ~bm;
+                const uint64_t lim = sure ? ((1ULL << __builtin_ctzll(sure)) - 1) : ~0ULL;
+                bool found = false;
+                if (((bm & lim) >> lane) & 1) {
+                    const uint64_t rr = hbm_probe(memo, cap_mask, gen, ct, nv, cm, my_probes);
+                    hslot = (uint32_t)rr;
+                    found = (rr >> 32) == 0;
+                    probed = true;
+                }
+                absent = cand & ~ballot(found);
+            }
+        }
+        PROF_MARK(q2); PROF_ADD(pc_probe, q0, q2);
+        if (absent) {
+            if (ins >= budget) { verdict = JH_UNKNOWN; break; }
+            if (A.claim && (ins & 1023) == 1023) {
+                // racing k_lin_bfs: stop if it settled this key first
+                int c = 0;
+                if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (readlane(c, 0)) { verdict = JH_CANCELLED; break; }
+            }
+            const int i = __builtin_ctzll(absent);
+            ins++;
+            const bool to_r = (uint32_t)i == r;
+            const uint32_t nt = to_r ? u_r : t;
+            const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
+            const uint32_t ns = (uint32_t)readlane((int)nv, i);
+            if constexpr (LEAN) {
+                const bool pick1 = n1 <= n2;
+                const uint32_t bs = pick1 ? b1 : b2, nsl = pick1 ? n1 : n2;
+                const bool full = nsl >= 4;
+                if (lane == i && !full) {
+                    lmemo[4 * bs + nsl] = ((uint64_t)khi << 32) | klo;
+                    ((uint8_t *)bcnt)[bs] = (uint8_t)(nsl + 1);
+                }
+                if ((ballot(full) >> i) & 1) {
+                    // both buckets full: HBM, and theta rises above the layer
+                    if (lane == i) {
+                        hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
+                        bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
+                    }
+                    theta = max(theta, nt + 1);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                } else if (++lcount >= M::EVICT) {
+                    DFS_STAT(n_evict++);
+                    const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
+                    // a call's result is divergent to the compiler: make it scalar again
+                    lcount = rfl((int)(uint32_t)er);
+                    theta = rflu((uint32_t)(er >> 32));
+                }
+            } else {
+                if (lane == i) {
+                    bloom_set<M>(bloom, memo_hash(ct, nv, cm));
+                    if (!probed) hbm_insert(memo, cap_mask, gen, ct, nv, cm);
+                    else {
+                        __hip_atomic_store(&memo[2 * (size_t)hslot], cm, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(&memo[2 * (size_t)hslot + 1],
+                                           gen_hi | ((uint64_t)ct << 20) | nv,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             }
+            // push the parent; a full ring spills its oldest half to HBM
+            if (depth - ring_lo == 64) {
+                const uint32_t k = ((uint32_t)lane - ring_lo) & 63;
+                if (k < 32) {
+                    Frame fr;
+                    fr.mask = ((uint64_t)fm_hi << 32) | fm_lo; fr.t_i = f_ti; fr.s = (int32_t)f_s;
+                    fr.rest = ((uint64_t)fr_hi << 32) | fr_lo; fr.pad[0] = fr.pad[1] = 0;
+                    stack[ring_lo + k] = fr;
+                }
+                ring_lo += 32;
+            }
+            {
+                const uint64_t rest = absent & (~1ULL << i);
+                if (lane == (int)(depth & 63)) {
+                    fm_lo = (uint32_t)mask; fm_hi = (uint32_t)(mask >> 32);
+                    f_ti = (t << 6) | (uint32_t)i; f_s = s;
+                    fr_lo = (uint32_t)rest; fr_hi = (uint32_t)(rest >> 32);
+                }
+            }
+            depth++;
+            mask = nmask;
+            s = ns;
+            PROF_MARK(q3); PROF_ADD(pc_ins, q2, q3);
             if (nt != t) {
                 if (nt >= n_ok) { t = nt; tmax = max(tmax, t); verdict = JH_VALID; break; }
                 // move the window forward layer by layer
                 for (uint32_t u = t; u < nt; u++) {
-                    const uint32_t ru = u == t ? r : (DELTA(u) >> 16) & 63;
-                    {
-                        const int sf = wave_shl1(lf), sv = wave_shl1((int)lv);
-                        if (lane >= (int)ru) { lf = sf; lv = (uint32_t)sv; }
-                    }
+                    const uint32_t ru = u == t ? r : (lay_hi(u) & 63);
+                    const uint32_t sh = (uint32_t)wave_shl1((int)wrq);
+                    if (lane >= (int)ru) wrq = sh;
                     w--;
-                    const int c = (int)(DELTA(u + 1) >> 22);
-                    const int dst = lane - w;
-                    if (dst >= 0 && dst < c) { const OpC o = ops[P + dst]; lf = (int)(o.fa & 3); lv = o.vv; }
-                    if (lane >= w + c) lf = 3;
-                    w += c; P += c;
+                    if (lane == w) wrq = RQ_EMPTY;
+                    const int c = (int)(lay_hi(u + 1) >> 6);
+                    if (c > 0) {
+                        if (P < pb || P + c > pb + 64) load_up(P);
+                        for (int k = 0; k < c; k++) {
+                            const uint32_t x = (uint32_t)readlane((int)urq, P - pb + k);
+                            if (lane == w + k) wrq = x;
+                        }
+                        w += c; P += c;
+                    }
                 }
                 t = nt;
                 tmax = max(tmax, t);
-                r = (DELTA(t) >> 16) & 63;
-                n_reload++;
+                r = lay_hi(t) & 63;
+                DFS_STAT(n_reload++);
             }
-            PROF_MARK(q4);
-            PROF_ADD(pc_fwd, q3, q4);
+            PROF_MARK(q4); PROF_ADD(pc_fwd, q3, q4);
         } else {
             if (depth == 0) { verdict = JH_INVALID; break; }
             depth--;
             if (depth < ring_lo) {
-                // ring empty: refill the half below from the HBM stack
+                // ring empty: refill up to 32 frames below from the HBM stack
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                const uint32_t lo = depth + 1 >= RING / 2 ? depth + 1 - RING / 2 : 0;
-                if (lane < (int)(depth + 1 - lo)) ring[(lo + lane) & (RING - 1)] = stack[lo + lane];
+                const uint32_t lo = depth + 1 >= 32 ? depth + 1 - 32 : 0;
+                const uint32_t k = ((uint32_t)lane - lo) & 63;
+                if (k <= depth - lo) {
+                    const Frame fr = stack[lo + k];
+                    fm_lo = (uint32_t)fr.mask; fm_hi = (uint32_t)(fr.mask >> 32); f_ti = fr.t_i; f_s = (uint32_t)fr.s;
+                    fr_lo = (uint32_t)fr.rest; fr_hi = (uint32_t)(fr.rest >> 32);
+                }
                 ring_lo = lo;
-                wave_sync();
             }
-            const Frame fr = ring[depth & (RING - 1)];
-            const uint32_t pt = fr.t_i >> 6;
-            mask = fr.mask; s = fr.s; start = (int)(fr.t_i & 63) + 1;
+            const int ln = (int)(depth & 63);
+            const uint32_t ti = (uint32_t)readlane((int)f_ti, ln);
+            const uint32_t pt = ti >> 6;
+            mask = ((uint64_t)(uint32_t)readlane((int)fm_hi, ln) << 32) | (uint32_t)readlane((int)fm_lo, ln);
+            s = (uint32_t)readlane((int)f_s, ln);
+            cand = ((uint64_t)(uint32_t)readlane((int)fr_hi, ln) << 32) | (uint32_t)readlane((int)fr_lo, ln);
+            fresh = false;
             if (pt != t) {
                 // move the window back: drop appended ops, re-insert RETs
                 for (uint32_t u = t; u > pt; u--) {
-                    const int c = (int)(DELTA(u) >> 22);
+                    const int c = (int)(lay_hi(u) >> 6);
                     w -= c; P -= c;
-                    if (lane >= w) lf = 3;
-                    const uint32_t d = DELTA(u - 1);
-                    const int ru = (int)((d >> 16) & 63);
-                    {
-                        const int sf = wave_shr1(lf), sv = wave_shr1((int)lv);
-                        if (lane > ru) { lf = sf; lv = (uint32_t)sv; }
-                    }
-                    if (lane == ru) { const OpC o = ops[d & 0xFFFF]; lf = (int)(o.fa & 3); lv = o.vv; }
+                    if (lane >= w) wrq = RQ_EMPTY;
+                    const uint32_t h = lay_hi(u - 1);
+                    const int ru = (int)(h & 63);
+                    const uint32_t sh = (uint32_t)wave_shr1((int)wrq);
+                    if (lane > ru) wrq = sh;
+                    const uint32_t x = (uint32_t)readlane((int)drq, (int)(u - 1 - tb0));
+                    if (lane == ru) wrq = x;
                     w++;
                 }
                 t = pt;
-                r = (DELTA(t) >> 16) & 63;
-                n_reload++;
+                r = lay_hi(t) & 63;
+                DFS_STAT(n_reload++);
             }
-            PROF_MARK(q5);
-            PROF_ADD(pc_pop, q2, q5);
+            PROF_MARK(q5); PROF_ADD(pc_pop, q2, q5);
         }
         if (depth >= A.stack_cap) { verdict = JH_UNKNOWN; if (lane == 0) atomicOr(A.flags, 4); break; }
     }
+    inserts = ins;
+    tmax_out = tmax;
 #ifdef JH_STEP_PROF
     if (A.dbg && lane == 0) {
         unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
         d[10] += pc_lift; d[11] += pc_probe; d[12] += pc_ins; d[13] += pc_fwd; d[14] += pc_pop;
+        d[0] += pc_cand; d[1] += pc_key; d[8] += pc_lds;
     }
 #endif
-    inserts = ins;
-    tmax_out = tmax;
+#ifdef JH_DFS_STATS
     if (A.dbg && lane == 0) {
         unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
-        d[4] += n_steps; d[5] += (unsigned long long)ins; d[6] += n_evict; d[7] += n_reload;
+        d[4] += n_steps; d[5] += (unsigned long long)ins; d[6] += n_evict; d[7] += n_reload; d[9] += n_slow;
     }
+#endif
     return verdict;
 }
 
-template <bool L>
+template <bool L, class M>
 __device__ void dfs_key(const DfsArgs &A, const KeySrc &src, const KeyInfo &K, char *gscr, int key,
                         int lane, uint64_t *memo, Frame *stack, unsigned long long &my_probes) {
     char *tb = tbl_base<L>(0, gscr);
@@ -976,11 +1157,11 @@ __device__ void dfs_key(const DfsArgs &A, const KeySrc &src, const KeyInfo &K, c
     }
     long long inserts = 0;
     uint32_t tmax = 0;
-    uint64_t *stage = (uint64_t *)(gscr + A.scratch_bytes - MEMO_SLOTS * 8);
+    uint64_t *stage = (uint64_t *)(gscr + A.scratch_bytes - M::SLOTS * 8);
     // the LDS memo packs states in 8 bits and masks in 40: else HBM table only
-    const bool lds_memo = A.states8 && maxw <= 40;
-    const int verdict = dfs_search<L>(A, K, tb, key, lane, memo, stack, stage, lds_memo, inserts,
-                                      tmax, my_probes);
+    const int verdict = A.states8 && maxw <= 40
+        ? dfs_search<L, true, M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes)
+        : dfs_search<L, false, M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
     if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 2] += __builtin_amdgcn_s_memtime() - c1;
     if (verdict == JH_CANCELLED) return;
     if (verdict == JH_UNKNOWN && A.defer && inserts >= A.budget) {
@@ -997,6 +1178,7 @@ __device__ void dfs_key(const DfsArgs &A, const KeySrc &src, const KeyInfo &K, c
     if (lane == 0) emit_verdict(A.out, A.claim, key, v);
 }
 
+template <class M>
 __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     const int lane = threadIdx.x;
     uint64_t *memo = A.memo + (size_t)blockIdx.x * A.memo_cap * 2;
@@ -1028,10 +1210,10 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
             continue;
         }
         const uint64_t need = tblc_bytes(K);
-        if (need <= (uint64_t)LDS_TBL) {
-            dfs_key<true>(A, src, K, gscr, key, lane, memo, stack, my_probes);
-        } else if (need + MEMO_SLOTS * 8 <= A.scratch_bytes) {
-            dfs_key<false>(A, src, K, gscr, key, lane, memo, stack, my_probes);
+        if (LDS_TBL > 0 && need <= (uint64_t)LDS_TBL) {
+            if constexpr (LDS_TBL > 0) dfs_key<true, M>(A, src, K, gscr, key, lane, memo, stack, my_probes);
+        } else if (need + M::SLOTS * 8 <= A.scratch_bytes) {
+            dfs_key<false, M>(A, src, K, gscr, key, lane, memo, stack, my_probes);
         } else {
             if (lane == 0) atomicOr(A.flags, 2);
             v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
@@ -1039,15 +1221,16 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         }
     }
     if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 9] = __builtin_amdgcn_s_memtime() - t_begin;
-    if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 15] = my_probes;
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
+    if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 15] = my_probes;
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
 }
 
 // phase 1: every key under the quick budget
-__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) { lin_dfs_waves(A); }
-// heavy keys: the full-budget sequential search racing k_lin_bfs
-__global__ void __launch_bounds__(64) k_lin_seq(DfsArgs A) { lin_dfs_waves(A); }
+__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) { lin_dfs_waves<MemoQ>(A); }
+// heavy keys: the full-budget sequential search racing k_lin_bfs, one wave
+// per CU with a 128 KB LDS memo
+__global__ void __launch_bounds__(64) k_lin_seq(DfsArgs A) { lin_dfs_waves<MemoH>(A); }
 
 // ---------------------------------------------------------------------------
 // Heavy keys: parallel breadth-first enumeration of the reachable
@@ -1444,8 +1627,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     long long vmin = rh.vmin, vmax = rh.vmax;
     if (init != JH_NIL) { vmin = std::min<long long>(vmin, init); vmax = std::max<long long>(vmax, init); }
     if (vmin > vmax) { vmin = 0; vmax = 0; }
-    if ((unsigned long long)(vmax - vmin) >= (unsigned long long)(STATE_MASK - 2))
-        throw_jh(JH_EUNSUPPORTED, "register values span more than 2^20 distinct states");
+    if ((unsigned long long)(vmax - vmin) >= (unsigned long long)(RQ_EMPTY - 2))
+        throw_jh(JH_EUNSUPPORTED, "register values span more than 65532 distinct states");
     const int init_state = init == JH_NIL ? 0 : (int)(init - vmin + 1);
 
     // partition by key
@@ -1489,12 +1672,13 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const uint32_t memo_cap1 = 1u << 16;
     int64_t quick = std::min<int64_t>(budget, memo_cap1 / 4);
     if (const char *e = getenv("JH_QUICK_BUDGET")) quick = std::max<int64_t>(1, std::min<int64_t>(quick, atoll(e)));
-    const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * (163840 / LDS_BYTES));
+    const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * (163840 / MemoQ::LDS));
     uint64_t *memo = ctx->ws<uint64_t>(WS_MEMO, (size_t)waves1 * memo_cap1 * 2, /*zero=*/true);
     if (clear_memo) HIP_TRY(hipMemsetAsync(memo, 0, ctx->bufs[WS_MEMO].bytes, st));
     const uint32_t stack_cap = (uint32_t)smax + 2;
     Frame *stack = ctx->ws<Frame>(WS_STACK, (size_t)waves1 * stack_cap);
-    const uint64_t scr_bytes = (((uint64_t)smax * 84 + 4096 + MEMO_SLOTS * 8) + 255) & ~255ULL;
+    const uint64_t scr_bytes = (((uint64_t)smax * 84 + 4096 + MemoQ::SLOTS * 8) + 255) & ~255ULL;
+    const uint64_t scr_bytes_h = (((uint64_t)smax * 84 + 4096 + MemoH::SLOTS * 8) + 255) & ~255ULL;
     char *scr = ctx->ws<char>(WS_SCRATCH, (size_t)waves1 * scr_bytes);
     int32_t *q = ctx->ws<int32_t>(WS_QUEUE, 16);
     int32_t *list = ctx->ws<int32_t>(WS_STATS, K);
@@ -1520,7 +1704,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         a.dbg = dbg;
     }
     HIP_TRY(hipEventRecord(ctx->ev[1], st));
-    k_lin_dfs<<<waves1, 64, LDS_BYTES, st>>>(a);
+    k_lin_dfs<<<waves1, 64, MemoQ::LDS, st>>>(a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[4], st));
     int32_t qh[16];
@@ -1574,6 +1758,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         if (!lds_attr) {
             HIP_TRY(hipFuncSetAttribute((const void *)k_lin_bfs, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         BFS_LDS_BYTES));
+            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        MemoH::LDS));
             lds_attr = true;
         }
 
@@ -1585,10 +1771,11 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
         if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
         Frame *stack2 = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap);
-        char *scr2 = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes);
+        char *scr2 = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes_h);
         DfsArgs b = a;
         b.list = defer; b.n_list = n_defer; b.queue = q + 6; b.defer = 0;
-        b.memo = memo2; b.memo_cap = cap2; b.stack = stack2; b.scratch = scr2; b.budget = budget;
+        b.memo = memo2; b.memo_cap = cap2; b.stack = stack2; b.scratch = scr2; b.scratch_bytes = scr_bytes_h;
+        b.budget = budget;
         b.gen_base = ctx->gen_base + (uint32_t)K + 1;
         b.dbg = dbg ? dbg + 16 * 256 : nullptr; b.claim = claim;
         b.probes = (unsigned long long *)(q + 8);
@@ -1598,7 +1785,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        k_lin_seq<<<waves2, 64, LDS_BYTES, ctx->aux>>>(b);
+        k_lin_seq<<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
         HIP_TRY(hipStreamWaitEvent(st, ctx->ev[7], 0));
@@ -1617,12 +1804,14 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             HIP_TRY(hipMemcpy(g.data(), dbg + 16 * 256, g.size() * 8, hipMemcpyDeviceToHost));
             for (int w = 0; w < waves2; w++)
                 if (g[16 * w + 4] > 0)
-                    fprintf(stderr, "[jh-seq] wave %d keys=%llu steps=%llu inserts=%llu evict=%llu reload=%llu search=%llu cyc/step=%.0f busy=%llu hbm-probes=%llu | lift %.0f probe %.0f ins %.0f fwd %.0f pop %.0f cyc/step\n",
+                    fprintf(stderr, "[jh-seq] wave %d keys=%llu steps=%llu inserts=%llu evict=%llu reload=%llu search=%llu cyc/step=%.0f busy=%llu hbm-probes=%llu | lift %.0f probe %.0f ins %.0f fwd %.0f pop %.0f cyc/step | cand %.0f key %.0f lds %.0f\n",
                             w, g[16 * w + 3], g[16 * w + 4], g[16 * w + 5], g[16 * w + 6], g[16 * w + 7], g[16 * w + 2],
                             (double)g[16 * w + 2] / std::max(1ULL, g[16 * w + 4]), g[16 * w + 9], g[16 * w + 15],
                             (double)g[16 * w + 10] / std::max(1ULL, g[16 * w + 4]), (double)g[16 * w + 11] / std::max(1ULL, g[16 * w + 4]),
                             (double)g[16 * w + 12] / std::max(1ULL, g[16 * w + 4]), (double)g[16 * w + 13] / std::max(1ULL, g[16 * w + 4]),
-                            (double)g[16 * w + 14] / std::max(1ULL, g[16 * w + 4]));
+                            (double)g[16 * w + 14] / std::max(1ULL, g[16 * w + 4]),
+                            (double)g[16 * w + 0] / std::max(1ULL, g[16 * w + 4]), (double)g[16 * w + 1] / std::max(1ULL, g[16 * w + 4]),
+                            (double)g[16 * w + 8] / std::max(1ULL, g[16 * w + 4]));
         }
     } else {
         HIP_TRY(hipEventRecord(ctx->ev[5], st));

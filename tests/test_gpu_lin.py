@@ -149,3 +149,21 @@ def test_keys_without_client_ops_and_unkeyed(ctx):
     # key "a": write 1 then read 1 -> valid; key "b": read 1 from nil -> invalid
     assert r["results"]["a"]["valid?"] is True and r["results"]["b"]["valid?"] is False
     assert r["failures"] == ["b"]
+
+
+@pytest.mark.parametrize("case", ["long_keys", "many_values", "wide_window"])
+def test_search_modes(ctx, case):
+    """Exercise every storage mode of the per-wave search: keys whose tables
+    exceed the LDS reservation (global tables, long layer windows, deep
+    stack spills), more than 255 register states (HBM-only memo), windows
+    wider than 40 (HBM-only memo)."""
+    kw = dict(n_keys=60, ops_per_key=1500, p_invalid=0.2, p_info=0.03, seed=4242)
+    if case == "many_values":
+        kw.update(n_keys=200, ops_per_key=200, n_values=600)
+    if case == "wide_window":
+        kw.update(n_keys=40, ops_per_key=300, threads_per_key=44, readers=10, groups=44,
+                  process_limit=10 ** 6, p_info=0.0)
+    cols, _ = synth.cas_register(**kw)
+    c, _ = oracle.check_cas_independent(cols, budget=20000, threads=8)
+    g, _ = ctx.check_cas_independent(cols, budget=20000)
+    _same(g, c)

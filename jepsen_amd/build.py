@@ -21,7 +21,10 @@ HEADERS = [os.path.join(CSRC, "jh_internal.h"), os.path.join(ROOT, "include", "j
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 HIPFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
-            "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+            "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable",
+            # keep uniform (scalar) branches of the DFS loop unstructurized: fewer
+            # copies and exec-mask moves per step (-5..8% per DFS step, measured)
+            "-mllvm", "-structurizecfg-skip-uniform-regions=1"]
 HIPFLAGS += os.environ.get("JH_HIPFLAGS", "").split()   # e.g. -DJH_STEP_PROF (profiling builds)
 
 

@@ -243,11 +243,12 @@ struct DfsArgs {
     jh_key_verdict *out;
     int32_t *defer_list;        // phase 1: keys over the quick budget
     int32_t *defer_count;
+    uint32_t *defer_prog;       // phase 1: progress of each deferred key (ordering of the heavy pass)
     uint64_t *memo;             // per wave: memo_cap entries x 2 words
     uint32_t memo_cap;          // power of two
     Frame *stack;               // per wave: stack_cap frames
     uint32_t stack_cap;
-    char *scratch;              // per wave global table space (keys too big for LDS)
+    char *scratch;              // per wave: the LDS memo eviction stage
     uint64_t scratch_bytes;
     int64_t budget;             // memo inserts before giving up
     int32_t defer;              // 1: over budget -> defer list; 0: -> :unknown
@@ -258,6 +259,9 @@ struct DfsArgs {
     int32_t states8;            // every interned state < 256 (LDS memo packing)
     unsigned long long *dbg;    // JH_DEBUG=2: per-wave cycle accounting (8 words)
     int32_t *claim;             // race with k_lin_bfs: per-key first-writer flag (or null)
+    const struct KeyMeta *meta; // per key: tables offset and sizes (k_key_tables)
+    const char *tables;         // the tables arena
+    const int32_t *n_list_dev;  // if set: the list length, on the device
 };
 
 constexpr int JH_CANCELLED = 3; // internal: the other search settled the key first
@@ -707,10 +711,11 @@ __device__ __forceinline__ uint32_t lk_t(uint64_t k) { return (uint32_t)(k >> 48
 __device__ __forceinline__ uint32_t lk_s(uint64_t k) { return (uint32_t)(k >> 40) & 0xFF; }
 __device__ __forceinline__ uint64_t lk_m(uint64_t k) { return k & ((1ULL << 40) - 1); }
 // two independent 32-bit hashes of a LEAN key: the top bits pick its two
-// buckets, folded low bits its two Bloom positions
+// buckets, folded low bits its two Bloom positions (one multiply each: the
+// fold is on the critical path of every DFS step)
 __device__ __forceinline__ void lk_hash(uint32_t klo, uint32_t khi, uint32_t &h1, uint32_t &h2) {
-    h1 = klo * 0x9E3779B1u ^ khi * 0x85EBCA77u;
-    h2 = klo * 0xC2B2AE3Du ^ khi * 0x27D4EB2Fu;
+    h1 = (klo ^ __builtin_rotateleft32(khi, 16)) * 0x9E3779B1u;
+    h2 = (klo + __builtin_rotateleft32(khi, 5)) * 0x85EBCA77u;
 }
 template <class M>
 __device__ __forceinline__ void lk_bkts(uint32_t h1, uint32_t h2, uint32_t &b1, uint32_t &b2) {
@@ -1140,85 +1145,402 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
     return verdict;
 }
 
-template <bool L, class M>
-__device__ void dfs_key(const DfsArgs &A, const KeySrc &src, const KeyInfo &K, char *gscr, int key,
-                        int lane, uint64_t *memo, Frame *stack, unsigned long long &my_probes) {
-    char *tb = tbl_base<L>(0, gscr);
-    jh_key_verdict v;
-    v.valid = JH_VALID; v.cause = 0; v.fail_entry = -1; v.explored = 0;
-    const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-    const int maxw = key_fill_c<L>(src, K, lane, tb);
-    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
-    if (A.dbg && lane == 0) { A.dbg[16 * (size_t)blockIdx.x + 1] += c1 - c0; A.dbg[16 * (size_t)blockIdx.x + 8] += L ? 1 : 0; }
-    if (maxw > 64) {
-        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-        if (lane == 0) emit_verdict(A.out, A.claim, key, v);
-        return;
-    }
-    long long inserts = 0;
-    uint32_t tmax = 0;
-    uint64_t *stage = (uint64_t *)(gscr + A.scratch_bytes - M::SLOTS * 8);
-    // the LDS memo packs states in 8 bits and masks in 40: else HBM table only
-    const int verdict = A.states8 && maxw <= 40
-        ? dfs_search<L, true, M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes)
-        : dfs_search<L, false, M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
-    if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 2] += __builtin_amdgcn_s_memtime() - c1;
-    if (verdict == JH_CANCELLED) return;
-    if (verdict == JH_UNKNOWN && A.defer && inserts >= A.budget) {
-        if (lane == 0) {
-            const int d = atomicAdd(A.defer_count, 1);
-            A.defer_list[d] = key;
+// The LEAN-mode search (window <= 40, states < 256). A lone wave issues at
+// most one instruction per 4 cycles whatever its kind (VALU, SALU, branch,
+// LDS), so a step costs ~4 cycles per instruction plus the LDS round trip:
+// this loop is shaped to issue few instructions per step.
+//   - no divergent control flow on the common path: non-candidate lanes
+//     probe bucket 0 (one broadcast LDS address) and are masked out of the
+//     ballots afterwards; lane selects are v_cndmask;
+//   - the RET child's lift is one scalar bit test in the common case (the
+//     next layer's RET position rn is kept with the layer);
+//   - a frame is (mask, t<<6|i, state) in lane depth mod 64; after a pop the
+//     remaining children are the candidates above i that are absent now
+//     (the memo only grows, so these are exactly WGL's remaining children);
+//   - budget, race-cancel and ring spill/refill checks are one compare each.
+// Search order, memo contents and the eviction/Bloom/HBM machinery are those
+// of dfs_search (the same WGL order as orc_wgl_canonical, oracle/jh_oracle.c).
+template <class M>
+__device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, const char *tb, int key, int lane,
+                        uint64_t *memo, Frame *stack, uint64_t *stage,
+                        long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes) {
+    const OpC *ops = (const OpC *)tb;
+    const Lay *lay = (const Lay *)(tb + tblc_ops_bytes(K));
+    const uint32_t n_ok = (uint32_t)K.n_ok;
+    const int n_ops = K.n_ops;
+    const uint32_t cap_mask = A.memo_cap - 1;
+    const uint32_t gen = (A.gen_base + (uint32_t)key + 1) & ((1u << GEN_BITS) - 1);
+    uint64_t *lmemo = (uint64_t *)(jh_lds + M::OFF_MEMO);
+    uint32_t *bloom = (uint32_t *)(jh_lds + M::OFF_BLOOM);
+    uint32_t *bcnt = (uint32_t *)(jh_lds + M::OFF_CNT);
+    uint8_t *bcnt8 = (uint8_t *)bcnt;
+    for (int i = lane; i < M::SLOTS; i += 64) lmemo[i] = 0;
+    for (int i = lane; i < M::BKT / 4; i += 64) bcnt[i] = 0;
+    for (int i = lane; i < M::BLOOM / 32; i += 64) bloom[i] = 0;
+    const uint32_t lb_lo = lane < 32 ? 1u << lane : 0u, lb_hi = lane >= 32 ? 1u << (lane - 32) : 0u;
+    uint32_t theta = 0;
+    int lcount = 0;
+    uint32_t n_steps = 0, n_lay = 0, n_up = 0, n_spill = 0, n_refill = 0, n_slow = 0, n_evict = 0;
+    const unsigned long long probes0 = my_probes;
+
+    // layer-table window: lane j holds lay[tb0 + j]
+    uint32_t tb0 = 0, drq = 0, dhi = 0;
+    auto load_lay = [&](uint32_t base) {
+        DFS_STAT(n_lay++);
+        tb0 = base;
+        const uint32_t u = base + (uint32_t)lane;
+        if (u < n_ok) { const Lay e = lay[u]; drq = e.rq; dhi = e.hi; }
+    };
+    auto lay_hi = [&](uint32_t u) -> uint32_t {
+        if (u - tb0 >= 64u) load_lay(u >= 32 ? u - 32 : 0);
+        return (uint32_t)readlane((int)dhi, (int)(u - tb0));
+    };
+    // next-ops window: lane j holds ops[pb + j]
+    int pb = 0;
+    uint32_t urq = RQ_EMPTY;
+    auto load_up = [&](int base) {
+        DFS_STAT(n_up++);
+        pb = base;
+        const int j = base + lane;
+        urq = j < n_ops ? ops[j].rq : RQ_EMPTY;
+    };
+    // DFS stack: frames [ring_lo, depth) in lane registers, lane = index mod 64
+    uint32_t fm_lo = 0, fm_hi = 0, f_ti = 0, f_s = 0;
+
+    load_lay(0);
+    uint32_t t = 0, tmax = 0, depth = 0, ring_lo = 0;
+    uint64_t mask = 0, above = ~0ULL;
+    uint32_t s = (uint32_t)A.init_state;
+    int verdict = -1;
+    uint32_t ins = 0;
+    const uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
+    uint32_t chk = min(budget, 1023u);               // next insert count that needs a check
+    int w = (int)(lay_hi(0) >> 6), P = w;
+    uint32_t r = lay_hi(0) & 63;                       // position of RET[t] in W(t)
+    uint32_t rn = n_ok > 1 ? (lay_hi(1) & 63) : 0;     // position of RET[t+1] in W(t+1)
+    uint32_t wrq = lane < w ? ops[lane].rq : RQ_EMPTY;
+    load_up(P);
+    wave_sync();
+    const ulonglong2 *B = (const ulonglong2 *)lmemo;
+    while (true) {
+        DFS_STAT(n_steps++);
+        const uint32_t req = wrq & 0xFFFF, nvl = wrq >> 16;
+        const uint64_t cand = (ballot(req == s) | ballot(req == RQ_ANY)) & ~mask & above;
+        above = ~0ULL;
+        uint64_t absent = 0;
+        uint32_t u_r = t;
+        uint64_t nm_r = 0;
+        uint32_t klo = 0, khi = 0, b1 = 0, b2 = 0, n1 = 0, n2 = 0, h1 = 0, h2 = 0;
+        if (cand) {
+            if ((cand >> r) & 1) {
+                // lift RET[t]: drop its bit, then keep lifting while the next
+                // layer's RET op is already linearized (rarely more than once)
+                uint64_t nm = drop_bit(mask, r);
+                uint32_t u = t + 1;
+                if (u >= n_ok) nm = 0;
+                else if ((nm >> rn) & 1) {
+                    uint32_t ru = rn;
+                    for (;;) {
+                        nm = drop_bit(nm, ru);
+                        u++;
+                        if (u >= n_ok) { nm = 0; break; }
+                        ru = lay_hi(u) & 63;
+                        if (!((nm >> ru) & 1)) break;
+                    }
+                }
+                u_r = u; nm_r = nm;
+            }
+            // child keys 1:1|t:15|state:8|mask:40, all lanes at once
+            const bool is_r = lane == (int)r;
+            const uint32_t hi_a = (uint32_t)(mask >> 32) | (t << 16) | 0x80000000u;
+            const uint32_t hi_r = (uint32_t)(nm_r >> 32) | (u_r << 16) | 0x80000000u;
+            klo = is_r ? (uint32_t)nm_r : ((uint32_t)mask | lb_lo);
+            khi = (is_r ? hi_r : (hi_a | lb_hi)) | (nvl << 8);
+            lk_hash(klo, khi, h1, h2);
+            lk_bkts<M>(h1, h2, b1, b2);
+            const uint64_t k = ((uint64_t)khi << 32) | klo;
+            // one LDS round trip; non-candidate lanes all read bucket 0 (broadcast)
+            const bool cl = (cand >> lane) & 1;
+            const uint32_t a1 = cl ? b1 : 0u, a2 = cl ? b2 : 0u;
+            const ulonglong2 x0 = B[2 * a1], x1 = B[2 * a1 + 1];
+            const ulonglong2 y0 = B[2 * a2], y1 = B[2 * a2 + 1];
+            n1 = bcnt8[a1]; n2 = bcnt8[a2];
+            const uint64_t hit = ballot(x0.x == k) | ballot(x0.y == k) | ballot(x1.x == k) | ballot(x1.y == k) |
+                                 ballot(y0.x == k) | ballot(y0.y == k) | ballot(y1.x == k) | ballot(y1.y == k);
+            absent = cand & ~hit;
+            if (t < theta && absent) {
+                DFS_STAT(n_slow++);
+                // children below theta may sit in HBM: Bloom, then HBM for
+                // the lanes before the first surely-absent one
+                uint64_t low = absent;
+                if (u_r >= theta) low &= ~(1ULL << r);
+                const uint32_t kt = khi >> 16 & 0x7FFF, ks = (khi >> 8) & 0xFF;
+                const uint64_t km = k & ((1ULL << 40) - 1);
+                const bool maybe = ((low >> lane) & 1) && bloom_test2<M>(bloom, lk_bl(h1), lk_bl(h2));
+                const uint64_t bm = ballot(maybe);
+                const uint64_t sure = absent & ~bm;
+                const uint64_t lim = sure ? ((1ULL << __builtin_ctzll(sure)) - 1) : ~0ULL;
+                bool found = false;
+                if (((bm & lim) >> lane) & 1)
+                    found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
+                absent &= ~ballot(found);
+            }
         }
-        return;
+        if (absent) {
+            if (ins >= chk) {
+                if (ins >= budget) { verdict = JH_UNKNOWN; break; }
+                if (A.claim) {
+                    // racing k_lin_bfs: stop if it settled this key first
+                    int c = 0;
+                    if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (readlane(c, 0)) { verdict = JH_CANCELLED; break; }
+                }
+                chk = min(budget, ins + 1024);
+            }
+            const int i = __builtin_ctzll(absent);
+            ins++;
+            const uint32_t ns = (uint32_t)readlane((int)nvl, i);
+            const bool to_r = (uint32_t)i == r;
+            const uint32_t nt = to_r ? u_r : t;
+            {
+                // into the emptier of the child's two buckets
+                const bool pick1 = n1 <= n2;
+                const uint32_t bs = pick1 ? b1 : b2, nsl = pick1 ? n1 : n2;
+                const uint64_t full_m = ballot(nsl >= 4);
+                if (!((full_m >> i) & 1)) {
+                    if (lane == i) {
+                        lmemo[4 * bs + nsl] = ((uint64_t)khi << 32) | klo;
+                        bcnt8[bs] = (uint8_t)(nsl + 1);
+                    }
+                    if (++lcount >= M::EVICT) {
+                        DFS_STAT(n_evict++);
+                        const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
+                        lcount = rfl((int)(uint32_t)er);
+                        theta = rflu((uint32_t)(er >> 32));
+                    }
+                } else {
+                    // both buckets full: HBM, and theta rises above the layer
+                    const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
+                    if (lane == i) {
+                        hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
+                        bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
+                    }
+                    theta = max(theta, nt + 1);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                }
+            }
+            // push the parent; a full ring spills its oldest half to HBM
+            if (depth - ring_lo == 64) {
+                DFS_STAT(n_spill++);
+                const uint32_t kk = ((uint32_t)lane - ring_lo) & 63;
+                if (kk < 32) {
+                    Frame fr;
+                    fr.mask = ((uint64_t)fm_hi << 32) | fm_lo; fr.t_i = f_ti; fr.s = (int32_t)f_s;
+                    fr.rest = 0; fr.pad[0] = fr.pad[1] = 0;
+                    stack[ring_lo + kk] = fr;
+                }
+                ring_lo += 32;
+            }
+            {
+                const bool me = lane == (int)(depth & 63);
+                fm_lo = me ? (uint32_t)mask : fm_lo;
+                fm_hi = me ? (uint32_t)(mask >> 32) : fm_hi;
+                f_ti = me ? ((t << 6) | (uint32_t)i) : f_ti;
+                f_s = me ? s : f_s;
+            }
+            depth++;
+            s = ns;
+            if (!to_r) {
+                mask |= 1ULL << i;
+            } else {
+                mask = nm_r;
+                if (nt >= n_ok) { t = nt; tmax = max(tmax, t); verdict = JH_VALID; break; }
+                // move the window forward layer by layer
+                for (uint32_t u = t; u < nt; u++) {
+                    const uint32_t ru = u == t ? r : (lay_hi(u) & 63);
+                    const uint32_t sh = (uint32_t)wave_shl1((int)wrq);
+                    if (lane >= (int)ru) wrq = sh;
+                    w--;
+                    if (lane == w) wrq = RQ_EMPTY;
+                    const int c = (int)(lay_hi(u + 1) >> 6);
+                    if (c > 0) {
+                        if (P < pb || P + c > pb + 64) load_up(c <= 32 && P >= 32 ? P - 32 : P);
+                        for (int kk = 0; kk < c; kk++) {
+                            const uint32_t x = (uint32_t)readlane((int)urq, P - pb + kk);
+                            if (lane == w + kk) wrq = x;
+                        }
+                        w += c; P += c;
+                    }
+                }
+                t = nt;
+                tmax = max(tmax, t);
+                r = lay_hi(t) & 63;
+                rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
+            }
+        } else {
+            if (depth == ring_lo) {
+                if (depth == 0) { verdict = JH_INVALID; break; }
+                // ring empty: refill up to 32 frames below from the HBM stack
+                DFS_STAT(n_refill++);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const uint32_t lo = depth >= 32 ? depth - 32 : 0;
+                const uint32_t kk = ((uint32_t)lane - lo) & 63;
+                if (kk < depth - lo) {
+                    const Frame fr = stack[lo + kk];
+                    fm_lo = (uint32_t)fr.mask; fm_hi = (uint32_t)(fr.mask >> 32); f_ti = fr.t_i; f_s = (uint32_t)fr.s;
+                }
+                ring_lo = lo;
+            }
+            depth--;
+            const int ln = (int)(depth & 63);
+            const uint32_t ti = (uint32_t)readlane((int)f_ti, ln);
+            const uint32_t pt = ti >> 6, pi = ti & 63;
+            mask = ((uint64_t)(uint32_t)readlane((int)fm_hi, ln) << 32) | (uint32_t)readlane((int)fm_lo, ln);
+            s = (uint32_t)readlane((int)f_s, ln);
+            above = pi == 63 ? 0ULL : (~0ULL << (pi + 1));
+            if (pt != t) {
+                // move the window back: drop appended ops, re-insert RETs
+                for (uint32_t u = t; u > pt; u--) {
+                    const int c = (int)(lay_hi(u) >> 6);
+                    w -= c; P -= c;
+                    if (lane >= w) wrq = RQ_EMPTY;
+                    const uint32_t h = lay_hi(u - 1);
+                    const int ru = (int)(h & 63);
+                    const uint32_t sh = (uint32_t)wave_shr1((int)wrq);
+                    if (lane > ru) wrq = sh;
+                    const uint32_t x = (uint32_t)readlane((int)drq, (int)(u - 1 - tb0));
+                    if (lane == ru) wrq = x;
+                    w++;
+                }
+                t = pt;
+                r = lay_hi(t) & 63;
+                rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
+            }
+        }
     }
-    v.valid = verdict;
-    v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
-    v.explored = inserts;
-    if (verdict == JH_INVALID) v.fail_entry = ret_row(src, K, tmax, lane);
-    if (lane == 0) emit_verdict(A.out, A.claim, key, v);
+    inserts = ins;
+    tmax_out = tmax;
+#ifdef JH_DFS_STATS
+    if (A.dbg && lane == 0) {
+        unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
+        d[4] += n_steps; d[5] += ins; d[6] += n_evict; d[7] += n_lay; d[10] += n_up;
+        d[11] += n_spill; d[12] += n_refill; d[13] += n_slow; d[14] += my_probes - probes0;
+    }
+#endif
+    return verdict;
 }
 
-template <class M>
+// Per-key search tables, built once per call for every key by one wave per
+// key (pass 1, then pass 2 + layer sweep into a bump-allocated slot of the
+// tables arena). The search kernels then only search: their hot loop does not
+// share registers with table building. Keys settled here (no search needed,
+// window wider than 64, beyond the compact encoding) get their verdict now.
+struct KeyMeta {
+    uint64_t off;      // byte offset of the key's tables in the arena
+    int32_t n_ops, n_ok;
+    int32_t maxw;      // widest window
+    int32_t pad;
+};
+
+struct TblArgs {
+    KeySrc src;
+    int64_t K;
+    KeyMeta *meta;
+    char *arena;
+    unsigned long long *bump;   // arena bytes used
+    jh_key_verdict *out;
+    int32_t *list;              // keys that need a search: LEAN mode
+    int32_t *n_list;
+    int32_t *list_w;            // keys that need a search: WIDE mode
+    int32_t *n_list_w;
+    int32_t states8;            // every interned state < 256
+};
+
+__global__ void __launch_bounds__(256) k_key_tables(TblArgs A) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t key = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); key < A.K; key += nw) {
+        KeyInfo K;
+        jh_key_verdict v;
+        bool need = key_pass1(A.src, (int)key, lane, K, v);
+        if (need && K.n_ok >= COMPACT_MAX_OK) {
+            // beyond the compact encoding (a < 2^14): not on this build's path
+            if (lane == 0) atomicOr(A.src.flags, 1);
+            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
+            need = false;
+        }
+        if (need) {
+            unsigned long long off = 0;
+            if (lane == 0) off = atomicAdd(A.bump, (unsigned long long)tblc_bytes(K));
+            off = (unsigned long long)rfl64(__shfl(off, 0));
+            const int maxw = key_fill_c<false>(A.src, K, lane, A.arena + off);
+            if (maxw > 64) {
+                v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
+                need = false;
+            } else if (lane == 0) {
+                KeyMeta m;
+                m.off = off; m.n_ops = K.n_ops; m.n_ok = K.n_ok; m.maxw = maxw; m.pad = 0;
+                A.meta[key] = m;
+                if (A.states8 && maxw <= 40) A.list[atomicAdd(A.n_list, 1)] = (int32_t)key;
+                else A.list_w[atomicAdd(A.n_list_w, 1)] = (int32_t)key;
+            }
+        }
+        if (!need && lane == 0) A.out[key] = v;
+    }
+}
+
+template <class M, bool LEAN>
 __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     const int lane = threadIdx.x;
     uint64_t *memo = A.memo + (size_t)blockIdx.x * A.memo_cap * 2;
     Frame *stack = A.stack + (size_t)blockIdx.x * A.stack_cap;
-    char *gscr = A.scratch + (size_t)blockIdx.x * A.scratch_bytes;
+    uint64_t *stage = (uint64_t *)(A.scratch + (size_t)blockIdx.x * A.scratch_bytes);
     unsigned long long my_probes = 0;
-    const KeySrc src{A.rec, A.pair, A.off, A.rows, A.viol, A.rank, A.flags};
+    const int n_list = A.n_list_dev ? *A.n_list_dev : A.n_list;
     const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
     for (;;) {
         int idx = 0;
         if (lane == 0) idx = atomicAdd(A.queue, 1);
         idx = readlane(idx, 0);
-        if (idx >= A.n_list) break;
+        if (idx >= n_list) break;
         const int key = A.list[idx];
+        const KeyMeta mt = A.meta[key];
         KeyInfo K;
+        K.n_ops = mt.n_ops; K.n_ok = mt.n_ok; K.sumW = 0;
+        K.s0 = 0; K.s1 = 0;
+        const char *tb = A.tables + mt.off;
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+        long long inserts = 0;
+        uint32_t tmax = 0;
+        // the LDS memo packs states in 8 bits and masks in 40 (LEAN); else
+        // the HBM table only (WIDE). One mode per kernel: the two searches do
+        // not share a register allocation.
+        if ((A.states8 && mt.maxw <= 40) != LEAN) continue;
+        int verdict;
+        if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
+        else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
+        if (A.dbg && lane == 0) { A.dbg[16 * (size_t)blockIdx.x + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * (size_t)blockIdx.x + 3] += 1; }
+        if (verdict == JH_CANCELLED) continue;
+        if (verdict == JH_UNKNOWN && A.defer && inserts >= A.budget) {
+            if (lane == 0) {
+                const int d = atomicAdd(A.defer_count, 1);
+                A.defer_list[d] = key;
+                // progress of the quick search (deepest layer / layers): the
+                // heavy-key pass starts with the least advanced keys
+                if (A.defer_prog) A.defer_prog[d] = (uint32_t)((uint64_t)tmax * 1000000u / (uint64_t)max(1, K.n_ok));
+            }
+            continue;
+        }
         jh_key_verdict v;
-        const unsigned long long p0 = __builtin_amdgcn_s_memtime();
-        const bool needed = key_pass1(src, key, lane, K, v);
-        if (A.dbg && lane == 0) { A.dbg[16 * (size_t)blockIdx.x + 0] += __builtin_amdgcn_s_memtime() - p0; A.dbg[16 * (size_t)blockIdx.x + 3] += 1; }
-        if (!needed) {
-            if (lane == 0) emit_verdict(A.out, A.claim, key, v);
-            continue;
-        }
-        if (K.n_ok >= COMPACT_MAX_OK) {
-            // beyond the compact encoding (a < 2^14): not on this build's path
-            if (lane == 0) atomicOr(A.flags, 1);
-            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-            if (lane == 0) emit_verdict(A.out, A.claim, key, v);
-            continue;
-        }
-        const uint64_t need = tblc_bytes(K);
-        if (LDS_TBL > 0 && need <= (uint64_t)LDS_TBL) {
-            if constexpr (LDS_TBL > 0) dfs_key<true, M>(A, src, K, gscr, key, lane, memo, stack, my_probes);
-        } else if (need + M::SLOTS * 8 <= A.scratch_bytes) {
-            dfs_key<false, M>(A, src, K, gscr, key, lane, memo, stack, my_probes);
-        } else {
-            if (lane == 0) atomicOr(A.flags, 2);
-            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-            if (lane == 0) emit_verdict(A.out, A.claim, key, v);
-        }
+        v.valid = verdict;
+        v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
+        v.explored = inserts;
+        v.fail_entry = -1;
+        // an invalid key's failing row is resolved by k_fail_rows from tmax
+        if (verdict == JH_INVALID) v.fail_entry = -(int64_t)tmax - 2;
+        if (lane == 0) emit_verdict(A.out, A.claim, key, v);
     }
     if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 9] = __builtin_amdgcn_s_memtime() - t_begin;
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
@@ -1227,10 +1549,12 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
 }
 
 // phase 1: every key under the quick budget
-__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) { lin_dfs_waves<MemoQ>(A); }
+template <bool LEAN>
+__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) { lin_dfs_waves<MemoQ, LEAN>(A); }
 // heavy keys: the full-budget sequential search racing k_lin_bfs, one wave
 // per CU with a 128 KB LDS memo
-__global__ void __launch_bounds__(64) k_lin_seq(DfsArgs A) { lin_dfs_waves<MemoH>(A); }
+template <bool LEAN>
+__global__ void __launch_bounds__(64) k_lin_seq(DfsArgs A) { lin_dfs_waves<MemoH, LEAN>(A); }
 
 // ---------------------------------------------------------------------------
 // Heavy keys: parallel breadth-first enumeration of the reachable
@@ -1558,6 +1882,21 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A) {
     }
 }
 
+// Invalid keys settled by the DFS carry -(tmax + 2): the failing row is the
+// ok completion of RET[tmax] (the first op no configuration gets past).
+__global__ void __launch_bounds__(256) k_fail_rows(KeySrc S, jh_key_verdict *out, int64_t K) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t key = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); key < K; key += nw) {
+        const int64_t fe = out[key].fail_entry;
+        if (fe > -2) continue;
+        KeyInfo Ki;
+        Ki.s0 = S.off[key]; Ki.s1 = S.off[key + 1];
+        const long long row = ret_row(S, Ki, (uint32_t)(-fe - 2), lane);
+        if (lane == 0) out[key].fail_entry = row;
+    }
+}
+
 __global__ void k_summary(const jh_key_verdict *__restrict__ v, int64_t K, long long *sum) {
     // sum: [0] valid max [1] n_invalid [2] n_unknown [3] first_fail [4] n_keys [5] explored
     long long vmax = 0, ninv = 0, nunk = 0, ff = LLONG_MAX, nk = 0, ex = 0;
@@ -1670,27 +2009,40 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
 
     // phase 1: every key, quick budget, persistent grid
     const uint32_t memo_cap1 = 1u << 16;
-    int64_t quick = std::min<int64_t>(budget, memo_cap1 / 4);
+    int64_t quick = std::min<int64_t>(budget, 4096);
     if (const char *e = getenv("JH_QUICK_BUDGET")) quick = std::max<int64_t>(1, std::min<int64_t>(quick, atoll(e)));
     const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * (163840 / MemoQ::LDS));
     uint64_t *memo = ctx->ws<uint64_t>(WS_MEMO, (size_t)waves1 * memo_cap1 * 2, /*zero=*/true);
     if (clear_memo) HIP_TRY(hipMemsetAsync(memo, 0, ctx->bufs[WS_MEMO].bytes, st));
     const uint32_t stack_cap = (uint32_t)smax + 2;
     Frame *stack = ctx->ws<Frame>(WS_STACK, (size_t)waves1 * stack_cap);
-    const uint64_t scr_bytes = (((uint64_t)smax * 84 + 4096 + MemoQ::SLOTS * 8) + 255) & ~255ULL;
-    const uint64_t scr_bytes_h = (((uint64_t)smax * 84 + 4096 + MemoH::SLOTS * 8) + 255) & ~255ULL;
+    const uint64_t scr_bytes = MemoQ::SLOTS * 8;          // per wave: the memo eviction stage
+    const uint64_t scr_bytes_h = MemoH::SLOTS * 8;
+    const uint64_t scr_bytes_bfs = (((uint64_t)smax * 84 + 4096) + 255) & ~255ULL;
     char *scr = ctx->ws<char>(WS_SCRATCH, (size_t)waves1 * scr_bytes);
     int32_t *q = ctx->ws<int32_t>(WS_QUEUE, 16);
     int32_t *list = ctx->ws<int32_t>(WS_STATS, K);
     int32_t *defer = ctx->ws<int32_t>(WS_DEFER, K + 1);
     unsigned long long *probes = (unsigned long long *)(q + 4);
     HIP_TRY(hipMemsetAsync(q, 0, 16 * sizeof(int32_t), st));
-    k_iota<<<grid_for(K, 256), 256, 0, st>>>(list, K);
+
+    // per-key search tables for every key (<= 8 B per entry + 32 B per key)
+    KeyMeta *meta = ctx->ws<KeyMeta>(WS_META, K);
+    char *arena = ctx->ws<char>(WS_ARENA, (size_t)m * 8 + (size_t)K * 32 + 256);
+    TblArgs ta{};
+    ta.src = KeySrc{rec, pair, off, rB, viol, rank, q + 2};
+    ta.K = K; ta.meta = meta; ta.arena = arena; ta.bump = (unsigned long long *)(q + 10);
+    int32_t *list_w = ctx->ws<int32_t>(WS_LIST_W, K);
+    ta.out = out_dev; ta.list = list; ta.n_list = q + 12; ta.list_w = list_w; ta.n_list_w = q + 13;
+    ta.states8 = (vmax - vmin + 2) <= 256 ? 1 : 0;
+    k_key_tables<<<(unsigned)std::min<int64_t>((K + 3) / 4, 8192), 256, 0, st>>>(ta);
 
     DfsArgs a{};
     a.rec = rec; a.pair = pair; a.off = off; a.rows = rB; a.viol = viol; a.rank = rank;
-    a.list = list; a.n_list = (int32_t)K; a.queue = q; a.out = out_dev;
-    a.defer_list = defer; a.defer_count = q + 1;
+    a.list = list; a.n_list = 0; a.n_list_dev = q + 12; a.queue = q; a.out = out_dev;
+    a.meta = meta; a.tables = arena;
+    uint32_t *defer_prog = ctx->ws<uint32_t>(WS_DEFER_PROG, K + 1);
+    a.defer_list = defer; a.defer_count = q + 1; a.defer_prog = defer_prog;
     a.memo = memo; a.memo_cap = memo_cap1; a.stack = stack; a.stack_cap = stack_cap;
     a.scratch = scr; a.scratch_bytes = scr_bytes; a.budget = quick; a.defer = quick < budget ? 1 : 0;
     a.init_state = init_state; a.gen_base = ctx->gen_base; a.flags = q + 2; a.probes = probes;
@@ -1704,22 +2056,42 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         a.dbg = dbg;
     }
     HIP_TRY(hipEventRecord(ctx->ev[1], st));
-    k_lin_dfs<<<waves1, 64, MemoQ::LDS, st>>>(a);
+    k_lin_dfs<true><<<waves1, 64, MemoQ::LDS, st>>>(a);
+    HIP_TRY(hipGetLastError());
+    {
+        DfsArgs aw = a;
+        aw.list = list_w; aw.n_list_dev = q + 13; aw.queue = q + 14;
+        k_lin_dfs<false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[4], st));
     int32_t qh[16];
     HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const int n_defer = qh[1];
+    if (n_defer > 1) {
+        // heavy keys, least advanced first (the likely longest searches start first)
+        std::vector<int32_t> dk(n_defer);
+        std::vector<uint32_t> dp(n_defer);
+        HIP_TRY(hipMemcpyAsync(dk.data(), defer, sizeof(int32_t) * n_defer, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(dp.data(), defer_prog, sizeof(uint32_t) * n_defer, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        std::vector<int> ix(n_defer);
+        for (int i = 0; i < n_defer; i++) ix[i] = i;
+        std::stable_sort(ix.begin(), ix.end(), [&](int x, int y) { return dp[x] < dp[y]; });
+        std::vector<int32_t> sk(n_defer);
+        for (int i = 0; i < n_defer; i++) sk[i] = dk[ix[i]];
+        HIP_TRY(hipMemcpyAsync(defer, sk.data(), sizeof(int32_t) * n_defer, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     if (dbg2) {
         std::vector<unsigned long long> h((size_t)waves1 * 16);
         HIP_TRY(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
         unsigned long long tot[16] = {0}, mx9 = 0;
         for (int w = 0; w < waves1; w++) { for (int k = 0; k < 16; k++) tot[k] += h[16 * w + k]; mx9 = std::max(mx9, h[16 * w + 9]); }
-        fprintf(stderr, "[jh-dfs] waves=%d keys=%llu pass1=%.0f fill=%.0f search=%.0f cyc/key | steps=%llu inserts=%llu evict=%llu reload=%llu | cyc/step=%.0f | lds-tables=%llu | wave-busy avg=%.0f max=%llu cyc\n",
-                waves1, tot[3], (double)tot[0] / std::max(1ULL, tot[3]), (double)tot[1] / std::max(1ULL, tot[3]),
-                (double)tot[2] / std::max(1ULL, tot[3]), tot[4], tot[5], tot[6], tot[7],
-                (double)tot[2] / std::max(1ULL, tot[4]), tot[8], (double)tot[9] / waves1, mx9);
+        fprintf(stderr, "[jh-dfs] waves=%d keys=%llu search=%.0f cyc/key | steps=%llu inserts=%llu evict=%llu lay-loads=%llu op-loads=%llu spills=%llu refills=%llu slow=%llu hbm-probes=%llu | cyc/step=%.0f | wave-busy avg=%.0f max=%llu cyc\n",
+                waves1, tot[3], (double)tot[2] / std::max(1ULL, tot[3]), tot[4], tot[5], tot[6], tot[7], tot[10],
+                tot[11], tot[12], tot[13], tot[14], (double)tot[2] / std::max(1ULL, tot[4]), (double)tot[9] / waves1, mx9);
         HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 512) * 16, st));
     }
     int n_unres = 0;
@@ -1743,7 +2115,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         const int wg2 = std::min(n_defer, 128);
         uint64_t *bset = ctx->ws<uint64_t>(WS_BFS_SET, (size_t)wg2 * set_cap);
         uint64_t *bq = ctx->ws<uint64_t>(WS_BFS_Q, (size_t)wg2 * 4 * q_cap);
-        char *bscr = ctx->ws<char>(WS_SCRATCH_BFS, (size_t)wg2 * scr_bytes);
+        char *bscr = ctx->ws<char>(WS_SCRATCH_BFS, (size_t)wg2 * scr_bytes_bfs);
         int32_t *unres = ctx->ws<int32_t>(WS_BFS_META, n_defer + 1);
         BfsArgs c{};
         c.src = KeySrc{rec, pair, off, rB, viol, rank, q + 2};
@@ -1751,14 +2123,16 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         c.unres_list = unres; c.unres_count = q + 3;
         c.gset = bset; c.gset_cap = set_cap; c.pend = bq; c.front = bq + (size_t)wg2 * 2 * q_cap;
         c.q_cap = q_cap;
-        c.scratch = bscr; c.scratch_bytes = scr_bytes; c.budget = budget;
+        c.scratch = bscr; c.scratch_bytes = scr_bytes_bfs; c.budget = budget;
         c.init_state = init_state; c.states_ok = (vmax - vmin + 2) < 4096 ? 1 : 0;
         c.dbg = dbg; c.claim = claim;
         static bool lds_attr = false;
         if (!lds_attr) {
             HIP_TRY(hipFuncSetAttribute((const void *)k_lin_bfs, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         BFS_LDS_BYTES));
-            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq, hipFuncAttributeMaxDynamicSharedMemorySize,
+            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        MemoH::LDS));
+            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         MemoH::LDS));
             lds_attr = true;
         }
@@ -1773,7 +2147,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         Frame *stack2 = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap);
         char *scr2 = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes_h);
         DfsArgs b = a;
-        b.list = defer; b.n_list = n_defer; b.queue = q + 6; b.defer = 0;
+        b.list = defer; b.n_list = n_defer; b.n_list_dev = nullptr; b.queue = q + 6; b.defer = 0;
         b.memo = memo2; b.memo_cap = cap2; b.stack = stack2; b.scratch = scr2; b.scratch_bytes = scr_bytes_h;
         b.budget = budget;
         b.gen_base = ctx->gen_base + (uint32_t)K + 1;
@@ -1785,7 +2159,12 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        k_lin_seq<<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
+        {
+            DfsArgs bw = b;
+            bw.queue = q + 7;
+            k_lin_seq<false><<<std::min(waves2, 32), 64, MemoH::LDS, ctx->aux>>>(bw);
+        }
+        k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
         HIP_TRY(hipStreamWaitEvent(st, ctx->ev[7], 0));
@@ -1804,14 +2183,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             HIP_TRY(hipMemcpy(g.data(), dbg + 16 * 256, g.size() * 8, hipMemcpyDeviceToHost));
             for (int w = 0; w < waves2; w++)
                 if (g[16 * w + 4] > 0)
-                    fprintf(stderr, "[jh-seq] wave %d keys=%llu steps=%llu inserts=%llu evict=%llu reload=%llu search=%llu cyc/step=%.0f busy=%llu hbm-probes=%llu | lift %.0f probe %.0f ins %.0f fwd %.0f pop %.0f cyc/step | cand %.0f key %.0f lds %.0f\n",
-                            w, g[16 * w + 3], g[16 * w + 4], g[16 * w + 5], g[16 * w + 6], g[16 * w + 7], g[16 * w + 2],
-                            (double)g[16 * w + 2] / std::max(1ULL, g[16 * w + 4]), g[16 * w + 9], g[16 * w + 15],
-                            (double)g[16 * w + 10] / std::max(1ULL, g[16 * w + 4]), (double)g[16 * w + 11] / std::max(1ULL, g[16 * w + 4]),
-                            (double)g[16 * w + 12] / std::max(1ULL, g[16 * w + 4]), (double)g[16 * w + 13] / std::max(1ULL, g[16 * w + 4]),
-                            (double)g[16 * w + 14] / std::max(1ULL, g[16 * w + 4]),
-                            (double)g[16 * w + 0] / std::max(1ULL, g[16 * w + 4]), (double)g[16 * w + 1] / std::max(1ULL, g[16 * w + 4]),
-                            (double)g[16 * w + 8] / std::max(1ULL, g[16 * w + 4]));
+                    fprintf(stderr, "[jh-seq] wave %d keys=%llu search=%llu cyc busy=%llu | steps=%llu inserts=%llu evict=%llu lay-loads=%llu op-loads=%llu spills=%llu refills=%llu slow=%llu hbm-probes=%llu | cyc/step=%.0f\n",
+                            w, g[16 * w + 3], g[16 * w + 2], g[16 * w + 9], g[16 * w + 4], g[16 * w + 5], g[16 * w + 6],
+                            g[16 * w + 7], g[16 * w + 10], g[16 * w + 11], g[16 * w + 12], g[16 * w + 13], g[16 * w + 14],
+                            (double)g[16 * w + 2] / std::max(1ULL, g[16 * w + 4]));
         }
     } else {
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
@@ -1820,6 +2195,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     HIP_TRY(hipEventRecord(ctx->ev[2], st));
     ctx->gen_base += gen_span;
 
+    k_fail_rows<<<(unsigned)std::min<int64_t>((K + 3) / 4, 4096), 256, 0, st>>>(
+        KeySrc{rec, pair, off, rB, viol, rank, q + 2}, out_dev, K);
     long long *sd = ctx->ws<long long>(WS_SUMMARY, 8);
     long long s_init[8] = {0, 0, 0, LLONG_MAX, 0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(sd, s_init, sizeof s_init, hipMemcpyHostToDevice, st));

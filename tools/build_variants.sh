@@ -1,6 +1,7 @@
 # A/B builds of jh_lin.hip: tools/build_variants.sh name "-DFLAG ..." [name "flags"]...
 set -e
 cd "$(dirname "$0")/.."
+python -c "from jepsen_amd import build as B; B.build_libjh()"
 mkdir -p jepsen_amd/variants
 while [ $# -ge 2 ]; do
   n=$1; f=$2; shift 2

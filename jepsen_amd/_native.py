@@ -126,8 +126,9 @@ class Context:
         return v.valid, v.cause, v.fail_entry, v.explored
 
     # -- counter / set -----------------------------------------------------
-    def check_counter(self, cols, reads_cap=None):
-        h = A.make_history(cols)
+    def check_counter(self, cols, reads_cap=None, on_device=False):
+        """on_device: cols' columns are device pointers (the history already in HBM)."""
+        h = A.make_history(cols, on_device=on_device)
         cap = cols.n if reads_cap is None else reads_cap
         reads = np.zeros(3 * max(cap, 1), np.int64)
         nr, ne, fe = C.c_int64(), C.c_int64(), C.c_int64()
@@ -141,9 +142,10 @@ class Context:
         return {"valid": valid.value, "cause": cause.value, "reads": reads[:3 * k].reshape(-1, 3),
                 "n_reads": nr.value, "n_errors": ne.value, "first_err_entry": fe.value}
 
-    def check_set(self, cols, runs_cap=None):
-        h = A.make_history(cols)
-        cap = (cols.n + len(cols.aux) + 2) if runs_cap is None else runs_cap
+    def check_set(self, cols, runs_cap=None, on_device=False):
+        h = A.make_history(cols, on_device=on_device)
+        n_aux = int(cols.n_aux) if on_device else len(cols.aux)
+        cap = (cols.n + n_aux + 2) if runs_cap is None else runs_cap
         runs = [np.zeros(2 * max(cap, 1), np.int64) for _ in range(4)]
         r = A.JhSetResult()
         err = C.create_string_buffer(1024)

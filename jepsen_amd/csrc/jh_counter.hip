@@ -64,8 +64,10 @@ __global__ void k_cnt_range(const int64_t *__restrict__ proc, const int64_t *__r
 
 // last row of every process: per-chunk LDS hash of (process -> max row),
 // then one global atomicMax per distinct process of the chunk
-__global__ void __launch_bounds__(256) k_cnt_last(const int64_t *__restrict__ proc, int64_t n,
-                                                  long long pmin, int32_t *__restrict__ last) {
+__global__ void __launch_bounds__(256) k_cnt_last(const int64_t *__restrict__ proc,
+                                                  const int64_t *__restrict__ type, int64_t n,
+                                                  long long pmin, int32_t *__restrict__ last,
+                                                  uint32_t *__restrict__ pt) {
     __shared__ long long hk[HSLOTS];
     __shared__ int hv[HSLOTS];
     const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
@@ -75,6 +77,7 @@ __global__ void __launch_bounds__(256) k_cnt_last(const int64_t *__restrict__ pr
         const int64_t r = c0 + i;
         if (r >= n) break;
         const long long p = proc[r];
+        pt[r] = ((uint32_t)(p - pmin) << 2) | (uint32_t)(type[r] & 3);   // span < 2^28
         uint32_t h = (uint32_t)jh_mix64((uint64_t)p) & (HSLOTS - 1);
         bool done = false;
         for (int probe = 0; probe < 64 && !done; probe++) {
@@ -94,22 +97,51 @@ __global__ void __launch_bounds__(256) k_cnt_last(const int64_t *__restrict__ pr
         if (hk[i] != LLONG_MIN) atomicMax(&last[hk[i] - pmin], hv[i]);
 }
 
-__global__ void k_cnt_pair(const int64_t *__restrict__ proc, const int64_t *__restrict__ type,
-                           int64_t n, long long pmin, const int32_t *__restrict__ last,
-                           int32_t *__restrict__ pair, CntMeta *m) {
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
-         r += (int64_t)gridDim.x * blockDim.x) {
-        if (type[r] != T_INVOKE) continue;
-        const long long p = proc[r];
-        const int lr = last[p - pmin];
-        for (int64_t j = r + 1; j <= lr; j++) {
-            if (proc[j] != p) continue;
-            const int64_t ty = type[j];
-            if (ty == T_INFO) continue;
-            if (ty == T_INVOKE)
-                atomicMin(&m->viol1, ((unsigned long long)j << 4) | JH_CAUSE_DOUBLE_INVOKE);
-            else { pair[r] = (int32_t)j; pair[j] = (int32_t)r; }
-            break;
+// complete pairing: an invocation's completion is the next non-:info row of
+// its process (util.clj:606-640). One wave per 64 consecutive rows: it reads
+// the packed (process, type) words 64 rows at a time and, for each distinct
+// process among its still-open invocations, one ballot over the window gives
+// every candidate row; each open lane takes the first one after its own row.
+// A lane gives up after its process' last row (no completion: stays open).
+__global__ void __launch_bounds__(256) k_cnt_pair(const uint32_t *__restrict__ pt, int64_t n,
+                                                  const int32_t *__restrict__ last,
+                                                  int32_t *__restrict__ pair, CntMeta *m) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); wv * 64 < n; wv += nw) {
+        const int64_t base = wv * 64, r = base + lane;
+        const uint32_t x = r < n ? pt[r] : 3u;
+        const uint32_t p = x >> 2;
+        const bool inv = r < n && (x & 3) == T_INVOKE;
+        const int64_t lr = inv ? (int64_t)last[p] : -1;
+        bool open = inv && lr > r;
+        int64_t got = -1;
+        for (int64_t wb = base; wb < n; wb += 64) {
+            if (!__ballot(open)) break;
+            const int64_t j = wb + lane;
+            const uint32_t y = j < n ? pt[j] : 3u;
+            uint64_t todo = __ballot(open);
+            while (todo) {
+                const int l = __builtin_ctzll(todo);
+                const uint32_t pl = (uint32_t)__builtin_amdgcn_readlane((int)p, l);
+                const uint64_t mine = __ballot(open && p == pl);
+                const uint64_t cand = __ballot((y >> 2) == pl && (y & 3) != T_INFO);
+                todo &= ~mine;
+                if ((mine >> lane) & 1) {
+                    // candidates strictly after this lane's row
+                    const int64_t rel = r - wb;          // in [-63.., 63]
+                    const uint64_t after = rel < 0 ? ~0ULL : (rel >= 63 ? 0ULL : (~0ULL << (rel + 1)));
+                    const uint64_t c = cand & after;
+                    if (c) { got = wb + __builtin_ctzll(c); open = false; }
+                }
+            }
+            // past the process' last row: no completion
+            if (open && wb + 63 >= lr) open = false;
+        }
+        if (got >= 0) {
+            if ((pt[got] & 3) == T_INVOKE)
+                atomicMin(&m->viol1, ((unsigned long long)got << 4) | JH_CAUSE_DOUBLE_INVOKE);
+            else { pair[r] = (int32_t)got; pair[got] = (int32_t)r; }
         }
     }
 }
@@ -219,8 +251,9 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
     int32_t *isread = ctx->ws<int32_t>(WS_C_FLAG, n), *ridx = ctx->ws<int32_t>(WS_C_IDX, n);
     HIP_TRY(hipMemsetAsync(last, 0xFF, sizeof(int32_t) * (span + 1), st));
     HIP_TRY(hipMemsetAsync(pair, 0xFF, sizeof(int32_t) * n, st));
-    k_cnt_last<<<(int)((n + CHUNK - 1) / CHUNK), 256, 0, st>>>(dh->process, n, mh.pmin, last);
-    k_cnt_pair<<<grid_for(n, 256), 256, 0, st>>>(dh->process, dh->type, n, mh.pmin, last, pair, m);
+    uint32_t *pt = ctx->ws<uint32_t>(WS_C_PT, n);
+    k_cnt_last<<<(int)((n + CHUNK - 1) / CHUNK), 256, 0, st>>>(dh->process, dh->type, n, mh.pmin, last, pt);
+    k_cnt_pair<<<grid_for((n + 63) / 64, 4, 16384), 256, 0, st>>>(pt, n, last, pair, m);
     k_cnt_orphan<<<grid_for(n, 256), 256, 0, st>>>(dh->type, n, pair, m);
     k_cnt_vals<<<grid_for(n, 256), 256, 0, st>>>(dh->type, dh->f, dh->value, n, pair, lo, hi, isread, m);
     size_t tb = 0, tb2 = 0;

@@ -90,7 +90,7 @@ enum WsSlot {
     WS_MEMO_DEEP, WS_STACK_DEEP, WS_SCRATCH_DEEP, WS_SUMMARY, WS_STATS,
     WS_C_PAIR, WS_C_LAST, WS_C_LO, WS_C_HI, WS_C_OUT, WS_C_FLAG, WS_C_TMP, WS_C_IDX,
     WS_S_BITS, WS_S_RUNS, WS_S_TMP, WS_S_CNT,
-    WS_BFS_SET, WS_BFS_Q, WS_BFS_META, WS_CLAIM, WS_SCRATCH_BFS, WS_DEBUG, WS_META, WS_ARENA, WS_DEFER_PROG, WS_LIST_W,
+    WS_BFS_SET, WS_BFS_Q, WS_BFS_META, WS_CLAIM, WS_SCRATCH_BFS, WS_DEBUG, WS_META, WS_ARENA, WS_DEFER_PROG, WS_LIST_W, WS_C_PT,
     WS_COUNT
 };
 

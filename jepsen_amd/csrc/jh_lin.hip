@@ -2112,7 +2112,11 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         uint32_t set_cap = 1u << 12;
         while ((int64_t)set_cap < 2 * budget && set_cap < (1u << 30)) set_cap <<= 1;
         const uint32_t q_cap = (uint32_t)std::min<int64_t>(budget + 64, (int64_t)1 << 30);
-        const int wg2 = std::min(n_defer, 128);
+        // CU split of the heavy-key pass (one BFS workgroup or one sequential
+        // wave per CU, by LDS): invalid keys are few, the sequential searches
+        // many (every valid deferred key), so most CUs go to the latter
+        const int bfs_cus = std::max(1, std::min(64, ctx->n_cu / 4));
+        const int wg2 = std::min(n_defer, getenv("JH_BFS_CUS") ? std::max(1, atoi(getenv("JH_BFS_CUS"))) : bfs_cus);
         uint64_t *bset = ctx->ws<uint64_t>(WS_BFS_SET, (size_t)wg2 * set_cap);
         uint64_t *bq = ctx->ws<uint64_t>(WS_BFS_Q, (size_t)wg2 * 4 * q_cap);
         char *bscr = ctx->ws<char>(WS_SCRATCH_BFS, (size_t)wg2 * scr_bytes_bfs);
@@ -2139,7 +2143,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
 
         uint32_t cap2 = 1u << 16;
         while ((int64_t)cap2 < 2 * budget && cap2 < (1u << 30)) cap2 <<= 1;
-        const int waves2 = std::min(n_defer, 128);
+        const int waves2 = std::min(n_defer, std::max(1, ctx->n_cu - wg2));
         // generation-tagged: zeroed once when allocated (and on wrap), not per call
         const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;
         uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);

@@ -62,25 +62,87 @@ __global__ void k_set_range(const int64_t *__restrict__ aux, int64_t off, int64_
     if ((threadIdx.x & 63) == 0) { atomicMin(&m->vmin, lo); atomicMax(&m->vmax, hi); }
 }
 
-__global__ void k_set_mark_rows(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
-                                const int64_t *__restrict__ val, int64_t n, long long vmin,
-                                uint32_t *__restrict__ A, uint32_t *__restrict__ D) {
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
-         r += (int64_t)gridDim.x * blockDim.x) {
+// Marking is privatised per workgroup: a chunk of MARK_CH rows (or read
+// elements) whose element range spans at most MARK_LW words is marked with
+// LDS atomics, then merged with one global atomicOr per non-zero word; a
+// chunk spanning more falls back to global atomics per element.
+constexpr int MARK_CH = 16384, MARK_LW = 8192;
+
+__device__ __forceinline__ void block_minmax(long long &lo, long long &hi, long long *sh) {
+    for (int o = 32; o > 0; o >>= 1) { lo = min(lo, __shfl_xor(lo, o)); hi = max(hi, __shfl_xor(hi, o)); }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh[2 * wv] = lo; sh[2 * wv + 1] = hi; }
+    __syncthreads();
+    lo = sh[0]; hi = sh[1];
+    for (int i = 1; i < (int)(blockDim.x >> 6); i++) { lo = min(lo, sh[2 * i]); hi = max(hi, sh[2 * i + 1]); }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_set_mark_rows(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
+                                                       const int64_t *__restrict__ val, int64_t n, long long vmin,
+                                                       uint32_t *__restrict__ A, uint32_t *__restrict__ D) {
+    __shared__ uint32_t la[MARK_LW], ld[MARK_LW];
+    __shared__ long long sh[16];
+    const int64_t c0 = (int64_t)blockIdx.x * MARK_CH, c1 = min(n, c0 + MARK_CH);
+    long long lo = LLONG_MAX, hi = LLONG_MIN;
+    for (int64_t r = c0 + threadIdx.x; r < c1; r += blockDim.x) {
+        if (f[r] != JH_F_ADD) continue;
+        const int64_t ty = type[r];
+        if (ty != T_INVOKE && ty != T_OK) continue;
+        lo = min(lo, (long long)val[r]); hi = max(hi, (long long)val[r]);
+    }
+    block_minmax(lo, hi, sh);
+    if (lo > hi) return;
+    const int64_t w0 = (lo - vmin) >> 5, nwc = ((hi - vmin) >> 5) - w0 + 1;
+    const bool priv = nwc <= MARK_LW;
+    if (priv) {
+        for (int i = threadIdx.x; i < nwc; i += blockDim.x) { la[i] = 0; ld[i] = 0; }
+        __syncthreads();
+    }
+    for (int64_t r = c0 + threadIdx.x; r < c1; r += blockDim.x) {
         if (f[r] != JH_F_ADD) continue;
         const int64_t ty = type[r];
         if (ty != T_INVOKE && ty != T_OK) continue;
         const uint64_t b = (uint64_t)(val[r] - vmin);
-        atomicOr(&(ty == T_INVOKE ? A : D)[b >> 5], 1u << (b & 31));
+        if (priv) atomicOr(&(ty == T_INVOKE ? la : ld)[(b >> 5) - w0], 1u << (b & 31));
+        else atomicOr(&(ty == T_INVOKE ? A : D)[b >> 5], 1u << (b & 31));
+    }
+    if (priv) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < nwc; i += blockDim.x) {
+            if (la[i]) atomicOr(&A[w0 + i], la[i]);
+            if (ld[i]) atomicOr(&D[w0 + i], ld[i]);
+        }
     }
 }
 
-__global__ void k_set_mark_read(const int64_t *__restrict__ aux, int64_t off, int64_t cnt,
-                                long long vmin, uint32_t *__restrict__ R) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cnt;
-         i += (int64_t)gridDim.x * blockDim.x) {
+__global__ void __launch_bounds__(256) k_set_mark_read(const int64_t *__restrict__ aux, int64_t off, int64_t cnt,
+                                                       long long vmin, uint32_t *__restrict__ R) {
+    __shared__ uint32_t lr[MARK_LW];
+    __shared__ long long sh[16];
+    const int64_t c0 = (int64_t)blockIdx.x * MARK_CH, c1 = min(cnt, c0 + MARK_CH);
+    long long lo = LLONG_MAX, hi = LLONG_MIN;
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+        const long long v = aux[off + i];
+        lo = min(lo, v); hi = max(hi, v);
+    }
+    block_minmax(lo, hi, sh);
+    if (lo > hi) return;
+    const int64_t w0 = (lo - vmin) >> 5, nwc = ((hi - vmin) >> 5) - w0 + 1;
+    const bool priv = nwc <= MARK_LW;
+    if (priv) {
+        for (int i = threadIdx.x; i < nwc; i += blockDim.x) lr[i] = 0;
+        __syncthreads();
+    }
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
         const uint64_t b = (uint64_t)(aux[off + i] - vmin);
-        atomicOr(&R[b >> 5], 1u << (b & 31));
+        if (priv) atomicOr(&lr[(b >> 5) - w0], 1u << (b & 31));
+        else atomicOr(&R[b >> 5], 1u << (b & 31));
+    }
+    if (priv) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < nwc; i += blockDim.x)
+            if (lr[i]) atomicOr(&R[w0 + i], lr[i]);
     }
 }
 
@@ -111,10 +173,19 @@ __global__ void k_set_count(const uint32_t *__restrict__ A, const uint32_t *__re
             starts[s * nw + w] = __popc(st);
         }
     }
+    // one atomic per counter per workgroup (per wave, 48K waves would
+    // serialise on six L2 lines)
+    __shared__ long long sc[4][6];
     for (int i = 0; i < 6; i++) {
         long long v = c[i];
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if ((threadIdx.x & 63) == 0 && v) atomicAdd((unsigned long long *)&m->cnt[i], (unsigned long long)v);
+        if ((threadIdx.x & 63) == 0) sc[threadIdx.x >> 6][i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        long long v = 0;
+        for (int k = 0; k < (int)(blockDim.x >> 6); k++) v += sc[k][threadIdx.x];
+        if (v) atomicAdd((unsigned long long *)&m->cnt[threadIdx.x], (unsigned long long)v);
     }
 }
 
@@ -215,11 +286,11 @@ void set_check(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, int64_t *r
     uint32_t *bits = ctx->ws<uint32_t>(WS_S_BITS, 3 * nw);
     uint32_t *A = bits, *D = bits + nw, *R = bits + 2 * nw;
     HIP_TRY(hipMemsetAsync(bits, 0, sizeof(uint32_t) * 3 * nw, st));
-    if (n > 0) k_set_mark_rows<<<grid_for(n, 256), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, A, D);
-    if (cnt > 0) k_set_mark_read<<<grid_for(cnt, 256), 256, 0, st>>>(dh->aux, off, cnt, vmin, R);
+    if (n > 0) k_set_mark_rows<<<(unsigned)((n + MARK_CH - 1) / MARK_CH), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, A, D);
+    if (cnt > 0) k_set_mark_read<<<(unsigned)((cnt + MARK_CH - 1) / MARK_CH), 256, 0, st>>>(dh->aux, off, cnt, vmin, R);
     uint32_t *starts = ctx->ws<uint32_t>(WS_S_RUNS, 8 * nw + 8);
     uint32_t *spos = starts + 4 * nw;
-    k_set_count<<<grid_for(nw, 256), 256, 0, st>>>(A, D, R, nw, starts, m);
+    k_set_count<<<grid_for(nw, 256, 2048), 256, 0, st>>>(A, D, R, nw, starts, m);
     size_t tb = 0;
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, starts, spos, (int)nw, st));
     void *tmp = ctx->ws<char>(WS_S_TMP, tb);

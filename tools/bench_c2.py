@@ -1,0 +1,137 @@
+"""C2 measurement (BASELINE.json configs[1]): checker/counter and checker/set on
+synthetic 100M-entry histories on one MI355X.
+
+Prints one JSON line per checker. The history is resident in HBM before the
+timed region (columns copied once); a step is one jh_check_counter /
+jh_check_set call, including its D2H of the result (the :reads triples or the
+run-length sets). `roofline` is whole-call algorithmic bytes (SURVEY 8(d):
+56 B per entry read once, +24 B per :reads triple, +16 B per run of the four
+result sets) over the call's time, against the 8 TB/s HBM peak; the
+per-kernel split is in the rocprofv3 --stats summary (profiles/).
+
+    python tools/bench_c2.py [--entries 100000000] [--steps 5] [--warmup 1]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PEAK_HBM_GBS = 8000.0
+
+
+class DevCols:
+    """Device-resident columns (torch tensors kept alive) in the include/jh.h layout."""
+
+    def __init__(self, cols, dev):
+        import torch
+        self._t = {}
+        for k in ("process", "type", "f", "key", "value", "value2"):
+            self._t[k] = torch.from_numpy(np.ascontiguousarray(getattr(cols, k))).to(dev)
+            setattr(self, k, self._t[k].data_ptr())
+        aux = getattr(cols, "aux", None)
+        if aux is not None and len(aux):
+            self._t["aux"] = torch.from_numpy(np.ascontiguousarray(aux)).to(dev)
+            self.aux, self.n_aux = self._t["aux"].data_ptr(), len(aux)
+        else:
+            self.aux, self.n_aux = 0, 0
+        self.n, self.n_keys = int(cols.n), int(cols.n_keys)
+
+
+def timed(fn, steps, warmup):
+    import torch
+    for _ in range(warmup):
+        r = fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = fn()
+    torch.cuda.synchronize()
+    return r, (time.perf_counter() - t0) / steps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--entries", type=int, default=100_000_000)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cpu-sample", type=int, default=10_000_000,
+                    help="entries of the same generator timed on the CPU oracle")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    import torch
+    from jepsen_amd import _native, synth
+    from oracle import oracle
+    dev = torch.device("cuda", 0)
+    ctx = _native.Context(0)
+    lines = []
+
+    # ---- counter: add:read = 100:1, add 1, p_fail 5%, p_info 1%, 10 bad reads
+    half = args.entries // 2
+    cols = synth.counter(n_ops=half, n_procs=10, read_every=101, p_fail=0.05, p_info=0.01,
+                         n_bad_reads=10, seed=2)
+    d = DevCols(cols, dev)
+    r, sec = timed(lambda: ctx.check_counter(d, reads_cap=1 << 24, on_device=True), args.steps, args.warmup)
+    n = int(cols.n)
+    alg = 56.0 * n + 24.0 * r["n_reads"]
+    cpu = None
+    if not args.no_cpu:
+        cs = synth.counter(n_ops=args.cpu_sample // 2, n_procs=10, read_every=101, p_fail=0.05,
+                           p_info=0.01, n_bad_reads=10, seed=2)
+        t0 = time.perf_counter()
+        oracle.check_counter(cs)
+        ct = time.perf_counter() - t0
+        cpu = {"value": cs.n / ct, "unit": "entries/s", "cores": 1, "kind": "port",
+               "sample": f"{int(cs.n)} entries of the same generator, oracle/jh_oracle.c counter ({ct:.2f} s)"}
+    lines.append({"metric": "history entries verified/sec, checker/counter (C2)", "value": n / sec,
+                  "unit": "entries/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+                  "ms_per_step": sec * 1e3, "higher_is_better": True, "dtype": "int64",
+                  "data": "synthetic (jepsen_amd/csrc/gen.cpp counter, seed 2)",
+                  "config": {"workload": "C2 counter", "entries": n, "reads": r["n_reads"],
+                             "errors": r["n_errors"], "valid": r["valid"]},
+                  "roofline": {"bound": "hbm", "kernel": "whole jh_check_counter call",
+                               "achieved": alg / sec / 1e9, "peak": PEAK_HBM_GBS,
+                               "unit": "GB/s", "frac": alg / sec / 1e9 / PEAK_HBM_GBS,
+                               "traffic": None},
+                  "cpu_baseline": cpu})
+    del d, cols
+    torch.cuda.empty_cache()
+
+    # ---- set: distinct adds, p_fail 5%, p_info 2%, 100 lost, 10 unexpected
+    cols = synth.set_history(n_adds=half, n_procs=10, p_fail=0.05, p_info=0.02, n_lost=100,
+                             n_unexpected=10, seed=2)
+    d = DevCols(cols, dev)
+    r, sec = timed(lambda: ctx.check_set(d, runs_cap=1 << 20, on_device=True), args.steps, args.warmup)
+    n = int(cols.n)
+    alg = 56.0 * n + 8.0 * d.n_aux + 16.0 * sum(r["n_runs"])
+    cpu = None
+    if not args.no_cpu:
+        cs = synth.set_history(n_adds=args.cpu_sample // 2, n_procs=10, p_fail=0.05, p_info=0.02,
+                               n_lost=100, n_unexpected=10, seed=2)
+        t0 = time.perf_counter()
+        oracle.check_set(cs)
+        ct = time.perf_counter() - t0
+        cpu = {"value": cs.n / ct, "unit": "entries/s", "cores": 1, "kind": "port",
+               "sample": f"{int(cs.n)} entries of the same generator, oracle/jh_oracle.c set ({ct:.2f} s)"}
+    lines.append({"metric": "history entries verified/sec, checker/set (C2)", "value": n / sec,
+                  "unit": "entries/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+                  "ms_per_step": sec * 1e3, "higher_is_better": True, "dtype": "int64",
+                  "data": "synthetic (jepsen_amd/csrc/gen.cpp set, seed 2)",
+                  "config": {"workload": "C2 set", "entries": n, "final_read": d.n_aux,
+                             "lost": r["lost_count"], "unexpected": r["unexpected_count"],
+                             "valid": r["valid"]},
+                  "roofline": {"bound": "hbm", "kernel": "whole jh_check_set call",
+                               "achieved": alg / sec / 1e9, "peak": PEAK_HBM_GBS,
+                               "unit": "GB/s", "frac": alg / sec / 1e9 / PEAK_HBM_GBS,
+                               "traffic": None},
+                  "cpu_baseline": cpu})
+    for ln in lines:
+        print(json.dumps(ln))
+
+
+if __name__ == "__main__":
+    main()

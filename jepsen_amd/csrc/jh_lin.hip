@@ -1147,19 +1147,25 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
 
 // The LEAN-mode search (window <= 40, states < 256). A lone wave issues at
 // most one instruction per 4 cycles whatever its kind (VALU, SALU, branch,
-// LDS), so a step costs ~4 cycles per instruction plus the LDS round trip:
-// this loop is shaped to issue few instructions per step.
+// LDS), so a step costs ~4 cycles per instruction plus its LDS round trips:
+// this loop is shaped to issue few instructions and few round trips.
 //   - no divergent control flow on the common path: non-candidate lanes
 //     probe bucket 0 (one broadcast LDS address) and are masked out of the
 //     ballots afterwards; lane selects are v_cndmask;
 //   - the RET child's lift is one scalar bit test in the common case (the
 //     next layer's RET position rn is kept with the layer);
-//   - a frame is (mask, t<<6|i, state) in lane depth mod 64; after a pop the
-//     remaining children are the candidates above i that are absent now
-//     (the memo only grows, so these are exactly WGL's remaining children);
+//   - a frame is (mask, t<<6|i, state, rest) in lane depth mod 64, where rest
+//     are the candidates after i found absent when the parent was expanded;
+//   - after a pop the memo is NOT probed again: a remaining child P+j holds
+//     the linearized set L(P)+{j}, while everything explored in between lies
+//     below P+i and holds L(P)+{i} (the canonical coordinates are a bijective
+//     image of (linearized set, state), and linearized sets only grow along
+//     edges), so every child in rest is still absent. The next child is
+//     inserted with one read of its bucket fill counts;
 //   - budget, race-cancel and ring spill/refill checks are one compare each.
-// Search order, memo contents and the eviction/Bloom/HBM machinery are those
-// of dfs_search (the same WGL order as orc_wgl_canonical, oracle/jh_oracle.c).
+// Search order and memo contents are exactly WGL's (orc_wgl_canonical,
+// oracle/jh_oracle.c, which does probe after a backtrack and never finds the
+// child present): explored counts stay identical.
 template <class M>
 __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, const char *tb, int key, int lane,
                         uint64_t *memo, Frame *stack, uint64_t *stage,
@@ -1205,11 +1211,12 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
         urq = j < n_ops ? ops[j].rq : RQ_EMPTY;
     };
     // DFS stack: frames [ring_lo, depth) in lane registers, lane = index mod 64
-    uint32_t fm_lo = 0, fm_hi = 0, f_ti = 0, f_s = 0;
+    uint32_t fm_lo = 0, fm_hi = 0, f_ti = 0, f_s = 0, fr_lo = 0, fr_hi = 0;
 
     load_lay(0);
     uint32_t t = 0, tmax = 0, depth = 0, ring_lo = 0;
-    uint64_t mask = 0, above = ~0ULL;
+    uint64_t mask = 0, rest = 0;
+    bool fresh = true;                                 // false: just popped, candidates = rest
     uint32_t s = (uint32_t)A.init_state;
     int verdict = -1;
     uint32_t ins = 0;
@@ -1224,15 +1231,19 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
     const ulonglong2 *B = (const ulonglong2 *)lmemo;
     while (true) {
         DFS_STAT(n_steps++);
-        const uint32_t req = wrq & 0xFFFF, nvl = wrq >> 16;
-        const uint64_t cand = (ballot(req == s) | ballot(req == RQ_ANY)) & ~mask & above;
-        above = ~0ULL;
-        uint64_t absent = 0;
+        const uint32_t nvl = wrq >> 16;
+        uint64_t absent;
+        if (fresh) {
+            const uint32_t req = wrq & 0xFFFF;
+            absent = (ballot(req == s) | ballot(req == RQ_ANY)) & ~mask;
+        } else {
+            absent = rest;
+        }
         uint32_t u_r = t;
         uint64_t nm_r = 0;
         uint32_t klo = 0, khi = 0, b1 = 0, b2 = 0, n1 = 0, n2 = 0, h1 = 0, h2 = 0;
-        if (cand) {
-            if ((cand >> r) & 1) {
+        if (absent) {
+            if ((absent >> r) & 1) {
                 // lift RET[t]: drop its bit, then keep lifting while the next
                 // layer's RET op is already linearized (rarely more than once)
                 uint64_t nm = drop_bit(mask, r);
@@ -1258,32 +1269,34 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
             khi = (is_r ? hi_r : (hi_a | lb_hi)) | (nvl << 8);
             lk_hash(klo, khi, h1, h2);
             lk_bkts<M>(h1, h2, b1, b2);
-            const uint64_t k = ((uint64_t)khi << 32) | klo;
-            // one LDS round trip; non-candidate lanes all read bucket 0 (broadcast)
-            const bool cl = (cand >> lane) & 1;
+            const bool cl = (absent >> lane) & 1;
             const uint32_t a1 = cl ? b1 : 0u, a2 = cl ? b2 : 0u;
-            const ulonglong2 x0 = B[2 * a1], x1 = B[2 * a1 + 1];
-            const ulonglong2 y0 = B[2 * a2], y1 = B[2 * a2 + 1];
-            n1 = bcnt8[a1]; n2 = bcnt8[a2];
-            const uint64_t hit = ballot(x0.x == k) | ballot(x0.y == k) | ballot(x1.x == k) | ballot(x1.y == k) |
-                                 ballot(y0.x == k) | ballot(y0.y == k) | ballot(y1.x == k) | ballot(y1.y == k);
-            absent = cand & ~hit;
-            if (t < theta && absent) {
-                DFS_STAT(n_slow++);
-                // children below theta may sit in HBM: Bloom, then HBM for
-                // the lanes before the first surely-absent one
-                uint64_t low = absent;
-                if (u_r >= theta) low &= ~(1ULL << r);
-                const uint32_t kt = khi >> 16 & 0x7FFF, ks = (khi >> 8) & 0xFF;
-                const uint64_t km = k & ((1ULL << 40) - 1);
-                const bool maybe = ((low >> lane) & 1) && bloom_test2<M>(bloom, lk_bl(h1), lk_bl(h2));
-                const uint64_t bm = ballot(maybe);
-                const uint64_t sure = absent & ~bm;
-                const uint64_t lim = sure ? ((1ULL << __builtin_ctzll(sure)) - 1) : ~0ULL;
-                bool found = false;
-                if (((bm & lim) >> lane) & 1)
-                    found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
-                absent &= ~ballot(found);
+            if (fresh) {
+                // one LDS round trip; non-candidate lanes all read bucket 0 (broadcast)
+                const uint64_t k = ((uint64_t)khi << 32) | klo;
+                const ulonglong2 x0 = B[2 * a1], x1 = B[2 * a1 + 1];
+                const ulonglong2 y0 = B[2 * a2], y1 = B[2 * a2 + 1];
+                n1 = bcnt8[a1]; n2 = bcnt8[a2];
+                const uint64_t hit = ballot(x0.x == k) | ballot(x0.y == k) | ballot(x1.x == k) | ballot(x1.y == k) |
+                                     ballot(y0.x == k) | ballot(y0.y == k) | ballot(y1.x == k) | ballot(y1.y == k);
+                absent &= ~hit;
+                if (t < theta && absent) {
+                    DFS_STAT(n_slow++);
+                    // children below theta may sit in HBM: Bloom, then HBM for
+                    // every Bloom-positive lane (all at once), so that absent is
+                    // exact: the frame's rest relies on it
+                    uint64_t low = absent;
+                    if (u_r >= theta) low &= ~(1ULL << r);
+                    const uint32_t kt = khi >> 16 & 0x7FFF, ks = (khi >> 8) & 0xFF;
+                    const uint64_t km = k & ((1ULL << 40) - 1);
+                    const bool maybe = ((low >> lane) & 1) && bloom_test2<M>(bloom, lk_bl(h1), lk_bl(h2));
+                    bool found = false;
+                    if (maybe) found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
+                    absent &= ~ballot(found);
+                }
+            } else {
+                // every child in rest is absent: only the fill counts are needed
+                n1 = bcnt8[a1]; n2 = bcnt8[a2];
             }
         }
         if (absent) {
@@ -1337,20 +1350,24 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
                 if (kk < 32) {
                     Frame fr;
                     fr.mask = ((uint64_t)fm_hi << 32) | fm_lo; fr.t_i = f_ti; fr.s = (int32_t)f_s;
-                    fr.rest = 0; fr.pad[0] = fr.pad[1] = 0;
+                    fr.rest = ((uint64_t)fr_hi << 32) | fr_lo; fr.pad[0] = fr.pad[1] = 0;
                     stack[ring_lo + kk] = fr;
                 }
                 ring_lo += 32;
             }
             {
+                const uint64_t nrest = absent & (absent - 1);
                 const bool me = lane == (int)(depth & 63);
                 fm_lo = me ? (uint32_t)mask : fm_lo;
                 fm_hi = me ? (uint32_t)(mask >> 32) : fm_hi;
                 f_ti = me ? ((t << 6) | (uint32_t)i) : f_ti;
                 f_s = me ? s : f_s;
+                fr_lo = me ? (uint32_t)nrest : fr_lo;
+                fr_hi = me ? (uint32_t)(nrest >> 32) : fr_hi;
             }
             depth++;
             s = ns;
+            fresh = true;
             if (!to_r) {
                 mask |= 1ULL << i;
             } else {
@@ -1390,16 +1407,17 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
                 if (kk < depth - lo) {
                     const Frame fr = stack[lo + kk];
                     fm_lo = (uint32_t)fr.mask; fm_hi = (uint32_t)(fr.mask >> 32); f_ti = fr.t_i; f_s = (uint32_t)fr.s;
+                    fr_lo = (uint32_t)fr.rest; fr_hi = (uint32_t)(fr.rest >> 32);
                 }
                 ring_lo = lo;
             }
             depth--;
             const int ln = (int)(depth & 63);
-            const uint32_t ti = (uint32_t)readlane((int)f_ti, ln);
-            const uint32_t pt = ti >> 6, pi = ti & 63;
+            const uint32_t pt = (uint32_t)readlane((int)f_ti, ln) >> 6;
             mask = ((uint64_t)(uint32_t)readlane((int)fm_hi, ln) << 32) | (uint32_t)readlane((int)fm_lo, ln);
             s = (uint32_t)readlane((int)f_s, ln);
-            above = pi == 63 ? 0ULL : (~0ULL << (pi + 1));
+            rest = ((uint64_t)(uint32_t)readlane((int)fr_hi, ln) << 32) | (uint32_t)readlane((int)fr_lo, ln);
+            fresh = false;
             if (pt != t) {
                 // move the window back: drop appended ops, re-insert RETs
                 for (uint32_t u = t; u > pt; u--) {

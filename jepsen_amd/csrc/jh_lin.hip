@@ -1215,8 +1215,7 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
 
     load_lay(0);
     uint32_t t = 0, tmax = 0, depth = 0, ring_lo = 0;
-    uint64_t mask = 0, rest = 0;
-    bool fresh = true;                                 // false: just popped, candidates = rest
+    uint64_t mask = 0;
     uint32_t s = (uint32_t)A.init_state;
     int verdict = -1;
     uint32_t ins = 0;
@@ -1229,215 +1228,231 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
     load_up(P);
     wave_sync();
     const ulonglong2 *B = (const ulonglong2 *)lmemo;
-    while (true) {
-        DFS_STAT(n_steps++);
-        const uint32_t nvl = wrq >> 16;
-        uint64_t absent;
-        if (fresh) {
-            const uint32_t req = wrq & 0xFFFF;
-            absent = (ballot(req == s) | ballot(req == RQ_ANY)) & ~mask;
-        } else {
-            absent = rest;
+    // per-step values shared by the two ways into an insert
+    uint64_t absent = 0, nm_r = 0;
+    uint32_t u_r = 0, klo = 0, khi = 0, b1 = 0, b2 = 0, n1 = 0, n2 = 0, h1 = 0, h2 = 0, nvl = 0;
+    // the RET child of the current configuration (lifted) and the child keys of all lanes
+    auto child_keys = [&]() {
+        u_r = t; nm_r = 0;
+        if ((absent >> r) & 1) {
+            // lift RET[t]: drop its bit, then keep lifting while the next
+            // layer's RET op is already linearized (rarely more than once)
+            uint64_t nm = drop_bit(mask, r);
+            uint32_t u = t + 1;
+            if (u >= n_ok) nm = 0;
+            else if ((nm >> rn) & 1) {
+                uint32_t ru = rn;
+                for (;;) {
+                    nm = drop_bit(nm, ru);
+                    u++;
+                    if (u >= n_ok) { nm = 0; break; }
+                    ru = lay_hi(u) & 63;
+                    if (!((nm >> ru) & 1)) break;
+                }
+            }
+            u_r = u; nm_r = nm;
         }
-        uint32_t u_r = t;
-        uint64_t nm_r = 0;
-        uint32_t klo = 0, khi = 0, b1 = 0, b2 = 0, n1 = 0, n2 = 0, h1 = 0, h2 = 0;
-        if (absent) {
-            if ((absent >> r) & 1) {
-                // lift RET[t]: drop its bit, then keep lifting while the next
-                // layer's RET op is already linearized (rarely more than once)
-                uint64_t nm = drop_bit(mask, r);
-                uint32_t u = t + 1;
-                if (u >= n_ok) nm = 0;
-                else if ((nm >> rn) & 1) {
-                    uint32_t ru = rn;
-                    for (;;) {
-                        nm = drop_bit(nm, ru);
-                        u++;
-                        if (u >= n_ok) { nm = 0; break; }
-                        ru = lay_hi(u) & 63;
-                        if (!((nm >> ru) & 1)) break;
-                    }
-                }
-                u_r = u; nm_r = nm;
-            }
-            // child keys 1:1|t:15|state:8|mask:40, all lanes at once
-            const bool is_r = lane == (int)r;
-            const uint32_t hi_a = (uint32_t)(mask >> 32) | (t << 16) | 0x80000000u;
-            const uint32_t hi_r = (uint32_t)(nm_r >> 32) | (u_r << 16) | 0x80000000u;
-            klo = is_r ? (uint32_t)nm_r : ((uint32_t)mask | lb_lo);
-            khi = (is_r ? hi_r : (hi_a | lb_hi)) | (nvl << 8);
-            lk_hash(klo, khi, h1, h2);
-            lk_bkts<M>(h1, h2, b1, b2);
-            const bool cl = (absent >> lane) & 1;
-            const uint32_t a1 = cl ? b1 : 0u, a2 = cl ? b2 : 0u;
-            if (fresh) {
-                // one LDS round trip; non-candidate lanes all read bucket 0 (broadcast)
-                const uint64_t k = ((uint64_t)khi << 32) | klo;
-                const ulonglong2 x0 = B[2 * a1], x1 = B[2 * a1 + 1];
-                const ulonglong2 y0 = B[2 * a2], y1 = B[2 * a2 + 1];
-                n1 = bcnt8[a1]; n2 = bcnt8[a2];
-                const uint64_t hit = ballot(x0.x == k) | ballot(x0.y == k) | ballot(x1.x == k) | ballot(x1.y == k) |
-                                     ballot(y0.x == k) | ballot(y0.y == k) | ballot(y1.x == k) | ballot(y1.y == k);
-                absent &= ~hit;
-                if (t < theta && absent) {
-                    DFS_STAT(n_slow++);
-                    // children below theta may sit in HBM: Bloom, then HBM for
-                    // every Bloom-positive lane (all at once), so that absent is
-                    // exact: the frame's rest relies on it
-                    uint64_t low = absent;
-                    if (u_r >= theta) low &= ~(1ULL << r);
-                    const uint32_t kt = khi >> 16 & 0x7FFF, ks = (khi >> 8) & 0xFF;
-                    const uint64_t km = k & ((1ULL << 40) - 1);
-                    const bool maybe = ((low >> lane) & 1) && bloom_test2<M>(bloom, lk_bl(h1), lk_bl(h2));
-                    bool found = false;
-                    if (maybe) found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
-                    absent &= ~ballot(found);
-                }
-            } else {
-                // every child in rest is absent: only the fill counts are needed
-                n1 = bcnt8[a1]; n2 = bcnt8[a2];
-            }
-        }
-        if (absent) {
-            if (ins >= chk) {
-                if (ins >= budget) { verdict = JH_UNKNOWN; break; }
-                if (A.claim) {
-                    // racing k_lin_bfs: stop if it settled this key first
-                    int c = 0;
-                    if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (readlane(c, 0)) { verdict = JH_CANCELLED; break; }
-                }
-                chk = min(budget, ins + 1024);
-            }
-            const int i = __builtin_ctzll(absent);
-            ins++;
-            const uint32_t ns = (uint32_t)readlane((int)nvl, i);
-            const bool to_r = (uint32_t)i == r;
-            const uint32_t nt = to_r ? u_r : t;
-            {
-                // into the emptier of the child's two buckets
-                const bool pick1 = n1 <= n2;
-                const uint32_t bs = pick1 ? b1 : b2, nsl = pick1 ? n1 : n2;
-                const uint64_t full_m = ballot(nsl >= 4);
-                if (!((full_m >> i) & 1)) {
-                    if (lane == i) {
-                        lmemo[4 * bs + nsl] = ((uint64_t)khi << 32) | klo;
-                        bcnt8[bs] = (uint8_t)(nsl + 1);
-                    }
-                    if (++lcount >= M::EVICT) {
-                        DFS_STAT(n_evict++);
-                        const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
-                        lcount = rfl((int)(uint32_t)er);
-                        theta = rflu((uint32_t)(er >> 32));
-                    }
-                } else {
-                    // both buckets full: HBM, and theta rises above the layer
-                    const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
-                    if (lane == i) {
-                        hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
-                        bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
-                    }
-                    theta = max(theta, nt + 1);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                }
-            }
-            // push the parent; a full ring spills its oldest half to HBM
-            if (depth - ring_lo == 64) {
-                DFS_STAT(n_spill++);
-                const uint32_t kk = ((uint32_t)lane - ring_lo) & 63;
-                if (kk < 32) {
-                    Frame fr;
-                    fr.mask = ((uint64_t)fm_hi << 32) | fm_lo; fr.t_i = f_ti; fr.s = (int32_t)f_s;
-                    fr.rest = ((uint64_t)fr_hi << 32) | fr_lo; fr.pad[0] = fr.pad[1] = 0;
-                    stack[ring_lo + kk] = fr;
-                }
-                ring_lo += 32;
-            }
-            {
-                const uint64_t nrest = absent & (absent - 1);
-                const bool me = lane == (int)(depth & 63);
-                fm_lo = me ? (uint32_t)mask : fm_lo;
-                fm_hi = me ? (uint32_t)(mask >> 32) : fm_hi;
-                f_ti = me ? ((t << 6) | (uint32_t)i) : f_ti;
-                f_s = me ? s : f_s;
-                fr_lo = me ? (uint32_t)nrest : fr_lo;
-                fr_hi = me ? (uint32_t)(nrest >> 32) : fr_hi;
-            }
-            depth++;
-            s = ns;
-            fresh = true;
-            if (!to_r) {
-                mask |= 1ULL << i;
-            } else {
-                mask = nm_r;
-                if (nt >= n_ok) { t = nt; tmax = max(tmax, t); verdict = JH_VALID; break; }
-                // move the window forward layer by layer
-                for (uint32_t u = t; u < nt; u++) {
-                    const uint32_t ru = u == t ? r : (lay_hi(u) & 63);
-                    const uint32_t sh = (uint32_t)wave_shl1((int)wrq);
-                    if (lane >= (int)ru) wrq = sh;
-                    w--;
-                    if (lane == w) wrq = RQ_EMPTY;
-                    const int c = (int)(lay_hi(u + 1) >> 6);
-                    if (c > 0) {
-                        if (P < pb || P + c > pb + 64) load_up(c <= 32 && P >= 32 ? P - 32 : P);
-                        for (int kk = 0; kk < c; kk++) {
-                            const uint32_t x = (uint32_t)readlane((int)urq, P - pb + kk);
-                            if (lane == w + kk) wrq = x;
-                        }
-                        w += c; P += c;
-                    }
-                }
-                t = nt;
-                tmax = max(tmax, t);
-                r = lay_hi(t) & 63;
-                rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
-            }
-        } else {
-            if (depth == ring_lo) {
-                if (depth == 0) { verdict = JH_INVALID; break; }
-                // ring empty: refill up to 32 frames below from the HBM stack
-                DFS_STAT(n_refill++);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                const uint32_t lo = depth >= 32 ? depth - 32 : 0;
-                const uint32_t kk = ((uint32_t)lane - lo) & 63;
-                if (kk < depth - lo) {
-                    const Frame fr = stack[lo + kk];
-                    fm_lo = (uint32_t)fr.mask; fm_hi = (uint32_t)(fr.mask >> 32); f_ti = fr.t_i; f_s = (uint32_t)fr.s;
-                    fr_lo = (uint32_t)fr.rest; fr_hi = (uint32_t)(fr.rest >> 32);
-                }
-                ring_lo = lo;
-            }
-            depth--;
-            const int ln = (int)(depth & 63);
-            const uint32_t pt = (uint32_t)readlane((int)f_ti, ln) >> 6;
-            mask = ((uint64_t)(uint32_t)readlane((int)fm_hi, ln) << 32) | (uint32_t)readlane((int)fm_lo, ln);
-            s = (uint32_t)readlane((int)f_s, ln);
-            rest = ((uint64_t)(uint32_t)readlane((int)fr_hi, ln) << 32) | (uint32_t)readlane((int)fr_lo, ln);
-            fresh = false;
-            if (pt != t) {
-                // move the window back: drop appended ops, re-insert RETs
-                for (uint32_t u = t; u > pt; u--) {
-                    const int c = (int)(lay_hi(u) >> 6);
-                    w -= c; P -= c;
-                    if (lane >= w) wrq = RQ_EMPTY;
-                    const uint32_t h = lay_hi(u - 1);
-                    const int ru = (int)(h & 63);
-                    const uint32_t sh = (uint32_t)wave_shr1((int)wrq);
-                    if (lane > ru) wrq = sh;
-                    const uint32_t x = (uint32_t)readlane((int)drq, (int)(u - 1 - tb0));
-                    if (lane == ru) wrq = x;
-                    w++;
-                }
-                t = pt;
-                r = lay_hi(t) & 63;
-                rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
-            }
+        // child keys 1:1|t:15|state:8|mask:40, all lanes at once
+        nvl = wrq >> 16;
+        const bool is_r = lane == (int)r;
+        const uint32_t hi_a = (uint32_t)(mask >> 32) | (t << 16) | 0x80000000u;
+        const uint32_t hi_r = (uint32_t)(nm_r >> 32) | (u_r << 16) | 0x80000000u;
+        klo = is_r ? (uint32_t)nm_r : ((uint32_t)mask | lb_lo);
+        khi = (is_r ? hi_r : (hi_a | lb_hi)) | (nvl << 8);
+        lk_hash(klo, khi, h1, h2);
+        lk_bkts<M>(h1, h2, b1, b2);
+    };
+
+expand:
+    // a configuration entered by a push: probe every candidate child
+    DFS_STAT(n_steps++);
+    {
+        const uint32_t req = wrq & 0xFFFF;
+        absent = (ballot(req == s) | ballot(req == RQ_ANY)) & ~mask;
+    }
+    if (!absent) goto pop;
+    child_keys();
+    {
+        // one LDS round trip; non-candidate lanes all read bucket 0 (broadcast)
+        const bool cl = (absent >> lane) & 1;
+        const uint32_t a1 = cl ? b1 : 0u, a2 = cl ? b2 : 0u;
+        const uint64_t k = ((uint64_t)khi << 32) | klo;
+        const ulonglong2 x0 = B[2 * a1], x1 = B[2 * a1 + 1];
+        const ulonglong2 y0 = B[2 * a2], y1 = B[2 * a2 + 1];
+        n1 = bcnt8[a1]; n2 = bcnt8[a2];
+        const uint64_t hit = ballot(x0.x == k) | ballot(x0.y == k) | ballot(x1.x == k) | ballot(x1.y == k) |
+                             ballot(y0.x == k) | ballot(y0.y == k) | ballot(y1.x == k) | ballot(y1.y == k);
+        absent &= ~hit;
+        if (t < theta && absent) {
+            DFS_STAT(n_slow++);
+            // children below theta may sit in HBM: Bloom, then HBM for every
+            // Bloom-positive lane (all at once), so that absent is exact: the
+            // frame's rest relies on it
+            uint64_t low = absent;
+            if (u_r >= theta) low &= ~(1ULL << r);
+            const uint32_t kt = khi >> 16 & 0x7FFF, ks = (khi >> 8) & 0xFF;
+            const uint64_t km = k & ((1ULL << 40) - 1);
+            const bool maybe = ((low >> lane) & 1) && bloom_test2<M>(bloom, lk_bl(h1), lk_bl(h2));
+            bool found = false;
+            if (maybe) found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
+            absent &= ~ballot(found);
         }
     }
+    if (!absent) goto pop;
+
+insert:
+    {
+        if (ins >= chk) {
+            if (ins >= budget) { verdict = JH_UNKNOWN; goto done; }
+            if (A.claim) {
+                // racing k_lin_bfs: stop if it settled this key first
+                int c = 0;
+                if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (readlane(c, 0)) { verdict = JH_CANCELLED; goto done; }
+            }
+            chk = min(budget, ins + 1024);
+        }
+        const int i = __builtin_ctzll(absent);
+        ins++;
+        const uint32_t ns = (uint32_t)readlane((int)nvl, i);
+        const bool to_r = (uint32_t)i == r;
+        const uint32_t nt = to_r ? u_r : t;
+        {
+            // into the emptier of the child's two buckets
+            const bool pick1 = n1 <= n2;
+            const uint32_t bs = pick1 ? b1 : b2, nsl = pick1 ? n1 : n2;
+            const uint64_t full_m = ballot(nsl >= 4);
+            if (!((full_m >> i) & 1)) {
+                if (lane == i) {
+                    lmemo[4 * bs + nsl] = ((uint64_t)khi << 32) | klo;
+                    bcnt8[bs] = (uint8_t)(nsl + 1);
+                }
+                if (++lcount >= M::EVICT) {
+                    DFS_STAT(n_evict++);
+                    const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
+                    lcount = rfl((int)(uint32_t)er);
+                    theta = rflu((uint32_t)(er >> 32));
+                }
+            } else {
+                // both buckets full: HBM, and theta rises above the layer
+                const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
+                if (lane == i) {
+                    hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
+                    bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
+                }
+                theta = max(theta, nt + 1);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
+        }
+        // push the parent; a full ring spills its oldest half to HBM
+        if (depth - ring_lo == 64) {
+            DFS_STAT(n_spill++);
+            const uint32_t kk = ((uint32_t)lane - ring_lo) & 63;
+            if (kk < 32) {
+                Frame fr;
+                fr.mask = ((uint64_t)fm_hi << 32) | fm_lo; fr.t_i = f_ti; fr.s = (int32_t)f_s;
+                fr.rest = ((uint64_t)fr_hi << 32) | fr_lo; fr.pad[0] = fr.pad[1] = 0;
+                stack[ring_lo + kk] = fr;
+            }
+            ring_lo += 32;
+        }
+        {
+            const uint64_t nrest = absent & (absent - 1);
+            const bool me = lane == (int)(depth & 63);
+            fm_lo = me ? (uint32_t)mask : fm_lo;
+            fm_hi = me ? (uint32_t)(mask >> 32) : fm_hi;
+            f_ti = me ? ((t << 6) | (uint32_t)i) : f_ti;
+            f_s = me ? s : f_s;
+            fr_lo = me ? (uint32_t)nrest : fr_lo;
+            fr_hi = me ? (uint32_t)(nrest >> 32) : fr_hi;
+        }
+        depth++;
+        s = ns;
+        if (!to_r) {
+            mask |= 1ULL << i;
+            goto expand;
+        }
+        mask = nm_r;
+        if (nt >= n_ok) { t = nt; tmax = max(tmax, t); verdict = JH_VALID; goto done; }
+        // move the window forward layer by layer
+        for (uint32_t u = t; u < nt; u++) {
+            const uint32_t ru = u == t ? r : (lay_hi(u) & 63);
+            const uint32_t sh = (uint32_t)wave_shl1((int)wrq);
+            if (lane >= (int)ru) wrq = sh;
+            w--;
+            if (lane == w) wrq = RQ_EMPTY;
+            const int c = (int)(lay_hi(u + 1) >> 6);
+            if (c > 0) {
+                if (P < pb || P + c > pb + 64) load_up(c <= 32 && P >= 32 ? P - 32 : P);
+                for (int kk = 0; kk < c; kk++) {
+                    const uint32_t x = (uint32_t)readlane((int)urq, P - pb + kk);
+                    if (lane == w + kk) wrq = x;
+                }
+                w += c; P += c;
+            }
+        }
+        t = nt;
+        tmax = max(tmax, t);
+        r = lay_hi(t) & 63;
+        rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
+        goto expand;
+    }
+
+pop:
+    DFS_STAT(n_steps++);
+    if (depth == ring_lo) {
+        if (depth == 0) { verdict = JH_INVALID; goto done; }
+        // ring empty: refill up to 32 frames below from the HBM stack
+        DFS_STAT(n_refill++);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t lo = depth >= 32 ? depth - 32 : 0;
+        const uint32_t kk = ((uint32_t)lane - lo) & 63;
+        if (kk < depth - lo) {
+            const Frame fr = stack[lo + kk];
+            fm_lo = (uint32_t)fr.mask; fm_hi = (uint32_t)(fr.mask >> 32); f_ti = fr.t_i; f_s = (uint32_t)fr.s;
+            fr_lo = (uint32_t)fr.rest; fr_hi = (uint32_t)(fr.rest >> 32);
+        }
+        ring_lo = lo;
+    }
+    depth--;
+    {
+        const int ln = (int)(depth & 63);
+        absent = ((uint64_t)(uint32_t)readlane((int)fr_hi, ln) << 32) | (uint32_t)readlane((int)fr_lo, ln);
+        const uint32_t pt = (uint32_t)readlane((int)f_ti, ln) >> 6;
+        mask = ((uint64_t)(uint32_t)readlane((int)fm_hi, ln) << 32) | (uint32_t)readlane((int)fm_lo, ln);
+        s = (uint32_t)readlane((int)f_s, ln);
+        if (pt != t) {
+            // move the window back: drop appended ops, re-insert RETs
+            for (uint32_t u = t; u > pt; u--) {
+                const int c = (int)(lay_hi(u) >> 6);
+                w -= c; P -= c;
+                if (lane >= w) wrq = RQ_EMPTY;
+                const uint32_t h = lay_hi(u - 1);
+                const int ru = (int)(h & 63);
+                const uint32_t sh = (uint32_t)wave_shr1((int)wrq);
+                if (lane > ru) wrq = sh;
+                const uint32_t x = (uint32_t)readlane((int)drq, (int)(u - 1 - tb0));
+                if (lane == ru) wrq = x;
+                w++;
+            }
+            t = pt;
+            r = lay_hi(t) & 63;
+            rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
+        }
+    }
+    // every child in rest is absent (see above): only its bucket fill counts are needed
+    if (!absent) goto pop;
+    child_keys();
+    {
+        const bool cl = (absent >> lane) & 1;
+        const uint32_t a1 = cl ? b1 : 0u, a2 = cl ? b2 : 0u;
+        n1 = bcnt8[a1]; n2 = bcnt8[a2];
+    }
+    goto insert;
+
+done:
     inserts = ins;
     tmax_out = tmax;
 #ifdef JH_DFS_STATS

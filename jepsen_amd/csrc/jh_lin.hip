@@ -1277,9 +1277,11 @@ expand:
         const bool cl = (absent >> lane) & 1;
         const uint32_t a1 = cl ? b1 : 0u, a2 = cl ? b2 : 0u;
         const uint64_t k = ((uint64_t)khi << 32) | klo;
+        // the fill counts first, in the same LDS round trip as the slots
+        n1 = bcnt8[a1]; n2 = bcnt8[a2];
+        __builtin_amdgcn_sched_barrier(0);
         const ulonglong2 x0 = B[2 * a1], x1 = B[2 * a1 + 1];
         const ulonglong2 y0 = B[2 * a2], y1 = B[2 * a2 + 1];
-        n1 = bcnt8[a1]; n2 = bcnt8[a2];
         const uint64_t hit = ballot(x0.x == k) | ballot(x0.y == k) | ballot(x1.x == k) | ballot(x1.y == k) |
                              ballot(y0.x == k) | ballot(y0.y == k) | ballot(y1.x == k) | ballot(y1.y == k);
         absent &= ~hit;

@@ -194,26 +194,57 @@ __global__ void k_gather(const int64_t *__restrict__ proc, const int64_t *__rest
 
 // knossos.history/complete pairing (cassandra/src/cassandra/checker.clj:7-62):
 // the completion of an invocation is the next entry of the same process
-// that is not :info; an :invoke there is a double invocation.
-__global__ void k_pair(const Rec *__restrict__ rec, const uint32_t *__restrict__ sk,
-                       const uint32_t *__restrict__ off, int64_t m, int32_t *__restrict__ pair,
-                       unsigned long long *__restrict__ viol) {
-    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < m;
-         p += (int64_t)gridDim.x * blockDim.x) {
-        Rec x = rec[p];
-        if (x.proc < 0 || x.type != T_INVOKE) continue;
-        uint32_t k = sk[p];
-        uint32_t end = off[k + 1];
-        for (uint32_t j = (uint32_t)p + 1; j < end; j++) {
-            Rec y = rec[j];
-            if (y.proc != x.proc || y.type == T_INFO) continue;
-            if (y.type == T_INVOKE) {
-                atomicMin(&viol[k], ((unsigned long long)j << 4) | JH_CAUSE_DOUBLE_INVOKE);
-            } else {
-                pair[p] = (int32_t)j;
-                pair[j] = (int32_t)p;
+// that is not :info; an :invoke there is a double invocation. One wave per
+// 64 consecutive sorted positions walks 64-row windows of the records: for
+// each distinct (key, process) among its still-open invocations one ballot
+// gives every candidate row, and each open lane takes the first one after
+// its own position; a lane stops at its key segment's end.
+__global__ void __launch_bounds__(256) k_pair(const Rec *__restrict__ rec, const uint32_t *__restrict__ sk,
+                                              const uint32_t *__restrict__ off, int64_t m,
+                                              int32_t *__restrict__ pair,
+                                              unsigned long long *__restrict__ viol) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); wv * 64 < m; wv += nw) {
+        const int64_t base = wv * 64, p = base + lane;
+        int32_t xp = -1, xt = T_INFO;
+        uint32_t k = 0;
+        if (p < m) { const Rec x = rec[p]; xp = x.proc; xt = x.type; k = sk[p]; }
+        const bool inv = p < m && xp >= 0 && xt == T_INVOKE;
+        const int64_t end = inv ? (int64_t)off[k + 1] : 0;
+        bool open = inv && end > p + 1;
+        int64_t got = -1;
+        int gtype = 0;
+        for (int64_t wb = base; wb < m; wb += 64) {
+            if (!__ballot(open)) break;
+            const int64_t j = wb + lane;
+            int32_t yp = -1, yt = T_INFO;
+            uint32_t yk = 0xFFFFFFFFu;
+            if (j < m) { const Rec y = rec[j]; yp = y.proc; yt = y.type; yk = sk[j]; }
+            uint64_t todo = __ballot(open);
+            while (todo) {
+                const int l = __builtin_ctzll(todo);
+                const int32_t pl = __builtin_amdgcn_readlane(xp, l);
+                const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)k, l);
+                const uint64_t mine = __ballot(open && xp == pl && k == kl);
+                const uint64_t cand = __ballot(yp == pl && yk == kl && yt != T_INFO);
+                const uint64_t cinv = __ballot(yt == T_INVOKE);
+                todo &= ~mine;
+                if ((mine >> lane) & 1) {
+                    const int64_t rel = p - wb;
+                    const uint64_t after = rel < 0 ? ~0ULL : (rel >= 63 ? 0ULL : (~0ULL << (rel + 1)));
+                    const uint64_t c = cand & after;
+                    if (c) {
+                        const int b = __builtin_ctzll(c);
+                        got = wb + b; gtype = (int)((cinv >> b) & 1); open = false;
+                    }
+                }
             }
-            break;
+            if (open && wb + 64 >= end) open = false;
+        }
+        if (got >= 0) {
+            if (gtype) atomicMin(&viol[k], ((unsigned long long)got << 4) | JH_CAUSE_DOUBLE_INVOKE);
+            else { pair[p] = (int32_t)got; pair[got] = (int32_t)p; }
         }
     }
 }
@@ -2033,7 +2064,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipMemsetAsync(pair, 0xFF, sizeof(int32_t) * m, st));
         k_gather<<<grid_for(m, 256), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, dh->value2,
                                                    rB, m, vmin, rec);
-        k_pair<<<grid_for(m, 256), 256, 0, st>>>(rec, kB, off, m, pair, viol);
+        k_pair<<<grid_for((m + 63) / 64, 4, 16384), 256, 0, st>>>(rec, kB, off, m, pair, viol);
         k_orphan<<<grid_for(m, 256), 256, 0, st>>>(rec, kB, m, pair, viol);
     }
 

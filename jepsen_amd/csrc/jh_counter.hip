@@ -37,7 +37,7 @@ struct CntMeta {
     long long n_reads;
 };
 
-__global__ void k_cnt_range(const int64_t *__restrict__ proc, const int64_t *__restrict__ type,
+__global__ void __launch_bounds__(256) k_cnt_range(const int64_t *__restrict__ proc, const int64_t *__restrict__ type,
                             const int64_t *__restrict__ f, const int64_t *__restrict__ val,
                             int64_t n, CntMeta *m) {
     long long lo = LLONG_MAX, hi = LLONG_MIN, am = 0, na = 0;
@@ -51,14 +51,15 @@ __global__ void k_cnt_range(const int64_t *__restrict__ proc, const int64_t *__r
             na++;
         }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        lo = min(lo, __shfl_xor(lo, o)); hi = max(hi, __shfl_xor(hi, o));
-        am = max(am, __shfl_xor(am, o)); na += __shfl_xor(na, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
+    __shared__ long long sh[4];
+    lo = block_reduce256(lo, RedMin(), sh);
+    hi = block_reduce256(hi, RedMax(), sh);
+    am = block_reduce256(am, RedMax(), sh);
+    na = block_reduce256(na, RedSum(), sh);
+    if (threadIdx.x == 0) {
         atomicMin(&m->pmin, lo); atomicMax(&m->pmax, hi);
         atomicMax(&m->amax_abs, am);
-        atomicAdd((unsigned long long *)&m->n_add, (unsigned long long)na);
+        if (na) atomicAdd((unsigned long long *)&m->n_add, (unsigned long long)na);
     }
 }
 

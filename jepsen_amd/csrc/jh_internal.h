@@ -101,6 +101,22 @@ __device__ __forceinline__ uint64_t jh_mix64(uint64_t x) {
     x ^= x >> 33; return x;
 }
 
+// Block-wide reduction for 256-thread blocks (4 waves): one value per block,
+// so a reduction kernel issues one global atomic per block, not per wave
+// (per-wave atomics on a few addresses serialise in L2).
+template <class T, class Op>
+__device__ __forceinline__ T block_reduce256(T v, Op op, T *sh /* [4] shared */) {
+    for (int o = 32; o > 0; o >>= 1) v = op(v, (T)__shfl_xor(v, o));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return op(op(sh[0], sh[1]), op(sh[2], sh[3]));
+}
+struct RedMin { template <class T> __device__ T operator()(T a, T b) const { return a < b ? a : b; } };
+struct RedMax { template <class T> __device__ T operator()(T a, T b) const { return a > b ? a : b; } };
+struct RedSum { template <class T> __device__ T operator()(T a, T b) const { return a + b; } };
+struct RedOr { template <class T> __device__ T operator()(T a, T b) const { return a | b; } };
+
 inline int grid_for(int64_t n, int block, int cap = 65536) {
     int64_t g = (n + block - 1) / block;
     if (g < 1) g = 1;

@@ -100,7 +100,7 @@ __device__ __forceinline__ int f_code(int64_t f) {
     return f == JH_F_READ ? F_READ : f == JH_F_WRITE ? F_WRITE : f == JH_F_CAS ? F_CAS : F_OTHER;
 }
 
-__global__ void k_range(const int64_t *__restrict__ proc, const int64_t *__restrict__ f,
+__global__ void __launch_bounds__(256) k_range(const int64_t *__restrict__ proc, const int64_t *__restrict__ f,
                         const int64_t *__restrict__ key, const int64_t *__restrict__ v1,
                         const int64_t *__restrict__ v2, int64_t n, int keyed, RangeOut *out) {
     long long lo = LLONG_MAX, hi = LLONG_MIN, pm = -1;
@@ -121,17 +121,16 @@ __global__ void k_range(const int64_t *__restrict__ proc, const int64_t *__restr
             }
         }
     }
-    // wave reduce
-    for (int o = 32; o > 0; o >>= 1) {
-        lo = min(lo, __shfl_xor(lo, o));
-        hi = max(hi, __shfl_xor(hi, o));
-        pm = max(pm, __shfl_xor(pm, o));
-        unk |= __shfl_xor(unk, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicMin(&out->vmin, lo);
-        atomicMax(&out->vmax, hi);
-        atomicMax(&out->pmax, pm);
+    __shared__ long long sh[4];
+    __shared__ int shi[4];
+    lo = block_reduce256(lo, RedMin(), sh);
+    hi = block_reduce256(hi, RedMax(), sh);
+    pm = block_reduce256(pm, RedMax(), sh);
+    unk = block_reduce256(unk, RedOr(), shi);
+    if (threadIdx.x == 0) {
+        if (lo != LLONG_MAX) atomicMin(&out->vmin, lo);
+        if (hi != LLONG_MIN) atomicMax(&out->vmax, hi);
+        if (pm >= 0) atomicMax(&out->pmax, pm);
         if (unk) atomicOr(&out->unkeyed_client, 1);
     }
 }

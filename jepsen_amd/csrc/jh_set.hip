@@ -26,7 +26,7 @@ struct SetMeta {
     unsigned long long first_lost_row;
 };
 
-__global__ void k_set_scan(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
+__global__ void __launch_bounds__(256) k_set_scan(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
                            const int64_t *__restrict__ val, int64_t n, SetMeta *m) {
     long long lo = LLONG_MAX, hi = LLONG_MIN, fr = -1;
     int na = 0, nd = 0;
@@ -39,27 +39,36 @@ __global__ void k_set_scan(const int64_t *__restrict__ type, const int64_t *__re
             else { lo = min(lo, (long long)v); hi = max(hi, (long long)v); }
         } else if (ff == JH_F_READ && ty == T_OK) fr = max(fr, (long long)r);
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        lo = min(lo, __shfl_xor(lo, o)); hi = max(hi, __shfl_xor(hi, o));
-        fr = max(fr, __shfl_xor(fr, o));
-        na |= __shfl_xor(na, o); nd |= __shfl_xor(nd, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicMin(&m->vmin, lo); atomicMax(&m->vmax, hi); atomicMax(&m->final_row, fr);
+    __shared__ long long sh[4];
+    __shared__ int shi[4];
+    lo = block_reduce256(lo, RedMin(), sh);
+    hi = block_reduce256(hi, RedMax(), sh);
+    fr = block_reduce256(fr, RedMax(), sh);
+    na = block_reduce256(na, RedOr(), shi);
+    nd = block_reduce256(nd, RedOr(), shi);
+    if (threadIdx.x == 0) {
+        if (lo != LLONG_MAX) atomicMin(&m->vmin, lo);
+        if (hi != LLONG_MIN) atomicMax(&m->vmax, hi);
+        if (fr >= 0) atomicMax(&m->final_row, fr);
         if (na) atomicOr(&m->nil_attempt, 1);
         if (nd) atomicOr(&m->nil_add, 1);
     }
 }
 
-__global__ void k_set_range(const int64_t *__restrict__ aux, int64_t off, int64_t cnt, SetMeta *m) {
+__global__ void __launch_bounds__(256) k_set_range(const int64_t *__restrict__ aux, int64_t off, int64_t cnt, SetMeta *m) {
     long long lo = LLONG_MAX, hi = LLONG_MIN;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cnt;
          i += (int64_t)gridDim.x * blockDim.x) {
         const long long v = aux[off + i];
         lo = min(lo, v); hi = max(hi, v);
     }
-    for (int o = 32; o > 0; o >>= 1) { lo = min(lo, __shfl_xor(lo, o)); hi = max(hi, __shfl_xor(hi, o)); }
-    if ((threadIdx.x & 63) == 0) { atomicMin(&m->vmin, lo); atomicMax(&m->vmax, hi); }
+    __shared__ long long sh[4];
+    lo = block_reduce256(lo, RedMin(), sh);
+    hi = block_reduce256(hi, RedMax(), sh);
+    if (threadIdx.x == 0) {
+        if (lo != LLONG_MAX) atomicMin(&m->vmin, lo);
+        if (hi != LLONG_MIN) atomicMax(&m->vmax, hi);
+    }
 }
 
 // Marking is privatised per workgroup: a chunk of MARK_CH rows (or read

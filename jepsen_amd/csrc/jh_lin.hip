@@ -1845,8 +1845,14 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         while (sh.nfront > 0 && !sh.status) {
             rounds++;
             const unsigned nf = sh.nfront;
-            if (tid == 0) sh.nnext = 0;
+            if (tid == 0) {
+                sh.nnext = 0;
+                // the sequential search settled this key: stop at the next round
+                if (A.claim && __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    sh.status |= 4;
+            }
             __syncthreads();
+            if (sh.status & 4) break;
             for (;;) {
             for (unsigned i = tid; i < nf; i += BFS_THREADS) {
                 const uint64_t c = fcur[i];

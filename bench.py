@@ -26,6 +26,18 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: 8 TB/s HBM3E (spec)
 BYTES_PER_ENTRY = 56           # 7 x int64 columns read once
 BYTES_PER_PROBE = 16           # one memo entry {mask, t|state|gen}
+# HBM bytes per launch of k_lin_dfs<LEAN> from the rocprofv3 FETCH_SIZE and
+# WRITE_SIZE passes of the same workload (tools/gpu_profile.sh ->
+# tools/pmc_traffic.py); PMC counters cannot be read inside a timed run
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic_k_lin_dfs.json")
+
+
+def pmc_traffic():
+    try:
+        with open(TRAFFIC_JSON) as fh:
+            return float(json.load(fh)["traffic_bytes"])
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def parse():
@@ -165,7 +177,7 @@ def main():
                        "unknown_keys": int(s.n_unknown), "device_ms": float(np.mean(dev_ms))},
             "roofline": {"bound": "hbm", "kernel": "k_lin_dfs (phase 1: every key, quick budget)", "achieved": achieved,
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                         "traffic": None, "kernel_ms": dfs_avg * 1e3,
+                         "traffic": pmc_traffic(), "kernel_ms": dfs_avg * 1e3,
                          "alg_bytes": alg_bytes},
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,

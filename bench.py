@@ -40,16 +40,37 @@ def pmc_traffic():
         return None
 
 
+# SURVEY.md 8(d) configurations. Each rank checks its own shard (weak scaling).
+WORKLOADS = {
+    "c3": dict(desc="C3: independent cas-register, 10000 keys x ~1k entries per GPU", keys=10000,
+               seed=3, cpu_keys=10000,
+               gen=dict(threads_per_key=10, readers=5, n_values=5, process_limit=20, groups=10,
+                        init_nil=True, p_info=0.02, p_invalid=0.01, nemesis_every=10000)),
+    "c4": dict(desc="C4: independent cas-register, 1M keys over 8 GPUs: a 125000-key shard "
+                    "(~125M entries) per GPU", keys=125000, seed=4, cpu_keys=3000,
+               gen=dict(threads_per_key=10, readers=5, n_values=5, process_limit=20, groups=10,
+                        init_nil=True, p_info=0.02, p_invalid=0.01, nemesis_every=10000)),
+    "c5": dict(desc="C5: independent cas-register, 1000 keys x ~1k entries, 50 threads per key, "
+                    "p_info 0.2 (deep searches, HBM memo stress)", keys=1000, seed=5, cpu_keys=48,
+               gen=dict(threads_per_key=50, readers=25, n_values=5, process_limit=100, groups=10,
+                        init_nil=True, p_info=0.2, p_invalid=0.01, nemesis_every=10000)),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--keys", type=int, default=10000)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
+                    help="c3 (default, BASELINE.json's metric): 10k keys per GPU; c4: a 125k-key "
+                         "shard of the 1M-key history (1/8 per GPU); c5: 50 threads per key, many :info")
+    ap.add_argument("--keys", type=int, default=None)
     ap.add_argument("--ops-per-key", type=int, default=500)
-    ap.add_argument("--cpu-sample-keys", type=int, default=10000,
-                    help="keys of the rank-0 history timed on the CPU (default: the whole C3 workload)")
+    ap.add_argument("--cpu-sample-keys", type=int, default=None,
+                    help="keys of the rank-0 history timed on the CPU (default per workload)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--e2e", type=int, default=1, help="also time one call from host buffers (PCIe-inclusive)")
     ap.add_argument("--no-parity", action="store_true")
     return ap.parse_args()
 
@@ -72,11 +93,10 @@ def main():
     from jepsen_amd import _native, synth
 
     # ---- workload: this rank's shard of the C3 configuration -------------
-    seed = 3 + 7919 * rank
-    cols, truth = synth.cas_register(n_keys=args.keys, ops_per_key=args.ops_per_key,
-                                     threads_per_key=10, readers=5, n_values=5, process_limit=20,
-                                     groups=10, init_nil=True, p_info=0.02, p_invalid=0.01,
-                                     nemesis_every=10000, seed=seed)
+    wl = WORKLOADS[args.workload]
+    n_keys = args.keys or wl["keys"]
+    seed = wl["seed"] + 7919 * rank
+    cols, truth = synth.cas_register(n_keys=n_keys, ops_per_key=args.ops_per_key, seed=seed, **wl["gen"])
     n_entries = int(cols.n)
     names = ["process", "type", "f", "key", "value", "value2"]
     dcols = {k: torch.from_numpy(getattr(cols, k)).to(dev) for k in names}
@@ -145,6 +165,14 @@ def main():
     alg_bytes = BYTES_PER_ENTRY * n_entries + BYTES_PER_PROBE * float(np.mean(probes))
     achieved = alg_bytes / dfs_avg / 1e9 if dfs_avg > 0 else 0.0
 
+    # end-to-end from host columns (H2D copy + check + verdicts D2H): the
+    # boundary's host-buffer entry point, reported beside the HBM-resident value
+    e2e_ms = None
+    if args.e2e:
+        t1 = time.perf_counter()
+        ctx.check_cas_independent(cols)
+        e2e_ms = (time.perf_counter() - t1) * 1e3
+
     out = None
     if rank == 0:
         parity = None
@@ -155,7 +183,7 @@ def main():
             parity = bool(all((hv[f] == ov[f]).all() for f in ("valid", "cause", "fail_entry", "explored")))
         cpu = None
         if not args.no_cpu and world == 1:
-            cpu = cpu_baseline(cols, args.cpu_sample_keys)
+            cpu = cpu_baseline(cols, args.cpu_sample_keys or wl["cpu_keys"], args.workload.upper())
         out = {
             "metric": "history ops verified/sec (node), independent cas-register 10k keys, 1/2/4/8 GPU",
             "value": value,
@@ -169,12 +197,14 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (seeded jepsen-shaped histories, jepsen_amd/csrc/gen.cpp)",
-            "config": {"workload": "C3: independent cas-register, 10000 keys x ~1k entries per GPU",
+            "config": {"workload": wl["desc"],
                        "keys_per_gpu": int(cols.n_keys), "entries_per_gpu": n_entries,
-                       "threads_per_key": 10, "process_limit": 20, "p_info": 0.02,
-                       "p_invalid": 0.01, "budget": A.DEFAULT_BUDGET,
+                       "threads_per_key": wl["gen"]["threads_per_key"],
+                       "process_limit": wl["gen"]["process_limit"], "p_info": wl["gen"]["p_info"],
+                       "p_invalid": wl["gen"]["p_invalid"], "budget": A.DEFAULT_BUDGET,
                        "explored_per_step": int(s.explored), "invalid_keys": int(s.n_invalid),
-                       "unknown_keys": int(s.n_unknown), "device_ms": float(np.mean(dev_ms))},
+                       "unknown_keys": int(s.n_unknown), "device_ms": float(np.mean(dev_ms)),
+                       "e2e_ms_host_buffers": e2e_ms},
             "roofline": {"bound": "hbm", "kernel": "k_lin_dfs (phase 1: every key, quick budget)", "achieved": achieved,
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                          "traffic": pmc_traffic(), "kernel_ms": dfs_avg * 1e3,
@@ -189,7 +219,7 @@ def main():
     return out
 
 
-def cpu_baseline(cols, sample_keys):
+def cpu_baseline(cols, sample_keys, name="C3"):
     """The oracle, reference-faithful mode (independent.clj:234-245's O(K*N)
     per-key subhistory scan + knossos-style linked-list/BitSet WGL), on the
     host cores, over a bounded sample of this rank's keys."""
@@ -202,7 +232,7 @@ def cpu_baseline(cols, sample_keys):
     counts = np.bincount(cols.key[cols.key >= 0], minlength=cols.n_keys)
     ent = int(counts[:k1].sum())
     return {"value": ent / dt, "unit": "entries/s", "cores": threads, "kind": "port",
-            "sample": f"keys 0..{k1 - 1} ({ent} entries) of the rank-0 C3 history, "
+            "sample": f"keys 0..{k1 - 1} ({ent} entries) of the rank-0 {name} history, "
                       f"reference-faithful oracle (O(K*N) subhistory + list WGL), {dt:.2f} s"}
 
 

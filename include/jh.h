@@ -86,7 +86,7 @@ extern "C" {
 #define JH_CAUSE_NIL_VALUE    6  /* nil where the checker does arithmetic     */
 #define JH_CAUSE_OVERFLOW     7  /* long overflow (Clojure + throws)          */
 
-#define JH_MAX_WINDOW 64
+#define JH_MAX_WINDOW 256
 
 typedef struct jh_history {
     int64_t n;                 /* entries */

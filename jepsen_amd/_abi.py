@@ -27,7 +27,7 @@ CAUSES = {
     7: "overflow",
 }
 
-MAX_WINDOW = 64
+MAX_WINDOW = 256
 DEFAULT_BUDGET = 1 << 20
 
 _p64 = C.POINTER(C.c_int64)

@@ -77,6 +77,7 @@ int jh_open(int device, jh_ctx **out) {
         HIP_TRY(hipSetDevice(device));
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking));
         for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -99,6 +100,7 @@ void jh_close(jh_ctx *ctx) {
         for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+        if (ctx->aux2) (void)hipStreamDestroy(ctx->aux2);
     }
     delete ctx;
 }

@@ -52,9 +52,10 @@ struct jh_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;     // second stream for racing searches (jh_lin.hip)
+    hipStream_t aux2 = nullptr;    // third stream: windows wider than 64 (jh_lin.hip)
     std::mutex mu;
     std::vector<Buf> bufs;
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[12] = {};
     uint32_t gen_base = 0;        // memo generation tags (see jh_lin.hip)
     int n_cu = 256;
     void *pinned = nullptr;       // small pinned staging for scalars
@@ -91,6 +92,8 @@ enum WsSlot {
     WS_C_PAIR, WS_C_LAST, WS_C_LO, WS_C_HI, WS_C_OUT, WS_C_FLAG, WS_C_TMP, WS_C_IDX,
     WS_S_BITS, WS_S_RUNS, WS_S_TMP, WS_S_CNT,
     WS_BFS_SET, WS_BFS_Q, WS_BFS_META, WS_CLAIM, WS_SCRATCH_BFS, WS_DEBUG, WS_META, WS_ARENA, WS_DEFER_PROG, WS_LIST_W, WS_C_PT,
+    WS_DEFER3, WS_MEMO_P3, WS_STACK_P3, WS_SCRATCH_P3,
+    WS_LIST_X, WS_MEMO_X, WS_STACK_X, WS_SCRATCH_X,
     WS_COUNT
 };
 

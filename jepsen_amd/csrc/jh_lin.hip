@@ -61,6 +61,7 @@ struct MemoCfg {
 };
 using MemoQ = MemoCfg<8, 14>;    // phase 1: 8 KB memo + 2 KB Bloom = 10.25 KB -> 15 waves/CU
 using MemoH = MemoCfg<12, 16>;   // heavy keys: 128 KB memo + 8 KB Bloom = 140 KB -> 1 wave/CU
+using MemoM = MemoCfg<10, 15>;   // very heavy keys: 32 KB memo + 4 KB Bloom = 37 KB -> 4 waves/CU
 constexpr int STATE_BITS = 20, T_BITS = 20, GEN_BITS = 24;
 constexpr uint32_t STATE_MASK = (1u << STATE_BITS) - 1, T_MASK = (1u << T_BITS) - 1;
 
@@ -295,6 +296,7 @@ struct DfsArgs {
 };
 
 constexpr int JH_CANCELLED = 3; // internal: the other search settled the key first
+constexpr int64_t P2_BUDGET = 1 << 16;  // phase-2 inserts before a key moves to phase 3
 
 // write a key's verdict; in a race only the first finisher writes
 __device__ __forceinline__ void emit_verdict(jh_key_verdict *out, int32_t *claim, int key,
@@ -314,6 +316,10 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
     return ((uint64_t)hi << 32) | lo;
 }
 __device__ __forceinline__ int readlane(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+}
 // whole-wave lane shifts on the VALU (DPP), no LDS round trip:
 // lane i <- lane i+1 (lane 63 keeps its value) / lane i <- lane i-1 (lane 0 keeps)
 __device__ __forceinline__ int wave_shl1(int x) { return __builtin_amdgcn_update_dpp(x, x, 0x130, 0xF, 0xF, false); }
@@ -439,7 +445,7 @@ __device__ bool key_pass1(const KeySrc &S, int key, int lane, KeyInfo &K, jh_key
     }
     if (n_ok == 0) return false;
     K.sumW = (long long)n_ok * (n_ok + 1) / 2 - sum_a_ok + (long long)n_crash * n_ok - sum_a_crash;
-    if (K.sumW > 64LL * n_ok) {                // the average window is wider than 64
+    if (K.sumW > (long long)JH_MAX_WINDOW * n_ok) {   // the average window is wider than the widest
         v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
         return false;
     }
@@ -693,46 +699,67 @@ __device__ __forceinline__ void bloom_set(uint32_t *bloom, uint64_t h) {
 
 // insert a configuration absent from this wave's HBM table (CAS on the first
 // slot of its chain whose generation tag is stale)
+// The wave's HBM table: entries {mask, gen:24 | t:20 | state:20} of 16 B in
+// buckets of 4 (one 64-byte line). A key hashes to a bucket; within the
+// current generation a bucket fills front to back and a full bucket chains
+// to the next one, so a probe reads one line per bucket (four 16-byte loads
+// in flight at once) and stops at the first slot of another generation:
+// one HBM round trip for nearly every probe, hit or miss (at load <= 1/2 a
+// bucket is full ~14% of the time), where a linear probe over single
+// entries took ~2.5 dependent round trips per miss.
+constexpr uint32_t HB = 4;
+
 __device__ __forceinline__ void hbm_insert(uint64_t *memo, uint32_t cap_mask, uint32_t gen,
                                            uint32_t ct, uint32_t cs, uint64_t cm) {
-    uint32_t h = (uint32_t)memo_hash(ct, cs, cm) & cap_mask;
+    uint32_t b = (uint32_t)memo_hash(ct, cs, cm) & cap_mask & ~(HB - 1);
     const uint64_t w1 = ((uint64_t)gen << 40) | ((uint64_t)ct << 20) | cs;
     for (;;) {
-        const uint64_t e1 = __hip_atomic_load(&memo[2 * (size_t)h + 1], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-        if ((e1 >> 40) != gen) {
-            unsigned long long exp = e1;
-            if (__hip_atomic_compare_exchange_strong((unsigned long long *)&memo[2 * (size_t)h + 1],
-                                                     &exp, (unsigned long long)w1,
-                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                __hip_atomic_store(&memo[2 * (size_t)h], cm, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                return;
-            }
-            continue;
+        const ulonglong2 *B = (const ulonglong2 *)(memo + 2 * (size_t)b);
+        ulonglong2 e[HB];
+#pragma unroll
+        for (uint32_t j = 0; j < HB; j++) e[j] = B[j];
+        int j0 = -1;
+#pragma unroll
+        for (int j = HB - 1; j >= 0; j--)
+            if ((e[j].y >> 40) != gen) j0 = j;
+        if (j0 < 0) { b = (b + HB) & cap_mask; continue; }
+        // lanes of one wave may race for a slot (evictions insert from all
+        // lanes at once): claim it with a CAS on the tag word
+        unsigned long long exp = e[j0].y;
+        if (__hip_atomic_compare_exchange_strong((unsigned long long *)&memo[2 * (size_t)(b + j0) + 1],
+                                                 &exp, (unsigned long long)w1,
+                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            __hip_atomic_store(&memo[2 * (size_t)(b + j0)], cm, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
         }
-        h = (h + 1) & cap_mask;
     }
 }
 
-// Probe this wave's HBM table. Returns slot | absent << 32.
+// Probe this wave's HBM table. Returns slot | absent << 32 (absent: the slot
+// an insert of this key would take).
 __device__ __forceinline__ uint64_t hbm_probe(const uint64_t *memo, uint32_t cap_mask, uint32_t gen,
                                               uint32_t ct, uint32_t cs, uint64_t cm,
                                               unsigned long long &probes) {
     const uint64_t w1want = ((uint64_t)gen << 40) | ((uint64_t)ct << 20) | cs;
-    uint32_t h = (uint32_t)memo_hash(ct, cs, cm) & cap_mask;
+    uint32_t b = (uint32_t)memo_hash(ct, cs, cm) & cap_mask & ~(HB - 1);
     for (;;) {
-        const uint64_t e1 = __hip_atomic_load(&memo[2 * (size_t)h + 1], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+        const ulonglong2 *B = (const ulonglong2 *)(memo + 2 * (size_t)b);
+        ulonglong2 e[HB];
+#pragma unroll
+        for (uint32_t j = 0; j < HB; j++) e[j] = B[j];
         probes++;
-        if ((e1 >> 40) != gen) return (1ULL << 32) | h;
-        if (e1 == w1want) {
-            const uint64_t e0 = __hip_atomic_load(&memo[2 * (size_t)h], __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (e0 == cm) return h;
+        int empty = -1, hit = -1;
+#pragma unroll
+        for (int j = HB - 1; j >= 0; j--) {
+            if ((e[j].y >> 40) != gen) empty = j;
+            if (e[j].y == w1want && e[j].x == cm) hit = j;
         }
-        h = (h + 1) & cap_mask;
+        // current-generation entries form a prefix of the bucket
+        if (hit >= 0 && (empty < 0 || hit < empty)) return b + (uint32_t)hit;
+        if (empty >= 0) return (1ULL << 32) | (b + (uint32_t)empty);
+        b = (b + HB) & cap_mask;
     }
 }
 
@@ -1502,6 +1529,12 @@ done:
 // tables arena). The search kernels then only search: their hot loop does not
 // share registers with table building. Keys settled here (no search needed,
 // window wider than 64, beyond the compact encoding) get their verdict now.
+// bytes of a k_lin_xw key's tables (ops, windows per layer)
+__device__ __forceinline__ uint64_t a16(uint64_t x) { return (x + 15) & ~15ULL; }
+__device__ __forceinline__ uint64_t xw_bytes(int n_ops, int n_ok, long long sumW) {
+    return 3 * a16((uint64_t)n_ops * 4) + a16((uint64_t)(n_ok + 1) * 4) + a16((uint64_t)sumW * 2 + 512);
+}
+
 struct KeyMeta {
     uint64_t off;      // byte offset of the key's tables in the arena
     int32_t n_ops, n_ok;
@@ -1520,6 +1553,9 @@ struct TblArgs {
     int32_t *n_list;
     int32_t *list_w;            // keys that need a search: WIDE mode
     int32_t *n_list_w;
+    int32_t *list_x;            // keys that need a search: windows wider than 64 (k_lin_xw)
+    int32_t *n_list_x;
+    int32_t *xw_max;            // the largest k_lin_xw table (bytes)
     int32_t states8;            // every interned state < 256
 };
 
@@ -1537,19 +1573,27 @@ __global__ void __launch_bounds__(256) k_key_tables(TblArgs A) {
             need = false;
         }
         if (need) {
-            unsigned long long off = 0;
-            if (lane == 0) off = atomicAdd(A.bump, (unsigned long long)tblc_bytes(K));
-            off = (unsigned long long)rfl64(__shfl(off, 0));
-            const int maxw = key_fill_c<false>(A.src, K, lane, A.arena + off);
-            if (maxw > 64) {
-                v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-                need = false;
-            } else if (lane == 0) {
+            int maxw = 65;
+            if (K.sumW <= 64LL * K.n_ok) {
+                unsigned long long off = 0;
+                if (lane == 0) off = atomicAdd(A.bump, (unsigned long long)tblc_bytes(K));
+                off = (unsigned long long)rfl64(__shfl(off, 0));
+                maxw = key_fill_c<false>(A.src, K, lane, A.arena + off);
+                if (maxw <= 64 && lane == 0) {
+                    KeyMeta m;
+                    m.off = off; m.n_ops = K.n_ops; m.n_ok = K.n_ok; m.maxw = maxw; m.pad = 0;
+                    A.meta[key] = m;
+                    if (A.states8 && maxw <= 40) A.list[atomicAdd(A.n_list, 1)] = (int32_t)key;
+                    else A.list_w[atomicAdd(A.n_list_w, 1)] = (int32_t)key;
+                }
+            }
+            if (maxw > 64 && lane == 0) {
+                // wider than 64 (up to JH_MAX_WINDOW): k_lin_xw builds its own tables
                 KeyMeta m;
-                m.off = off; m.n_ops = K.n_ops; m.n_ok = K.n_ok; m.maxw = maxw; m.pad = 0;
+                m.off = 0; m.n_ops = K.n_ops; m.n_ok = K.n_ok; m.maxw = -1; m.pad = (int32_t)K.sumW;
                 A.meta[key] = m;
-                if (A.states8 && maxw <= 40) A.list[atomicAdd(A.n_list, 1)] = (int32_t)key;
-                else A.list_w[atomicAdd(A.n_list_w, 1)] = (int32_t)key;
+                A.list_x[atomicAdd(A.n_list_x, 1)] = (int32_t)key;
+                atomicMax(A.xw_max, (int32_t)xw_bytes(K.n_ops, K.n_ok, K.sumW));
             }
         }
         if (!need && lane == 0) A.out[key] = v;
@@ -1620,6 +1664,12 @@ __global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) { lin_dfs_waves<MemoQ
 // per CU with a 128 KB LDS memo
 template <bool LEAN>
 __global__ void __launch_bounds__(64) k_lin_seq(DfsArgs A) { lin_dfs_waves<MemoH, LEAN>(A); }
+// very heavy keys (over the phase-2 budget, mostly on their way to the full
+// budget, i.e. :unknown): their memo lives in HBM whatever the LDS holds, so
+// a step waits on an HBM round trip; four waves per CU (one per SIMD) keep
+// four times as many of those searches in flight
+template <bool LEAN>
+__global__ void __launch_bounds__(64) k_lin_seq3(DfsArgs A) { lin_dfs_waves<MemoM, LEAN>(A); }
 
 // ---------------------------------------------------------------------------
 // Heavy keys: parallel breadth-first enumeration of the reachable
@@ -1955,6 +2005,342 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A) {
 
 // Invalid keys settled by the DFS carry -(tmax + 2): the failing row is the
 // ok completion of RET[tmax] (the first op no configuration gets past).
+// ---------------------------------------------------------------------------
+// Windows wider than 64 (up to JH_MAX_WINDOW = 256 members): the same WGL
+// search in the same canonical coordinates (orc_wgl_canonical with its
+// 4-word masks, oracle/jh_oracle.c), one wave per key, member j of W(t) in
+// lane j mod 64 of slice j / 64. Such keys are rare (C5's 50-thread keys
+// with many crashed ops) and almost all of them are deep searches, so this
+// path is kept simple: tables in global scratch (ops, windows W(t) listed
+// per layer), every configuration in the wave's HBM table (48-byte entries
+// {mask[4], gen|t|state}, buckets of 4), the stack in HBM. A step is one
+// HBM round trip per probed slice (plus one per pop).
+constexpr int XW_SL = JH_MAX_WINDOW / 64;        // mask words / member slices
+constexpr uint32_t XW_HB = 4;                    // entries per bucket
+constexpr int XW_EW = 6;                         // words per entry
+
+struct XwArgs {
+    KeySrc src;
+    const int32_t *list;
+    int32_t n_list;
+    int32_t *queue;
+    const KeyMeta *meta;
+    jh_key_verdict *out;
+    char *scratch;              // per wave: the key's tables
+    uint64_t scratch_bytes;
+    uint64_t *memo;             // per wave: memo_cap entries x XW_EW words
+    uint32_t memo_cap;          // power of two
+    uint64_t *stack;            // per wave: stack_cap frames x XW_EW words
+    uint32_t stack_cap;
+    int64_t budget;
+    int32_t init_state;
+    uint32_t gen_base;
+    int32_t *flags;
+    unsigned long long *probes;
+};
+
+struct XwTbl {
+    uint32_t *rq;     // need | becomes << 16 (cas-register step, 04-checker.md:58-72)
+    int32_t *rr;      // ok-return rank, -1 crashed
+    int32_t *a;       // ok returns before the invocation (the op joins W(a))
+    int32_t *woff;    // W(t) = W[woff[t] .. woff[t+1])
+    uint16_t *W;
+};
+__device__ __forceinline__ XwTbl xw_tbl(char *tb, int n_ops, int n_ok) {
+    XwTbl T;
+    uint64_t o = 0;
+    T.rq = (uint32_t *)(tb + o); o += a16((uint64_t)n_ops * 4);
+    T.rr = (int32_t *)(tb + o); o += a16((uint64_t)n_ops * 4);
+    T.a = (int32_t *)(tb + o); o += a16((uint64_t)n_ops * 4);
+    T.woff = (int32_t *)(tb + o); o += a16((uint64_t)(n_ok + 1) * 4);
+    T.W = (uint16_t *)(tb + o);
+    return T;
+}
+
+// ops in call order and the windows of every layer; returns the widest
+// window (JH_MAX_WINDOW + 1 if wider: the key is :unknown, cause window)
+__device__ int xw_fill(const KeySrc &S, uint32_t s0, uint32_t s1, int n_ops, int n_ok,
+                       long long sumW, int lane, const XwTbl &T) {
+    {
+        int nok = 0;
+        for (uint32_t base = s0; base < s1; base += 64) {
+            const uint32_t p = base + lane;
+            const bool valid = p < s1;
+            const int rk = valid ? S.rank[p] : -1;
+            const bool kept = rk >= 0, ret = rk <= -2;
+            const uint64_t br = ballot(ret);
+            if (kept) {
+                Rec x = S.rec[p];
+                const int q = S.pair[p];
+                int rr = -1, v1c = x.v1, v2c = x.v2;
+                if (q >= 0) {
+                    Rec y = S.rec[q];
+                    if (y.type == T_OK) {
+                        rr = -(S.rank[q] + 2);
+                        if (x.f == F_CAS) { if (x.v1 == 0 && x.v2 == 0) { v1c = y.v1; v2c = y.v2; } }
+                        else if (x.v1 == 0) v1c = y.v1;
+                    }
+                }
+                T.rq[rk] = x.f == F_READ ? ((uint32_t)v1c | ((uint32_t)v1c << 16))
+                         : x.f == F_WRITE ? (RQ_ANY | ((uint32_t)v1c << 16))
+                         : ((uint32_t)v1c | ((uint32_t)v2c << 16));
+                T.rr[rk] = rr;
+                T.a[rk] = nok + mbcnt(br);
+            }
+            nok += __popcll(br);
+        }
+    }
+    wave_sync();
+    // W(t) = W(t-1) - {RET[t-1]} + the ops with a == t, in call order
+    int maxw = 0, w = 0, nxt = 0;
+    long long offt = 0, offp = 0;
+    for (int t = 0; t < n_ok; t++) {
+        int nk = 0;
+        if (t > 0) {
+            for (int k = 0; k < XW_SL; k++) {
+                const int idx = 64 * k + lane;
+                int prev = 0;
+                bool keep = false;
+                if (idx < w) { prev = T.W[offp + idx]; keep = T.rr[prev] != t - 1; }
+                const uint64_t bk = ballot(keep);
+                if (keep) T.W[offt + nk + mbcnt(bk)] = (uint16_t)prev;
+                nk += __popcll(bk);
+            }
+        }
+        int added = 0;
+        for (;;) {
+            const int j = nxt + lane;
+            const bool in = j < n_ops && T.a[j] <= t;
+            const uint64_t ba = ballot(in);
+            const int c = __popcll(ba);             // a is non-decreasing: a prefix
+            if (in && nk + added + lane < JH_MAX_WINDOW) T.W[offt + nk + added + lane] = (uint16_t)j;
+            added += c; nxt += c;
+            if (c < 64) break;
+        }
+        w = nk + added;
+        maxw = max(maxw, w);
+        if (w > JH_MAX_WINDOW || offt + w > sumW) { maxw = max(maxw, JH_MAX_WINDOW + 1); break; }
+        if (lane == 0) T.woff[t] = (int32_t)offt;
+        offp = offt;
+        offt += w;
+        wave_sync();
+    }
+    if (lane == 0) T.woff[n_ok] = (int32_t)offt;
+    wave_sync();
+    return maxw;
+}
+
+__device__ __forceinline__ uint64_t xw_hash(uint32_t t, uint32_t s, const uint64_t *m) {
+    uint64_t h = jh_mix64(((uint64_t)t << 32) | s);
+#pragma unroll
+    for (int w = 0; w < XW_SL; w++) h = jh_mix64(h ^ (m[w] + (uint64_t)w * 0x9E3779B97F4A7C15ULL));
+    return h;
+}
+
+// probe: slot | absent << 32 (absent: the slot an insert of this key takes)
+__device__ uint64_t xw_probe(const uint64_t *memo, uint32_t cap_mask, uint32_t gen, uint32_t t,
+                             uint32_t s, const uint64_t *m, unsigned long long &probes) {
+    const uint64_t want = ((uint64_t)gen << 40) | ((uint64_t)t << 20) | s;
+    uint32_t b = (uint32_t)xw_hash(t, s, m) & cap_mask & ~(XW_HB - 1);
+    for (;;) {
+        const ulonglong2 *B = (const ulonglong2 *)(memo + (size_t)b * XW_EW);
+        ulonglong2 e[XW_HB * 3];
+#pragma unroll
+        for (uint32_t j = 0; j < XW_HB * 3; j++) e[j] = B[j];
+        probes++;
+        int empty = -1, hit = -1;
+#pragma unroll
+        for (int j = XW_HB - 1; j >= 0; j--) {
+            const uint64_t w1 = e[3 * j + 2].x;
+            if ((w1 >> 40) != gen) empty = j;
+            if (w1 == want && e[3 * j].x == m[0] && e[3 * j].y == m[1] && e[3 * j + 1].x == m[2] &&
+                e[3 * j + 1].y == m[3]) hit = j;
+        }
+        if (hit >= 0 && (empty < 0 || hit < empty)) return b + (uint32_t)hit;
+        if (empty >= 0) return (1ULL << 32) | (b + (uint32_t)empty);
+        b = (b + XW_HB) & cap_mask;
+    }
+}
+
+__device__ __forceinline__ void xw_store(uint64_t *memo, uint32_t slot, uint32_t gen, uint32_t t,
+                                         uint32_t s, const uint64_t *m) {
+    uint64_t *e = memo + (size_t)slot * XW_EW;
+    for (int w = 0; w < XW_SL; w++)
+        __hip_atomic_store(&e[w], m[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&e[4], ((uint64_t)gen << 40) | ((uint64_t)t << 20) | s, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
+    const int lane = threadIdx.x;
+    __shared__ unsigned long long nm_sh[XW_SL];
+    char *tb = A.scratch + (size_t)blockIdx.x * A.scratch_bytes;
+    uint64_t *memo = A.memo + (size_t)blockIdx.x * A.memo_cap * XW_EW;
+    uint64_t *stk = A.stack + (size_t)blockIdx.x * A.stack_cap * XW_EW;
+    const uint32_t cap_mask = A.memo_cap - 1;
+    unsigned long long my_probes = 0;
+    for (;;) {
+        int idx = 0;
+        if (lane == 0) idx = atomicAdd(A.queue, 1);
+        idx = readlane(idx, 0);
+        if (idx >= A.n_list) break;
+        const int key = A.list[idx];
+        const KeyMeta mt = A.meta[key];
+        const int n_ops = mt.n_ops, n_ok = mt.n_ok;
+        const long long sumW = (long long)(uint32_t)mt.pad;
+        jh_key_verdict v;
+        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW; v.fail_entry = -1; v.explored = 0;
+        if (xw_bytes(n_ops, n_ok, sumW) > A.scratch_bytes || (uint32_t)n_ops + 2 > A.stack_cap) {
+            if (lane == 0) { atomicOr(A.flags, 2); A.out[key] = v; }
+            continue;
+        }
+        const XwTbl T = xw_tbl(tb, n_ops, n_ok);
+        const int maxw = xw_fill(A.src, A.src.off[key], A.src.off[key + 1], n_ops, n_ok, sumW, lane, T);
+        if (maxw > JH_MAX_WINDOW) {
+            if (lane == 0) A.out[key] = v;
+            continue;
+        }
+        const uint32_t gen = (A.gen_base + (uint32_t)key + 1) & ((1u << GEN_BITS) - 1);
+        const uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
+
+        // the current layer's members: member 64k + lane in slice k
+        uint32_t t = 0, tmax = 0, s = (uint32_t)A.init_state, ins = 0, depth = 0;
+        uint64_t mask[XW_SL] = {0, 0, 0, 0};
+        uint32_t mrq[XW_SL];
+        int32_t mrr[XW_SL];
+        int w = 0, r = 0, start = 0;
+        auto load_layer = [&]() {
+            const int o = T.woff[t];
+            w = T.woff[t + 1] - o;
+            r = 0;
+#pragma unroll
+            for (int k = 0; k < XW_SL; k++) {
+                const int j = 64 * k + lane;
+                mrq[k] = RQ_EMPTY; mrr[k] = -2;
+                if (j < w) { const int id = T.W[o + j]; mrq[k] = T.rq[id]; mrr[k] = T.rr[id]; }
+                const uint64_t b = ballot(j < w && mrr[k] == (int32_t)t);
+                if (b) r = 64 * k + __builtin_ctzll(b);
+            }
+        };
+        load_layer();
+        int verdict = -1;
+        for (;;) {
+            // expand: candidates from `start` on, in call order, slice by slice
+            bool took = false;
+            uint32_t u_r = t;
+            uint64_t nm_r[XW_SL] = {0, 0, 0, 0};
+            bool lifted = false;
+#pragma unroll 1
+            for (int k = 0; k < XW_SL && !took; k++) {
+                if (64 * k >= w) break;
+                const int j = 64 * k + lane;
+                const uint32_t req = mrq[k] & 0xFFFF;
+                const bool cl = j < w && j >= start && !((mask[k] >> lane) & 1) && (req == s || req == RQ_ANY);
+                const uint64_t cand = ballot(cl);
+                if (!cand) continue;
+                if (!lifted && (r >> 6) == k && ((cand >> (r & 63)) & 1)) {
+                    // the RET child: lift RET[t], keep lifting while the next
+                    // layer's RET op is already linearized, compact onto W(u)
+                    lifted = true;
+                    uint64_t lin[XW_SL];
+#pragma unroll
+                    for (int q = 0; q < XW_SL; q++) lin[q] = mask[q];
+                    lin[r >> 6] |= 1ULL << (r & 63);
+                    uint32_t u = t + 1;
+                    while (u < (uint32_t)n_ok) {
+                        bool hit = false;
+#pragma unroll
+                        for (int q = 0; q < XW_SL; q++) hit |= ((lin[q] >> lane) & 1) && mrr[q] == (int32_t)u;
+                        if (!ballot(hit)) break;
+                        u++;
+                    }
+                    u_r = u;
+                    if (u < (uint32_t)n_ok) {
+                        if (lane < XW_SL) nm_sh[lane] = 0;
+                        wave_sync();
+                        int base = 0;
+#pragma unroll
+                        for (int q = 0; q < XW_SL; q++) {
+                            const bool kept = 64 * q + lane < w && (mrr[q] < 0 || mrr[q] >= (int32_t)u);
+                            const uint64_t bk = ballot(kept);
+                            const int pos = base + mbcnt(bk);
+                            if (kept && ((lin[q] >> lane) & 1)) atomicOr(&nm_sh[pos >> 6], 1ULL << (pos & 63));
+                            base += __popcll(bk);
+                        }
+                        wave_sync();
+#pragma unroll
+                        for (int q = 0; q < XW_SL; q++) nm_r[q] = rfl64(nm_sh[q]);
+                        wave_sync();
+                    }
+                }
+                // every candidate lane probes its child
+                const bool is_r = j == r;
+                uint64_t cm[XW_SL];
+#pragma unroll
+                for (int q = 0; q < XW_SL; q++) cm[q] = is_r ? nm_r[q] : (mask[q] | (q == k ? (1ULL << lane) : 0ULL));
+                const uint32_t ct = is_r ? u_r : t, cs = mrq[k] >> 16;
+                bool found = false;
+                uint32_t slot = 0;
+                if (cl) {
+                    const uint64_t pr = xw_probe(memo, cap_mask, gen, ct, cs, cm, my_probes);
+                    found = (pr >> 32) == 0;
+                    slot = (uint32_t)pr;
+                }
+                const uint64_t absent = cand & ~ballot(found);
+                if (!absent) continue;
+                const int i = __builtin_ctzll(absent);
+                if (ins >= budget) { verdict = JH_UNKNOWN; break; }
+                ins++;
+                if (lane == i) xw_store(memo, slot, gen, ct, cs, cm);
+                // push the parent (t, s, member, mask)
+                if (lane == 0) {
+                    uint64_t *f = stk + (size_t)depth * XW_EW;
+                    f[0] = mask[0]; f[1] = mask[1]; f[2] = mask[2]; f[3] = mask[3];
+                    f[4] = ((uint64_t)t << 32) | (uint32_t)(64 * k + i);
+                    f[5] = s;
+                }
+                depth++;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                s = (uint32_t)readlane((int)cs, i);
+                const uint32_t nt = (uint32_t)readlane((int)ct, i);
+#pragma unroll
+                for (int q = 0; q < XW_SL; q++) mask[q] = readlane64(cm[q], i);
+                took = true;
+                start = 0;
+                if (nt != t) {
+                    t = nt;
+                    tmax = max(tmax, t);
+                    if (t >= (uint32_t)n_ok) { verdict = JH_VALID; break; }
+                    load_layer();
+                }
+            }
+            if (verdict >= 0) break;
+            if (took) continue;
+            // pop
+            if (depth == 0) { verdict = JH_INVALID; break; }
+            depth--;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const uint64_t *f = stk + (size_t)depth * XW_EW;
+#pragma unroll
+            for (int q = 0; q < XW_SL; q++) mask[q] = rfl64(f[q]);
+            const uint64_t ti = rfl64(f[4]);
+            s = (uint32_t)rfl64(f[5]);
+            start = (int)(uint32_t)ti + 1;
+            const uint32_t pt = (uint32_t)(ti >> 32);
+            if (pt != t) { t = pt; load_layer(); }
+        }
+        v.valid = verdict;
+        v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
+        v.explored = ins;
+        v.fail_entry = verdict == JH_INVALID ? -(int64_t)tmax - 2 : -1;
+        if (lane == 0) A.out[key] = v;
+    }
+    for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
+    if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
+}
+
 __global__ void __launch_bounds__(256) k_fail_rows(KeySrc S, jh_key_verdict *out, int64_t K) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * 4;
@@ -2074,7 +2460,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     }
 
     // memo generation tags: distinct per (call, key, pass); wrap -> clear
-    const uint32_t gen_span = (uint32_t)(2 * K + 2);
+    const uint32_t gen_span = (uint32_t)(3 * K + 3);
     bool clear_memo = false;
     if ((uint64_t)ctx->gen_base + gen_span >= (1u << GEN_BITS) - 1) { ctx->gen_base = 0; clear_memo = true; }
 
@@ -2091,11 +2477,11 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const uint64_t scr_bytes_h = MemoH::SLOTS * 8;
     const uint64_t scr_bytes_bfs = (((uint64_t)smax * 84 + 4096) + 255) & ~255ULL;
     char *scr = ctx->ws<char>(WS_SCRATCH, (size_t)waves1 * scr_bytes);
-    int32_t *q = ctx->ws<int32_t>(WS_QUEUE, 16);
+    int32_t *q = ctx->ws<int32_t>(WS_QUEUE, 32);
     int32_t *list = ctx->ws<int32_t>(WS_STATS, K);
     int32_t *defer = ctx->ws<int32_t>(WS_DEFER, K + 1);
     unsigned long long *probes = (unsigned long long *)(q + 4);
-    HIP_TRY(hipMemsetAsync(q, 0, 16 * sizeof(int32_t), st));
+    HIP_TRY(hipMemsetAsync(q, 0, 32 * sizeof(int32_t), st));
 
     // per-key search tables for every key (<= 8 B per entry + 32 B per key)
     KeyMeta *meta = ctx->ws<KeyMeta>(WS_META, K);
@@ -2105,6 +2491,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     ta.K = K; ta.meta = meta; ta.arena = arena; ta.bump = (unsigned long long *)(q + 10);
     int32_t *list_w = ctx->ws<int32_t>(WS_LIST_W, K);
     ta.out = out_dev; ta.list = list; ta.n_list = q + 12; ta.list_w = list_w; ta.n_list_w = q + 13;
+    int32_t *list_x = ctx->ws<int32_t>(WS_LIST_X, K);
+    ta.list_x = list_x; ta.n_list_x = q + 19; ta.xw_max = q + 20;
     ta.states8 = (vmax - vmin + 2) <= 256 ? 1 : 0;
     k_key_tables<<<(unsigned)std::min<int64_t>((K + 3) / 4, 8192), 256, 0, st>>>(ta);
 
@@ -2136,7 +2524,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[4], st));
-    int32_t qh[16];
+    int32_t qh[32];
     HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const int n_defer = qh[1];
@@ -2165,7 +2553,32 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 tot[11], tot[12], tot[13], tot[14], (double)tot[2] / std::max(1ULL, tot[4]), (double)tot[9] / waves1, mx9);
         HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 512) * 16, st));
     }
-    int n_unres = 0;
+    // windows wider than 64: k_lin_xw on the third stream, alongside phases 2 and 3
+    const int n_x = qh[19];
+    if (n_x > 0) {
+        uint32_t capx = 1u << 12;
+        while ((int64_t)capx < 2 * budget && capx < (1u << 30)) capx <<= 1;
+        const int waves_x = std::min(n_x, getenv("JH_XW_WAVES") ? std::max(1, atoi(getenv("JH_XW_WAVES"))) : 128);
+        const uint64_t scr_x = ((uint64_t)qh[20] + 255) & ~255ULL;
+        const bool freshx = ctx->ws_fresh(WS_MEMO_X) || ctx->bufs[WS_MEMO_X].bytes < (size_t)waves_x * capx * XW_EW * 8;
+        uint64_t *memox = ctx->ws<uint64_t>(WS_MEMO_X, (size_t)waves_x * capx * XW_EW, /*zero=*/true);
+        if (clear_memo && !freshx) HIP_TRY(hipMemsetAsync(memox, 0, ctx->bufs[WS_MEMO_X].bytes, st));
+        XwArgs x{};
+        x.src = KeySrc{rec, pair, off, rB, viol, rank, q + 2};
+        x.list = list_x; x.n_list = n_x; x.queue = q + 21; x.meta = meta; x.out = out_dev;
+        x.scratch = ctx->ws<char>(WS_SCRATCH_X, (size_t)waves_x * scr_x); x.scratch_bytes = scr_x;
+        x.memo = memox; x.memo_cap = capx;
+        x.stack = ctx->ws<uint64_t>(WS_STACK_X, (size_t)waves_x * stack_cap * XW_EW); x.stack_cap = stack_cap;
+        x.budget = budget; x.init_state = init_state;
+        x.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;   // its own table: any gen range works
+        x.flags = q + 2; x.probes = (unsigned long long *)(q + 22);
+        HIP_TRY(hipEventRecord(ctx->ev[8], st));
+        HIP_TRY(hipStreamWaitEvent(ctx->aux2, ctx->ev[8], 0));
+        k_lin_xw<<<waves_x, 64, 0, ctx->aux2>>>(x);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->ev[9], ctx->aux2));
+    }
+    int n_unres = 0, n_defer3 = 0;
     if (n_defer > 0) {
         // Heavy keys: two exact searches race per key and the first to settle
         // it writes its verdict (emit_verdict), the other abandons it.
@@ -2221,10 +2634,16 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
         Frame *stack2 = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap);
         char *scr2 = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes_h);
+        // phase 2 stops at P2_BUDGET inserts and hands the key to phase 3
+        int64_t p2 = P2_BUDGET;
+        if (const char *e = getenv("JH_P2_BUDGET")) p2 = std::max<int64_t>(quick + 1, atoll(e));
+        const bool split3 = budget > p2;
+        int32_t *defer3 = ctx->ws<int32_t>(WS_DEFER3, n_defer + 1);
         DfsArgs b = a;
-        b.list = defer; b.n_list = n_defer; b.n_list_dev = nullptr; b.queue = q + 6; b.defer = 0;
+        b.list = defer; b.n_list = n_defer; b.n_list_dev = nullptr; b.queue = q + 6; b.defer = split3 ? 1 : 0;
+        b.defer_list = defer3; b.defer_count = q + 16; b.defer_prog = nullptr;
         b.memo = memo2; b.memo_cap = cap2; b.stack = stack2; b.scratch = scr2; b.scratch_bytes = scr_bytes_h;
-        b.budget = budget;
+        b.budget = split3 ? p2 : budget;
         b.gen_base = ctx->gen_base + (uint32_t)K + 1;
         b.dbg = dbg ? dbg + 16 * 256 : nullptr; b.claim = claim;
         b.probes = (unsigned long long *)(q + 8);
@@ -2241,6 +2660,43 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         }
         k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
+        if (split3) {
+            // phase 3: the keys phase 2 handed over, full budget, 4 waves per CU
+            int32_t q16 = 0;
+            HIP_TRY(hipMemcpyAsync(&q16, q + 16, sizeof q16, hipMemcpyDeviceToHost, ctx->aux));
+            HIP_TRY(hipStreamSynchronize(ctx->aux));
+            n_defer3 = q16;
+        }
+        if (n_defer3 > 0) {
+            int waves3 = std::min(n_defer3, 4 * ctx->n_cu);
+            if (const char *e = getenv("JH_P3_WAVES")) waves3 = std::max(1, std::min(waves3, atoi(e)));
+            const bool fresh3 = ctx->ws_fresh(WS_MEMO_P3) || ctx->bufs[WS_MEMO_P3].bytes < (size_t)waves3 * cap2 * 16;
+            uint64_t *memo3 = ctx->ws<uint64_t>(WS_MEMO_P3, (size_t)waves3 * cap2 * 2, /*zero=*/true);
+            if (clear_memo && !fresh3) HIP_TRY(hipMemsetAsync(memo3, 0, ctx->bufs[WS_MEMO_P3].bytes, ctx->aux));
+            Frame *stack3 = ctx->ws<Frame>(WS_STACK_P3, (size_t)waves3 * stack_cap);
+            char *scr3 = ctx->ws<char>(WS_SCRATCH_P3, (size_t)waves3 * MemoH::SLOTS * 8);
+            DfsArgs c3 = b;
+            c3.list = defer3; c3.n_list = n_defer3; c3.queue = q + 17; c3.defer = 0;
+            c3.memo = memo3; c3.stack = stack3; c3.scratch = scr3; c3.scratch_bytes = MemoH::SLOTS * 8;
+            c3.budget = budget;
+            // a fresh generation range: phase 2's table entries of these keys are not reused
+            c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
+            c3.dbg = nullptr;
+            {
+                DfsArgs cw = c3;
+                cw.queue = q + 18;
+                k_lin_seq3<false><<<std::min(waves3, 128), 64, MemoM::LDS, ctx->aux>>>(cw);
+            }
+            if (n_defer3 <= ctx->n_cu - wg2) {
+                // few of them (no more than phase 2's CUs): a lone wave and
+                // the 128 KB LDS memo each, as in phase 2
+                k_lin_seq<true><<<waves3, 64, MemoH::LDS, ctx->aux>>>(c3);
+            } else {
+                k_lin_seq3<true><<<waves3, 64, MemoM::LDS, ctx->aux>>>(c3);
+            }
+            HIP_TRY(hipGetLastError());
+        }
         HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
         HIP_TRY(hipStreamWaitEvent(st, ctx->ev[7], 0));
         if (dbg2) {
@@ -2267,6 +2723,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
         HIP_TRY(hipEventRecord(ctx->ev[7], st));
     }
+    if (n_x > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[9], 0));
     HIP_TRY(hipEventRecord(ctx->ev[2], st));
     ctx->gen_base += gen_span;
 
@@ -2301,8 +2758,11 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             float d = 0;
             HIP_TRY(hipEventElapsedTime(&d, ctx->ev[4], ctx->ev[7]));
             HIP_TRY(hipEventElapsedTime(&c, ctx->ev[4], ctx->ev[5]));
-            fprintf(stderr, "[jh] keys=%lld prep=%.3f ms phase1=%.3f ms (waves %d) deferred=%d bfs=%.3f ms (gave up %d) seq=%.3f ms\n",
-                    (long long)K, a, b, waves1, n_defer, c, n_unres, d);
+            float xw = 0, p2 = 0;
+            if (n_x > 0) HIP_TRY(hipEventElapsedTime(&xw, ctx->ev[8], ctx->ev[9]));
+            if (n_defer > 0) HIP_TRY(hipEventElapsedTime(&p2, ctx->ev[4], ctx->ev[10]));
+            fprintf(stderr, "[jh] keys=%lld prep=%.3f ms phase1=%.3f ms (waves %d) deferred=%d bfs=%.3f ms (gave up %d) seq=%.3f ms (phase 2 %.3f ms, phase 3: %d keys) wide=%d keys %.3f ms\n",
+                    (long long)K, a, b, waves1, n_defer, c, n_unres, d, p2, n_defer3, n_x, xw);
         }
     }
 }

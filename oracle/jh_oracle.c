@@ -212,66 +212,80 @@ void orc_key_free(orc_key *k) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* Memo set of canonical configurations (t, state, mask).                   */
-typedef struct { uint32_t t; int64_t s; uint64_t m; } cfg;
+/* Memo set of canonical configurations (t, state, mask). The mask is over
+ * the window W(t), at most JH_MAX_WINDOW = 256 members: MW 64-bit words.   */
+#define MW (JH_MAX_WINDOW / 64)
+typedef struct { uint32_t t; int64_t s; uint64_t m[MW]; } cfg;
 typedef struct { cfg *e; uint8_t *used; int64_t cap, n; } cset;
-static uint64_t cfg_hash(cfg c) {
-    return mix64(c.m * 0x9E3779B97F4A7C15ULL ^ mix64((uint64_t)c.s + ((uint64_t)c.t << 40)));
+static uint64_t cfg_hash(const cfg *c) {
+    uint64_t h = mix64((uint64_t)c->s + ((uint64_t)c->t << 40));
+    for (int w = 0; w < MW; w++) h = mix64(h ^ c->m[w] * 0x9E3779B97F4A7C15ULL) + (uint64_t)w;
+    return h;
+}
+static int cfg_eq(const cfg *a, const cfg *b) {
+    if (a->t != b->t || a->s != b->s) return 0;
+    for (int w = 0; w < MW; w++) if (a->m[w] != b->m[w]) return 0;
+    return 1;
 }
 static void cset_init(cset *s) {
     s->cap = 1024; s->n = 0;
     s->e = (cfg *)malloc(sizeof(cfg) * s->cap); s->used = (uint8_t *)calloc(s->cap, 1);
 }
 static void cset_free(cset *s) { free(s->e); free(s->used); }
-static int cset_has(const cset *s, cfg c) {
+static int cset_has(const cset *s, const cfg *c) {
     uint64_t i = cfg_hash(c) & (s->cap - 1);
     while (s->used[i]) {
-        if (s->e[i].t == c.t && s->e[i].s == c.s && s->e[i].m == c.m) return 1;
+        if (cfg_eq(&s->e[i], c)) return 1;
         i = (i + 1) & (s->cap - 1);
     }
     return 0;
 }
-static void cset_add(cset *s, cfg c);
+static void cset_add(cset *s, const cfg *c);
 static void cset_grow(cset *s) {
     cset o = *s; s->cap = o.cap * 2; s->n = 0;
     s->e = (cfg *)malloc(sizeof(cfg) * s->cap); s->used = (uint8_t *)calloc(s->cap, 1);
-    for (int64_t i = 0; i < o.cap; i++) if (o.used[i]) cset_add(s, o.e[i]);
+    for (int64_t i = 0; i < o.cap; i++) if (o.used[i]) cset_add(s, &o.e[i]);
     cset_free(&o);
 }
-static void cset_add(cset *s, cfg c) {
+static void cset_add(cset *s, const cfg *c) {
     if (2 * (s->n + 1) > s->cap) cset_grow(s);
     uint64_t i = cfg_hash(c) & (s->cap - 1);
     while (s->used[i]) i = (i + 1) & (s->cap - 1);
-    s->used[i] = 1; s->e[i] = c; s->n++;
+    s->used[i] = 1; s->e[i] = *c; s->n++;
 }
+static inline int bit_get(const uint64_t *m, int i) { return (int)((m[i >> 6] >> (i & 63)) & 1); }
+static inline void bit_set(uint64_t *m, int i) { m[i >> 6] |= 1ULL << (i & 63); }
 
 /* Lift window member i of configuration (t, mask): the op takes effect now.
  * If it is the op whose return defines R, R advances to the next ok return
  * whose op is not yet linearized, and the mask is compacted onto W(t'). */
-static void cfg_lift(const orc_key *k, uint32_t t, uint64_t mask, int i,
+static void cfg_lift(const orc_key *k, uint32_t t, const uint64_t *mask, int i,
                      uint32_t *t_out, uint64_t *mask_out) {
     const int32_t *W = k->w_ops + k->w_off[t];
     int w = k->w_off[t + 1] - k->w_off[t];
-    mask |= 1ULL << i;
-    if (W[i] != k->ret_op[t]) { *t_out = t; *mask_out = mask; return; }
+    uint64_t lin[MW];
+    memcpy(lin, mask, sizeof lin);
+    bit_set(lin, i);
+    if (W[i] != k->ret_op[t]) { *t_out = t; memcpy(mask_out, lin, sizeof lin); return; }
     uint32_t u = t + 1;
     while (u < (uint32_t)k->n_ok) {
-        int lin = 0;
+        int found = 0;
         for (int j = 0; j < w; j++)
-            if (((mask >> j) & 1) && k->ops[W[j]].rr == (int32_t)u) { lin = 1; break; }
-        if (!lin) break;
+            if (bit_get(lin, j) && k->ops[W[j]].rr == (int32_t)u) { found = 1; break; }
+        if (!found) break;
         u++;
     }
-    if (u == (uint32_t)k->n_ok) { *t_out = u; *mask_out = 0; return; }
-    uint64_t nm = 0; int b = 0;
+    memset(mask_out, 0, sizeof(uint64_t) * MW);
+    *t_out = u;
+    if (u == (uint32_t)k->n_ok) return;
+    int b = 0;
     for (int j = 0; j < w; j++) {
         const orc_op *o = &k->ops[W[j]];
         if (o->rr < 0 || o->rr >= (int32_t)u) {
-            if ((mask >> j) & 1) nm |= 1ULL << b;
+            if (bit_get(lin, j)) bit_set(mask_out, b);
             b++;
         }
     }
-    *t_out = u; *mask_out = nm;
 }
 
 /* The WGL depth-first search (Lowe 2017 Fig. 3, as knossos.wgl/analysis) in
@@ -281,7 +295,7 @@ static void cfg_lift(const orc_key *k, uint32_t t, uint64_t mask, int i,
  * if the model allows it and the child configuration is not in the cache,
  * which it is then added to; after a lift the scan restarts at the first
  * candidate, after a backtrack it resumes after the popped one. */
-typedef struct { uint32_t t; int32_t i; int64_t s; uint64_t m; } frame;
+typedef struct { uint32_t t; int32_t i; int64_t s; uint64_t m[MW]; } frame;
 
 int orc_wgl_canonical(const orc_key *k, int64_t init, int64_t budget,
                       int64_t *explored, int64_t *fail_entry) {
@@ -291,25 +305,26 @@ int orc_wgl_canonical(const orc_key *k, int64_t init, int64_t budget,
     cset memo; cset_init(&memo);
     int64_t cap = 256, depth = 0;
     frame *st = (frame *)malloc(sizeof(frame) * cap);
-    uint32_t t = 0, tmax = 0; int64_t s = init; uint64_t mask = 0; int start = 0;
+    uint32_t t = 0, tmax = 0; int64_t s = init; int start = 0;
+    uint64_t mask[MW] = {0};
     int verdict;
     for (;;) {
         const int32_t *W = k->w_ops + k->w_off[t];
         int w = k->w_off[t + 1] - k->w_off[t];
         int took = 0;
         for (int i = start; i < w; i++) {
-            if ((mask >> i) & 1) continue;
+            if (bit_get(mask, i)) continue;
             const orc_op *o = &k->ops[W[i]];
             int64_t s2;
             if (!cas_step(o->f, o->v1, o->v2, s, &s2)) continue;
             cfg c; c.s = s2;
-            cfg_lift(k, t, mask, i, &c.t, &c.m);
-            if (cset_has(&memo, c)) continue;
+            cfg_lift(k, t, mask, i, &c.t, c.m);
+            if (cset_has(&memo, &c)) continue;
             if (memo.n >= budget) { verdict = JH_UNKNOWN; goto done; }
-            cset_add(&memo, c);
+            cset_add(&memo, &c);
             if (depth == cap) { cap *= 2; st = (frame *)realloc(st, sizeof(frame) * cap); }
-            st[depth].t = t; st[depth].i = i; st[depth].s = s; st[depth].m = mask; depth++;
-            t = c.t; s = c.s; mask = c.m; start = 0;
+            st[depth].t = t; st[depth].i = i; st[depth].s = s; memcpy(st[depth].m, mask, sizeof mask); depth++;
+            t = c.t; s = c.s; memcpy(mask, c.m, sizeof mask); start = 0;
             if (t > tmax) tmax = t;
             if (t == (uint32_t)k->n_ok) { verdict = JH_VALID; goto done; }
             took = 1;
@@ -322,7 +337,7 @@ int orc_wgl_canonical(const orc_key *k, int64_t init, int64_t budget,
             goto done;
         }
         depth--;
-        t = st[depth].t; s = st[depth].s; mask = st[depth].m; start = st[depth].i + 1;
+        t = st[depth].t; s = st[depth].s; memcpy(mask, st[depth].m, sizeof mask); start = st[depth].i + 1;
     }
 done:
     *explored = memo.n;
@@ -873,7 +888,7 @@ int orc_reachable(const orc_key *k, int64_t init, int64_t cap, int64_t *res) {
     cset seen; cset_init(&seen);
     int64_t qcap = 1024, qh = 0, qt = 0;
     cfg *q = (cfg *)malloc(sizeof(cfg) * qcap);
-    cfg c0 = {0, init, 0};
+    cfg c0; memset(&c0, 0, sizeof c0); c0.s = init;
     q[qt++] = c0;
     int term = 0;
     while (qh < qt) {
@@ -882,14 +897,14 @@ int orc_reachable(const orc_key *k, int64_t init, int64_t cap, int64_t *res) {
         const int32_t *W = k->w_ops + k->w_off[c.t];
         int w = k->w_off[c.t + 1] - k->w_off[c.t];
         for (int i = 0; i < w; i++) {
-            if ((c.m >> i) & 1) continue;
+            if (bit_get(c.m, i)) continue;
             const orc_op *o = &k->ops[W[i]];
             int64_t s2;
             if (!cas_step(o->f, o->v1, o->v2, c.s, &s2)) continue;
             cfg d; d.s = s2;
-            cfg_lift(k, c.t, c.m, i, &d.t, &d.m);
-            if (cset_has(&seen, d)) continue;
-            cset_add(&seen, d);
+            cfg_lift(k, c.t, c.m, i, &d.t, d.m);
+            if (cset_has(&seen, &d)) continue;
+            cset_add(&seen, &d);
             if (seen.n > cap) goto out;
             if (qt == qcap) { qcap *= 2; q = (cfg *)realloc(q, sizeof(cfg) * qcap); }
             q[qt++] = d;

@@ -80,6 +80,49 @@ def test_heavy_key_paths(ctx, quick, monkeypatch):
     _same(g, c)
 
 
+@pytest.mark.parametrize("p2", ["4097", "9000"])
+def test_phase3_handover(ctx, p2, monkeypatch):
+    """Keys past the phase-2 budget restart in phase 3 (4 waves per CU, HBM
+    memo): forcing a small phase-2 budget must not change any result, with
+    the full budget or a budget in between."""
+    cols, _ = synth.cas_register(n_keys=300, ops_per_key=400, p_invalid=0.1, p_info=0.05, seed=91)
+    monkeypatch.setenv("JH_P2_BUDGET", p2)
+    for budget in (None, 20000):
+        g, _ = ctx.check_cas_independent(cols, budget=budget)
+        c, _ = oracle.check_cas_independent(cols, budget=budget or A.DEFAULT_BUDGET, threads=8)
+        _same(g, c)
+
+
+@pytest.mark.parametrize("waves", [None, "1"])
+def test_windows_wider_than_64(ctx, waves, monkeypatch):
+    """Windows of 65..256 members (k_lin_xw, 4-word masks) and wider than
+    256 (:unknown, cause window): verdict, cause, failing row and WGL cache
+    size equal the oracle's at several budgets; one wave (JH_XW_WAVES=1)
+    checks every wide key in turn with the same HBM table."""
+    if waves:
+        monkeypatch.setenv("JH_XW_WAVES", waves)
+    cols, _ = synth.cas_register(n_keys=24, ops_per_key=260, threads_per_key=120, readers=20,
+                                 groups=120, process_limit=10 ** 6, p_info=0.08, p_invalid=0.2,
+                                 seed=61)
+    for budget in (3000, 40000) if waves else (3000, 40000, None):
+        g, _ = ctx.check_cas_independent(cols, budget=budget)
+        c, _ = oracle.check_cas_independent(cols, budget=budget or A.DEFAULT_BUDGET, threads=16)
+        _same(g, c)
+    assert (c["cause"] != 2).sum() > 0
+
+
+def test_c5_shape(ctx):
+    """C5-shaped keys (50 threads per key, 20% :info): deep searches that
+    mostly end :unknown at the full budget (phase 3, HBM memo at full load),
+    windows over 64, a few settled keys; identical to the oracle."""
+    cols, _ = synth.cas_register(n_keys=24, ops_per_key=500, threads_per_key=50, readers=25,
+                                 process_limit=100, p_info=0.2, p_invalid=0.05, seed=5)
+    g, gs = ctx.check_cas_independent(cols)
+    c, cs = oracle.check_cas_independent(cols, threads=16)
+    _same(g, c)
+    assert gs.n_unknown == cs.n_unknown and gs.n_unknown > 0
+
+
 def test_c3_scale_properties(ctx):
     """BASELINE config C3 (10k keys x ~1k entries): every key the generator
     did not fault is valid, and the device equals the oracle on every key."""

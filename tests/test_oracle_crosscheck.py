@@ -118,3 +118,26 @@ def test_history_completion_errors(built):
     v = oracle.check_cas(enc([inv(0, "write", 1), ok(0, "write", 1), inv(0, "write", 2),
                               ok(0, "write", 2), inv(1, "read", None), ok(1, "read", 1)]))
     assert v[0] == A.INVALID and v[2] == 5
+
+
+@pytest.mark.parametrize("seed", [61, 62])
+def test_wide_windows_agree(built, seed):
+    """Windows of 65..256 members (multi-word masks): canonical == list WGL,
+    verdict and cache size, at the full budget and at a small one; wider
+    than 256 is :unknown with cause window in both."""
+    cols, _ = synth.cas_register(n_keys=24, ops_per_key=260, threads_per_key=120, readers=20,
+                                 groups=120, process_limit=10 ** 6, p_info=0.08, p_invalid=0.2,
+                                 seed=seed)
+    widths, settled = [], 0
+    for k in range(cols.n_keys):
+        sub = _sub(cols, k)
+        for budget in (3000, 40000):
+            r = oracle.key_selftest(sub, budget=budget)
+            widths.append(r["max_window"])
+            if r["max_window"] > A.MAX_WINDOW:
+                assert r["status"] == 2 and r["canonical"] == A.UNKNOWN      # cause window
+                continue
+            assert r["canonical"] == r["list"], r
+            assert r["canonical_explored"] == r["list_explored"], r
+            settled += r["canonical"] != A.UNKNOWN
+    assert sum(64 < w <= A.MAX_WINDOW for w in widths) >= 8 and settled >= 2

@@ -3,20 +3,25 @@
 // Replaces (checker/counter), jepsen/src/jepsen/checker.clj:679-734:
 //   history/complete, (remove :fails?), (remove op/fail?), then a sequential
 //   loop carrying lower/upper bounds and pending reads.
-// The loop is two exclusive prefix sums over the rows, in history order:
+// The loop is two prefix sums over the rows, in history order:
 //   lower(row) = sum of :ok :add values before row        (checker.clj:725-726)
 //   upper(row) = sum of non-failed :invoke :add values     (checker.clj:722-723)
 // and each :ok :read emits [lower(its invocation) value upper(itself)]
 // (checker.clj:713-720); errors are the triples with not (<= lower v upper).
 //
-//   k_cnt_last   last row of each process (LDS-privatised per chunk)
-//   k_cnt_pair   complete pairing: next non-:info row of the same process,
-//                stopping at the process' last row
-//   k_cnt_orphan :ok/:fail with no open invocation
-//   k_cnt_vals   per-row add contributions (+ :fails? / nil checks)
-//   2 x hipcub ExclusiveSum (int64)
-//   k_cnt_reads  compact the :ok :read triples in history order, count
-//                errors, first failing row
+// HBM-bound streaming passes (bytes per row read / written):
+//   k_cnt_prange  process range                                        8 / 0
+//   k_cnt_pack    packed row code (process - pmin) << 4 | f2 << 2 | type,
+//                 last row per process (LDS-privatised), add-value range   32 / 4
+//   k_cnt_pair    complete pairing over the codes (64-row ballot windows)  ~8 / 4
+//   scan          ONE decoupled look-back inclusive scan (rocprim) of
+//                 {lower, upper, reads, flags-of-this-row} over a transform
+//                 of (code, pair, value): per-row contributions, :fails?,
+//                 orphans and nil checks fused in; its output iterator
+//                 writes only at read rows (the ok read's row and upper,
+//                 the invoke read's lower)                                  16 / ~0
+//   k_cnt_reads   the triples, in history order, errors, first failing row
+//                 (over the ~1% read rows only)
 #include "jh_internal.h"
 #include <hipcub/hipcub.hpp>
 
@@ -37,48 +42,52 @@ struct CntMeta {
     long long n_reads;
 };
 
-__global__ void __launch_bounds__(256) k_cnt_range(const int64_t *__restrict__ proc, const int64_t *__restrict__ type,
-                            const int64_t *__restrict__ f, const int64_t *__restrict__ val,
-                            int64_t n, CntMeta *m) {
-    long long lo = LLONG_MAX, hi = LLONG_MIN, am = 0, na = 0;
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
-         r += (int64_t)gridDim.x * blockDim.x) {
-        long long p = proc[r];
-        lo = min(lo, p); hi = max(hi, p);
-        if (f[r] == JH_F_ADD && (type[r] == T_INVOKE || type[r] == T_OK)) {
-            long long v = val[r];
-            if (v != JH_NIL) { am = max(am, v < 0 ? (v == LLONG_MIN ? LLONG_MAX : -v) : v); }
-            na++;
-        }
+constexpr uint32_t F2_OTHER = 0, F2_ADD = 1, F2_READ = 2;
+constexpr int RF_OKREAD = 1, RF_INVREAD = 2;
+
+__global__ void __launch_bounds__(256) k_cnt_prange(const int64_t *__restrict__ proc, int64_t n, CntMeta *m) {
+    long long lo = LLONG_MAX, hi = LLONG_MIN;
+    const int64_t n2 = n / 2;
+    const longlong2 *p2 = (const longlong2 *)proc;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += (int64_t)gridDim.x * blockDim.x) {
+        const longlong2 x = p2[i];
+        lo = min(lo, min(x.x, x.y)); hi = max(hi, max(x.x, x.y));
     }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) { lo = min(lo, (long long)proc[n - 1]); hi = max(hi, (long long)proc[n - 1]); }
     __shared__ long long sh[4];
     lo = block_reduce256(lo, RedMin(), sh);
     hi = block_reduce256(hi, RedMax(), sh);
-    am = block_reduce256(am, RedMax(), sh);
-    na = block_reduce256(na, RedSum(), sh);
-    if (threadIdx.x == 0) {
-        atomicMin(&m->pmin, lo); atomicMax(&m->pmax, hi);
-        atomicMax(&m->amax_abs, am);
-        if (na) atomicAdd((unsigned long long *)&m->n_add, (unsigned long long)na);
-    }
+    if (threadIdx.x == 0) { atomicMin(&m->pmin, lo); atomicMax(&m->pmax, hi); }
 }
 
-// last row of every process: per-chunk LDS hash of (process -> max row),
-// then one global atomicMax per distinct process of the chunk
-__global__ void __launch_bounds__(256) k_cnt_last(const int64_t *__restrict__ proc,
-                                                  const int64_t *__restrict__ type, int64_t n,
+// packed row codes + last row of every process (per-chunk LDS hash of
+// (process -> max row), then one global atomicMax per distinct process) +
+// the add-value range for the overflow check
+__global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ proc,
+                                                  const int64_t *__restrict__ type,
+                                                  const int64_t *__restrict__ f,
+                                                  const int64_t *__restrict__ val, int64_t n,
                                                   long long pmin, int32_t *__restrict__ last,
-                                                  uint32_t *__restrict__ pt) {
+                                                  uint32_t *__restrict__ code, CntMeta *m) {
     __shared__ long long hk[HSLOTS];
     __shared__ int hv[HSLOTS];
+    __shared__ long long sh[4];
     const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
     for (int i = threadIdx.x; i < HSLOTS; i += blockDim.x) { hk[i] = LLONG_MIN; hv[i] = -1; }
     __syncthreads();
+    long long am = 0, na = 0;
     for (int i = threadIdx.x; i < CHUNK; i += blockDim.x) {
         const int64_t r = c0 + i;
         if (r >= n) break;
         const long long p = proc[r];
-        pt[r] = ((uint32_t)(p - pmin) << 2) | (uint32_t)(type[r] & 3);   // span < 2^28
+        const int64_t ty = type[r] & 3, ff = f[r];
+        const uint32_t f2 = ff == JH_F_ADD ? F2_ADD : ff == JH_F_READ ? F2_READ : F2_OTHER;
+        code[r] = ((uint32_t)(p - pmin) << 4) | (f2 << 2) | (uint32_t)ty;   // span < 2^28
+        if (f2 == F2_ADD && (ty == T_INVOKE || ty == T_OK)) {
+            const long long v = val[r];
+            if (v != JH_NIL) am = max(am, v < 0 ? (v == LLONG_MIN ? LLONG_MAX : -v) : v);
+            na++;
+        }
         uint32_t h = (uint32_t)jh_mix64((uint64_t)p) & (HSLOTS - 1);
         bool done = false;
         for (int probe = 0; probe < 64 && !done; probe++) {
@@ -93,10 +102,182 @@ __global__ void __launch_bounds__(256) k_cnt_last(const int64_t *__restrict__ pr
         }
         if (!done) atomicMax(&last[p - pmin], (int)r);
     }
+    am = block_reduce256(am, RedMax(), sh);
+    na = block_reduce256(na, RedSum(), sh);
+    if (threadIdx.x == 0) {
+        if (am) atomicMax(&m->amax_abs, am);
+        if (na) atomicAdd((unsigned long long *)&m->n_add, (unsigned long long)na);
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < HSLOTS; i += blockDim.x)
         if (hk[i] != LLONG_MIN) atomicMax(&last[hk[i] - pmin], hv[i]);
 }
+
+// per-row contributions and prefixes of lower / upper / ok reads; flags mark
+// the read rows
+struct CntAcc {
+    long long lo, hi;
+    int nr, flags;
+};
+
+// per-row contribution (checker.clj:709-727 after complete / remove :fails?);
+// orphans, :fails? and nil checks fused in
+__device__ __forceinline__ CntAcc cnt_row(const uint32_t *__restrict__ code, const int32_t *__restrict__ pair,
+                                          const int64_t *__restrict__ val, CntMeta *m, int64_t r) {
+    const uint32_t x = code[r];
+    const uint32_t ty = x & 3, f2 = (x >> 2) & 3;
+    const int32_t c = pair[r];
+    CntAcc a{0, 0, 0, 0};
+    if ((ty == T_OK || ty == T_FAIL) && c < 0)
+        atomicMin(&m->viol1, ((unsigned long long)r << 4) | JH_CAUSE_ORPHAN);
+    if (f2 == F2_ADD) {
+        if (ty == T_INVOKE) {
+            const bool failed = c >= 0 && (code[c] & 3) == T_FAIL;
+            if (!failed) {
+                long long v = val[r];
+                if (v == JH_NIL && c >= 0) v = val[c];          // (or inv ok)
+                if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
+                else a.hi = v;
+            }
+        } else if (ty == T_OK) {
+            const long long v = val[r];
+            if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
+            else a.lo = v;
+        }
+    } else if (f2 == F2_READ) {
+        if (ty == T_OK) {
+            // its pending read must come from an [:invoke :read] (checker.clj:713-716)
+            if (c < 0 || ((code[c] >> 2) & 3) != F2_READ)
+                atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_ORPHAN);
+            else { a.nr = 1; a.flags = RF_OKREAD; }
+        } else if (ty == T_INVOKE) {
+            a.flags = RF_INVREAD;
+        }
+    }
+    return a;
+}
+
+// Reduce-then-scan over tiles of CNT_TILE rows (the rows of a tile are read
+// twice, 16 B each time: 32 B/row in all, coalesced).
+constexpr int CNT_TILE = 2048, CNT_PER = CNT_TILE / 256;
+
+__global__ void __launch_bounds__(256) k_cnt_tile_sums(const uint32_t *__restrict__ code,
+                                                       const int32_t *__restrict__ pair,
+                                                       const int64_t *__restrict__ val, int64_t n,
+                                                       CntMeta *m, CntAcc *__restrict__ agg) {
+    __shared__ long long sh[4];
+    const int64_t base = (int64_t)blockIdx.x * CNT_TILE;
+    long long lo = 0, hi = 0, nr = 0;
+#pragma unroll
+    for (int k = 0; k < CNT_PER; k++) {
+        const int64_t r = base + k * 256 + threadIdx.x;
+        if (r < n) { const CntAcc a = cnt_row(code, pair, val, m, r); lo += a.lo; hi += a.hi; nr += a.nr; }
+    }
+    lo = block_reduce256(lo, RedSum(), sh);
+    hi = block_reduce256(hi, RedSum(), sh);
+    nr = block_reduce256(nr, RedSum(), sh);
+    if (threadIdx.x == 0) agg[blockIdx.x] = CntAcc{lo, hi, (int)nr, 0};
+}
+
+// rows in order within the tile (LDS transpose: thread t takes rows
+// CNT_PER*t ..), from the tile's exclusive prefix; writes only at read rows
+__global__ void __launch_bounds__(256) k_cnt_tile_scan(const uint32_t *__restrict__ code,
+                                                       const int32_t *__restrict__ pair,
+                                                       const int64_t *__restrict__ val, int64_t n,
+                                                       CntMeta *m, const CntAcc *__restrict__ pre,
+                                                       int32_t *__restrict__ rd_row, int64_t *__restrict__ rd_hi,
+                                                       int64_t *__restrict__ lo_at, CntAcc *total) {
+    // a row feeds at most one of lower / upper / reads: LDS holds its value
+    // and a kind byte (20 KB per block: occupancy hides the HBM latency)
+    constexpr int PAD = CNT_TILE + CNT_TILE / CNT_PER;
+    __shared__ long long s_v[PAD];
+    __shared__ uint8_t s_k[PAD];
+    __shared__ long long sc[3][4];
+    const int tid = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * CNT_TILE;
+#pragma unroll
+    for (int k = 0; k < CNT_PER; k++) {
+        const int j = k * 256 + tid;
+        const int64_t r = base + j;
+        CntAcc a{0, 0, 0, 0};
+        if (r < n) a = cnt_row(code, pair, val, m, r);
+        const int q = j + j / CNT_PER;
+        s_v[q] = a.lo ? a.lo : a.hi;
+        s_k[q] = (uint8_t)(a.lo ? 1 : a.hi ? 2 : a.flags == RF_OKREAD ? 3 : a.flags == RF_INVREAD ? 4 : 0);
+    }
+    __syncthreads();
+    long long lo = 0, hi = 0, nr = 0;
+    const int q0 = tid * (CNT_PER + 1);
+#pragma unroll
+    for (int j = 0; j < CNT_PER; j++) {
+        const int kd = s_k[q0 + j];
+        const long long v = s_v[q0 + j];
+        lo += kd == 1 ? v : 0; hi += kd == 2 ? v : 0; nr += kd == 3;
+    }
+    // block exclusive scan of the per-thread sums: wave shuffles, then the
+    // totals of the waves before
+    long long il = lo, ih = hi, in = nr;
+    const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long a0 = __shfl_up(il, o), a1 = __shfl_up(ih, o), a2 = __shfl_up(in, o);
+        if (lane >= o) { il += a0; ih += a1; in += a2; }
+    }
+    if (lane == 63) { sc[0][wv] = il; sc[1][wv] = ih; sc[2][wv] = in; }
+    __syncthreads();
+    for (int w = 0; w < wv; w++) { il += sc[0][w]; ih += sc[1][w]; in += sc[2][w]; }
+    const CntAcc p = pre[blockIdx.x];
+    long long rl = p.lo + il - lo, rh = p.hi + ih - hi, rn = p.nr + in - nr;
+#pragma unroll
+    for (int j = 0; j < CNT_PER; j++) {
+        const int kd = s_k[q0 + j];
+        const long long v = s_v[q0 + j];
+        rl += kd == 1 ? v : 0; rh += kd == 2 ? v : 0; rn += kd == 3;
+        const int64_t r = base + (int64_t)tid * CNT_PER + j;
+        if (kd == 3) { rd_row[rn - 1] = (int32_t)r; rd_hi[rn - 1] = rh; }
+        else if (kd == 4) lo_at[r] = rl;
+        if (r == n - 1) *total = CntAcc{rl, rh, (int)rn, 0};
+    }
+}
+
+struct CntSumOp {
+    __host__ __device__ CntAcc operator()(const CntAcc &a, const CntAcc &b) const {
+        return CntAcc{a.lo + b.lo, a.hi + b.hi, a.nr + b.nr, 0};
+    }
+};
+
+__global__ void k_cnt_triples(const int32_t *__restrict__ rd_row, const int64_t *__restrict__ rd_hi,
+                              const int64_t *__restrict__ lo_at, const int32_t *__restrict__ pair,
+                              const int64_t *__restrict__ val, int64_t nr, int64_t *__restrict__ out,
+                              int64_t cap, CntMeta *m) {
+    long long nerr = 0;
+    unsigned long long ferr = ~0ULL;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nr;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = rd_row[i];
+        const int32_t inv = pair[r];
+        int64_t v = val[inv];
+        if (v == JH_NIL) v = val[r];
+        const int64_t l = lo_at[inv], u = rd_hi[i];
+        if (i < cap) { out[3 * i] = l; out[3 * i + 1] = v; out[3 * i + 2] = u; }
+        if (v == JH_NIL) {
+            atomicMin(&m->viol3, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
+        } else if (!(l <= v && v <= u)) {
+            nerr++;
+            ferr = min(ferr, (unsigned long long)r);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        nerr += __shfl_xor(nerr, o);
+        ferr = min(ferr, __shfl_xor(ferr, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (nerr) atomicAdd((unsigned long long *)&m->n_errors, (unsigned long long)nerr);
+        if (ferr != ~0ULL) atomicMin(&m->first_err, ferr);
+    }
+}
+
+
 
 // complete pairing: an invocation's completion is the next non-:info row of
 // its process (util.clj:606-640). One wave per 64 consecutive rows: it reads
@@ -112,7 +293,7 @@ __global__ void __launch_bounds__(256) k_cnt_pair(const uint32_t *__restrict__ p
     for (int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); wv * 64 < n; wv += nw) {
         const int64_t base = wv * 64, r = base + lane;
         const uint32_t x = r < n ? pt[r] : 3u;
-        const uint32_t p = x >> 2;
+        const uint32_t p = x >> 4;
         const bool inv = r < n && (x & 3) == T_INVOKE;
         const int64_t lr = inv ? (int64_t)last[p] : -1;
         bool open = inv && lr > r;
@@ -126,7 +307,7 @@ __global__ void __launch_bounds__(256) k_cnt_pair(const uint32_t *__restrict__ p
                 const int l = __builtin_ctzll(todo);
                 const uint32_t pl = (uint32_t)__builtin_amdgcn_readlane((int)p, l);
                 const uint64_t mine = __ballot(open && p == pl);
-                const uint64_t cand = __ballot((y >> 2) == pl && (y & 3) != T_INFO);
+                const uint64_t cand = __ballot((y >> 4) == pl && (y & 3) != T_INFO);
                 todo &= ~mine;
                 if ((mine >> lane) & 1) {
                     // candidates strictly after this lane's row
@@ -147,81 +328,8 @@ __global__ void __launch_bounds__(256) k_cnt_pair(const uint32_t *__restrict__ p
     }
 }
 
-__global__ void k_cnt_orphan(const int64_t *__restrict__ type, int64_t n,
-                             const int32_t *__restrict__ pair, CntMeta *m) {
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
-         r += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t ty = type[r];
-        if ((ty == T_OK || ty == T_FAIL) && pair[r] < 0)
-            atomicMin(&m->viol1, ((unsigned long long)r << 4) | JH_CAUSE_ORPHAN);
-    }
-}
 
-__global__ void k_cnt_vals(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
-                           const int64_t *__restrict__ val, int64_t n,
-                           const int32_t *__restrict__ pair, int64_t *__restrict__ okadd,
-                           int64_t *__restrict__ invadd, int32_t *__restrict__ isread, CntMeta *m) {
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
-         r += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t ty = type[r], ff = f[r];
-        const int32_t c = pair[r];
-        int64_t lo = 0, hi = 0;
-        int rd = 0;
-        if (ty == T_INVOKE && ff == JH_F_ADD) {
-            const bool failed = c >= 0 && type[c] == T_FAIL;
-            if (!failed) {
-                int64_t v = val[r];
-                if (v == JH_NIL && c >= 0) v = val[c];          // (or inv ok)
-                if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
-                else hi = v;
-            }
-        } else if (ty == T_OK && ff == JH_F_ADD) {
-            const int64_t v = val[r];
-            if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
-            else lo = v;
-        } else if (ty == T_OK && ff == JH_F_READ) {
-            // its pending read must come from an [:invoke :read] (checker.clj:713-716)
-            if (c < 0 || f[c] != JH_F_READ)
-                atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_ORPHAN);
-            else rd = 1;
-        }
-        okadd[r] = lo; invadd[r] = hi; isread[r] = rd;
-    }
-}
 
-__global__ void k_cnt_reads(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
-                            const int64_t *__restrict__ val, int64_t n,
-                            const int32_t *__restrict__ pair, const int64_t *__restrict__ lo,
-                            const int64_t *__restrict__ hi, const int32_t *__restrict__ isread,
-                            const int32_t *__restrict__ ridx, int64_t *__restrict__ out,
-                            int64_t cap, CntMeta *m) {
-    long long nerr = 0;
-    unsigned long long ferr = ~0ULL;
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
-         r += (int64_t)gridDim.x * blockDim.x) {
-        if (!isread[r]) continue;
-        const int32_t inv = pair[r];
-        int64_t v = val[inv];
-        if (v == JH_NIL) v = val[r];
-        const int64_t l = lo[inv], u = hi[r];
-        const int64_t i = ridx[r];
-        if (i < cap) { out[3 * i] = l; out[3 * i + 1] = v; out[3 * i + 2] = u; }
-        if (v == JH_NIL) {
-            atomicMin(&m->viol3, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
-        } else if (!(l <= v && v <= u)) {
-            nerr++;
-            ferr = min(ferr, (unsigned long long)r);
-        }
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        nerr += __shfl_xor(nerr, o);
-        ferr = min(ferr, __shfl_xor(ferr, o));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        if (nerr) atomicAdd((unsigned long long *)&m->n_errors, (unsigned long long)nerr);
-        if (ferr != ~0ULL) atomicMin(&m->first_err, ferr);
-    }
-}
 
 }  // namespace
 
@@ -235,44 +343,51 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
     CntMeta *m = ctx->ws<CntMeta>(WS_C_TMP, 1);
     CntMeta mi{LLONG_MAX, LLONG_MIN, 0, 0, ~0ULL, ~0ULL, ~0ULL, ~0ULL, 0, 0};
     HIP_TRY(hipMemcpyAsync(m, &mi, sizeof mi, hipMemcpyHostToDevice, st));
-    k_cnt_range<<<grid_for(n, 256, 4096), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n, m);
+    k_cnt_prange<<<grid_for(n / 2 + 1, 256, 2048), 256, 0, st>>>(dh->process, n, m);
     CntMeta mh;
     HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const unsigned long long span = (unsigned long long)(mh.pmax - mh.pmin);
     if (span >= (1ULL << 28)) throw_jh(JH_EUNSUPPORTED, "process ids span more than 2^28");
+
+    int32_t *last = ctx->ws<int32_t>(WS_C_LAST, span + 1);
+    int32_t *pair = ctx->ws<int32_t>(WS_C_PAIR, n);
+    uint32_t *code = ctx->ws<uint32_t>(WS_C_PT, n);
+    HIP_TRY(hipMemsetAsync(last, 0xFF, sizeof(int32_t) * (span + 1), st));
+    HIP_TRY(hipMemsetAsync(pair, 0xFF, sizeof(int32_t) * n, st));
+    k_cnt_pack<<<(int)((n + CHUNK - 1) / CHUNK), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
+                                                              mh.pmin, last, code, m);
+    HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
+    k_cnt_pair<<<grid_for((n + 63) / 64, 4, 16384), 256, 0, st>>>(code, n, last, pair, m);
+    HIP_TRY(hipStreamSynchronize(st));
     // Clojure + throws on long overflow; if no prefix can overflow we need no
     // ordered overflow check (else the shim falls back to the JVM checker).
     if (mh.amax_abs > 0 && (unsigned long long)mh.amax_abs > (unsigned long long)(LLONG_MAX / std::max(1LL, mh.n_add)))
         throw_jh(JH_EUNSUPPORTED, "add values large enough to overflow a long");
 
-    int32_t *last = ctx->ws<int32_t>(WS_C_LAST, span + 1);
-    int32_t *pair = ctx->ws<int32_t>(WS_C_PAIR, n);
-    int64_t *lo = ctx->ws<int64_t>(WS_C_LO, n), *hi = ctx->ws<int64_t>(WS_C_HI, n);
-    int32_t *isread = ctx->ws<int32_t>(WS_C_FLAG, n), *ridx = ctx->ws<int32_t>(WS_C_IDX, n);
-    HIP_TRY(hipMemsetAsync(last, 0xFF, sizeof(int32_t) * (span + 1), st));
-    HIP_TRY(hipMemsetAsync(pair, 0xFF, sizeof(int32_t) * n, st));
-    uint32_t *pt = ctx->ws<uint32_t>(WS_C_PT, n);
-    k_cnt_last<<<(int)((n + CHUNK - 1) / CHUNK), 256, 0, st>>>(dh->process, dh->type, n, mh.pmin, last, pt);
-    k_cnt_pair<<<grid_for((n + 63) / 64, 4, 16384), 256, 0, st>>>(pt, n, last, pair, m);
-    k_cnt_orphan<<<grid_for(n, 256), 256, 0, st>>>(dh->type, n, pair, m);
-    k_cnt_vals<<<grid_for(n, 256), 256, 0, st>>>(dh->type, dh->f, dh->value, n, pair, lo, hi, isread, m);
-    size_t tb = 0, tb2 = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, lo, lo, (int)n, st));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, isread, ridx, (int)n, st));
-    void *tmp = ctx->ws<char>(WS_S_TMP, std::max(tb, tb2));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, lo, lo, (int)n, st));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, hi, hi, (int)n, st));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, isread, ridx, (int)n, st));
-    int32_t last_idx = 0, last_flag = 0;
-    HIP_TRY(hipMemcpyAsync(&last_idx, ridx + n - 1, 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(&last_flag, isread + n - 1, 4, hipMemcpyDeviceToHost, st));
+    // reduce-then-scan over tiles of rows
+    int32_t *rd_row = ctx->ws<int32_t>(WS_C_IDX, n);
+    int64_t *rd_hi = ctx->ws<int64_t>(WS_C_HI, n);
+    int64_t *lo_at = ctx->ws<int64_t>(WS_C_LO, n);
+    const int64_t n_tiles = (n + CNT_TILE - 1) / CNT_TILE;
+    CntAcc *agg = ctx->ws<CntAcc>(WS_C_OUT2, 2 * n_tiles + 1);
+    CntAcc *pre = agg + n_tiles;
+    CntAcc *total = pre + n_tiles;
+    k_cnt_tile_sums<<<(unsigned)n_tiles, 256, 0, st>>>(code, pair, dh->value, n, m, agg);
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, tb, agg, pre, CntSumOp(), CntAcc{0, 0, 0, 0}, (int)n_tiles, st));
+    void *tmp = ctx->ws<char>(WS_S_TMP, tb);
+    HIP_TRY(hipcub::DeviceScan::ExclusiveScan(tmp, tb, agg, pre, CntSumOp(), CntAcc{0, 0, 0, 0}, (int)n_tiles, st));
+    k_cnt_tile_scan<<<(unsigned)n_tiles, 256, 0, st>>>(code, pair, dh->value, n, m, pre, rd_row, rd_hi, lo_at, total);
+    CntAcc th;
+    HIP_TRY(hipMemcpyAsync(&th, total, sizeof th, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    const int64_t nr = (int64_t)last_idx + last_flag;
+    const int64_t nr = th.nr;
     const int64_t cap = std::min(nr, reads_cap);
     int64_t *out = ctx->ws<int64_t>(WS_C_OUT, 3 * std::max<int64_t>(cap, 1));
-    k_cnt_reads<<<grid_for(n, 256), 256, 0, st>>>(dh->type, dh->f, dh->value, n, pair, lo, hi, isread,
-                                                  ridx, out, cap, m);
+    if (nr > 0)
+        k_cnt_triples<<<grid_for(nr, 256, 4096), 256, 0, st>>>(rd_row, rd_hi, lo_at, pair, dh->value, nr,
+                                                              out, cap, m);
     HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
     if (cap > 0 && reads_out)
         HIP_TRY(hipMemcpyAsync(reads_out, out, sizeof(int64_t) * 3 * cap, hipMemcpyDeviceToHost, st));

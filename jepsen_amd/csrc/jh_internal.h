@@ -93,7 +93,7 @@ enum WsSlot {
     WS_S_BITS, WS_S_RUNS, WS_S_TMP, WS_S_CNT,
     WS_BFS_SET, WS_BFS_Q, WS_BFS_META, WS_CLAIM, WS_SCRATCH_BFS, WS_DEBUG, WS_META, WS_ARENA, WS_DEFER_PROG, WS_LIST_W, WS_C_PT,
     WS_DEFER3, WS_MEMO_P3, WS_STACK_P3, WS_SCRATCH_P3,
-    WS_LIST_X, WS_MEMO_X, WS_STACK_X, WS_SCRATCH_X,
+    WS_LIST_X, WS_MEMO_X, WS_STACK_X, WS_SCRATCH_X, WS_C_OUT2,
     WS_COUNT
 };
 

@@ -2627,6 +2627,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
 
         uint32_t cap2 = 1u << 16;
         while ((int64_t)cap2 < 2 * budget && cap2 < (1u << 30)) cap2 <<= 1;
+        if (const char *e = getenv("JH_MEMO_CAP_SHIFT")) cap2 <<= std::max(0, std::min(3, atoi(e)));   // experiments
         const int waves2 = std::min(n_defer, std::max(1, ctx->n_cu - wg2));
         // generation-tagged: zeroed once when allocated (and on wrap), not per call
         const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;

@@ -12,7 +12,7 @@ import numpy as np
 
 from . import _abi as A
 from . import history as H
-from .model import CASRegister
+from .model import CASRegister, Mutex, Register, to_device_ops
 
 UNKNOWN = "unknown"
 
@@ -185,11 +185,13 @@ class Linearizable(Checker):
         self.budget = opts.get("budget")
 
     def supported(self):
-        return isinstance(self.model, CASRegister)
+        return isinstance(self.model, (CASRegister, Register, Mutex))
 
     def check(self, test, history, opts):
         if not self.supported():
             raise NotImplementedError(f"model {self.model!r} has no device implementation")
+        if not isinstance(history, H.Columns):
+            history = to_device_ops(self.model, list(history))
         cols = _cols(history, keyed=False)
         v, c, fe, ex = _ctx().check_cas(cols, init=_init_state(self.model, cols), budget=self.budget)
         return lin_result(v, c, fe, ex, cols)

@@ -9,6 +9,7 @@ from . import _abi as A
 from . import history as H
 from .checker import (Checker, Compose, Linearizable, check_safe, lin_result, merge_valid,
                       _init_state, _ctx)
+from .model import to_device_ops
 
 DIR = "independent"
 tuple_ = H.tuple_
@@ -65,7 +66,12 @@ class IndependentChecker(Checker):
         history = list(history)
         name, lin = _lin_member(self.inner)
         if lin is not None:
-            cols = H.encode(history, keyed=True)
+            try:
+                dev_history = to_device_ops(lin.model, history)
+            except ValueError:
+                dev_history = None        # an op the model has no clause for: per key below
+        if lin is not None and dev_history is not None:
+            cols = H.encode(dev_history, keyed=True)
             unkeyed_client = any(int(p) >= 0 and int(k) < 0 for p, k in zip(cols.process, cols.key))
             if cols.n_keys and not unkeyed_client:
                 verdicts, _ = _ctx().check_cas_independent(

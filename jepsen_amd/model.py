@@ -48,3 +48,91 @@ class CASRegister:
 def cas_register(value=None):
     """(knossos.model/cas-register) / (cas-register v)."""
     return CASRegister(value)
+
+
+@dataclass(frozen=True)
+class Register:
+    """knossos.model/register (used as (model/register 0) at
+    raftis/src/jepsen/raftis.clj:121): a read/write register. knossos 0.3.4 is
+    not vendored; its step is the cas-register's read and write (restated
+    from doc/tutorial/04-checker.md:58-72) and any other :f has no clause.
+    Parity unpinned: no reference test exercises it."""
+    value: Any = None
+
+    def step(self, op):
+        if op.get("f") == "cas":
+            raise ValueError("No matching clause: cas")
+        r = CASRegister(self.value).step(op)
+        return r if is_inconsistent(r) else Register(r.value)
+
+
+def register(value=None):
+    return Register(value)
+
+
+@dataclass(frozen=True)
+class Mutex:
+    """knossos.model/mutex (used at hazelcast/src/jepsen/hazelcast.clj:675,684):
+    :acquire when free takes the lock, :release when held frees it, anything
+    else is inconsistent. Parity unpinned (knossos is not vendored)."""
+    locked: bool = False
+
+    @property
+    def value(self):
+        # the device searches it as a cas-register over {0 free, 1 held}
+        return 1 if self.locked else 0
+
+    def step(self, op):
+        f = op.get("f")
+        if f == "acquire":
+            return inconsistent("already held") if self.locked else Mutex(True)
+        if f == "release":
+            return Mutex(False) if self.locked else inconsistent("not held")
+        raise ValueError(f"No matching clause: {f}")
+
+
+def mutex():
+    return Mutex()
+
+
+_MUTEX_CAS = {"acquire": [0, 1], "release": [1, 0]}
+
+
+def to_device_ops(model, history):
+    """The op maps the device's cas-register search checks for `model`:
+    identity for a cas-register; a register refuses :cas; a mutex is the
+    cas-register over {0 free, 1 held} with :acquire = cas 0->1 and :release =
+    cas 1->0 (the same transitions as Mutex.step). Independent tuples keep
+    their key. Raises ValueError for an :f the model has no clause for, which
+    check-safe turns into {:valid? :unknown} as the reference does."""
+    if isinstance(model, CASRegister):
+        return history
+    out = []
+    for op in history:
+        p = op.get("process")
+        client = isinstance(p, int) and not isinstance(p, bool) and p >= 0
+        f = op.get("f")
+        if isinstance(model, Register):
+            if client and f not in ("read", "write"):
+                raise ValueError(f"No matching clause: {f}")
+            out.append(op)
+            continue
+        if isinstance(model, Mutex):
+            if not client:
+                out.append(op)
+                continue
+            if f not in _MUTEX_CAS:
+                raise ValueError(f"No matching clause: {f}")
+            o = dict(op)
+            o["f"] = "cas"
+            v = op.get("value")
+            cas = list(_MUTEX_CAS[f])
+            if isinstance(v, tuple) and hasattr(v, "key"):     # an independent tuple
+                from .history import MapEntry
+                o["value"] = MapEntry(v.key, cas)
+            else:
+                o["value"] = cas
+            out.append(o)
+            continue
+        raise ValueError(f"model {model!r} has no device implementation")
+    return out

@@ -210,3 +210,55 @@ def test_search_modes(ctx, case):
     c, _ = oracle.check_cas_independent(cols, budget=20000, threads=8)
     g, _ = ctx.check_cas_independent(cols, budget=20000)
     _same(g, c)
+
+
+def test_mutex_and_register_models(ctx):
+    """knossos.model/mutex and register through the device search (the
+    cas-register over {0 free, 1 held} / read-write only), single history and
+    independent keys, against the oracle on the translated history."""
+    from jepsen_amd import checker as CK
+    from jepsen_amd import independent as IND
+    from jepsen_amd import model as M
+    acq = lambda p, t, v=None: {"process": p, "type": t, "f": "acquire", "value": v}
+    rel = lambda p, t, v=None: {"process": p, "type": t, "f": "release", "value": v}
+    good = [acq(0, "invoke"), acq(0, "ok"), rel(0, "invoke"), rel(0, "ok"), acq(1, "invoke"), acq(1, "ok")]
+    bad = [acq(0, "invoke"), acq(0, "ok"), acq(1, "invoke"), acq(1, "ok")]
+    lin = CK.linearizable({"model": M.mutex()})
+    assert lin.check(None, good, {})["valid?"] is True
+    assert lin.check(None, bad, {})["valid?"] is False
+    # independent: key "a" good, key "b" bad
+    h = []
+    for k, hist in (("a", good), ("b", bad)):
+        for op in hist:
+            h.append(dict(op, process=op["process"] + (10 if k == "b" else 0), value=H.tuple_(k, None)))
+    r = IND.IndependentChecker(lin).check(None, h, {})
+    assert r["results"]["a"]["valid?"] is True and r["results"]["b"]["valid?"] is False
+    assert r["failures"] == ["b"] and r["valid?"] is False
+    # random mutex histories: device == oracle on the translated encoding
+    cols_ops = []
+    import random
+    rng = random.Random(3)
+    for key in range(200):
+        busy = {}
+        for _ in range(40):
+            p = rng.randrange(4) + 10 * key
+            if p in busy:
+                cols_ops.append({"process": p, "type": rng.choice(["ok", "ok", "fail"]), "f": busy.pop(p),
+                                 "value": H.tuple_(key, None)})
+            else:
+                f = rng.choice(["acquire", "release"])
+                busy[p] = f
+                cols_ops.append({"process": p, "type": "invoke", "f": f, "value": H.tuple_(key, None)})
+    cols = H.encode(M.to_device_ops(M.mutex(), cols_ops), keyed=True)
+    g, _ = ctx.check_cas_independent(cols, init=0)
+    c, _ = oracle.check_cas_independent(cols, init=0)
+    _same(g, c)
+    # register: read/write only; a :cas op has no clause -> :unknown via check-safe
+    reg = CK.linearizable({"model": M.register(0)})
+    w = [{"process": 0, "type": "invoke", "f": "write", "value": 1},
+         {"process": 0, "type": "ok", "f": "write", "value": 1},
+         {"process": 1, "type": "invoke", "f": "read", "value": None},
+         {"process": 1, "type": "ok", "f": "read", "value": 1}]
+    assert reg.check(None, w, {})["valid?"] is True
+    r = CK.check_safe(reg, None, w + [{"process": 2, "type": "invoke", "f": "cas", "value": [1, 2]}], {})
+    assert r["valid?"] == CK.UNKNOWN

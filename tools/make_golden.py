@@ -180,10 +180,69 @@ def synthetic():
     return manifest
 
 
+def set_full():
+    """jepsen/test/jepsen/checker_test.clj:461-626 (set-full-test), transcribed:
+    the op bindings of each `let`, the histories given to `c`, and the
+    expected maps. `history` (checker_test.clj:448-459) indexes the ops and
+    gives op i the time i * 10^6 ns."""
+    def op(p, t, f, v):
+        return {"process": p, "type": t, "f": f, "value": v}
+
+    def hist(ops):
+        return [dict(o, index=i, time=i * 1000000) for i, o in enumerate(ops)]
+
+    lat = lambda x: {"0": x, "0.5": x, "0.95": x, "0.99": x, "1": x}
+    base = {"lost": [], "lost-count": 0, "never-read": [], "never-read-count": 0,
+            "stale-count": 0, "stale": [], "worst-stale": [], "stable-count": 0,
+            "duplicated-count": 0, "duplicated": {}}
+    cases = []
+
+    def case(name, line, ops_list, expected):
+        for i, ops in enumerate(ops_list):
+            cases.append({"name": f"{name}#{i}", "source": f"checker_test.clj:{line}",
+                          "history": hist(ops), "expected": dict(base, **expected)})
+
+    a, a_ = op(0, "invoke", "add", 0), op(0, "ok", "add", 0)
+    case("never read", 465, [[a, a_]],
+         {"attempt-count": 1, "never-read": [0], "never-read-count": 1, "valid?": "unknown"})
+    r, rp, rm = op(1, "invoke", "read", None), op(1, "ok", "read", [0]), op(1, "ok", "read", [])
+    case("never confirmed, never read", 485, [[a, r, rm]],
+         {"attempt-count": 1, "never-read": [0], "never-read-count": 1, "valid?": "unknown"})
+    case("successful read either concurrently or after", 499,
+         [[r, a, rp, a_], [r, a, a_, rp], [a, r, rp, a_], [a, r, a_, rp], [a, a_, r, rp]],
+         {"valid?": True, "attempt-count": 1, "stable-count": 1, "stable-latencies": lat(0)})
+    case("Absent read after", 520, [[a, a_, r, rm]],
+         {"valid?": False, "attempt-count": 1, "lost": [0], "lost-count": 1,
+          "lost-latencies": lat(0)})
+    case("Absent read concurrently", 536,
+         [[r, a, rm, a_], [r, a, a_, rm], [a, r, rm, a_], [a, r, a_, rm]],
+         {"valid?": "unknown", "attempt-count": 1, "never-read": [0], "never-read-count": 1})
+    a0, a0_ = op(0, "invoke", "add", 0), op(0, "ok", "add", 0)
+    a1, a1_ = op(1, "invoke", "add", 1), op(1, "ok", "add", 1)
+    r2, r3 = op(2, "invoke", "read", None), op(3, "invoke", "read", None)
+    r2e = op(2, "ok", "read", [])
+    r2_0, r3_1 = op(2, "ok", "read", [0]), op(3, "ok", "read", [1])
+    r2_1, r2_01 = op(2, "ok", "read", [1]), op(2, "ok", "read", [0, 1])
+    case("write, present, missing", 570,
+         [[a0, a1, r2, r2_1, a0_, a1_, r2, r2_01, r2, r2_0, r2, r2e]],
+         {"valid?": False, "attempt-count": 2, "lost": [0, 1], "lost-count": 2,
+          "lost-latencies": {"0": 3, "0.5": 4, "0.95": 4, "0.99": 4, "1": 4}})
+    h = [a0, a0_, a1, r2, r2_1, a1_, r2, r3, r3_1, r2_0]
+    case("write, flutter, stable/lost", 587, [h],
+         {"valid?": False, "attempt-count": 2, "lost": [0], "lost-count": 1,
+          "stale-count": 1, "stale": [1],
+          "worst-stale": [{"element": 1,
+                           "known": dict(r2_1, index=4, time=4000000),
+                           "last-absent": dict(r2, index=6, time=6000000),
+                           "lost-latency": None, "outcome": "stable", "stable-latency": 2}],
+          "stable-count": 1, "lost-latencies": lat(5), "stable-latencies": lat(2)})
+    return {"source": "jepsen/test/jepsen/checker_test.clj:448-626", "cases": cases}
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
     for name, fn in [("perf_test", perf_test), ("counter", counter), ("interval_str", interval_str),
-                     ("independent", independent)]:
+                     ("independent", independent), ("set_full", set_full)]:
         with open(os.path.join(GOLD, name + ".json"), "w") as f:
             json.dump(fn(), f, indent=1)
     man = synthetic()

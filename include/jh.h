@@ -15,6 +15,8 @@
  *                                 jepsen/src/jepsen/checker.clj:127-158
  *   jh_check_counter          <- (checker/counter)  jepsen/src/jepsen/checker.clj:679-734
  *   jh_check_set              <- (checker/set)      jepsen/src/jepsen/checker.clj:182-233
+ *   jh_check_set_full         <- (checker/set-full {:linearizable? b})
+ *                                                   jepsen/src/jepsen/checker.clj:236-534
  *
  * Plain pointers and sizes only. The caller owns every buffer; the library
  * never retains a caller pointer after returning. All entry points are
@@ -189,6 +191,48 @@ int jh_check_set(jh_ctx *ctx, const jh_history *h, jh_set_result *res,
                  int64_t *runs_ok, int64_t *runs_lost, int64_t *runs_unexpected,
                  int64_t *runs_recovered, int64_t runs_cap,
                  char *err, size_t errlen);
+
+/* (checker/set-full {:linearizable? linearizable}), checker.clj:236-534.
+ * Elements are the :value of every :invoke :add by an integer process; a
+ * set :read's :value is its CSR range in aux (value = offset, value2 =
+ * count; a nil :value reads as the empty set). `time` is the :time column
+ * (nanoseconds), indexed by row like the others (host or device pointer
+ * following h->on_device). Per element (set-full-element-results,
+ * checker.clj:289-345): known = the first :ok :add or :ok :read containing
+ * it, last-present / last-absent = the read INVOCATION of greatest index
+ * whose :ok read did / did not contain it; all counted from the element's
+ * last :invoke :add on (a re-invoke resets its state, checker.clj:483-487).
+ * The lost / never-read / stale element lists come back sorted, at most
+ * list_cap each (the counts are always complete); worst_stale holds the
+ * (take 8 (reverse (sort-by :stable-latency stale))) entries. */
+#define JH_SF_QUANTILES 5          /* points [0 0.5 0.95 0.99 1], checker.clj:412 */
+#define JH_SF_WORST 8
+
+typedef struct jh_set_full_elem {
+    int64_t element;
+    int64_t stable_latency;        /* ms */
+    int64_t known_entry;           /* row of the :known op */
+    int64_t last_absent_entry;     /* row of the :last-absent read invocation, or -1 */
+} jh_set_full_elem;
+
+typedef struct jh_set_full_result {
+    int32_t valid;                 /* JH_VALID / JH_INVALID / JH_UNKNOWN (no stable element) */
+    int32_t cause;
+    int64_t attempt_count, stable_count, lost_count, never_read_count, stale_count;
+    int32_t has_stable_latencies, has_lost_latencies;
+    int64_t stable_latencies[JH_SF_QUANTILES];   /* ms at the points above */
+    int64_t lost_latencies[JH_SF_QUANTILES];
+    int64_t n_worst;
+    jh_set_full_elem worst_stale[JH_SF_WORST];
+    int64_t n_reads;               /* :ok :reads by integer processes */
+    int64_t read_elements;         /* sum of their element counts (aux entries scanned) */
+    double  device_ms;             /* device time of the check (HIP events) */
+} jh_set_full_result;
+
+int jh_check_set_full(jh_ctx *ctx, const jh_history *h, const int64_t *time,
+                      int32_t linearizable, jh_set_full_result *res,
+                      int64_t *lost, int64_t *never_read, int64_t *stale, int64_t list_cap,
+                      char *err, size_t errlen);
 
 #ifdef __cplusplus
 }

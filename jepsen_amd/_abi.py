@@ -75,6 +75,29 @@ class JhSetResult(C.Structure):
                 ("n_runs", C.c_int64 * 4)]
 
 
+SF_QUANTILES = 5
+SF_WORST = 8
+SF_POINTS = (0, 0.5, 0.95, 0.99, 1)       # checker.clj:412
+
+
+class JhSetFullElem(C.Structure):
+    _fields_ = [("element", C.c_int64), ("stable_latency", C.c_int64),
+                ("known_entry", C.c_int64), ("last_absent_entry", C.c_int64)]
+
+
+class JhSetFullResult(C.Structure):
+    _fields_ = [("valid", C.c_int32), ("cause", C.c_int32),
+                ("attempt_count", C.c_int64), ("stable_count", C.c_int64),
+                ("lost_count", C.c_int64), ("never_read_count", C.c_int64),
+                ("stale_count", C.c_int64),
+                ("has_stable_latencies", C.c_int32), ("has_lost_latencies", C.c_int32),
+                ("stable_latencies", C.c_int64 * SF_QUANTILES),
+                ("lost_latencies", C.c_int64 * SF_QUANTILES),
+                ("n_worst", C.c_int64), ("worst_stale", JhSetFullElem * SF_WORST),
+                ("n_reads", C.c_int64), ("read_elements", C.c_int64),
+                ("device_ms", C.c_double)]
+
+
 # numpy structured dtype with the same layout as jh_key_verdict
 try:
     import numpy as _np

@@ -47,6 +47,8 @@ def lib():
                                            C.c_char_p, C.c_size_t]
             L.jh_check_set.argtypes = [C.c_void_p, H, C.POINTER(A.JhSetResult), p64, p64, p64, p64,
                                        C.c_int64, C.c_char_p, C.c_size_t]
+            L.jh_check_set_full.argtypes = [C.c_void_p, H, p64, C.c_int32, C.POINTER(A.JhSetFullResult),
+                                            p64, p64, p64, C.c_int64, C.c_char_p, C.c_size_t]
             if L.jh_version() != A.JH_ABI_VERSION:
                 raise RuntimeError("libjh.so ABI version mismatch")
             _lib = L
@@ -55,7 +57,7 @@ def lib():
 
 EXPORTED_SYMBOLS = ["jh_version", "jh_open", "jh_close", "jh_check_cas_independent",
                     "jh_check_cas", "jh_check_cas_independent_device", "jh_check_counter",
-                    "jh_check_set"]
+                    "jh_check_set", "jh_check_set_full"]
 
 
 def _raise(rc, err):
@@ -155,6 +157,28 @@ class Context:
         out = {name: getattr(r, name) for name, _ in A.JhSetResult._fields_ if name != "n_runs"}
         out["runs"] = [runs[i][:2 * min(r.n_runs[i], cap)].reshape(-1, 2) for i in range(4)]
         out["n_runs"] = list(r.n_runs)
+        return out
+
+    def check_set_full(self, cols, time, linearizable=False, list_cap=None, on_device=False):
+        """(checker/set-full {:linearizable? linearizable}). `time` is the :time
+        column (numpy int64, or a device pointer when on_device)."""
+        h = A.make_history(cols, on_device=on_device)
+        cap = int(cols.n) if list_cap is None else list_cap
+        lists = [np.zeros(max(cap, 1), np.int64) for _ in range(3)]
+        r = A.JhSetFullResult()
+        err = C.create_string_buffer(1024)
+        tp = C.cast(C.c_void_p(int(time)), C.POINTER(C.c_int64)) if on_device else A.ptr64(time)
+        rc = lib().jh_check_set_full(self._h, C.byref(h), tp, int(bool(linearizable)), C.byref(r),
+                                     *[A.ptr64(x) for x in lists], cap, err, len(err))
+        _raise(rc, err)
+        out = {name: getattr(r, name) for name, _ in A.JhSetFullResult._fields_}
+        out["stable_latencies"] = list(r.stable_latencies)
+        out["lost_latencies"] = list(r.lost_latencies)
+        out["worst_stale"] = [(w.element, w.stable_latency, w.known_entry, w.last_absent_entry)
+                              for w in r.worst_stale[:r.n_worst]]
+        for i, nm in enumerate(["lost", "never_read", "stale"]):
+            k = min(out[nm + "_count"], cap)
+            out[nm] = lists[i][:k]
         return out
 
 

@@ -245,3 +245,71 @@ class SetChecker(Checker):
 
 def set():  # noqa: A001 - the reference's name (checker.clj:182)
     return SetChecker()
+
+
+class SetFull(Checker):
+    """(checker/set-full {:linearizable? b}), checker.clj:236-534.
+
+    Same result map as the reference: per-element outcomes counted on the
+    device (jh_check_set_full); :worst-stale entries carry the :known and
+    :last-absent op maps of the history."""
+
+    def __init__(self, checker_opts=None):
+        self.opts = dict(checker_opts or {"linearizable?": False})
+
+    def check(self, test, history, opts):
+        ops = None if isinstance(history, H.Columns) else list(history)
+        cols = _cols(ops if ops is not None else history, keyed=False)
+        if not cols.ints_only:
+            raise TypeError("set-full elements must be integers on the device path")
+        if ops is not None:
+            time = np.asarray([int(o.get("time", 0) or 0) for o in ops], np.int64)
+        else:
+            time = getattr(cols, "time", None)
+            if time is None:
+                raise ValueError("set-full needs the :time of every op")
+        if len(time) == 0:
+            time = np.zeros(1, np.int64)
+        r = _ctx().check_set_full(cols, time, linearizable=bool(self.opts.get("linearizable?")))
+        return set_full_result(r, ops if ops is not None else cols, time)
+
+
+def set_full_result(r, ops, time=None):
+    """The (checker/set-full) result map from a jh_check_set_full result."""
+    def op_at(i):
+        if i is None or i < 0:
+            return None
+        if isinstance(ops, H.Columns):
+            o = H.decode_op(ops, int(i))
+            o["index"] = int(i)
+            if time is not None:
+                o["time"] = int(time[i])
+            return o
+        return ops[int(i)]
+
+    valid = {A.VALID: True, A.INVALID: False}.get(r["valid"], UNKNOWN)
+    worst = [{"element": int(e), "outcome": "stable", "stable-latency": int(lat),
+              "lost-latency": None, "known": op_at(k), "last-absent": op_at(la)}
+             for e, lat, k, la in r["worst_stale"]]
+    m = {"valid?": valid,
+         "attempt-count": int(r["attempt_count"]),
+         "stable-count": int(r["stable_count"]),
+         "lost-count": int(r["lost_count"]),
+         "lost": [int(x) for x in r["lost"]],
+         "never-read-count": int(r["never_read_count"]),
+         "never-read": [int(x) for x in r["never_read"]],
+         "stale-count": int(r["stale_count"]),
+         "stale": [int(x) for x in r["stale"]],
+         "worst-stale": worst}
+    if r["has_stable_latencies"]:
+        m["stable-latencies"] = dict(zip(A.SF_POINTS, (int(x) for x in r["stable_latencies"])))
+    if r["has_lost_latencies"]:
+        m["lost-latencies"] = dict(zip(A.SF_POINTS, (int(x) for x in r["lost_latencies"])))
+    # (frequencies v) counts are >= 1, so `(< v 1)` never holds (checker.clj:505-510)
+    m["duplicated-count"] = 0
+    m["duplicated"] = {}
+    return m
+
+
+def set_full(checker_opts=None):
+    return SetFull(checker_opts)

@@ -197,4 +197,20 @@ int jh_check_set(jh_ctx *ctx, const jh_history *h, jh_set_result *res, int64_t *
     });
 }
 
+int jh_check_set_full(jh_ctx *ctx, const jh_history *h, const int64_t *time, int32_t linearizable,
+                      jh_set_full_result *res, int64_t *lost, int64_t *never_read, int64_t *stale,
+                      int64_t list_cap, char *err, size_t errlen) {
+    if (!ctx || !res) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    std::lock_guard<std::mutex> g(ctx->mu);
+    return guarded(err, errlen, [&] {
+        check_hist(h);
+        if (h->n > 0 && !time) throw_jh(JH_EINVAL, "set-full needs the :time column");
+        HIP_TRY(hipSetDevice(ctx->device));
+        jh_history d = stage_history(ctx, h, false, true);
+        const int64_t *dt = h->on_device ? time : stage_col(ctx, WS_SF_TIME, time, h->n, ctx->stream);
+        int64_t *lists[3] = {lost, never_read, stale};
+        set_full_check(ctx, &d, dt, linearizable != 0, res, lists, list_cap < 0 ? 0 : list_cap, ctx->stream);
+    });
+}
+
 }  // extern "C"

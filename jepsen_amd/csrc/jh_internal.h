@@ -94,6 +94,8 @@ enum WsSlot {
     WS_BFS_SET, WS_BFS_Q, WS_BFS_META, WS_CLAIM, WS_SCRATCH_BFS, WS_DEBUG, WS_META, WS_ARENA, WS_DEFER_PROG, WS_LIST_W, WS_C_PT,
     WS_DEFER3, WS_MEMO_P3, WS_STACK_P3, WS_SCRATCH_P3,
     WS_LIST_X, WS_MEMO_X, WS_STACK_X, WS_SCRATCH_X, WS_C_OUT2,
+    WS_SF_META, WS_SF_FLAG, WS_SF_LUT, WS_SF_TMP, WS_SF_ELEM, WS_SF_STATE, WS_SF_RFLAG, WS_SF_READS,
+    WS_SF_BITS, WS_SF_OUT, WS_SF_FL, WS_SF_SEL, WS_SF_TIME, WS_SF_PART,
     WS_COUNT
 };
 
@@ -142,3 +144,6 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
 // set (jh_set.hip)
 void set_check(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, int64_t *runs[4],
                int64_t runs_cap, hipStream_t stream);
+// set-full (jh_setfull.hip); lists_out = {lost, never-read, stale}
+void set_full_check(jh_ctx *ctx, const jh_history *dh, const int64_t *time_dev, bool linearizable,
+                    jh_set_full_result *res, int64_t *lists_out[3], int64_t list_cap, hipStream_t stream);

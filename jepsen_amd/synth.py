@@ -11,6 +11,8 @@ import numpy as np
 
 from .history import Columns
 
+JH_NIL = -(1 << 63)
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
 
@@ -118,3 +120,106 @@ def set_history(n_adds=1000, n_procs=10, p_fail=0.05, p_info=0.02, n_lost=0,
         return _take(h, 0)[0]
     finally:
         lib.jhg_free(C.byref(h))
+
+
+def set_full_history(n_adds=2000, n_procs=10, n_readers=2, read_every=10, p_fail=0.05,
+                     p_info=0.02, n_lost=0, n_stale=0, row_ns=100_000, seed=6):
+    """A (checker/set-full) workload (checker.clj:236-534; the shape of
+    yugabyte/src/yugabyte/set.clj:92 and tidb/src/tidb/sets.clj:53): adds of
+    distinct integers 0..n_adds-1 by `n_procs` processes, `n_readers`
+    processes reading the WHOLE set every `read_every` rounds of adds.
+
+    A round invokes one add per process and completes them in random order;
+    a read invoked before a round completes after it. :ok adds are visible
+    from their completion on, adds concurrent with a read are seen with
+    probability 1/2, :info adds apply with probability 1/2 (and rename the
+    process, core.clj:349), :fail adds never apply. Faults: `n_lost`
+    acknowledged elements vanish from every read after the middle of the
+    history (lost), `n_stale` elements are missed by the first read invoked
+    after their :ok (stale, stable latency > 0). :time = row * row_ns.
+
+    Returns (Columns, time) with the set reads' elements in `aux` (CSR)."""
+    rng = np.random.default_rng(seed)
+    P, RD = n_procs, n_readers
+    rows_p, rows_t, rows_f, rows_v, rows_v2 = [], [], [], [], []
+    aux_parts, aux_len = [], 0
+    applied = np.zeros(n_adds, bool)          # visible from completion on
+    acked_row = np.full(n_adds, -1, np.int64)
+    proc_id = list(range(P))
+    next_proc = P + RD
+    n_rounds = (n_adds + P - 1) // P
+    lost = rng.choice(n_adds, size=n_lost, replace=False) if n_lost else np.zeros(0, np.int64)
+    stale = set(rng.choice(n_adds, size=n_stale, replace=False).tolist()) if n_stale else set()
+    stale_pending = []
+    reader = 0
+    mid_round = n_rounds // 2
+
+    def emit(p, t, f, v=JH_NIL, v2=JH_NIL):
+        rows_p.append(p); rows_t.append(t); rows_f.append(f); rows_v.append(v); rows_v2.append(v2)
+
+    for k in range(n_rounds):
+        els = list(range(k * P, min(n_adds, (k + 1) * P)))
+        rd = (k % read_every) == read_every - 1
+        if rd:
+            rp = P + (reader % RD)
+            reader += 1
+            emit(rp, 0, 0)                     # :invoke :read
+            hide, stale_pending = stale_pending, []   # acked before this read's invocation
+        for j, e in enumerate(els):
+            emit(proc_id[j], 0, 3, e)          # :invoke :add e
+        outcome = rng.random(len(els))
+        seen_conc = rng.random(len(els)) < 0.5
+        for j in rng.permutation(len(els)):
+            e = els[j]
+            if outcome[j] < p_fail:
+                emit(proc_id[j], 2, 3, e)
+            elif outcome[j] < p_fail + p_info:
+                emit(proc_id[j], 3, 3, e)
+                applied[e] = rng.random() < 0.5
+                proc_id[j] = next_proc
+                next_proc += 1
+            else:
+                applied[e] = True
+                acked_row[e] = len(rows_p)
+                emit(proc_id[j], 1, 3, e)
+                if e in stale:
+                    stale_pending.append(e)
+        if rd:
+            vis = applied.copy()
+            conc = np.asarray(els, np.int64)
+            vis[conc] = applied[conc] & seen_conc
+            if k >= mid_round and n_lost:
+                vis[lost] = False
+            for e in hide:
+                vis[e] = False
+            elems = np.flatnonzero(vis).astype(np.int64)
+            emit(rp, 1, 0, aux_len, len(elems))
+            aux_parts.append(elems)
+            aux_len += len(elems)
+    n = len(rows_p)
+    cols = Columns(n=n, process=np.asarray(rows_p, np.int64), type=np.asarray(rows_t, np.int64),
+                   f=np.asarray(rows_f, np.int64), key=np.full(n, -1, np.int64),
+                   value=np.asarray(rows_v, np.int64), value2=np.asarray(rows_v2, np.int64),
+                   n_keys=0, aux=np.concatenate(aux_parts) if aux_parts else np.zeros(1, np.int64))
+    time = np.arange(n, dtype=np.int64) * row_ns
+    return cols, time
+
+
+def columns_to_ops(cols, time):
+    """Op maps (jepsen_amd.history form) of a set-full Columns history, for the
+    pure-Python oracle and the checker mirror."""
+    names = {0: "invoke", 1: "ok", 2: "fail", 3: "info"}
+    fnames = {0: "read", 3: "add"}
+    ops = []
+    for i in range(cols.n):
+        t, f = int(cols.type[i]), int(cols.f[i])
+        if f == 0 and t == 1:
+            o, c = int(cols.value[i]), int(cols.value2[i])
+            v = cols.aux[o:o + c].tolist()
+        elif f == 0:
+            v = None
+        else:
+            v = int(cols.value[i])
+        ops.append({"process": int(cols.process[i]), "type": names[t], "f": fnames[f],
+                    "value": v, "index": i, "time": int(time[i])})
+    return ops

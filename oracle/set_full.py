@@ -66,7 +66,7 @@ def set_full(history, linearizable=False):
                 reads.pop(p, None)
             elif t == "ok":
                 inv = reads.get(p)
-                vs = set(v)
+                vs = set(v or ())                      # (c/set nil) = #{}
                 for el, e in elements.items():
                     if el in vs:                          # set-full-read-present
                         if e["known"] is None:

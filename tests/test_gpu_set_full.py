@@ -1,0 +1,126 @@
+"""(checker/set-full) on the device (jh_check_set_full) against the reference's
+own known answers (checker_test.clj:461-626, tests/golden/set_full.json) and,
+on seeded synthetic histories, against the CPU oracles (oracle/set_full.py,
+oracle/set_full_np.py) element list by element list."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD
+from jepsen_amd import checker, synth
+from oracle import set_full as SF
+from oracle import set_full_np as SN
+
+pytestmark = pytest.mark.gpu
+
+
+def _norm(x):
+    if isinstance(x, dict):
+        return {str(k): _norm(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_norm(v) for v in x]
+    if isinstance(x, float) and x.is_integer():
+        return int(x)
+    return x
+
+
+def _qkeys(m):
+    for k in ("stable-latencies", "lost-latencies"):
+        if k in m:
+            m[k] = {("0" if q == 0 else "1" if q == 1 else str(q)): v for q, v in m[k].items()}
+    return m
+
+
+def _flat_worst(m):
+    m = dict(m)
+    m["worst-stale"] = [(r["element"], r["stable-latency"], r["known"]["index"],
+                         r["last-absent"]["index"] if r["last-absent"] else -1) for r in m["worst-stale"]]
+    return m
+
+
+def test_set_full_known_answers(ctx):
+    d = json.load(open(os.path.join(GOLD, "set_full.json")))
+    assert len(d["cases"]) == 14
+    for c in d["cases"]:
+        got = _qkeys(checker.set_full().check({}, c["history"], {}))
+        assert _norm(got) == _norm(c["expected"]), (c["name"], got, c["expected"])
+
+
+def test_set_full_linearizable_option(ctx):
+    d = json.load(open(os.path.join(GOLD, "set_full.json")))
+    for c in d["cases"]:
+        want = SF.set_full(c["history"], linearizable=True)["valid?"]
+        got = checker.set_full({"linearizable?": True}).check({}, c["history"], {})["valid?"]
+        assert got == want, c["name"]
+
+
+@pytest.mark.parametrize("seed,lost,stale,lin", [(0, 0, 0, False), (1, 5, 7, False), (2, 0, 12, True),
+                                                 (3, 20, 0, False), (4, 0, 0, True)])
+def test_set_full_synthetic_vs_oracles(ctx, seed, lost, stale, lin):
+    cols, time = synth.set_full_history(n_adds=700, read_every=5, n_lost=lost, n_stale=stale, seed=seed)
+    ops = synth.columns_to_ops(cols, time)
+    want = _flat_worst(SF.set_full(ops, linearizable=lin))
+    assert want == SN.set_full_cols(cols, time, linearizable=lin)
+    got = _flat_worst(checker.set_full({"linearizable?": lin}).check({}, ops, {}))
+    assert got == want
+    got_cols = _flat_worst(checker.set_full({"linearizable?": lin}).check({}, _with_time(cols, time), {}))
+    assert got_cols == want
+
+
+def _with_time(cols, time):
+    cols.time = time
+    return cols
+
+
+@pytest.mark.parametrize("batch", [None, "1", "3"])
+def test_set_full_large_vs_numpy_oracle(ctx, batch, monkeypatch):
+    """200 K elements, 40 whole-set reads (~3.8 M read elements), read batches
+    of 1 and 3 reads (JH_SF_BATCH) as well as the default single batch."""
+    if batch:
+        monkeypatch.setenv("JH_SF_BATCH", batch)
+    cols, time = synth.set_full_history(n_adds=200_000, n_procs=20, read_every=250, n_lost=300,
+                                        n_stale=500, seed=11)
+    want = SN.set_full_cols(cols, time)
+    r = ctx.check_set_full(cols, time)
+    got = checker.set_full_result(r, cols, time)
+    assert _flat_worst(got) == want
+    n_ok_reads = int(((cols.f == 0) & (cols.type == 1) & (cols.process >= 0)).sum())
+    assert r["n_reads"] == n_ok_reads == 40 and r["read_elements"] == len(cols.aux)
+    assert r["stable_count"] + r["lost_count"] + r["never_read_count"] == r["attempt_count"] == 200_000
+
+
+def test_set_full_edge_cases(ctx):
+    sf = checker.set_full()
+    # empty history, and a history with adds but no reads
+    assert sf.check({}, [], {})["valid?"] == "unknown"
+    h = [{"process": 0, "type": "invoke", "f": "add", "value": 5, "time": 0},
+         {"process": 0, "type": "ok", "f": "add", "value": 5, "time": 10}]
+    assert _norm(sf.check({}, h, {})) == _norm(SF.set_full(_idx(h)))
+    # re-invoked add resets the element; nemesis reads are ignored; unsorted
+    # read values with elements that were never added; a nil read value
+    h = [{"process": 0, "type": "invoke", "f": "add", "value": 3, "time": 0},
+         {"process": 0, "type": "ok", "f": "add", "value": 3, "time": 1_000_000},
+         {"process": 1, "type": "invoke", "f": "read", "value": None, "time": 2_000_000},
+         {"process": 1, "type": "ok", "f": "read", "value": [], "time": 3_000_000},
+         {"process": 0, "type": "invoke", "f": "add", "value": 3, "time": 4_000_000},
+         {"process": 2, "type": "invoke", "f": "add", "value": 1, "time": 4_500_000},
+         {"process": 0, "type": "ok", "f": "add", "value": 3, "time": 5_000_000},
+         {"process": "nemesis", "type": "invoke", "f": "read", "value": None, "time": 5_500_000},
+         {"process": "nemesis", "type": "ok", "f": "read", "value": [], "time": 5_600_000},
+         {"process": 1, "type": "invoke", "f": "read", "value": None, "time": 6_000_000},
+         {"process": 1, "type": "ok", "f": "read", "value": [99, 3, 1, -7], "time": 9_000_000},
+         {"process": 2, "type": "info", "f": "add", "value": 1, "time": 9_500_000},
+         {"process": 1, "type": "invoke", "f": "read", "value": None, "time": 10_000_000},
+         {"process": 1, "type": "ok", "f": "read", "value": None, "time": 12_000_000},
+         {"process": 1, "type": "invoke", "f": "read", "value": None, "time": 13_000_000},
+         {"process": 1, "type": "ok", "f": "read", "value": [1, 3], "time": 15_000_000}]
+    h = _idx(h)
+    for lin in (False, True):
+        got = checker.set_full({"linearizable?": lin}).check({}, h, {})
+        assert _norm(_qkeys(got)) == _norm(_qkeys(SF.set_full(h, linearizable=lin)))
+
+
+def _idx(h):
+    return [dict(o, index=i) for i, o in enumerate(h)]

@@ -41,3 +41,16 @@ def test_set_full_linearizable_option():
     assert SF.set_full(c["history"], linearizable=True)["valid?"] is False
     ok = [x for x in d["cases"] if x["name"].startswith("successful read")][0]
     assert SF.set_full(ok["history"], linearizable=True)["valid?"] is True
+
+
+def test_set_full_numpy_oracle_matches_op_map_oracle():
+    """oracle/set_full_np.py (columnar, vectorised) == oracle/set_full.py on
+    seeded synthetic histories with lost and stale elements."""
+    from jepsen_amd import synth
+    from oracle import set_full_np as SN
+    for seed, (nl, nst, lin) in enumerate([(0, 0, False), (5, 7, False), (0, 12, True), (20, 0, False)]):
+        cols, time = synth.set_full_history(n_adds=600, read_every=4, n_lost=nl, n_stale=nst, seed=seed)
+        a = SF.set_full(synth.columns_to_ops(cols, time), linearizable=lin)
+        a["worst-stale"] = [(r["element"], r["stable-latency"], r["known"]["index"],
+                             r["last-absent"]["index"] if r["last-absent"] else -1) for r in a["worst-stale"]]
+        assert a == SN.set_full_cols(cols, time, linearizable=lin), seed

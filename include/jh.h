@@ -17,6 +17,9 @@
  *   jh_check_set              <- (checker/set)      jepsen/src/jepsen/checker.clj:182-233
  *   jh_check_set_full         <- (checker/set-full {:linearizable? b})
  *                                                   jepsen/src/jepsen/checker.clj:236-534
+ *   jh_check_total_queue      <- (checker/total-queue) jepsen/src/jepsen/checker.clj:536-628
+ *   jh_check_queue            <- (checker/queue (model/unordered-queue))
+ *                                                   jepsen/src/jepsen/checker.clj:160-180
  *
  * Plain pointers and sizes only. The caller owns every buffer; the library
  * never retains a caller pointer after returning. All entry points are
@@ -69,6 +72,9 @@ extern "C" {
 #define JH_F_WRITE 1
 #define JH_F_CAS   2
 #define JH_F_ADD   3
+#define JH_F_ENQUEUE 4
+#define JH_F_DEQUEUE 5
+#define JH_F_DRAIN   6  /* an :ok :drain's :value collection is a CSR range in aux, like a set read */
 
 #define JH_NIL INT64_MIN
 
@@ -233,6 +239,35 @@ int jh_check_set_full(jh_ctx *ctx, const jh_history *h, const int64_t *time,
                       int32_t linearizable, jh_set_full_result *res,
                       int64_t *lost, int64_t *never_read, int64_t *stale, int64_t list_cap,
                       char *err, size_t errlen);
+
+/* Queues. Values are the :value of :enqueue / :dequeue ops and the elements
+ * of :ok :drain ops (integers, or ids the shim interned; JH_NIL = nil).
+ * Multisets come back as (value, multiplicity) int64 pairs sorted by value,
+ * at most pairs_cap pairs per multiset (n_pairs is always complete). */
+typedef struct jh_queue_result {
+    int32_t valid;             /* JH_VALID / JH_INVALID */
+    int32_t cause;
+    int64_t attempt_count, acknowledged_count, ok_count, unexpected_count,
+            duplicated_count, lost_count, recovered_count;
+    int64_t n_pairs[4];        /* total-queue: lost, unexpected, duplicated, recovered;
+                                  queue: [0] = the final queue */
+    int64_t fail_entry;        /* queue: row of the first :ok :dequeue the model cannot
+                                  supply ("can't dequeue v"), else -1 */
+    int64_t fail_value;
+    double  device_ms;
+} jh_queue_result;
+
+/* (checker/total-queue), checker.clj:570-628, after expand-queue-drain-ops
+ * (:536-568; a crashed :drain is JH_EINVAL, as the reference throws). */
+int jh_check_total_queue(jh_ctx *ctx, const jh_history *h, jh_queue_result *res,
+                         int64_t *lost, int64_t *unexpected, int64_t *duplicated,
+                         int64_t *recovered, int64_t pairs_cap, char *err, size_t errlen);
+
+/* (checker/queue (model/unordered-queue)), checker.clj:160-180: the model
+ * reduced over :invoke :enqueue and :ok :dequeue ops in history order.
+ * final_queue receives the remaining multiset when valid. */
+int jh_check_queue(jh_ctx *ctx, const jh_history *h, jh_queue_result *res,
+                   int64_t *final_queue, int64_t pairs_cap, char *err, size_t errlen);
 
 #ifdef __cplusplus
 }

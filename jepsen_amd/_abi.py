@@ -11,6 +11,7 @@ JH_ABI_VERSION = 1
 JH_OK, JH_EINVAL, JH_EUNSUPPORTED, JH_EDEVICE, JH_ENOMEM = 0, 1, 2, 3, 4
 TYPE_INVOKE, TYPE_OK, TYPE_FAIL, TYPE_INFO = 0, 1, 2, 3
 F_READ, F_WRITE, F_CAS, F_ADD = 0, 1, 2, 3
+F_ENQUEUE, F_DEQUEUE, F_DRAIN = 4, 5, 6
 F_FIRST_INTERNED = 16
 NIL = -(1 << 63)
 
@@ -96,6 +97,15 @@ class JhSetFullResult(C.Structure):
                 ("n_worst", C.c_int64), ("worst_stale", JhSetFullElem * SF_WORST),
                 ("n_reads", C.c_int64), ("read_elements", C.c_int64),
                 ("device_ms", C.c_double)]
+
+
+class JhQueueResult(C.Structure):
+    _fields_ = [("valid", C.c_int32), ("cause", C.c_int32),
+                ("attempt_count", C.c_int64), ("acknowledged_count", C.c_int64),
+                ("ok_count", C.c_int64), ("unexpected_count", C.c_int64),
+                ("duplicated_count", C.c_int64), ("lost_count", C.c_int64),
+                ("recovered_count", C.c_int64), ("n_pairs", C.c_int64 * 4),
+                ("fail_entry", C.c_int64), ("fail_value", C.c_int64), ("device_ms", C.c_double)]
 
 
 # numpy structured dtype with the same layout as jh_key_verdict

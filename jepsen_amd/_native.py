@@ -49,6 +49,10 @@ def lib():
                                        C.c_int64, C.c_char_p, C.c_size_t]
             L.jh_check_set_full.argtypes = [C.c_void_p, H, p64, C.c_int32, C.POINTER(A.JhSetFullResult),
                                             p64, p64, p64, C.c_int64, C.c_char_p, C.c_size_t]
+            L.jh_check_total_queue.argtypes = [C.c_void_p, H, C.POINTER(A.JhQueueResult), p64, p64, p64, p64,
+                                               C.c_int64, C.c_char_p, C.c_size_t]
+            L.jh_check_queue.argtypes = [C.c_void_p, H, C.POINTER(A.JhQueueResult), p64, C.c_int64,
+                                         C.c_char_p, C.c_size_t]
             if L.jh_version() != A.JH_ABI_VERSION:
                 raise RuntimeError("libjh.so ABI version mismatch")
             _lib = L
@@ -57,7 +61,7 @@ def lib():
 
 EXPORTED_SYMBOLS = ["jh_version", "jh_open", "jh_close", "jh_check_cas_independent",
                     "jh_check_cas", "jh_check_cas_independent_device", "jh_check_counter",
-                    "jh_check_set", "jh_check_set_full"]
+                    "jh_check_set", "jh_check_set_full", "jh_check_total_queue", "jh_check_queue"]
 
 
 def _raise(rc, err):
@@ -180,6 +184,36 @@ class Context:
             k = min(out[nm + "_count"], cap)
             out[nm] = lists[i][:k]
         return out
+
+    # -- queues --------------------------------------------------------------
+    def _queue_out(self, r, pairs, names):
+        out = {name: getattr(r, name) for name, _ in A.JhQueueResult._fields_ if name != "n_pairs"}
+        out["n_pairs"] = list(r.n_pairs)
+        cap = len(pairs[0]) // 2
+        for i, nm in enumerate(names):
+            out[nm] = pairs[i][:2 * min(r.n_pairs[i], cap)].reshape(-1, 2)
+        return out
+
+    def check_total_queue(self, cols, pairs_cap=None, on_device=False):
+        h = A.make_history(cols, on_device=on_device)
+        cap = (cols.n + (int(cols.n_aux) if on_device else len(cols.aux)) + 1) if pairs_cap is None else pairs_cap
+        pairs = [np.zeros(2 * max(cap, 1), np.int64) for _ in range(4)]
+        r = A.JhQueueResult()
+        err = C.create_string_buffer(1024)
+        rc = lib().jh_check_total_queue(self._h, C.byref(h), C.byref(r), *[A.ptr64(x) for x in pairs],
+                                        cap, err, len(err))
+        _raise(rc, err)
+        return self._queue_out(r, pairs, ["lost", "unexpected", "duplicated", "recovered"])
+
+    def check_queue(self, cols, pairs_cap=None, on_device=False):
+        h = A.make_history(cols, on_device=on_device)
+        cap = (cols.n + 1) if pairs_cap is None else pairs_cap
+        pairs = [np.zeros(2 * max(cap, 1), np.int64)]
+        r = A.JhQueueResult()
+        err = C.create_string_buffer(1024)
+        rc = lib().jh_check_queue(self._h, C.byref(h), C.byref(r), A.ptr64(pairs[0]), cap, err, len(err))
+        _raise(rc, err)
+        return self._queue_out(r, pairs, ["final_queue"])
 
 
 _default = {}

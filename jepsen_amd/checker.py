@@ -12,7 +12,7 @@ import numpy as np
 
 from . import _abi as A
 from . import history as H
-from .model import CASRegister, Mutex, Register, to_device_ops
+from .model import CASRegister, Mutex, Register, UnorderedQueue, to_device_ops
 
 UNKNOWN = "unknown"
 
@@ -313,3 +313,61 @@ def set_full_result(r, ops, time=None):
 
 def set_full(checker_opts=None):
     return SetFull(checker_opts)
+
+
+def _unscalar(cols, x):
+    x = int(x)
+    if x == A.NIL:
+        return None
+    return cols.value_table[x] if cols.values_interned else x
+
+
+def _multiset(cols, pairs):
+    """(value, multiplicity) pairs -> collections.Counter (a multiset)."""
+    from collections import Counter
+    return Counter({_unscalar(cols, v): int(c) for v, c in pairs})
+
+
+class Queue(Checker):
+    """(checker/queue model), checker.clj:160-180, for knossos'
+    unordered-queue model (jh_check_queue)."""
+
+    def __init__(self, model):
+        self.model = model
+
+    def check(self, test, history, opts):
+        ops = None if isinstance(history, H.Columns) else list(history)
+        if self.model is None:
+            if ops is not None and not ops:
+                return {"valid?": True, "final-queue": None}
+            raise TypeError("(queue nil): model/step on nil")
+        if not isinstance(self.model, UnorderedQueue) or self.model.pending:
+            raise TypeError("the device queue checker takes an empty (model/unordered-queue)")
+        cols = _cols(ops if ops is not None else history, keyed=False)
+        r = _ctx().check_queue(cols)
+        if r["valid"] == A.INVALID:
+            return {"valid?": False, "error": "can't dequeue %s" % (_unscalar(cols, r["fail_value"]),),
+                    "fail-entry": int(r["fail_entry"])}
+        return {"valid?": True, "final-queue": _multiset(cols, r["final_queue"])}
+
+
+def queue(model):
+    return Queue(model)
+
+
+class TotalQueue(Checker):
+    """(checker/total-queue), checker.clj:536-628 (jh_check_total_queue)."""
+
+    def check(self, test, history, opts):
+        cols = _cols(history, keyed=False)
+        r = _ctx().check_total_queue(cols)
+        out = {"valid?": bool(r["valid"] == A.VALID)}
+        for k in ("attempt", "acknowledged", "ok", "unexpected", "duplicated", "lost", "recovered"):
+            out[k + "-count"] = int(r[k + "_count"])
+        for k in ("lost", "unexpected", "duplicated", "recovered"):
+            out[k] = _multiset(cols, r[k])
+        return out
+
+
+def total_queue():
+    return TotalQueue()

@@ -213,4 +213,30 @@ int jh_check_set_full(jh_ctx *ctx, const jh_history *h, const int64_t *time, int
     });
 }
 
+int jh_check_total_queue(jh_ctx *ctx, const jh_history *h, jh_queue_result *res, int64_t *lost,
+                         int64_t *unexpected, int64_t *duplicated, int64_t *recovered, int64_t pairs_cap,
+                         char *err, size_t errlen) {
+    if (!ctx || !res) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    std::lock_guard<std::mutex> g(ctx->mu);
+    return guarded(err, errlen, [&] {
+        check_hist(h);
+        HIP_TRY(hipSetDevice(ctx->device));
+        jh_history d = stage_history(ctx, h, false, true);
+        int64_t *outs[4] = {lost, unexpected, duplicated, recovered};
+        total_queue_check(ctx, &d, res, outs, pairs_cap < 0 ? 0 : pairs_cap, ctx->stream);
+    });
+}
+
+int jh_check_queue(jh_ctx *ctx, const jh_history *h, jh_queue_result *res, int64_t *final_queue,
+                   int64_t pairs_cap, char *err, size_t errlen) {
+    if (!ctx || !res) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    std::lock_guard<std::mutex> g(ctx->mu);
+    return guarded(err, errlen, [&] {
+        check_hist(h);
+        HIP_TRY(hipSetDevice(ctx->device));
+        jh_history d = stage_history(ctx, h, false, false);
+        queue_check(ctx, &d, res, final_queue, pairs_cap < 0 ? 0 : pairs_cap, ctx->stream);
+    });
+}
+
 }  // extern "C"

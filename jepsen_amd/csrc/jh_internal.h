@@ -96,6 +96,8 @@ enum WsSlot {
     WS_LIST_X, WS_MEMO_X, WS_STACK_X, WS_SCRATCH_X, WS_C_OUT2,
     WS_SF_META, WS_SF_FLAG, WS_SF_LUT, WS_SF_TMP, WS_SF_ELEM, WS_SF_STATE, WS_SF_RFLAG, WS_SF_READS,
     WS_SF_BITS, WS_SF_OUT, WS_SF_FL, WS_SF_SEL, WS_SF_TIME, WS_SF_PART,
+    WS_Q_META, WS_Q_PART, WS_Q_HIST, WS_Q_FLAG, WS_Q_ROWS, WS_Q_TMP, WS_Q_MULT, WS_Q_MFLAG, WS_Q_POS,
+    WS_Q_OUT, WS_Q_KEYS, WS_Q_MULT2,
     WS_COUNT
 };
 
@@ -147,3 +149,8 @@ void set_check(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, int64_t *r
 // set-full (jh_setfull.hip); lists_out = {lost, never-read, stale}
 void set_full_check(jh_ctx *ctx, const jh_history *dh, const int64_t *time_dev, bool linearizable,
                     jh_set_full_result *res, int64_t *lists_out[3], int64_t list_cap, hipStream_t stream);
+// queues (jh_queue.hip); outs = {lost, unexpected, duplicated, recovered}
+void total_queue_check(jh_ctx *ctx, const jh_history *dh, jh_queue_result *res, int64_t *outs[4],
+                       int64_t cap, hipStream_t stream);
+void queue_check(jh_ctx *ctx, const jh_history *dh, jh_queue_result *res, int64_t *final_out, int64_t cap,
+                 hipStream_t stream);

@@ -50,7 +50,8 @@ def is_tuple(v):
 
 TYPES = {"invoke": A.TYPE_INVOKE, "ok": A.TYPE_OK, "fail": A.TYPE_FAIL, "info": A.TYPE_INFO}
 TYPE_NAMES = {v: k for k, v in TYPES.items()}
-KNOWN_F = {"read": A.F_READ, "write": A.F_WRITE, "cas": A.F_CAS, "add": A.F_ADD}
+KNOWN_F = {"read": A.F_READ, "write": A.F_WRITE, "cas": A.F_CAS, "add": A.F_ADD,
+           "enqueue": A.F_ENQUEUE, "dequeue": A.F_DEQUEUE, "drain": A.F_DRAIN}
 
 
 def invoke_op(process, f, value):
@@ -188,12 +189,17 @@ def encode(history, keyed=True, intern_values=None):
         if fi == A.F_CAS and isinstance(v, (list, tuple)) and len(v) == 2:
             val[i] = scalar(v[0])
             val2[i] = scalar(v[1])
-        elif isinstance(v, (list, tuple, set, frozenset)) and fi == A.F_READ:
-            # a set read: its elements go to aux (CSR)
-            elems = sorted(v) if isinstance(v, (set, frozenset)) else list(v)
+        elif isinstance(v, (list, tuple, set, frozenset)) and fi in (A.F_READ, A.F_DRAIN):
+            # a set read / a drain: its elements go to aux (CSR)
+            elems = list(v)
+            if isinstance(v, (set, frozenset)):
+                try:
+                    elems = sorted(v)
+                except TypeError:
+                    pass
             val[i] = len(aux)
             val2[i] = len(elems)
-            aux.extend(int(x) for x in elems)
+            aux.extend(scalar(x) for x in elems)
         else:
             val[i] = scalar(v)
     return Columns(n=n, process=proc, type=typ, f=fcol, key=key, value=val, value2=val2,

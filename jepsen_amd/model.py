@@ -95,6 +95,34 @@ def mutex():
     return Mutex()
 
 
+@dataclass(frozen=True)
+class UnorderedQueue:
+    """knossos.model/unordered-queue (checker_test.clj:18-33, disque.clj:305,
+    rabbitmq_test.clj:56): a multiset of pending values; :enqueue adds its
+    value, :dequeue removes one copy or the model is inconsistent ("can't
+    dequeue v"). knossos 0.3.4 is not vendored: restated; checked on the
+    device by jh_check_queue."""
+    pending: tuple = ()
+
+    def step(self, op):
+        from collections import Counter
+        c = Counter(dict(self.pending))
+        f, v = op.get("f"), op.get("value")
+        if f == "enqueue":
+            c[v] += 1
+        elif f == "dequeue":
+            if c[v] <= 0:
+                return inconsistent("can't dequeue %s" % (v,))
+            c[v] -= 1
+        else:
+            raise ValueError(f"No matching clause: {f}")
+        return UnorderedQueue(tuple(sorted(((k, n) for k, n in c.items() if n > 0), key=repr)))
+
+
+def unordered_queue():
+    return UnorderedQueue()
+
+
 _MUTEX_CAS = {"acquire": [0, 1], "release": [1, 0]}
 
 

@@ -223,3 +223,91 @@ def columns_to_ops(cols, time):
         ops.append({"process": int(cols.process[i]), "type": names[t], "f": fnames[f],
                     "value": v, "index": i, "time": int(time[i])})
     return ops
+
+
+def queue_history(n_enqueues=2000, n_procs=5, p_fail=0.05, p_info=0.05, n_lost=0, n_unexpected=0,
+                  n_duplicated=0, n_repeat=0, drain_parts=2, seed=7):
+    """A queue workload for (checker/total-queue) and (checker/queue
+    (model/unordered-queue)) (checker.clj:160-180, 536-628; the shape of
+    disque.clj:305-309 and rabbitmq_test.clj:56-59): `n_procs` enqueuers, one
+    dequeuer taking a random pending element after every round, and a final
+    drain in `drain_parts` :drain ops. Values are distinct integers except
+    `n_repeat` values enqueued twice. :fail enqueues never apply, :info ones
+    apply with probability 1/2. Faults: `n_lost` acknowledged elements are
+    never dequeued, `n_unexpected` never-enqueued values are dequeued,
+    `n_duplicated` elements are dequeued twice. Returns Columns (drain
+    elements in aux)."""
+    rng = np.random.default_rng(seed)
+    P = n_procs
+    DQ = P                                  # dequeuer process
+    vals = rng.choice(10 * n_enqueues + 10, size=n_enqueues, replace=False).astype(np.int64)
+    if n_repeat:
+        vals[-n_repeat:] = vals[:n_repeat]
+    rows = []
+    aux = []
+    pending = []                            # applied, not yet dequeued
+    lost_left = n_lost
+    proc_id = list(range(P))
+    next_proc = P + 1
+    dup_left = n_duplicated
+    dequeued = []
+    for k in range(0, n_enqueues, P):
+        els = vals[k:k + P]
+        for j, v in enumerate(els):
+            rows.append((proc_id[j], 0, 4, int(v), JH_NIL))
+        for j in rng.permutation(len(els)):
+            v = int(els[j])
+            u = rng.random()
+            if u < p_fail:
+                rows.append((proc_id[j], 2, 4, v, JH_NIL))
+            elif u < p_fail + p_info:
+                rows.append((proc_id[j], 3, 4, v, JH_NIL))
+                proc_id[j] = next_proc
+                next_proc += 1
+                if rng.random() < 0.5:
+                    pending.append(v)
+            else:
+                rows.append((proc_id[j], 1, 4, v, JH_NIL))
+                if lost_left and rng.random() < 0.3:
+                    lost_left -= 1          # acknowledged, then lost
+                else:
+                    pending.append(v)
+        if pending:
+            i = int(rng.integers(len(pending)))
+            v = pending.pop(i)
+            rows.append((DQ, 0, 5, JH_NIL, JH_NIL))
+            rows.append((DQ, 1, 5, v, JH_NIL))
+            dequeued.append(v)
+            if dup_left and rng.random() < 0.2:
+                dup_left -= 1
+                rows.append((DQ, 0, 5, JH_NIL, JH_NIL))
+                rows.append((DQ, 1, 5, v, JH_NIL))
+    rest = pending + [int(x) for x in dequeued[:dup_left]]
+    rest += [int(10 * n_enqueues + 100 + i) for i in range(n_unexpected)]
+    rng.shuffle(rest)
+    parts = np.array_split(np.asarray(rest, np.int64), max(drain_parts, 1))
+    for part in parts:
+        rows.append((DQ, 0, 6, JH_NIL, JH_NIL))
+        rows.append((DQ, 1, 6, len(aux), len(part)))
+        aux.extend(part.tolist())
+    a = np.asarray(rows, np.int64).reshape(-1, 5)
+    n = len(a)
+    return Columns(n=n, process=a[:, 0].copy(), type=a[:, 1].copy(), f=a[:, 2].copy(),
+                   key=np.full(n, -1, np.int64), value=a[:, 3].copy(), value2=a[:, 4].copy(),
+                   n_keys=0, aux=np.asarray(aux, np.int64) if aux else np.zeros(1, np.int64))
+
+
+def queue_columns_to_ops(cols):
+    """Op maps of a queue_history (for the oracles and the checker mirror)."""
+    names = {0: "invoke", 1: "ok", 2: "fail", 3: "info"}
+    fnames = {4: "enqueue", 5: "dequeue", 6: "drain"}
+    ops = []
+    for i in range(cols.n):
+        t, f = int(cols.type[i]), int(cols.f[i])
+        v = int(cols.value[i])
+        if f == 6 and t == 1:
+            val = cols.aux[v:v + int(cols.value2[i])].tolist()
+        else:
+            val = None if v == JH_NIL else v
+        ops.append({"process": int(cols.process[i]), "type": names[t], "f": fnames[f], "value": val})
+    return ops

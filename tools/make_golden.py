@@ -239,10 +239,49 @@ def set_full():
     return {"source": "jepsen/test/jepsen/checker_test.clj:448-626", "cases": cases}
 
 
+def queue():
+    """jepsen/test/jepsen/checker_test.clj:13-88 (queue-test, total-queue-test),
+    transcribed. knossos.core's invoke-op / ok-op build {:process :type :f
+    :value}; keywords become strings; a multiset is a sorted [[value, count]]
+    list."""
+    def inv(p, f, v): return {"process": p, "type": "invoke", "f": f, "value": v}
+    def ok(p, f, v): return {"process": p, "type": "ok", "f": f, "value": v}
+    q = [{"name": "empty", "source": "checker_test.clj:14-15", "model": None, "history": [],
+          "valid?": True},
+         {"name": "Possible enqueue but no dequeue", "source": "checker_test.clj:17-19",
+          "model": "unordered-queue", "history": [inv(1, "enqueue", 1)], "valid?": True},
+         {"name": "Definite enqueue but no dequeue", "source": "checker_test.clj:21-23",
+          "model": "unordered-queue", "history": [ok(1, "enqueue", 1)], "valid?": True},
+         {"name": "concurrent enqueue/dequeue", "source": "checker_test.clj:25-29",
+          "model": "unordered-queue",
+          "history": [inv(2, "dequeue", None), inv(1, "enqueue", 1), ok(2, "dequeue", 1)], "valid?": True},
+         {"name": "dequeue but no enqueue", "source": "checker_test.clj:31-33",
+          "model": "unordered-queue", "history": [ok(1, "dequeue", 1)], "valid?": False}]
+    zero = {"duplicated": [], "lost": [], "unexpected": [], "recovered": []}
+    t = [{"name": "empty", "source": "checker_test.clj:36-37", "history": [], "expected": None},
+         {"name": "sane", "source": "checker_test.clj:39-58",
+          "history": [inv(1, "enqueue", 1), inv(2, "enqueue", 2), ok(2, "enqueue", 2),
+                      inv(3, "dequeue", 1), ok(3, "dequeue", 1), inv(3, "dequeue", 2), ok(3, "dequeue", 2)],
+          "expected": dict(zero, **{"valid?": True, "recovered": [[1, 1]], "attempt-count": 2,
+                                    "acknowledged-count": 1, "ok-count": 2, "unexpected-count": 0,
+                                    "lost-count": 0, "duplicated-count": 0, "recovered-count": 1})},
+         {"name": "pathological", "source": "checker_test.clj:60-87",
+          "history": [inv(1, "enqueue", "hung"), inv(2, "enqueue", "enqueued"), ok(2, "enqueue", "enqueued"),
+                      inv(3, "enqueue", "dup"), ok(3, "enqueue", "dup"), inv(4, "dequeue", None),
+                      inv(5, "dequeue", None), ok(5, "dequeue", "wtf"), inv(6, "dequeue", None),
+                      ok(6, "dequeue", "dup"), inv(7, "dequeue", None), ok(7, "dequeue", "dup")],
+          "expected": {"valid?": False, "lost": [["enqueued", 1]], "unexpected": [["wtf", 1]],
+                       "recovered": [], "duplicated": [["dup", 1]], "acknowledged-count": 2,
+                       "attempt-count": 3, "ok-count": 1, "lost-count": 1, "unexpected-count": 1,
+                       "duplicated-count": 1, "recovered-count": 0}}]
+    return {"source": "jepsen/test/jepsen/checker_test.clj:13-88", "queue": q, "total_queue": t}
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
     for name, fn in [("perf_test", perf_test), ("counter", counter), ("interval_str", interval_str),
-                     ("independent", independent), ("set_full", set_full)]:
+                     ("independent", independent), ("set_full", set_full),
+                     ("queue", queue)]:
         with open(os.path.join(GOLD, name + ".json"), "w") as f:
             json.dump(fn(), f, indent=1)
     man = synthetic()

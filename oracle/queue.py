@@ -62,7 +62,10 @@ def queue(history, model="unordered-queue"):
             raise TypeError("(queue nil) on a non-empty history: model/step on nil")
         return {"valid?": True, "final-queue": None}
     pending = Counter()
+    fail = None
     for i, o in enumerate(history):
+        if fail is not None:
+            continue          # an inconsistent model steps to itself; the reduce still visits every op
         f, t, v = o.get("f"), o.get("type"), o.get("value")
         if f == "enqueue" and t == "invoke":
             pending[v] += 1
@@ -70,5 +73,5 @@ def queue(history, model="unordered-queue"):
             if pending[v] > 0:
                 pending[v] -= 1
             else:
-                return {"valid?": False, "error": "can't dequeue %s" % (v,), "fail-index": i}
-    return {"valid?": True, "final-queue": +pending}
+                fail = {"valid?": False, "error": "can't dequeue %s" % (v,), "fail-index": i}
+    return fail if fail is not None else {"valid?": True, "final-queue": +pending}

@@ -53,6 +53,26 @@ int main(void) {{
     assert A.VERDICT_DTYPE.itemsize == C.sizeof(A.JhKeyVerdict)
 
 
+def test_ctypes_layout_set_full_and_queue(tmp_path):
+    prog = tmp_path / "sz2.c"
+    prog.write_text(f'''#include <stdio.h>
+#include <stddef.h>
+#include "{HEADER}"
+int main(void) {{
+  printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(jh_set_full_result), offsetof(jh_set_full_result, worst_stale),
+         offsetof(jh_set_full_result, device_ms), sizeof(jh_queue_result),
+         offsetof(jh_queue_result, fail_entry), sizeof(jh_set_full_elem));
+  return 0; }}''')
+    exe = tmp_path / "sz2"
+    subprocess.run(["gcc", "-o", str(exe), str(prog)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    want = [C.sizeof(A.JhSetFullResult), A.JhSetFullResult.worst_stale.offset,
+            A.JhSetFullResult.device_ms.offset, C.sizeof(A.JhQueueResult),
+            A.JhQueueResult.fail_entry.offset, C.sizeof(A.JhSetFullElem)]
+    assert got == want
+
+
 def test_open_without_gpu_fails_loudly(built):
     """No CPU fallback: without a device the product path raises."""
     import torch

@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--e2e", type=int, default=1, help="also time one call from host buffers (PCIe-inclusive)")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--seed-rank", type=int, default=None,
+                    help="generate the history rank R of a multi-GPU run would check (rehearsal on one GPU)")
     return ap.parse_args()
 
 
@@ -95,7 +97,7 @@ def main():
     # ---- workload: this rank's shard of the C3 configuration -------------
     wl = WORKLOADS[args.workload]
     n_keys = args.keys or wl["keys"]
-    seed = wl["seed"] + 7919 * rank
+    seed = wl["seed"] + 7919 * (rank if args.seed_rank is None else args.seed_rank)
     cols, truth = synth.cas_register(n_keys=n_keys, ops_per_key=args.ops_per_key, seed=seed, **wl["gen"])
     n_entries = int(cols.n)
     names = ["process", "type", "f", "key", "value", "value2"]

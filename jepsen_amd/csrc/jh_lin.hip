@@ -293,9 +293,27 @@ struct DfsArgs {
     const struct KeyMeta *meta; // per key: tables offset and sizes (k_key_tables)
     const char *tables;         // the tables arena
     const int32_t *n_list_dev;  // if set: the list length, on the device
+    int64_t budget_full;        // defer mode: past `budget` a search keeps going up to this
+                                // budget once the queue has no key left for its wave
 };
 
 constexpr int JH_CANCELLED = 3; // internal: the other search settled the key first
+
+// Phase 2 hands a key that reaches its budget to phase 3, which restarts it
+// with the full budget, so that one long search does not hold back the keys
+// queued behind it. Once every key of the list has been taken there is
+// nothing to hold back: the search raises its budget to the full one and
+// carries on (same DFS, same insert count) instead of starting over.
+__device__ __forceinline__ bool extend_budget(const DfsArgs &A, uint32_t &budget) {
+    if (A.budget_full <= (int64_t)budget) return false;
+    int q = 0;
+    if ((threadIdx.x & 63) == 0) q = __hip_atomic_load(A.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    q = __builtin_amdgcn_readlane(q, 0);
+    const int n = A.n_list_dev ? *A.n_list_dev : A.n_list;
+    if (q < n) return false;
+    budget = (uint32_t)min<int64_t>(A.budget_full, 0x7FFFFFFF);
+    return true;
+}
 constexpr int64_t P2_BUDGET = 1 << 16;  // phase-2 inserts before a key moves to phase 3
 
 // write a key's verdict; in a race only the first finisher writes
@@ -937,7 +955,7 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
     unsigned long long pc_lift = 0, pc_probe = 0, pc_ins = 0, pc_fwd = 0, pc_pop = 0, pc_cand = 0, pc_key = 0, pc_lds = 0;          // cand = the legal un-linearized members (else: a popped frame's rest)
     int verdict = -1;
     uint32_t ins = 0;
-    const uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
+    uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
     uint32_t n_steps = 0, n_evict = 0, n_reload = 0, n_slow = 0;
     // the window of layer t in lane registers
     int w = (int)(lay_hi(0) >> 6), P = w;
@@ -1039,7 +1057,7 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
         }
         PROF_MARK(q2); PROF_ADD(pc_probe, q0, q2);
         if (absent) {
-            if (ins >= budget) { verdict = JH_UNKNOWN; break; }
+            if (ins >= budget && !extend_budget(A, budget)) { verdict = JH_UNKNOWN; break; }
             if (A.claim && (ins & 1023) == 1023) {
                 // racing k_lin_bfs: stop if it settled this key first
                 int c = 0;
@@ -1276,7 +1294,7 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
     uint32_t s = (uint32_t)A.init_state;
     int verdict = -1;
     uint32_t ins = 0;
-    const uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
+    uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
     uint32_t chk = min(budget, 1023u);               // next insert count that needs a check
     int w = (int)(lay_hi(0) >> 6), P = w;
     uint32_t r = lay_hi(0) & 63;                       // position of RET[t] in W(t)
@@ -1362,7 +1380,7 @@ expand:
 insert:
     {
         if (ins >= chk) {
-            if (ins >= budget) { verdict = JH_UNKNOWN; goto done; }
+            if (ins >= budget && !extend_budget(A, budget)) { verdict = JH_UNKNOWN; goto done; }
             if (A.claim) {
                 // racing k_lin_bfs: stop if it settled this key first
                 int c = 0;
@@ -1632,7 +1650,8 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         if (A.dbg && lane == 0) { A.dbg[16 * (size_t)blockIdx.x + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * (size_t)blockIdx.x + 3] += 1; }
         if (verdict == JH_CANCELLED) continue;
-        if (verdict == JH_UNKNOWN && A.defer && inserts >= A.budget) {
+        if (verdict == JH_UNKNOWN && A.defer && inserts >= A.budget &&
+            (A.budget_full == 0 || inserts < A.budget_full)) {
             if (lane == 0) {
                 const int d = atomicAdd(A.defer_count, 1);
                 A.defer_list[d] = key;
@@ -2645,6 +2664,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         b.defer_list = defer3; b.defer_count = q + 16; b.defer_prog = nullptr;
         b.memo = memo2; b.memo_cap = cap2; b.stack = stack2; b.scratch = scr2; b.scratch_bytes = scr_bytes_h;
         b.budget = split3 ? p2 : budget;
+        b.budget_full = split3 ? budget : 0;
         b.gen_base = ctx->gen_base + (uint32_t)K + 1;
         b.dbg = dbg ? dbg + 16 * 256 : nullptr; b.claim = claim;
         b.probes = (unsigned long long *)(q + 8);

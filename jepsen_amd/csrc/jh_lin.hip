@@ -1696,14 +1696,20 @@ __global__ void __launch_bounds__(64) k_lin_seq3(DfsArgs A) { lin_dfs_waves<Memo
 // configuration (invalid) WGL's cache ends up holding exactly this set, so
 // verdict, explored count and the furthest return rank (fail_entry) are
 // identical to the sequential search. A key where a terminal configuration
-// is reachable (valid) or the set outgrows the budget is handed to the
-// sequential search (only it defines where :unknown starts for those).
+// is reachable (valid) is settled here only if the complete reachable set is
+// at least BFS_VALID_MIN and below the budget (then WGL cannot reach
+// :unknown); otherwise, and when the set outgrows the budget, it is handed to
+// the sequential search (which alone defines where :unknown starts).
 constexpr int BFS_THREADS = 512;
 constexpr int BFS_HDR = 1024;                      // shared scalars + the layer's window
 constexpr int BFS_TBL = 28672;                     // W-format tables (ops, woff, W) + r[]
 constexpr int LSET = 8192;                         // layer set slots (8 B keys)
 constexpr int BFS_LDS_BYTES = BFS_HDR + BFS_TBL + LSET * 8;   // ~94 KB: one workgroup per CU
 constexpr uint64_t BFS_EMPTY = ~0ULL;
+// A valid key is settled by the BFS (instead of waiting for the sequential
+// search) when its whole reachable set is complete and smaller than the
+// budget; only for sets this large, which the DFS takes milliseconds over.
+constexpr long long BFS_VALID_MIN = 1 << 16;
 
 struct BfsArgs {
     unsigned long long *dbg;  // JH_DEBUG=2: per-workgroup accounting (16 words)
@@ -1730,7 +1736,7 @@ struct BfsArgs {
 struct BfsShared {
     KeyInfo K;
     jh_key_verdict v;
-    int key, need, maxw, status, mode, gclear, ovf;
+    int key, need, maxw, status, mode, gclear, ovf, term;
     unsigned npend, npend2, nfront, nnext, tmax, lcount, r;
     unsigned long long count;
     uint32_t win_vv[64];    // the current layer's window: v1 | v2 << 16
@@ -1806,7 +1812,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
     }
     if (tid == 0) {
         pend[0] = bfs_pack(0, (uint32_t)A.init_state, 0);
-        sh.npend = 1; sh.tmax = 0; sh.count = 0; sh.status = 0; sh.gclear = 0;
+        sh.npend = 1; sh.tmax = 0; sh.count = 0; sh.status = 0; sh.gclear = 0; sh.term = 0;
     }
     __syncthreads();
     const unsigned long long b0 = __builtin_amdgcn_s_memtime();
@@ -1943,7 +1949,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                             ru = rpos[u];
                             if (!((nm >> ru) & 1)) break;
                         }
-                        if (u >= n_ok) { atomicOr(&sh.status, 1); continue; }
+                        if (u >= n_ok) { sh.term = 1; continue; }   // a terminal configuration
                         const unsigned pos = atomicAdd(&sh.npend, 1u);
                         if (pos < A.q_cap) pcur[pos] = bfs_pack(u, (uint32_t)s2, (uint32_t)nm);
                         else atomicOr(&sh.status, 2);
@@ -1973,8 +1979,19 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
         d[0] += __builtin_amdgcn_s_memtime() - b0; d[1] += rounds; d[3] += sh.count; d[4] += 1;
     }
-    if (sh.status) {
+    if (sh.status || (sh.term && !((long long)sh.count - 1 >= BFS_VALID_MIN &&
+                                   (long long)sh.count - 1 < A.budget))) {
         if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
+    } else if (sh.term) {
+        // Valid, and WGL could not have reached :unknown: its cache only ever
+        // holds reachable non-terminal configurations (count - 1 of them, the
+        // initial one is not cached), fewer than the budget. The insert count
+        // of the DFS itself is not known here: explored = -2.
+        if (tid == 0) {
+            jh_key_verdict v;
+            v.valid = JH_VALID; v.cause = 0; v.fail_entry = -1; v.explored = -2;
+            emit_verdict(A.out, A.claim, key, v);
+        }
     } else if (wid == 0) {
         jh_key_verdict v;
         v.valid = JH_INVALID; v.cause = 0;
@@ -2379,8 +2396,8 @@ __global__ void k_summary(const jh_key_verdict *__restrict__ v, int64_t K, long 
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < K;
          k += (int64_t)gridDim.x * blockDim.x) {
         jh_key_verdict x = v[k];
-        if (x.explored < 0) continue;
-        nk++; ex += x.explored;
+        if (x.explored == -1) continue;                 // a key in no tuple
+        nk++; ex += x.explored > 0 ? x.explored : 0;     // -2: settled by the BFS, size unknown
         vmax = max(vmax, (long long)x.valid);
         if (x.valid == JH_INVALID) { ninv++; ff = min(ff, (long long)x.fail_entry); }
         if (x.valid == JH_UNKNOWN) nunk++;

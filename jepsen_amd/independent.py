@@ -79,7 +79,7 @@ class IndependentChecker(Checker):
                 lin_res = {}
                 for kid, key in enumerate(cols.keys):
                     v = verdicts[kid]
-                    if int(v["explored"]) < 0:
+                    if int(v["explored"]) == -1:      # a key in no tuple (-2: settled by the BFS, valid)
                         continue
                     lin_res[key] = lin_result(int(v["valid"]), int(v["cause"]), int(v["fail_entry"]),
                                               int(v["explored"]), cols)

@@ -1,4 +1,4 @@
-# phase-2 budget extension: lin GPU tests, bench (rank 0), rehearsal of ranks 3 and 6
+# lin GPU tests, bench (rank 0 with CPU baseline), rehearsal of ranks 3 and 6
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/p2
 timeout -k 10 600 python -u -m pytest tests/test_gpu_lin.py -x -v --timeout 300 --timeout-method thread > gpurun_out/p2/tests.log 2>&1 || exit 1

@@ -60,7 +60,11 @@ struct MemoCfg {
     static constexpr int LDS = OFF_CNT + BKT;
 };
 using MemoQ = MemoCfg<8, 14>;    // phase 1: 8 KB memo + 2 KB Bloom = 10.25 KB -> 15 waves/CU
-using MemoH = MemoCfg<12, 16>;   // heavy keys: 128 KB memo + 8 KB Bloom = 140 KB -> 1 wave/CU
+#ifndef JH_MEMOH_BLOOM
+#define JH_MEMOH_BLOOM 17
+#endif
+using MemoH = MemoCfg<12, JH_MEMOH_BLOOM>;   // heavy keys: 128 KB memo + 16 KB Bloom = 152 KB -> 1 wave/CU
+                                              // (16 KB Bloom vs 8 KB: -4..7% on the heaviest C3 keys)
 using MemoM = MemoCfg<10, 15>;   // very heavy keys: 32 KB memo + 4 KB Bloom = 37 KB -> 4 waves/CU
 constexpr int STATE_BITS = 20, T_BITS = 20, GEN_BITS = 24;
 constexpr uint32_t STATE_MASK = (1u << STATE_BITS) - 1, T_MASK = (1u << T_BITS) - 1;
@@ -301,16 +305,23 @@ constexpr int JH_CANCELLED = 3; // internal: the other search settled the key fi
 
 // Phase 2 hands a key that reaches its budget to phase 3, which restarts it
 // with the full budget, so that one long search does not hold back the keys
-// queued behind it. Once every key of the list has been taken there is
-// nothing to hold back: the search raises its budget to the full one and
-// carries on (same DFS, same insert count) instead of starting over.
+// queued behind it. Once every key of the list has been taken, and no key
+// has gone to phase 3 yet, there is nothing to hold back: the search raises
+// its budget to the full one and carries on (same DFS, same insert count)
+// instead of starting over.
 __device__ __forceinline__ bool extend_budget(const DfsArgs &A, uint32_t &budget) {
     if (A.budget_full <= (int64_t)budget) return false;
-    int q = 0;
-    if ((threadIdx.x & 63) == 0) q = __hip_atomic_load(A.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int q = 0, d = 0;
+    if ((threadIdx.x & 63) == 0) {
+        q = __hip_atomic_load(A.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        d = __hip_atomic_load(A.defer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     q = __builtin_amdgcn_readlane(q, 0);
+    d = __builtin_amdgcn_readlane(d, 0);
     const int n = A.n_list_dev ? *A.n_list_dev : A.n_list;
-    if (q < n) return false;
+    // with keys already handed to phase 3 it runs anyway (4 waves per CU for
+    // many deep searches): join it rather than delay its start
+    if (q < n || d > 0) return false;
     budget = (uint32_t)min<int64_t>(A.budget_full, 0x7FFFFFFF);
     return true;
 }

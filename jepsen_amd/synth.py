@@ -231,8 +231,8 @@ def queue_history(n_enqueues=2000, n_procs=5, p_fail=0.05, p_info=0.05, n_lost=0
     (model/unordered-queue)) (checker.clj:160-180, 536-628; the shape of
     disque.clj:305-309 and rabbitmq_test.clj:56-59): `n_procs` enqueuers, one
     dequeuer taking a random pending element after every round, and a final
-    drain in `drain_parts` :drain ops. Values are distinct integers except
-    `n_repeat` values enqueued twice. :fail enqueues never apply, :info ones
+    drain in `drain_parts` :drain ops. Values are consecutive integers (as
+    gen/queue, generator.clj:405-416) except `n_repeat` values enqueued twice. :fail enqueues never apply, :info ones
     apply with probability 1/2. Faults: `n_lost` acknowledged elements are
     never dequeued, `n_unexpected` never-enqueued values are dequeued,
     `n_duplicated` elements are dequeued twice. Returns Columns (drain
@@ -240,7 +240,8 @@ def queue_history(n_enqueues=2000, n_procs=5, p_fail=0.05, p_info=0.05, n_lost=0
     rng = np.random.default_rng(seed)
     P = n_procs
     DQ = P                                  # dequeuer process
-    vals = rng.choice(10 * n_enqueues + 10, size=n_enqueues, replace=False).astype(np.int64)
+    # consecutive integers, as gen/queue enqueues them (generator.clj:405-416)
+    vals = np.arange(n_enqueues, dtype=np.int64)
     if n_repeat:
         vals[-n_repeat:] = vals[:n_repeat]
     rows = []
@@ -283,7 +284,7 @@ def queue_history(n_enqueues=2000, n_procs=5, p_fail=0.05, p_info=0.05, n_lost=0
                 rows.append((DQ, 0, 5, JH_NIL, JH_NIL))
                 rows.append((DQ, 1, 5, v, JH_NIL))
     rest = pending + [int(x) for x in dequeued[:dup_left]]
-    rest += [int(10 * n_enqueues + 100 + i) for i in range(n_unexpected)]
+    rest += [int(n_enqueues + 100 + i) for i in range(n_unexpected)]
     rng.shuffle(rest)
     parts = np.array_split(np.asarray(rest, np.int64), max(drain_parts, 1))
     for part in parts:

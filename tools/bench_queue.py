@@ -1,7 +1,7 @@
 """checker/total-queue and checker/queue (model/unordered-queue) measurement
 (jepsen/src/jepsen/checker.clj:160-180, 536-628) on one MI355X: a
-synthetic queue history of 4 M enqueues (~9 M entries; jepsen_amd/synth.py
-queue_history, seed 8) with lost, unexpected and duplicated elements and a
+synthetic queue history of 4 M consecutive-integer enqueues (gen/queue,
+generator.clj:405-416; ~9 M entries; jepsen_amd/synth.py queue_history, seed 8) with lost, unexpected and duplicated elements and a
 final drain.
 
 One JSON line per checker. The history is resident in HBM before the timed

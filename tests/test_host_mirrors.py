@@ -39,3 +39,18 @@ def test_queue_multisets_unintern_values():
     a_id = cols.value_table.index("a")
     ms = checker._multiset(cols, [(a_id, 2), (A.NIL, 1)])
     assert dict(ms) == {"a": 2, None: 1}
+
+
+def test_unsupported_inputs_raise_before_the_device():
+    """The device checkers refuse what they do not cover (the JVM shim then
+    falls back to the reference checker)."""
+    import pytest
+    from jepsen_amd import model
+    with pytest.raises(TypeError):
+        checker.set_full().check({}, [{"process": 0, "type": "invoke", "f": "add", "value": "x",
+                                       "time": 0}], {})
+    with pytest.raises(TypeError):
+        checker.queue(model.cas_register()).check({}, [{"process": 0, "type": "invoke",
+                                                        "f": "enqueue", "value": 1}], {})
+    # (queue nil) on an empty history is valid (checker_test.clj:14-15)
+    assert checker.queue(None).check({}, [], {})["valid?"] is True

@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(256) k_sf_inv(const int64_t *__restrict__ proc
 }
 
 constexpr int BITS_CHUNK = 4096;    // aux entries per workgroup in k_sf_bits
-constexpr int BITS_UNROLL = 4;      // 64-entry groups per wave in flight
+constexpr int BITS_UNROLL = 4;      // 64-entry groups per wave in flight (8: no change, 246 -> 244 us)
 
 // OR of `b` over each run of equal `w` in the wave (runs are contiguous lane
 // ranges; heads = first lane of each run): a segmented Hillis-Steele suffix

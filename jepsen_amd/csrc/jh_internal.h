@@ -97,7 +97,7 @@ enum WsSlot {
     WS_SF_META, WS_SF_FLAG, WS_SF_LUT, WS_SF_TMP, WS_SF_ELEM, WS_SF_STATE, WS_SF_RFLAG, WS_SF_READS,
     WS_SF_BITS, WS_SF_OUT, WS_SF_FL, WS_SF_SEL, WS_SF_TIME, WS_SF_PART,
     WS_Q_META, WS_Q_PART, WS_Q_HIST, WS_Q_FLAG, WS_Q_ROWS, WS_Q_TMP, WS_Q_MULT, WS_Q_MFLAG, WS_Q_POS,
-    WS_Q_OUT, WS_Q_KEYS, WS_Q_MULT2,
+    WS_Q_OUT, WS_Q_KEYS, WS_Q_MULT2, WS_LCOST, WS_LSORT, WS_LTMP,
     WS_COUNT
 };
 

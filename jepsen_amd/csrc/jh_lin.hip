@@ -1610,7 +1610,9 @@ __global__ void __launch_bounds__(256) k_key_tables(TblArgs A) {
                 maxw = key_fill_c<false>(A.src, K, lane, A.arena + off);
                 if (maxw <= 64 && lane == 0) {
                     KeyMeta m;
-                    m.off = off; m.n_ops = K.n_ops; m.n_ok = K.n_ok; m.maxw = maxw; m.pad = 0;
+                    // pad: the window sum, the phase-1 ordering's cost estimate (k_list_cost)
+                    m.off = off; m.n_ops = K.n_ops; m.n_ok = K.n_ok; m.maxw = maxw;
+                    m.pad = (int32_t)min(K.sumW, (long long)0x7FFFFFFE);
                     A.meta[key] = m;
                     if (A.states8 && maxw <= 40) A.list[atomicAdd(A.n_list, 1)] = (int32_t)key;
                     else A.list_w[atomicAdd(A.n_list_w, 1)] = (int32_t)key;
@@ -1685,6 +1687,28 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
     if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 15] = my_probes;
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
+}
+
+// Phase 1 hands keys out in list order and ends when its slowest wave ends;
+// a wave that takes a costly key late leaves a tail. Largest estimated cost
+// first (LPT): the cost is the key's window sum (sum over ok returns of the
+// open calls, which bounds each layer's branching). Slots past the list's
+// length get cost 0 and sort last. Only the order changes: every key is
+// still searched by the same DFS.
+__global__ void __launch_bounds__(256) k_list_cost(const int32_t *__restrict__ list, const int32_t *__restrict__ n_list,
+                                                   const KeyMeta *__restrict__ meta, int64_t K, uint32_t *cost,
+                                                   int32_t *val) {
+    const int n = *n_list;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i < n) {
+            const int32_t k = list[i];
+            cost[i] = (uint32_t)meta[k].pad + 1u;
+            val[i] = k;
+        } else {
+            cost[i] = 0;
+            val[i] = -1;
+        }
+    }
 }
 
 // phase 1: every key under the quick budget
@@ -2543,9 +2567,21 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     ta.states8 = (vmax - vmin + 2) <= 256 ? 1 : 0;
     k_key_tables<<<(unsigned)std::min<int64_t>((K + 3) / 4, 8192), 256, 0, st>>>(ta);
 
+    int32_t *list1 = list;
+    if (!getenv("JH_NO_LPT") && K > 1) {
+        uint32_t *cost = ctx->ws<uint32_t>(WS_LCOST, 2 * K);
+        int32_t *lv = ctx->ws<int32_t>(WS_LSORT, 2 * K);
+        k_list_cost<<<grid_for(K, 256, 4096), 256, 0, st>>>(list, q + 12, meta, K, cost, lv);
+        size_t tbl = 0;
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tbl, cost, cost + K, lv, lv + K, (int)K, 0, 32, st));
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(ctx->ws<char>(WS_LTMP, tbl), tbl, cost, cost + K, lv,
+                                                             lv + K, (int)K, 0, 32, st));
+        list1 = lv + K;
+    }
+
     DfsArgs a{};
     a.rec = rec; a.pair = pair; a.off = off; a.rows = rB; a.viol = viol; a.rank = rank;
-    a.list = list; a.n_list = 0; a.n_list_dev = q + 12; a.queue = q; a.out = out_dev;
+    a.list = list1; a.n_list = 0; a.n_list_dev = q + 12; a.queue = q; a.out = out_dev;
     a.meta = meta; a.tables = arena;
     uint32_t *defer_prog = ctx->ws<uint32_t>(WS_DEFER_PROG, K + 1);
     a.defer_list = defer; a.defer_count = q + 1; a.defer_prog = defer_prog;

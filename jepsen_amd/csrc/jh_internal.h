@@ -57,6 +57,7 @@ struct jh_ctx {
     std::vector<Buf> bufs;
     hipEvent_t ev[12] = {};
     uint32_t gen_base = 0;        // memo generation tags (see jh_lin.hip)
+    bool lds_attr = false;        // >64 KB dynamic-LDS attributes set for this device's kernels
     int n_cu = 256;
     void *pinned = nullptr;       // small pinned staging for scalars
     size_t pinned_bytes = 0;

@@ -2674,7 +2674,6 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
         HIP_TRY(hipMemsetAsync(q + 3, 0, sizeof(int32_t), st));
         HIP_TRY(hipMemsetAsync(q + 6, 0, sizeof(int32_t), st));
-        HIP_TRY(hipEventRecord(ctx->ev[6], st));
 
         uint32_t set_cap = 1u << 12;
         while ((int64_t)set_cap < 2 * budget && set_cap < (1u << 30)) set_cap <<= 1;
@@ -2697,15 +2696,15 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         c.scratch = bscr; c.scratch_bytes = scr_bytes_bfs; c.budget = budget;
         c.init_state = init_state; c.states_ok = (vmax - vmin + 2) < 4096 ? 1 : 0;
         c.dbg = dbg; c.claim = claim;
-        static bool lds_attr = false;
-        if (!lds_attr) {
+        // per context (= per device; calls on one context are serialised by its mutex)
+        if (!ctx->lds_attr) {
             HIP_TRY(hipFuncSetAttribute((const void *)k_lin_bfs, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         BFS_LDS_BYTES));
             HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         MemoH::LDS));
             HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         MemoH::LDS));
-            lds_attr = true;
+            ctx->lds_attr = true;
         }
 
         uint32_t cap2 = 1u << 16;
@@ -2716,6 +2715,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;
         uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
         if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
+        // the fork point: everything the phase-2 searches read (claims, queue
+        // counters, the cleared memo on a generation wrap) is ordered before it
+        HIP_TRY(hipEventRecord(ctx->ev[6], st));
         Frame *stack2 = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap);
         char *scr2 = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes_h);
         // phase 2 stops at P2_BUDGET inserts and hands the key to phase 3

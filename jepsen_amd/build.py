@@ -66,7 +66,7 @@ def build_gen():
     src = os.path.join(CSRC, "gen.cpp")
     lib = os.path.join(HERE, "libjhgen.so")
     if _newer(lib, [src, os.path.join(ROOT, "include", "jh.h")]):
-        _run(["g++", "-O2", "-g", "-fPIC", "-shared", "-std=c++17", "-Wall", "-o", lib, src])
+        _run(["g++", "-O2", "-g", "-fPIC", "-shared", "-std=c++17", "-Wall", "-pthread", "-o", lib, src])
     return lib
 
 

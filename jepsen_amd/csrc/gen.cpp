@@ -22,6 +22,7 @@
 #include <vector>
 #include <queue>
 #include <algorithm>
+#include <thread>
 #include "../../include/jh.h"
 
 namespace {
@@ -252,7 +253,7 @@ int jhg_counter(const jhg_counter_params *P, jhg_hist *h) {
     for (int i = 0; i < N; i++) { th[i].proc = i; th[i].phase = 0; pq.push({rng.uni() * 0.1, seq++, i}); }
     // choose which reads are corrupted: every k-th read after the midpoint
     int64_t approx_reads = P->n_ops / std::max(1, P->read_every);
-    int64_t bad_stride = P->n_bad_reads > 0 ? std::max<int64_t>(1, approx_reads / (2 * P->n_bad_reads)) : 0;
+    int64_t bad_stride = P->n_bad_reads > 0 ? std::max<int64_t>(1, approx_reads / (4 * P->n_bad_reads)) : 0;
     int64_t reads_done = 0, bad_left = P->n_bad_reads;
     while (!pq.empty()) {
         Ev e = pq.top(); pq.pop();
@@ -281,7 +282,10 @@ int jhg_counter(const jhg_counter_params *P, jhg_hist *h) {
                 int64_t v = x.res;
                 reads_done++;
                 if (bad_left > 0 && reads_done > approx_reads / 2 && bad_stride && reads_done % bad_stride == 0) {
-                    v += 1000; bad_left--;
+                    // below every lower bound past the midpoint (the :info adds
+                    // widen [lower, upper] without limit, so "v + k" need not be
+                    // out of bounds in a long history)
+                    v = -bad_left; bad_left--;
                 }
                 o->push(x.proc, JH_TYPE_OK, x.f, -1, v, NIL);
             } else o->push(x.proc, JH_TYPE_OK, x.f, -1, x.v, NIL);
@@ -362,6 +366,57 @@ int jhg_set(const jhg_set_params *P, jhg_hist *h) {
     o->process[o->process.size() - 1] = fresh + 1;
     o->process[o->process.size() - 2] = fresh + 1;
     export_out(o, h, 0);
+    return 0;
+}
+
+/* A large independent history built from `parts` sub-histories generated in
+ * parallel (one host thread each): part i holds keys [i*K/parts, (i+1)*K/parts)
+ * and is simulated with seed P->seed * 1000003 + i, as if `parts` groups of
+ * keys had run side by side; the parts are concatenated (each key's entries
+ * stay in their own part's order, which is all the per-key checkers read).
+ * For the 1M-key C4 history, whose single-threaded event simulation would take
+ * minutes. truth[k] is per global key. */
+int jhg_cas_par(const jhg_cas_params *P, int32_t parts, jhg_hist *h) {
+    if (parts < 1) parts = 1;
+    if (parts > P->n_keys) parts = (int32_t)std::max<int64_t>(1, P->n_keys);
+    std::vector<jhg_hist> sub(parts);
+    std::vector<jhg_cas_params> sp(parts, *P);
+    std::vector<int64_t> k0(parts + 1);
+    for (int i = 0; i <= parts; i++) k0[i] = P->n_keys * i / parts;
+    std::vector<std::thread> ts;
+    for (int i = 0; i < parts; i++) {
+        sp[i].n_keys = k0[i + 1] - k0[i];
+        sp[i].seed = P->seed * 1000003ULL + (uint64_t)i;
+        memset(&sub[i], 0, sizeof sub[i]);
+        ts.emplace_back([&, i] { jhg_cas(&sp[i], &sub[i]); });
+    }
+    for (auto &t : ts) t.join();
+    Out *o = new Out();
+    int64_t n = 0;
+    for (auto &x : sub) n += x.n;
+    for (auto *v : {&o->process, &o->type, &o->f, &o->key, &o->value, &o->value2}) v->resize(n);
+    o->truth.assign(P->n_keys, 0);
+    std::vector<int64_t> r0(parts + 1, 0);
+    for (int i = 0; i < parts; i++) r0[i + 1] = r0[i] + sub[i].n;
+    ts.clear();
+    for (int i = 0; i < parts; i++) {
+        ts.emplace_back([&, i] {
+            const jhg_hist &x = sub[i];
+            const int64_t b = r0[i];
+            memcpy(o->process.data() + b, x.process, 8 * x.n);
+            memcpy(o->type.data() + b, x.type, 8 * x.n);
+            memcpy(o->f.data() + b, x.f, 8 * x.n);
+            memcpy(o->value.data() + b, x.value, 8 * x.n);
+            memcpy(o->value2.data() + b, x.value2, 8 * x.n);
+            for (int64_t r = 0; r < x.n; r++) o->key[b + r] = x.key[r] >= 0 ? x.key[r] + k0[i] : x.key[r];
+            // process ids repeat across parts: every op of a part completes
+            // (or crashes and renames its process) before the next part starts
+            if (P->keyed) memcpy(o->truth.data() + k0[i], x.truth, 8 * (k0[i + 1] - k0[i]));
+            jhg_free(&sub[i]);
+        });
+    }
+    for (auto &t : ts) t.join();
+    export_out(o, h, P->keyed ? P->n_keys : 0);
     return 0;
 }
 

@@ -57,6 +57,7 @@ def _load():
             raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
         _lib = C.CDLL(path)
         _lib.jhg_cas.argtypes = [C.POINTER(_CasParams), C.POINTER(_Hist)]
+        _lib.jhg_cas_par.argtypes = [C.POINTER(_CasParams), C.c_int32, C.POINTER(_Hist)]
         _lib.jhg_counter.argtypes = [C.POINTER(_CounterParams), C.POINTER(_Hist)]
         _lib.jhg_set.argtypes = [C.POINTER(_SetParams), C.POINTER(_Hist)]
         _lib.jhg_free.argtypes = [C.POINTER(_Hist)]
@@ -81,9 +82,11 @@ def _take(h, n_truth):
 
 def cas_register(n_keys=10000, ops_per_key=500, threads_per_key=10, readers=5,
                  n_values=5, process_limit=20, groups=10, init_nil=True,
-                 p_info=0.02, p_invalid=0.01, nemesis_every=10000, seed=3, keyed=True):
+                 p_info=0.02, p_invalid=0.01, nemesis_every=10000, seed=3, keyed=True, parts=1):
     """Independent cas-register history (C3 defaults: 10k keys x ~1k entries).
 
+    parts > 1 generates the keys as that many sub-histories on parallel host
+    threads and concatenates them (gen.cpp jhg_cas_par; the C4 1M-key history).
     Returns (Columns, injected) where injected[k] = 1 for keys with a
     stale read injected (all other keys are linearizable by construction)."""
     lib = _load()
@@ -91,7 +94,10 @@ def cas_register(n_keys=10000, ops_per_key=500, threads_per_key=10, readers=5,
                    groups, 1 if init_nil else 0, p_info, p_invalid, nemesis_every, seed,
                    1 if keyed else 0, 0)
     h = _Hist()
-    lib.jhg_cas(C.byref(p), C.byref(h))
+    if parts > 1:
+        lib.jhg_cas_par(C.byref(p), parts, C.byref(h))
+    else:
+        lib.jhg_cas(C.byref(p), C.byref(h))
     try:
         return _take(h, n_keys)
     finally:

@@ -1,0 +1,250 @@
+"""Every BASELINE.json configuration through the device
+path, at full size, against the oracle (and, where the oracle cannot finish at
+full size, against size-independent properties plus oracle equality on a
+bounded slice of the same generator).
+
+  C1  single key, 5 processes, 10k entries: init nil, init 0, and one injected
+      stale read at 50 % depth                          checker.clj:127-158
+  C2  counter (valid and invalid variants) and set at 100M entries
+                                                        checker.clj:679-734, 182-233
+  C3  see test_gpu_lin.py::test_c3_scale_properties (10k keys, every key)
+  C4  1M keys through shard.py (world = 1, one device): properties on every
+      key, oracle equality on 3 x 1000 sampled keys     independent.clj:247-298
+  C5  1000 keys x 50 threads, p_info 0.2: every key equal to the oracle
+  independent o compose{linearizable, other}           linearizable_register.clj:34-38
+"""
+import numpy as np
+import pytest
+
+from jepsen_amd import _abi as A
+from jepsen_amd import checker as CK
+from jepsen_amd import history as H
+from jepsen_amd import independent as IND
+from jepsen_amd import model as M
+from jepsen_amd import shard, synth
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(gpu, cpu):
+    for f in ("valid", "cause", "fail_entry", "explored"):
+        bad = np.nonzero(gpu[f] != cpu[f])[0]
+        assert len(bad) == 0, (f, bad[:10], gpu[bad[:5]], cpu[bad[:5]])
+
+
+# ---------------------------------------------------------------- C1 -------
+@pytest.mark.parametrize("variant", ["init_nil", "init_0", "stale_read"])
+def test_c1_variants(ctx, variant):
+    """C1: one key, 5 processes (2 reserved readers), 10k
+    entries, gen/cas mix, p_info 1 %; (cas-register) and (cas-register 0),
+    and an injected stale read at half the key's ops (several seeds, since a
+    stale read concurrent with a write can still be linearizable). An invalid
+    single key must exhaust its whole reachable set (4.0M and 14.8M
+    configurations for seeds 3 and 2): the budget is raised to 2^24 so that it
+    resolves instead of ending :unknown at the 2^20 default."""
+    init_nil = variant != "init_0"
+    init = None if init_nil else 0
+    seeds = [1] if variant != "stale_read" else [1, 2, 3]
+    budget = (1 << 24) if variant == "stale_read" else None
+    verdicts = []
+    for seed in seeds:
+        cols, truth = synth.cas_register(n_keys=1, ops_per_key=5000, threads_per_key=5, readers=2,
+                                         groups=1, p_info=0.01, seed=seed, keyed=False,
+                                         init_nil=init_nil, process_limit=10 ** 6,
+                                         p_invalid=1.0 if variant == "stale_read" else 0.0)
+        assert cols.n >= 9000
+        g = ctx.check_cas(cols, init=init, budget=budget)
+        c = oracle.check_cas(cols, init=A.NIL if init is None else init, budget=budget or A.DEFAULT_BUDGET)
+        assert tuple(g) == tuple(c), (variant, seed, g, c)
+        verdicts.append(g[0])
+        if variant != "stale_read":
+            assert g[0] == A.VALID
+    if variant == "stale_read":
+        assert verdicts == [A.VALID, A.INVALID, A.INVALID]
+
+
+# ---------------------------------------------------------------- C2 -------
+def test_c2_counter_invalid_100m(ctx):
+    """C2 counter, invalid variant at 100M entries: the 10 injected
+    out-of-bound reads are exactly the errors; bounds are self-consistent."""
+    cols = synth.counter(n_ops=50_000_000, n_procs=10, read_every=101, p_fail=0.05, p_info=0.01,
+                         n_bad_reads=10, seed=2)
+    assert cols.n >= 99_000_000
+    g = ctx.check_counter(cols, reads_cap=1 << 22)
+    assert g["valid"] == A.INVALID and g["n_errors"] == 10
+    r = g["reads"]
+    assert len(r) == g["n_reads"]
+    bad = ~((r[:, 0] <= r[:, 1]) & (r[:, 1] <= r[:, 2]))
+    assert int(bad.sum()) == 10
+    assert (r[:, 0] <= r[:, 2]).all()                      # lower <= upper always
+    assert (np.diff(r[:, 0]) >= 0).all()                   # the lower bound never decreases
+    # the first error's row is an :ok :read row
+    fe = g["first_err_entry"]
+    assert cols.type[fe] == A.TYPE_OK and cols.f[fe] == A.F_READ
+
+
+def test_c2_counter_slice_vs_oracle(ctx):
+    """The same generator at 10M entries: identical to the oracle."""
+    cols = synth.counter(n_ops=5_000_000, n_procs=10, read_every=101, p_fail=0.05, p_info=0.01,
+                         n_bad_reads=10, seed=2)
+    g = ctx.check_counter(cols)
+    c = oracle.check_counter(cols)
+    for k in ("valid", "cause", "n_reads", "n_errors", "first_err_entry"):
+        assert g[k] == c[k], k
+    assert (g["reads"] == c["reads"]).all()
+
+
+def _runs_ok(runs):
+    if len(runs) == 0:
+        return True
+    return bool((runs[:, 0] <= runs[:, 1]).all() and (runs[1:, 0] > runs[:-1, 1] + 1).all())
+
+
+def _runs_count(runs):
+    return int((runs[:, 1] - runs[:, 0] + 1).sum()) if len(runs) else 0
+
+
+def _in_runs(vals, runs):
+    i = np.searchsorted(runs[:, 0], vals, side="right") - 1
+    ok = i >= 0
+    ok[ok] = vals[ok] <= runs[i[ok], 1]
+    return ok
+
+
+def test_c2_set_100m(ctx):
+    """C2 set at 100M entries (50M distinct adds, p_fail 5 %, p_info 2 %, 100
+    lost and 10 unexpected elements): counts add up, the four run sets are
+    sorted and disjoint, exactly the injected faults are found, and the first
+    failing row is the smallest :ok :add row of a lost element."""
+    cols = synth.set_history(n_adds=50_000_000, n_procs=10, p_fail=0.05, p_info=0.02,
+                             n_lost=100, n_unexpected=10, seed=2)
+    assert cols.n >= 100_000_000
+    g = ctx.check_set(cols, runs_cap=40_000_000)
+    assert g["valid"] == A.INVALID
+    assert g["lost_count"] == 100 and g["unexpected_count"] == 10
+    assert g["attempt_count"] == 50_000_000
+    runs = g["runs"]
+    for i in range(4):
+        assert g["n_runs"][i] == len(runs[i]) and _runs_ok(runs[i]), i
+    assert _runs_count(runs[0]) == g["ok_count"] and _runs_count(runs[1]) == 100
+    assert _runs_count(runs[2]) == 10 and _runs_count(runs[3]) == g["recovered_count"]
+    fr = g["final_read_entry"]
+    read = np.unique(cols.aux[cols.value[fr]:cols.value[fr] + cols.value2[fr]])
+    assert g["ok_count"] + g["unexpected_count"] == len(read)
+    ok_add = (cols.type == A.TYPE_OK) & (cols.f == A.F_ADD)
+    assert g["acknowledged_count"] == int(ok_add.sum())
+    # ok = read & attempts, lost = acknowledged - read, recovered = ok - acknowledged
+    assert g["ok_count"] - g["recovered_count"] == g["acknowledged_count"] - g["lost_count"]
+    lost_rows = np.nonzero(ok_add & _in_runs(cols.value, runs[1]))[0]
+    assert len(lost_rows) == 100 and g["first_fail_entry"] == int(lost_rows[0])
+    assert not _in_runs(read, runs[1]).any()
+
+
+def test_c2_set_slice_vs_oracle(ctx):
+    """The same generator at 10M entries: identical to the oracle."""
+    cols = synth.set_history(n_adds=5_000_000, n_procs=10, p_fail=0.05, p_info=0.02,
+                             n_lost=100, n_unexpected=10, seed=2)
+    g = ctx.check_set(cols)
+    c = oracle.check_set(cols)
+    for k in ("valid", "cause", "attempt_count", "acknowledged_count", "ok_count", "lost_count",
+              "recovered_count", "unexpected_count", "first_fail_entry", "final_read_entry"):
+        assert g[k] == c[k], k
+    for i in range(4):
+        assert g["n_runs"][i] == c["n_runs"][i] and (g["runs"][i] == c["runs"][i]).all(), i
+
+
+# ---------------------------------------------------------------- C4 -------
+def test_c4_one_million_keys(ctx):
+    """C4: 1,000,000 keys x ~1k entries (~0.95G entries) as one history,
+    sharded by shard.py with world = 1 (every key on this device, the LPT and
+    renumbering path the multi-GPU run uses), verdict all-reduce over one rank.
+    Properties on every key: no key without an injected fault is invalid, every
+    key present gets a verdict, the summary matches the verdict array. Oracle
+    equality, key by key, on 3 x 1000 keys (start, middle, end)."""
+    K = 1_000_000
+    cols, truth = synth.cas_register(n_keys=K, seed=4, parts=16)
+    assert cols.n_keys == K and cols.n > 900_000_000
+
+    def check_fn(sub, init, budget):
+        return ctx.check_cas_independent(sub)
+
+    mine, v, summ = shard.check_cas_independent_sharded(cols, 0, 1, check_fn)
+    assert len(mine) == K and (mine == np.arange(K)).all()
+    assert not ((v["valid"] == A.INVALID) & (truth[mine] == 0)).any()
+    # every key has client ops (-2: a valid key settled by its complete reachable set)
+    assert ((v["explored"] >= 0) | ((v["explored"] == -2) & (v["valid"] == A.VALID))).all()
+    assert summ["n_keys"] == K
+    assert summ["n_invalid"] == int((v["valid"] == A.INVALID).sum())
+    assert summ["n_unknown"] == int((v["valid"] == A.UNKNOWN).sum())
+    inv = v["valid"] == A.INVALID
+    assert summ["first_fail_entry"] == (int(v["fail_entry"][inv].min()) if inv.any() else -1)
+    assert int(inv.sum()) >= int(truth.sum()) // 3         # most injected faults are caught
+    for k0 in (0, K // 2, K - 1000):
+        c = oracle.check_cas_independent_range(cols, k0, k0 + 1000, threads=16)
+        g = v[k0:k0 + 1000]
+        bfs = g["explored"] == -2
+        assert (c["valid"][bfs] == A.VALID).all()
+        g["explored"][bfs] = c["explored"][bfs]
+        _same(g, c)
+
+
+# ---------------------------------------------------------------- C5 -------
+def test_c5_full(ctx):
+    """C5 at its full size: 1000 keys x ~1k entries, 50 threads per key (25
+    readers), process-limit 100, p_info 0.2 (deep searches, windows wider
+    than 64, budget exhaustion): every key equal to the oracle."""
+    cols, _ = synth.cas_register(n_keys=1000, threads_per_key=50, readers=25, process_limit=100,
+                                 p_info=0.2, p_invalid=0.01, seed=5)
+    g, gs = ctx.check_cas_independent(cols)
+    c, cs = oracle.check_cas_independent(cols, threads=16)
+    _same(g, c)
+    assert (gs.valid, gs.n_invalid, gs.n_unknown, gs.first_fail_entry) == \
+           (cs.valid, cs.n_invalid, cs.n_unknown, cs.first_fail_entry)
+
+
+# --------------------------------------------------- independent o compose --
+class _Recorder(CK.Checker):
+    """A non-linearizable member of the composition (the timeline/html slot of
+    linearizable_register.clj:34-38): records the subhistory it was given."""
+
+    def __init__(self):
+        self.seen = {}
+
+    def check(self, test, history, opts):
+        self.seen[opts["history-key"]] = [(o["index"], o["value"]) for o in history]
+        return {"valid?": True}
+
+
+def test_independent_compose(ctx):
+    """(independent/checker (checker/compose {:linear (linearizable cas-register)
+    :timeline t})): the linearizable member is checked for every key in one
+    device call, the other member receives exactly (subhistory k history)
+    (independent.clj:234-245, including the un-keyed nemesis ops), and the
+    merged maps equal the oracle's per-key verdicts."""
+    cols, truth = synth.cas_register(n_keys=1500, ops_per_key=120, threads_per_key=8, readers=3,
+                                     groups=8, p_info=0.05, p_invalid=0.05, nemesis_every=500,
+                                     seed=31)
+    hist = [H.decode_op(cols, i) for i in range(cols.n)]
+    rec = _Recorder()
+    chk = IND.checker(CK.compose({"linear": CK.linearizable({"model": M.cas_register()}),
+                                  "timeline": rec}))
+    r = chk.check(None, hist, {})
+    c, cs = oracle.check_cas_independent(cols, threads=8)
+    assert set(r["results"]) == set(range(cols.n_keys))
+    for k in range(cols.n_keys):
+        lr = r["results"][k]["linear"]
+        exp = {A.VALID: True, A.INVALID: False, A.UNKNOWN: CK.UNKNOWN}[int(c["valid"][k])]
+        assert lr["valid?"] == exp and lr["explored"] == int(c["explored"][k]), k
+        if exp is False:
+            assert lr["fail-entry"] == int(c["fail_entry"][k])
+            assert lr["op"]["index"] == int(c["fail_entry"][k])
+        assert r["results"][k]["timeline"] == {"valid?": True}
+        assert r["results"][k]["valid?"] == exp
+    assert sorted(r["failures"]) == sorted(np.nonzero(c["valid"] == A.INVALID)[0].tolist())
+    assert r["valid?"] == {0: True, 1: CK.UNKNOWN, 2: False}[int(cs.valid)]
+    # the other member saw (subhistory k history) for every key
+    for k in (0, 1, 777, cols.n_keys - 1):
+        exp = [(o["index"], o["value"]) for o in IND.subhistory(k, hist)]
+        assert rec.seen[k] == exp
+    assert any(o["process"] == "nemesis" for o in IND.subhistory(0, hist))

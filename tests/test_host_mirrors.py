@@ -54,3 +54,18 @@ def test_unsupported_inputs_raise_before_the_device():
                                                         "f": "enqueue", "value": 1}], {})
     # (queue nil) on an empty history is valid (checker_test.clj:14-15)
     assert checker.queue(None).check({}, [], {})["valid?"] is True
+
+
+def test_subhistories_one_pass_equals_subhistory():
+    """independent.subhistories (one pass) == subhistory per key
+    (independent.clj:234-245), un-keyed and nemesis ops included, in order."""
+    from jepsen_amd import independent as IND
+    from jepsen_amd import synth
+    from jepsen_amd import history as H
+    cols, _ = synth.cas_register(n_keys=40, ops_per_key=30, nemesis_every=25, seed=9)
+    hist = [H.decode_op(cols, i) for i in range(cols.n)]
+    hist.insert(7, {"process": 3, "type": "invoke", "f": "read", "value": None})
+    subs = IND.subhistories(hist)
+    assert list(subs) == IND.history_keys(hist)
+    for k in subs:
+        assert subs[k] == IND.subhistory(k, hist)

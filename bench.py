@@ -178,19 +178,12 @@ def main():
     out = None
     if rank == 0:
         parity = None
-        parity_keys_bfs_valid = None
         if not args.no_parity:
             from oracle import oracle
             hv = np.frombuffer(verd.cpu().numpy().tobytes(), dtype=A.VERDICT_DTYPE)
             ov, os_ = oracle.check_cas_independent(cols, threads=min(16, len(os.sched_getaffinity(0))))
-            # verdict, cause and failing row of every key; WGL's cache size for
-            # every key the DFS settled (explored -2: a valid key the BFS settled
-            # by its complete reachable set, jh.h)
-            bfs_valid = (hv["explored"] == -2) & (ov["explored"] >= 0)
-            parity = bool(all((hv[f] == ov[f]).all() for f in ("valid", "cause", "fail_entry")) and
-                          (hv["explored"][~bfs_valid] == ov["explored"][~bfs_valid]).all() and
-                          (hv["valid"][bfs_valid] == A.VALID).all())
-            parity_keys_bfs_valid = int(bfs_valid.sum())
+            # verdict, cause, failing row and WGL's cache size of every key
+            parity = bool(all((hv[f] == ov[f]).all() for f in ("valid", "cause", "fail_entry", "explored")))
         cpu = None
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(cols, args.cpu_sample_keys or wl["cpu_keys"], args.workload.upper())
@@ -223,7 +216,6 @@ def main():
                          "alg_bytes": alg_bytes},
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
-            "parity_keys_settled_by_bfs": parity_keys_bfs_valid,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -124,11 +124,8 @@ typedef struct jh_key_verdict {
     int32_t cause;             /* JH_CAUSE_* */
     int64_t fail_entry;        /* invalid: history row of the ok completion of the
                                   first op no linearization can get past; else -1 */
-    int64_t explored;          /* memo inserts (WGL cache size) for this key; -2 for a
-                                  valid key settled by the complete reachable-set
-                                  enumeration (>= 2^16 and < budget configurations:
-                                  WGL cannot reach :unknown there); -1 for a key
-                                  in no tuple */
+    int64_t explored;          /* memo inserts (WGL cache size) for this key, the same
+                                  on every run; -1 for a key in no tuple */
 } jh_key_verdict;
 
 typedef struct jh_summary {

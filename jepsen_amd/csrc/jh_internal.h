@@ -58,6 +58,7 @@ struct jh_ctx {
     hipEvent_t ev[12] = {};
     uint32_t gen_base = 0;        // memo generation tags (see jh_lin.hip)
     bool lds_attr = false;        // >64 KB dynamic-LDS attributes set for this device's kernels
+    bool lds_attr_wg = false;
     int n_cu = 256;
     void *pinned = nullptr;       // small pinned staging for scalars
     size_t pinned_bytes = 0;
@@ -98,7 +99,7 @@ enum WsSlot {
     WS_SF_META, WS_SF_FLAG, WS_SF_LUT, WS_SF_TMP, WS_SF_ELEM, WS_SF_STATE, WS_SF_RFLAG, WS_SF_READS,
     WS_SF_BITS, WS_SF_OUT, WS_SF_FL, WS_SF_SEL, WS_SF_TIME, WS_SF_PART,
     WS_Q_META, WS_Q_PART, WS_Q_HIST, WS_Q_FLAG, WS_Q_ROWS, WS_Q_TMP, WS_Q_MULT, WS_Q_MFLAG, WS_Q_POS,
-    WS_Q_OUT, WS_Q_KEYS, WS_Q_MULT2, WS_LCOST, WS_LSORT, WS_LTMP,
+    WS_Q_OUT, WS_Q_KEYS, WS_Q_MULT2, WS_LCOST, WS_LSORT, WS_LTMP, WS_ACC_STATS, WS_WG_GSET, WS_WG_WORK, WS_WG_WTAB, WS_WG_PEND, WS_STATS_KEYS,
     WS_COUNT
 };
 

@@ -793,7 +793,7 @@ __device__ __forceinline__ uint64_t hbm_probe(const uint64_t *memo, uint32_t cap
 }
 
 // LEAN key fields
-__device__ __forceinline__ uint32_t lk_t(uint64_t k) { return (uint32_t)(k >> 48) & 0x7FFF; }
+__device__ __forceinline__ uint32_t lk_t(uint64_t k) { return (uint32_t)(k >> 48) & 0x3FFF; }   // t < COMPACT_MAX_OK < 2^14
 __device__ __forceinline__ uint32_t lk_s(uint64_t k) { return (uint32_t)(k >> 40) & 0xFF; }
 __device__ __forceinline__ uint64_t lk_m(uint64_t k) { return k & ((1ULL << 40) - 1); }
 // two independent 32-bit hashes of a LEAN key: the top bits pick its two
@@ -1726,6 +1726,945 @@ template <bool LEAN>
 __global__ void __launch_bounds__(64) k_lin_seq3(DfsArgs A) { lin_dfs_waves<MemoM, LEAN>(A); }
 
 // ---------------------------------------------------------------------------
+// Phase 2 (deferred LEAN keys): one workgroup per key. Wave 0 runs the WGL
+// DFS (dfs_acc: dfs_lean's search plus the hooks below); every wave of the
+// workgroup joins an exhaustive parallel enumeration (wg_enum_work) when the
+// DFS spends many inserts below one stack node.
+//
+// Why the count stays exactly WGL's. Let X be an open node of the DFS stack
+// and M_X the memo when X was inserted. If no terminal configuration is
+// reachable from X ("X is dead"), the sequential DFS inserts exactly
+// Reach(X) \ M_X before it pops X: it visits every node reachable from X that
+// is not in the memo, and a node already there is closed and dead (a child of
+// an expanded node can only be an ancestor on the stack in a cycle, and the
+// graph is a DAG: linearized sets grow along edges), so its reach is in the
+// memo too. The nodes inserted below X so far belong to that set, and the
+// still-open ones (the stack from X to the current node) are its only members
+// whose children may not all be in the memo. So an enumeration from the roots
+// {open nodes from X down}, pruned at the current memo, yields
+// N = Reach(X) \ memo_now; if it meets no terminal configuration, X is dead
+// and memo_now + N is exactly the memo the sequential DFS holds when it pops
+// X: the search merges N, adds |N| to its insert count and pops X. If the
+// enumeration meets a terminal configuration, X is live (the DFS never pops a
+// live node: it ends below it), N is dropped and the DFS goes on untouched.
+// The frames' "rest" sets stay exact: a sibling P+j of X holds L(P)+{j}, while
+// every node of N contains L(P)+{i} (i = X's member), so no sibling is in N.
+// Verdict, explored count (WGL's cache size) and the deepest layer reached
+// (the failing row of an invalid key) are the sequential search's; the tests
+// compare them with oracle/jh_oracle.c's orc_wgl_canonical key by key.
+//
+// Policy (simulated on every deferred key of the C3 histories, all exact):
+// every ACC_T inserts, accelerate the deepest open node with >= ACC_T/2
+// inserts below it that is not known to be live (and, after an inconclusive
+// try, has twice as many); after a success, try its parent at once (climb)
+// until a live node is met. An enumeration gives up (inconclusive) past
+// max(ACC_CAPMIN, ACC_CAPF x the inserts below X) new nodes.
+#ifndef JH_WG_THREADS
+#define JH_WG_THREADS 512
+#endif
+constexpr int WG_THREADS = JH_WG_THREADS;
+// One workgroup per CU: a 64 KB LDS memo and a 64 KB Bloom filter (the merged
+// dead regions live in HBM: a small filter would send most DFS steps there)
+using MemoW = MemoCfg<11, 19>;
+constexpr uint32_t ACC_T = 1024, ACC_CAPF = 4, ACC_CAPMIN = 2048;
+constexpr int ACC_MAXROOTS = 65;    // X lies in the register ring: <= 64 frames + the current node
+constexpr int CMD_ENUM = 1, CMD_DONE = 2;
+constexpr int ENUM_LIVE = 1, ENUM_CAP = 2;
+
+struct WgShared {
+    int cmd, key, merge, status;
+    uint32_t n_roots, n_ok, theta, acc_lo, acc_hi, gen;
+    uint32_t cap_total;       // work positions this call may fill (roots + new nodes)
+    uint32_t head, tail, active;   // the current layer's queue: work[head, tail)
+    uint32_t tmin_new, tmax_new;
+    uint32_t t_cur, t_next;   // the layer being closed / the lowest pending layer
+    uint32_t npend, npend2, pend_sel, gset_used;
+    uint32_t w_cur, r_cur;    // the current layer's window size and RET position
+    uint32_t nchild;          // children of the staged chunk
+    uint32_t win[64];         // the current layer's window: need | becomes << 16 per member
+    const uint32_t *woff;     // the key's window table (wtab_build)
+    const uint32_t *wrq;
+    const uint8_t *rpos;
+};
+constexpr int WG_SH_OFF = (MemoW::LDS + 255) & ~255;
+constexpr int ESET = 2048;          // LDS set of the current layer's configurations (8-byte keys)
+constexpr int ESET_PROBES = 16;     // a key whose first 16 slots are taken goes to the HBM set
+constexpr int WG_ESET_OFF = WG_SH_OFF + (int)((sizeof(WgShared) + 255) & ~255);
+// a round's configurations are expanded child by child across all worker
+// lanes: FL_CHUNK of them at a time are staged (key, candidate bits, prefix)
+constexpr int FL_CHUNK = 512;
+constexpr int WG_STAGE_OFF = WG_ESET_OFF + ESET * 8;
+constexpr int WG_LDS = WG_STAGE_OFF + FL_CHUNK * 20;
+
+struct WgArgs {
+    DfsArgs d;                 // the search: per-workgroup memo / stack / stage, budget, gen, tables
+    uint64_t *gset;            // per workgroup: gset_cap slots, all zero between enumerations
+    uint32_t gset_cap;         // power of two
+    uint64_t *work;            // per workgroup: work_cap keys, all zero between enumerations
+    uint32_t work_cap;
+    char *wtab;                // per workgroup: the current key's window table
+    uint64_t wtab_bytes;
+    uint64_t *pend;            // per workgroup: 2 x pend_cap configurations waiting for a later layer
+    uint32_t pend_cap;
+    unsigned long long *key_prof;    // JH_DEBUG=4: per key {cycles, inserts, verdict | workgroup << 8}
+    uint32_t acc_t;            // inserts between acceleration attempts (ACC_T; 0: plain DFS)
+    unsigned long long *acc_stats;   // [0] enumerations [1] their new nodes [2] dead [3] live [4] inconclusive
+};
+
+__device__ __forceinline__ uint64_t lk_make(uint32_t t, uint32_t s, uint64_t m) {
+    return (1ULL << 63) | ((uint64_t)t << 48) | ((uint64_t)s << 40) | m;
+}
+// enumeration roots are marked with bit 62 (t < 2^14 leaves it clear in every key)
+constexpr uint64_t LK_ROOT = 1ULL << 62;
+
+// Random-access window table of a key for the enumeration, from the compact
+// tables (dfs_lean's lane-resident window moved layer by layer): W(t) is
+// wrq[woff[t] .. woff[t+1]) (need | becomes << 16 per member, call order) and
+// rpos[t] the position of RET[t] in W(t).
+__device__ void wtab_build(const KeyInfo &K, const char *tb, int lane, uint32_t *woff, uint32_t *wrq,
+                           uint8_t *rpos) {
+    const OpC *ops = (const OpC *)tb;
+    const Lay *lay = (const Lay *)(tb + tblc_ops_bytes(K));
+    const int n_ok = K.n_ok;
+    int w = (int)(lay[0].hi >> 6), P = w;
+    uint32_t wr = lane < w ? ops[lane].rq : RQ_EMPTY;
+    uint32_t off = 0;
+    for (int t = 0; t < n_ok; t++) {
+        const uint32_t r = lay[t].hi & 63;
+        if (lane == 0) { woff[t] = off; rpos[t] = (uint8_t)r; }
+        if (lane < w) wrq[off + lane] = wr;
+        off += (uint32_t)w;
+        if (t + 1 < n_ok) {
+            const uint32_t sh = (uint32_t)wave_shl1((int)wr);
+            if (lane >= (int)r) wr = sh;
+            w--;
+            if (lane == w) wr = RQ_EMPTY;
+            const int c = (int)(lay[t + 1].hi >> 6);
+            if (lane >= w && lane < w + c) wr = ops[P + (lane - w)].rq;
+            w += c; P += c;
+        }
+    }
+    if (lane == 0) woff[n_ok] = off;
+}
+
+__device__ __forceinline__ uint32_t wtab_bytes_for(uint32_t max_ok) {
+    return (((max_ok + 1) * 4 + 255) & ~255u) + ((max_ok * 40 * 4 + 255) & ~255u) + ((max_ok + 255) & ~255u);
+}
+
+// Is the configuration in the DFS memo? The LDS table always; the HBM table
+// (behind the Bloom filter) for layers below theta and in the merged range.
+__device__ unsigned int g_prof_hbm, g_prof_gset, g_prof_rounds, g_prof_layers;
+__device__ unsigned long long g_prof_form, g_prof_close, g_prof_merge;
+__device__ __forceinline__ bool wg_memo_has(uint64_t k, const WgShared &sh, const uint64_t *memo,
+                                            uint32_t cap_mask, unsigned long long &probes) {
+    const ulonglong2 *B = (const ulonglong2 *)(jh_lds + MemoW::OFF_MEMO);
+    const uint32_t *bloom = (const uint32_t *)(jh_lds + MemoW::OFF_BLOOM);
+    uint32_t h1, h2, b1, b2;
+    lk_hash((uint32_t)k, (uint32_t)(k >> 32), h1, h2);
+    lk_bkts<MemoW>(h1, h2, b1, b2);
+    const ulonglong2 x0 = B[2 * b1], x1 = B[2 * b1 + 1], y0 = B[2 * b2], y1 = B[2 * b2 + 1];
+    if ((x0.x == k) | (x0.y == k) | (x1.x == k) | (x1.y == k) | (y0.x == k) | (y0.y == k) | (y1.x == k) |
+        (y1.y == k))
+        return true;
+    const uint32_t t = lk_t(k);
+    if ((t < sh.theta || (t >= sh.acc_lo && t <= sh.acc_hi)) && bloom_test2<MemoW>(bloom, lk_bl(h1), lk_bl(h2))) {
+#ifdef JH_ENUM_PROF
+        atomicAdd(&g_prof_hbm, 1u);
+#endif
+        return (hbm_probe(memo, cap_mask, sh.gen, t, lk_s(k), lk_m(k), probes) >> 32) == 0;
+    }
+    return false;
+}
+
+// the enumeration's own set of new nodes (HBM, open addressing, CAS claim)
+__device__ __forceinline__ bool gset_insert(uint64_t *g, uint32_t gmask, uint64_t k, uint32_t &slot,
+                                            int32_t *flags) {
+    uint32_t h = (uint32_t)jh_mix64(k) & gmask;
+    for (uint32_t n = 0;; n++) {
+        if (n > gmask) { atomicOr(flags, 64); return false; }
+        const unsigned long long prev = atomicCAS((unsigned long long *)&g[h], 0ULL, (unsigned long long)k);
+        if (prev == 0) { slot = h; return true; }
+        if (prev == k) return false;
+        h = (h + 1) & gmask;
+    }
+}
+// the slot holding k (every key looked up here was inserted), or ~0u
+__device__ __forceinline__ uint32_t gset_find(const uint64_t *g, uint32_t gmask, uint64_t k) {
+    uint32_t h = (uint32_t)jh_mix64(k) & gmask;
+    for (uint32_t n = 0; n <= gmask; n++) {
+        const uint64_t x = __hip_atomic_load(&g[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (x == k) return h;
+        if (x == 0) return ~0u;
+        h = (h + 1) & gmask;
+    }
+    return ~0u;
+}
+
+// The current layer's set: an LDS table, with the HBM set behind it for a key
+// whose first ESET_PROBES slots are taken. Slots are never freed during a
+// layer, so every inserter of one key sees the same slots and makes the same
+// choice (LDS or HBM): a key is counted once. Returns true if k is new.
+__device__ __forceinline__ bool layer_insert(WgShared &sh, uint64_t *gset, uint32_t gmask, uint64_t k,
+                                             int32_t *flags) {
+    uint64_t *es = (uint64_t *)(jh_lds + WG_ESET_OFF);
+    uint32_t h = (uint32_t)jh_mix64(k) & (ESET - 1);
+    for (int n = 0; n < ESET_PROBES; n++) {
+        const unsigned long long prev = atomicCAS((unsigned long long *)&es[h], 0ULL, (unsigned long long)k);
+        if (prev == 0) return true;
+        if (prev == k) return false;
+        h = (h + 1) & (ESET - 1);
+    }
+    if (!sh.gset_used) sh.gset_used = 1;
+#ifdef JH_ENUM_PROF
+    atomicAdd(&g_prof_gset, 1u);
+#endif
+    uint32_t slot;
+    return gset_insert(gset, gmask, k, slot, flags);
+}
+
+// Append a configuration to the work array (the current layer's queue and the
+// list of new nodes). Past the cap it is still recorded, in the slack that is
+// never claimed, so that the clean-up finds every HBM-set entry.
+__device__ __forceinline__ void wg_append(WgShared &sh, uint64_t *work, uint32_t work_cap, uint64_t e,
+                                          int32_t *flags) {
+    const uint32_t pos = atomicAdd(&sh.tail, 1u);
+    if (pos < work_cap) __hip_atomic_store(&work[pos], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else atomicOr(flags, 64);
+    if (pos >= sh.cap_total) atomicOr(&sh.status, ENUM_CAP);
+}
+
+// The children of a configuration of the current layer the model allows,
+// as window-member bits (the lane-parallel expansion takes them one by one).
+__device__ __forceinline__ uint64_t wg_cands(uint64_t k, const WgShared &sh) {
+    const uint32_t s = lk_s(k);
+    const uint64_t mask = lk_m(k);
+    const uint32_t w = sh.w_cur;
+    uint64_t c = 0;
+    for (uint32_t j = 0; j < w; j++) {
+        const uint32_t need = sh.win[j] & 0xFFFF;
+        c |= (uint64_t)(need == s || need == RQ_ANY) << j;
+    }
+    return c & ~mask;
+}
+
+// One child (member j) of configuration k of the current layer: a same-layer
+// child that is neither in the memo nor in the layer's set joins the layer's
+// queue; the RET child (a later layer) waits in the pending list; a terminal
+// child ends the enumeration (the node is live).
+__device__ __forceinline__ void wg_child(uint64_t k, uint32_t j, WgShared &sh, uint64_t *gset, uint32_t gmask,
+                                         uint64_t *work, uint32_t work_cap, uint64_t *pcur, uint32_t pend_cap,
+                                         const uint64_t *memo, uint32_t cap_mask, unsigned long long &probes,
+                                         int32_t *flags) {
+    const uint32_t t = lk_t(k);
+    const uint64_t mask = lk_m(k);
+    const uint32_t nv = sh.win[j] >> 16;
+    if (j == sh.r_cur) {
+        // lift RET[t], then every next RET op already linearized
+        const uint32_t n_ok = sh.n_ok;
+        uint64_t nm = drop_bit(mask, j);
+        uint32_t u = t + 1;
+        for (;;) {
+            if (u >= n_ok) break;
+            const uint32_t ru = sh.rpos[u];
+            if (!((nm >> ru) & 1)) break;
+            nm = drop_bit(nm, ru);
+            u++;
+        }
+        if (u >= n_ok) { atomicOr(&sh.status, ENUM_LIVE); return; }   // a terminal configuration
+        const uint32_t q = atomicAdd(&sh.npend, 1u);
+        if (q < pend_cap) {
+            __hip_atomic_store(&pcur[q], lk_make(u, nv, nm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            atomicMin(&sh.t_next, u);
+        } else {
+            atomicOr(&sh.status, ENUM_CAP);
+        }
+        return;
+    }
+    const uint64_t ck = lk_make(t, nv, mask | (1ULL << j));
+    if (wg_memo_has(ck, sh, memo, cap_mask, probes)) return;
+    if (!layer_insert(sh, gset, gmask, ck, flags)) return;
+    wg_append(sh, work, work_cap, ck, flags);
+}
+
+// All waves: the enumeration wave 0 set up in sh (its roots in the pending
+// list, marked LK_ROOT), layer by layer: form the lowest pending layer from its
+// pending entries (deduplicated in the layer set, pruned at the memo), close
+// it under same-layer lifts with every worker taking queued configurations,
+// go on with the next pending layer. Then, if it met neither a terminal
+// configuration nor the cap and sh.merge is set, merge the new nodes into the
+// DFS memo (HBM table + Bloom), and clean up (HBM set and work array all zero).
+__device__ __forceinline__ void wg_enum_work(const WgArgs &W, WgShared &sh, int tid, uint64_t *gset, uint64_t *work,
+                                          uint64_t *memo, uint64_t *pend, unsigned long long &probes) {
+    const int lane = tid & 63;
+    // Waves 1.. do the work; wave 0 (the DFS, which calls in from deep inside
+    // its loop) only takes part in the barriers.
+    const bool worker = tid >= 64;
+    const int wid = tid >> 6;
+    const uint32_t wt = (uint32_t)tid - 64, WN = WG_THREADS - 64;
+    const uint32_t gmask = W.gset_cap - 1, cap_mask = W.d.memo_cap - 1;
+    uint64_t *es = (uint64_t *)(jh_lds + WG_ESET_OFF);
+    int32_t *flags = W.d.flags;
+    const unsigned long long cw0 = __builtin_amdgcn_s_memtime();
+    if (worker)
+        for (uint32_t i = wt; i < (uint32_t)ESET; i += WN) es[i] = 0;
+    for (;;) {
+        // ---- form the lowest pending layer ------------------------------------
+        __syncthreads();
+#ifdef JH_ENUM_PROF
+        const unsigned long long pf0 = __builtin_amdgcn_s_memtime();
+        if (tid == 64) atomicAdd(&g_prof_layers, 1u);
+#endif
+        if (tid == 64) {
+            sh.t_cur = sh.t_next; sh.t_next = 0xFFFFFFFFu; sh.npend2 = 0;
+            sh.head = sh.tail; sh.active = 0;
+        }
+        __syncthreads();
+        const uint32_t tc = sh.t_cur, np = sh.npend, sel = sh.pend_sel;
+        uint64_t *pin = pend + (size_t)sel * W.pend_cap, *pout = pend + (size_t)(sel ^ 1) * W.pend_cap;
+        if (worker && wt < 64) {
+            // the layer's window into LDS (the closure reads it for every configuration)
+            const uint32_t base = sh.woff[tc], w = sh.woff[tc + 1] - base;
+            if (wt < w) sh.win[wt] = sh.wrq[base + wt];
+            if (wt == 0) { sh.w_cur = w; sh.r_cur = sh.rpos[tc]; }
+        }
+        if (worker) {
+            for (uint32_t i = wt; i < np; i += WN) {
+                const uint64_t e = __hip_atomic_load(&pin[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint32_t u = lk_t(e);
+                if (u == tc) {
+                    const bool root = (e & LK_ROOT) != 0;
+                    const uint64_t key = e & ~LK_ROOT;
+                    if (!root && wg_memo_has(key, sh, memo, cap_mask, probes)) continue;
+                    if (!layer_insert(sh, gset, gmask, key, flags)) continue;
+                    wg_append(sh, work, W.work_cap, e, flags);
+                } else {
+                    const uint32_t q = atomicAdd(&sh.npend2, 1u);
+                    __hip_atomic_store(&pout[q], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    atomicMin(&sh.t_next, u);
+                }
+            }
+        }
+        __syncthreads();
+        if (tid == 64) { sh.pend_sel = sel ^ 1; sh.npend = sh.npend2; }
+        __syncthreads();
+        uint64_t *pcur = pout;
+#ifdef JH_ENUM_PROF
+        const unsigned long long pf1 = __builtin_amdgcn_s_memtime();
+        if (tid == 64) atomicAdd(&g_prof_form, pf1 - pf0);
+#endif
+        // ---- close it, round by round (what a round appends is the next one):
+        // stage the round's configurations with their candidate children, then
+        // every worker lane takes one child at a time, so that the memo probes
+        // and set inserts of a round are all in flight together
+        uint64_t *st_key = (uint64_t *)(jh_lds + WG_STAGE_OFF);
+        uint64_t *st_cand = st_key + FL_CHUNK;
+        uint32_t *st_pre = (uint32_t *)(st_cand + FL_CHUNK);
+        for (;;) {
+            const uint32_t ra = sh.head, rb = min(sh.tail, sh.cap_total);
+            __syncthreads();
+            if (tid == 64) sh.head = rb;
+            for (uint32_t c0 = ra; c0 < rb; c0 += FL_CHUNK) {
+                const uint32_t nI = min((uint32_t)FL_CHUNK, rb - c0);
+                if (worker)
+                    for (uint32_t q = wt; q < nI; q += WN) {
+                        const uint64_t k = __hip_atomic_load(&work[c0 + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~LK_ROOT;
+                        const uint64_t c = wg_cands(k, sh);
+                        st_key[q] = k; st_cand[q] = c; st_pre[q] = (uint32_t)__popcll(c);
+                    }
+                __syncthreads();
+                if (wid == 1) {
+                    // exclusive prefix of the children counts (one wave)
+                    uint32_t carry = 0;
+                    for (uint32_t b0 = 0; b0 < nI; b0 += 64) {
+                        const uint32_t v = b0 + lane < nI ? st_pre[b0 + lane] : 0u;
+                        uint32_t x = v;
+                        for (int o = 1; o < 64; o <<= 1) {
+                            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+                            if (lane >= o) x += y;
+                        }
+                        if (b0 + lane < nI) st_pre[b0 + lane] = carry + x - v;
+                        carry += (uint32_t)readlane((int)x, 63);
+                    }
+                    if (lane == 0) sh.nchild = carry;
+                }
+                __syncthreads();
+                const uint32_t C = sh.nchild;
+                if (worker && !sh.status)
+                    for (uint32_t ci = wt; ci < C; ci += WN) {
+                        // the staged configuration holding child ci, then its (ci - pre)-th candidate bit
+                        uint32_t lo = 0, hi = nI;
+                        while (hi - lo > 1) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (st_pre[mid] <= ci) lo = mid; else hi = mid;
+                        }
+                        uint64_t c = st_cand[lo];
+                        for (uint32_t n = ci - st_pre[lo]; n > 0; n--) c &= c - 1;
+                        wg_child(st_key[lo], (uint32_t)__builtin_ctzll(c), sh, gset, gmask, work, W.work_cap, pcur,
+                                 W.pend_cap, memo, cap_mask, probes, flags);
+                    }
+                __syncthreads();
+            }
+#ifdef JH_ENUM_PROF
+            if (tid == 64) atomicAdd(&g_prof_rounds, 1u);
+#endif
+            if (sh.status || sh.tail == rb) break;
+        }
+        __syncthreads();
+#ifdef JH_ENUM_PROF
+        if (tid == 64) atomicAdd(&g_prof_close, __builtin_amdgcn_s_memtime() - pf1);
+#endif
+        if (worker)
+            for (uint32_t i = wt; i < (uint32_t)ESET; i += WN) es[i] = 0;
+        if (sh.status || sh.npend == 0) break;
+    }
+    if (tid == 64 && W.acc_stats) atomicAdd(&W.acc_stats[6], __builtin_amdgcn_s_memtime() - cw0);
+    __syncthreads();
+    // new nodes: the work entries without the root mark
+    const uint32_t end = worker ? min(sh.tail, sh.cap_total) : 0;
+    const uint32_t rec_end = worker ? min(sh.tail, W.work_cap) : 0;     // recorded keys, slack included
+    if (worker) {
+        uint32_t tmin = 0xFFFFFFFFu, tmax = 0;
+        for (uint32_t i = wt; i < end; i += WN) {
+            const uint64_t k = __hip_atomic_load(&work[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (!(k & LK_ROOT)) { tmin = min(tmin, lk_t(k)); tmax = max(tmax, lk_t(k)); }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            tmin = min(tmin, (uint32_t)__shfl_xor((int)tmin, o));
+            tmax = max(tmax, (uint32_t)__shfl_xor((int)tmax, o));
+        }
+        if (lane == 0) { atomicMin(&sh.tmin_new, tmin); atomicMax(&sh.tmax_new, tmax); }
+        if (sh.merge && sh.status == 0) {
+            uint32_t *bloom = (uint32_t *)(jh_lds + MemoW::OFF_BLOOM);
+            for (uint32_t i = wt; i < end; i += WN) {
+                const uint64_t k = __hip_atomic_load(&work[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (k & LK_ROOT) continue;
+                hbm_insert(memo, cap_mask, sh.gen, lk_t(k), lk_s(k), lk_m(k));
+                uint32_t h1, h2;
+                lk_hash((uint32_t)k, (uint32_t)(k >> 32), h1, h2);
+                bloom_set2<MemoW>(bloom, lk_bl(h1), lk_bl(h2));
+            }
+        }
+    }
+    // clean-up in two passes: locate every HBM-set slot first (zeroing as we
+    // went would cut the probe chains of keys placed after a zeroed slot)
+    const bool gu = sh.gset_used != 0;
+    if (gu)
+        for (uint32_t i = wt; i < rec_end; i += WN) {
+            const uint64_t k = __hip_atomic_load(&work[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t slot = (k & LK_ROOT) ? ~0u : gset_find(gset, gmask, k);
+            __hip_atomic_store(&work[i], (uint64_t)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    __syncthreads();
+    for (uint32_t i = wt; i < rec_end; i += WN) {
+        if (gu) {
+            const uint32_t slot = (uint32_t)__hip_atomic_load(&work[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (slot != ~0u) __hip_atomic_store(&gset[slot], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __hip_atomic_store(&work[i], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (tid == 64 && W.acc_stats) {
+        atomicAdd(&W.acc_stats[0], 1ULL);
+        atomicAdd(&W.acc_stats[1], (unsigned long long)(end - min(end, sh.n_roots)));
+        atomicAdd(&W.acc_stats[sh.status == 0 ? 2 : (sh.status & ENUM_LIVE) ? 3 : 4], 1ULL);
+    }
+    // every store of this call (merged memo entries, zeroed set and work
+    // slots) is complete before any wave goes on: the next call's atomics and
+    // the DFS's memo probes must not race a late store (workgroup scope: the
+    // waves of a workgroup share this CU's L1)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// dfs_lean with the acceleration hooks (see above). Only wave 0 runs it; the
+// other waves wait at the workgroup barrier for wg_enum_work.
+template <class M>
+__device__ int dfs_acc(const WgArgs &W, WgShared &sh, const KeyInfo &K, const char *tb, int key, int lane,
+                       uint64_t *memo, Frame *stack, uint64_t *stage, uint64_t *gset, uint64_t *work, char *wtab,
+                       uint64_t *pend, long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes) {
+    const DfsArgs &A = W.d;
+    const OpC *ops = (const OpC *)tb;
+    const Lay *lay = (const Lay *)(tb + tblc_ops_bytes(K));
+    const uint32_t n_ok = (uint32_t)K.n_ok;
+    const int n_ops = K.n_ops;
+    const uint32_t cap_mask = A.memo_cap - 1;
+    const uint32_t gen = (A.gen_base + (uint32_t)key + 1) & ((1u << GEN_BITS) - 1);
+    uint64_t *lmemo = (uint64_t *)(jh_lds + M::OFF_MEMO);
+    uint32_t *bloom = (uint32_t *)(jh_lds + M::OFF_BLOOM);
+    uint32_t *bcnt = (uint32_t *)(jh_lds + M::OFF_CNT);
+    uint8_t *bcnt8 = (uint8_t *)bcnt;
+    for (int i = lane; i < M::SLOTS; i += 64) lmemo[i] = 0;
+    for (int i = lane; i < M::BKT / 4; i += 64) bcnt[i] = 0;
+    for (int i = lane; i < M::BLOOM / 32; i += 64) bloom[i] = 0;
+    const uint32_t lb_lo = lane < 32 ? 1u << lane : 0u, lb_hi = lane >= 32 ? 1u << (lane - 32) : 0u;
+    uint32_t theta = 0;
+    int lcount = 0;
+
+    uint32_t tb0 = 0, drq = 0, dhi = 0;
+    auto load_lay = [&](uint32_t base) {
+        tb0 = base;
+        const uint32_t u = base + (uint32_t)lane;
+        if (u < n_ok) { const Lay e = lay[u]; drq = e.rq; dhi = e.hi; }
+    };
+    auto lay_hi = [&](uint32_t u) -> uint32_t {
+        if (u - tb0 >= 64u) load_lay(u >= 32 ? u - 32 : 0);
+        return (uint32_t)readlane((int)dhi, (int)(u - tb0));
+    };
+    int pb = 0;
+    uint32_t urq = RQ_EMPTY;
+    auto load_up = [&](int base) {
+        pb = base;
+        const int j = base + lane;
+        urq = j < n_ops ? ops[j].rq : RQ_EMPTY;
+    };
+    // DFS stack ring: frames [ring_lo, depth) in lane registers (lane = depth mod 64);
+    // f_seq / f_inc: the frame node's insert index and its last inconclusive size
+    uint32_t fm_lo = 0, fm_hi = 0, f_ti = 0, f_s = 0, fr_lo = 0, fr_hi = 0, f_seq = 0, f_inc = 0;
+
+    load_lay(0);
+    uint32_t t = 0, tmax = 0, depth = 0, ring_lo = 0;
+    uint64_t mask = 0;
+    uint32_t s = (uint32_t)A.init_state;
+    int verdict = -1;
+    uint32_t ins = 0;
+    const uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
+    const uint32_t acc_t = W.acc_t ? W.acc_t : 0x7FFFFFFFu;
+    uint32_t next_acc = acc_t;
+    uint32_t chk = min(budget, acc_t);
+    uint32_t cur_seq = 0xFFFFFFFFu, cur_inc = 0;      // the root: seq -1
+    int l_live = -1;                                   // deepest node known to be live
+    uint32_t acc_lo = 1, acc_hi = 0;                   // layers holding merged (HBM) entries
+    bool wtab_ready = false, climb = false;
+    uint32_t climb_jump = 1;                           // levels the next climb test goes up
+    uint32_t n_steps = 0, n_acc = 0;
+    int w = (int)(lay_hi(0) >> 6), P = w;
+    uint32_t r = lay_hi(0) & 63;
+    uint32_t rn = n_ok > 1 ? (lay_hi(1) & 63) : 0;
+    uint32_t wrq = lane < w ? ops[lane].rq : RQ_EMPTY;
+    load_up(P);
+    wave_sync();
+    const ulonglong2 *B = (const ulonglong2 *)lmemo;
+    uint64_t absent = 0, nm_r = 0;
+    uint32_t u_r = 0, klo = 0, khi = 0, b1 = 0, b2 = 0, n1 = 0, n2 = 0, h1 = 0, h2 = 0, nvl = 0;
+    auto child_keys = [&]() {
+        u_r = t; nm_r = 0;
+        if ((absent >> r) & 1) {
+            uint64_t nm = drop_bit(mask, r);
+            uint32_t u = t + 1;
+            if (u >= n_ok) nm = 0;
+            else if ((nm >> rn) & 1) {
+                uint32_t ru = rn;
+                for (;;) {
+                    nm = drop_bit(nm, ru);
+                    u++;
+                    if (u >= n_ok) { nm = 0; break; }
+                    ru = lay_hi(u) & 63;
+                    if (!((nm >> ru) & 1)) break;
+                }
+            }
+            u_r = u; nm_r = nm;
+        }
+        nvl = wrq >> 16;
+        const bool is_r = lane == (int)r;
+        const uint32_t hi_a = (uint32_t)(mask >> 32) | (t << 16) | 0x80000000u;
+        const uint32_t hi_r = (uint32_t)(nm_r >> 32) | (u_r << 16) | 0x80000000u;
+        klo = is_r ? (uint32_t)nm_r : ((uint32_t)mask | lb_lo);
+        khi = (is_r ? hi_r : (hi_a | lb_hi)) | (nvl << 8);
+        lk_hash(klo, khi, h1, h2);
+        lk_bkts<M>(h1, h2, b1, b2);
+    };
+    // Accelerate the open node at depth d (ring_lo <= d <= depth, or d == depth):
+    // 0 dead (merged unless d == 0), 1 live, 2 inconclusive.
+    uint32_t acc_new = 0, acc_tmax = 0, acc_tmin = 0;
+    auto accel = [&](uint32_t d) -> int {
+        const uint32_t seq_d = d == depth ? cur_seq : (uint32_t)readlane((int)f_seq, (int)(d & 63));
+        const uint32_t below = ins - seq_d;
+        int64_t cap = max<int64_t>(ACC_CAPMIN, (int64_t)ACC_CAPF * below);
+        cap = min<int64_t>(cap, (int64_t)budget - ins + 1);
+        const uint32_t n_roots = depth - d + 1;
+        cap = min<int64_t>(cap, (int64_t)W.work_cap - 16384 - n_roots);
+        if (n_roots > W.pend_cap) return 2;
+        if (cap <= 0) return 2;
+        if (!wtab_ready) {
+            uint32_t *woff = (uint32_t *)wtab;
+            uint32_t *wrqt = (uint32_t *)(wtab + (((n_ok + 1) * 4 + 255) & ~255u));
+            uint8_t *rp = (uint8_t *)((char *)wrqt + ((n_ok * 40 * 4 + 255) & ~255u));
+            wtab_build(K, tb, lane, woff, wrqt, rp);
+            if (lane == 0) { sh.woff = woff; sh.wrq = wrqt; sh.rpos = rp; }
+            wtab_ready = true;
+        }
+        // roots: the frames' nodes at depths [d, depth) and the current node,
+        // as pending entries marked LK_ROOT (expanded, not counted)
+        {
+            const uint32_t fd = ring_lo + (((uint32_t)lane - ring_lo) & 63);
+            if (fd >= d && fd < depth)
+                __hip_atomic_store(&pend[fd - d], lk_make(f_ti >> 6, f_s, ((uint64_t)fm_hi << 32) | fm_lo) | LK_ROOT,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lane == 0)
+                __hip_atomic_store(&pend[depth - d], lk_make(t, s, mask) | LK_ROOT, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        const uint32_t t_x = d == depth ? t : ((uint32_t)readlane((int)f_ti, (int)(d & 63)) >> 6);
+        if (lane == 0) {
+            sh.cmd = CMD_ENUM; sh.merge = d > 0 ? 1 : 0; sh.status = 0;
+            sh.n_roots = n_roots; sh.n_ok = n_ok; sh.theta = theta; sh.acc_lo = acc_lo; sh.acc_hi = acc_hi;
+            sh.gen = gen; sh.cap_total = n_roots + (uint32_t)cap;
+            sh.head = 0; sh.tail = 0; sh.active = 0; sh.tmin_new = 0xFFFFFFFFu; sh.tmax_new = 0;
+            sh.t_next = t_x; sh.npend = n_roots; sh.pend_sel = 0; sh.gset_used = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();                    // the helpers wait here (k_lin_wg)
+        const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+        unsigned long long *d8 = A.dbg && n_acc < 31 ? A.dbg + 256 * (size_t)blockIdx.x + 8 * n_acc : nullptr;
+        if (d8 && lane == 0) {
+            // JH_DEBUG=3 trace: one record per enumeration (the workgroup's first 31)
+            d8[0] = key; d8[1] = d; d8[2] = depth; d8[3] = n_roots; d8[4] = (unsigned long long)cap;
+            d8[5] = 99; d8[6] = 0; d8[7] = ins;
+        }
+        wg_enum_work(W, sh, lane, gset, work, memo, pend, my_probes);
+        const int st = sh.status;
+        if (d8 && lane == 0) { d8[5] = st; d8[6] = sh.tail; }
+        if (W.acc_stats && lane == 0) atomicAdd(&W.acc_stats[5], __builtin_amdgcn_s_memtime() - c0);
+        n_acc++;
+        if (st & ENUM_LIVE) return 1;
+        if (st) return 2;
+        acc_new = sh.tail - n_roots;
+        acc_tmax = sh.tmax_new; acc_tmin = sh.tmin_new;
+        return 0;
+    };
+
+expand:
+    if (++n_steps > (1u << 28)) {       // watchdog: far beyond any budget's step count
+        if (lane == 0) atomicOr(A.flags, 128);
+        verdict = JH_UNKNOWN;
+        goto done;
+    }
+    {
+        const uint32_t req = wrq & 0xFFFF;
+        absent = (ballot(req == s) | ballot(req == RQ_ANY)) & ~mask;
+    }
+    if (!absent) goto pop;
+    child_keys();
+    {
+        const bool cl = (absent >> lane) & 1;
+        const uint32_t a1 = cl ? b1 : 0u, a2 = cl ? b2 : 0u;
+        const uint64_t k = ((uint64_t)khi << 32) | klo;
+        n1 = bcnt8[a1]; n2 = bcnt8[a2];
+        __builtin_amdgcn_sched_barrier(0);
+        const ulonglong2 x0 = B[2 * a1], x1 = B[2 * a1 + 1];
+        const ulonglong2 y0 = B[2 * a2], y1 = B[2 * a2 + 1];
+        const uint64_t hit = ballot(x0.x == k) | ballot(x0.y == k) | ballot(x1.x == k) | ballot(x1.y == k) |
+                             ballot(y0.x == k) | ballot(y0.y == k) | ballot(y1.x == k) | ballot(y1.y == k);
+        absent &= ~hit;
+        // children that may sit in HBM: below theta, or in a merged layer range
+        const bool t_slow = t < theta || (t >= acc_lo && t <= acc_hi);
+        const bool r_slow = u_r < theta || (u_r >= acc_lo && u_r <= acc_hi);
+        if ((t_slow || r_slow) && absent) {
+            uint64_t low = t_slow ? absent : 0ULL;
+            low = r_slow ? (low | (absent & (1ULL << r))) : (low & ~(1ULL << r));
+            const uint32_t kt = khi >> 16 & 0x7FFF, ks = (khi >> 8) & 0xFF;
+            const uint64_t km = k & ((1ULL << 40) - 1);
+            const bool maybe = ((low >> lane) & 1) && bloom_test2<M>(bloom, lk_bl(h1), lk_bl(h2));
+            bool found = false;
+            if (maybe) found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
+            absent &= ~ballot(found);
+        }
+    }
+    if (!absent) goto pop;
+
+insert:
+    {
+        if (ins >= chk) {
+            if (ins >= budget) { verdict = JH_UNKNOWN; goto done; }
+            if (ins >= next_acc) {
+                next_acc = ins + acc_t;
+                // the deepest open node with >= ACC_T/2 inserts below it, not known live
+                auto ok_node = [&](uint32_t sq, uint32_t inc) {
+                    const uint32_t b = ins - sq;
+                    return b >= acc_t / 2 && (inc == 0 || b >= 2 * inc);
+                };
+                int64_t d = -1;
+                if ((int)depth > l_live && ok_node(cur_seq, cur_inc)) d = depth;
+                else {
+                    const uint32_t q = ((uint32_t)lane - ring_lo) & 63, fd = ring_lo + q;
+                    const uint64_t bm = ballot(fd < depth && (int)fd > l_live && ok_node(f_seq, f_inc));
+                    if (bm) {
+                        // rotate so bit q = frame ring_lo + q; take the highest
+                        const uint32_t rs = ring_lo & 63;
+                        const uint64_t rot = rs ? ((bm >> rs) | (bm << (64 - rs))) : bm;
+                        d = (int64_t)ring_lo + (63 - __builtin_clzll(rot));
+                    }
+                }
+                if (d >= 0) {
+                    const int res = accel((uint32_t)d);
+                    if (res == 0) {
+                        ins += acc_new;
+                        tmax = max(tmax, acc_tmax);
+                        if (ins > budget) { ins = budget; verdict = JH_UNKNOWN; goto done; }
+                        if (d == 0) { verdict = JH_INVALID; goto done; }
+                        if (acc_new) {
+                            acc_lo = acc_lo > acc_hi ? acc_tmin : min(acc_lo, acc_tmin);
+                            acc_hi = max(acc_hi, acc_tmax);
+                        }
+                        next_acc = ins + acc_t;
+                        depth = (uint32_t)d;
+                        climb = true; climb_jump = 1;
+                        goto pop;
+                    }
+                    if (res == 1) l_live = (int)d;
+                    else {
+                        const uint32_t b = ins - (d == depth ? cur_seq : (uint32_t)readlane((int)f_seq, (int)(d & 63)));
+                        if ((uint32_t)d == depth) cur_inc = b;
+                        else if (lane == (int)(d & 63)) f_inc = b;
+                    }
+                }
+            }
+            chk = min(budget, min(ins + 1024, next_acc));
+        }
+        const int i = __builtin_ctzll(absent);
+        const uint32_t myseq = ins;
+        ins++;
+        const uint32_t ns = (uint32_t)readlane((int)nvl, i);
+        const bool to_r = (uint32_t)i == r;
+        const uint32_t nt = to_r ? u_r : t;
+        {
+            const bool pick1 = n1 <= n2;
+            const uint32_t bs = pick1 ? b1 : b2, nsl = pick1 ? n1 : n2;
+            const uint64_t full_m = ballot(nsl >= 4);
+            if (!((full_m >> i) & 1)) {
+                if (lane == i) {
+                    lmemo[4 * bs + nsl] = ((uint64_t)khi << 32) | klo;
+                    bcnt8[bs] = (uint8_t)(nsl + 1);
+                }
+                if (++lcount >= M::EVICT) {
+                    const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
+                    lcount = rfl((int)(uint32_t)er);
+                    theta = rflu((uint32_t)(er >> 32));
+                }
+            } else {
+                const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
+                if (lane == i) {
+                    hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
+                    bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
+                }
+                theta = max(theta, nt + 1);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
+        }
+        if (depth - ring_lo == 64) {
+            const uint32_t kk = ((uint32_t)lane - ring_lo) & 63;
+            if (kk < 32) {
+                Frame fr;
+                fr.mask = ((uint64_t)fm_hi << 32) | fm_lo; fr.t_i = f_ti; fr.s = (int32_t)f_s;
+                fr.rest = ((uint64_t)fr_hi << 32) | fr_lo; fr.pad[0] = f_seq; fr.pad[1] = f_inc;
+                stack[ring_lo + kk] = fr;
+            }
+            ring_lo += 32;
+        }
+        {
+            const uint64_t nrest = absent & (absent - 1);
+            const bool me = lane == (int)(depth & 63);
+            fm_lo = me ? (uint32_t)mask : fm_lo;
+            fm_hi = me ? (uint32_t)(mask >> 32) : fm_hi;
+            f_ti = me ? ((t << 6) | (uint32_t)i) : f_ti;
+            f_s = me ? s : f_s;
+            fr_lo = me ? (uint32_t)nrest : fr_lo;
+            fr_hi = me ? (uint32_t)(nrest >> 32) : fr_hi;
+            f_seq = me ? cur_seq : f_seq;
+            f_inc = me ? cur_inc : f_inc;
+        }
+        depth++;
+        s = ns;
+        cur_seq = myseq; cur_inc = 0;
+        if (!to_r) {
+            mask |= 1ULL << i;
+            goto expand;
+        }
+        mask = nm_r;
+        if (nt >= n_ok) { t = nt; tmax = max(tmax, t); verdict = JH_VALID; goto done; }
+        for (uint32_t u = t; u < nt; u++) {
+            const uint32_t ru = u == t ? r : (lay_hi(u) & 63);
+            const uint32_t sh2 = (uint32_t)wave_shl1((int)wrq);
+            if (lane >= (int)ru) wrq = sh2;
+            w--;
+            if (lane == w) wrq = RQ_EMPTY;
+            const int c = (int)(lay_hi(u + 1) >> 6);
+            if (c > 0) {
+                if (P < pb || P + c > pb + 64) load_up(c <= 32 && P >= 32 ? P - 32 : P);
+                for (int kk = 0; kk < c; kk++) {
+                    const uint32_t x = (uint32_t)readlane((int)urq, P - pb + kk);
+                    if (lane == w + kk) wrq = x;
+                }
+                w += c; P += c;
+            }
+        }
+        t = nt;
+        tmax = max(tmax, t);
+        r = lay_hi(t) & 63;
+        rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
+        goto expand;
+    }
+
+pop:
+    if (depth == ring_lo) {
+        if (depth == 0) { verdict = JH_INVALID; goto done; }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t lo = depth >= 32 ? depth - 32 : 0;
+        const uint32_t kk = ((uint32_t)lane - lo) & 63;
+        if (kk < depth - lo) {
+            const Frame fr = stack[lo + kk];
+            fm_lo = (uint32_t)fr.mask; fm_hi = (uint32_t)(fr.mask >> 32); f_ti = fr.t_i; f_s = (uint32_t)fr.s;
+            fr_lo = (uint32_t)fr.rest; fr_hi = (uint32_t)(fr.rest >> 32); f_seq = fr.pad[0]; f_inc = fr.pad[1];
+        }
+        ring_lo = lo;
+    }
+    depth--;
+    {
+        const int ln = (int)(depth & 63);
+        absent = ((uint64_t)(uint32_t)readlane((int)fr_hi, ln) << 32) | (uint32_t)readlane((int)fr_lo, ln);
+        const uint32_t pt = (uint32_t)readlane((int)f_ti, ln) >> 6;
+        mask = ((uint64_t)(uint32_t)readlane((int)fm_hi, ln) << 32) | (uint32_t)readlane((int)fm_lo, ln);
+        s = (uint32_t)readlane((int)f_s, ln);
+        cur_seq = (uint32_t)readlane((int)f_seq, ln);
+        cur_inc = (uint32_t)readlane((int)f_inc, ln);
+        if (pt != t) {
+            for (uint32_t u = t; u > pt; u--) {
+                const int c = (int)(lay_hi(u) >> 6);
+                w -= c; P -= c;
+                if (lane >= w) wrq = RQ_EMPTY;
+                const uint32_t h = lay_hi(u - 1);
+                const int ru = (int)(h & 63);
+                const uint32_t sh2 = (uint32_t)wave_shr1((int)wrq);
+                if (lane > ru) wrq = sh2;
+                const uint32_t x = (uint32_t)readlane((int)drq, (int)(u - 1 - tb0));
+                if (lane == ru) wrq = x;
+                w++;
+            }
+            t = pt;
+            r = lay_hi(t) & 63;
+            rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
+        }
+    }
+    if (climb) {
+        // After a dead node, test its ancestors at once, climbing 1, 2, 4, ...
+        // levels per success (an invalid key reaches its root in a few
+        // steps); a live node ends the climb, after a live far ancestor the
+        // climb restarts one level at a time from the current node.
+        climb = false;
+        for (;;) {
+            uint32_t dt = depth >= climb_jump - 1 ? depth - (climb_jump - 1) : 0;
+            dt = max(dt, max(ring_lo, (uint32_t)(l_live + 1)));
+            if ((int)dt <= l_live || dt > depth) break;
+            const int res = accel(dt);
+            if (res == 0) {
+                ins += acc_new;
+                tmax = max(tmax, acc_tmax);
+                if (ins > budget) { ins = budget; verdict = JH_UNKNOWN; goto done; }
+                if (dt == 0) { verdict = JH_INVALID; goto done; }
+                if (acc_new) {
+                    acc_lo = acc_lo > acc_hi ? acc_tmin : min(acc_lo, acc_tmin);
+                    acc_hi = max(acc_hi, acc_tmax);
+                }
+                next_acc = ins + acc_t;
+                chk = min(budget, min(ins + 1024, next_acc));
+                climb = true;
+                climb_jump = min(climb_jump * 2, 64u);
+                depth = dt;
+                goto pop;          // pops node dt (pop decrements depth)
+            }
+            if (res == 1) {
+                l_live = (int)dt;
+                if (dt < depth && climb_jump > 1) { climb_jump = 1; continue; }
+            } else {
+                const uint32_t b = ins - (dt == depth ? cur_seq : (uint32_t)readlane((int)f_seq, (int)(dt & 63)));
+                if (dt == depth) cur_inc = b;
+                else if (lane == (int)(dt & 63)) f_inc = b;
+            }
+            climb_jump = 1;
+            break;
+        }
+        chk = min(budget, min(ins + 1024, next_acc));
+    }
+    if (!absent) goto pop;
+    child_keys();
+    {
+        const bool cl = (absent >> lane) & 1;
+        const uint32_t a1 = cl ? b1 : 0u, a2 = cl ? b2 : 0u;
+        n1 = bcnt8[a1]; n2 = bcnt8[a2];
+    }
+    goto insert;
+
+done:
+    inserts = ins;
+    tmax_out = tmax;
+    return verdict;
+}
+
+__global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
+    WgShared &sh = *(WgShared *)(jh_lds + WG_SH_OFF);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const DfsArgs &A = W.d;
+    uint64_t *memo = A.memo + (size_t)blockIdx.x * A.memo_cap * 2;
+    Frame *stack = A.stack + (size_t)blockIdx.x * A.stack_cap;
+    uint64_t *stage = (uint64_t *)(A.scratch + (size_t)blockIdx.x * A.scratch_bytes);
+    uint64_t *gset = W.gset + (size_t)blockIdx.x * W.gset_cap;
+    uint64_t *work = W.work + (size_t)blockIdx.x * W.work_cap;
+    char *wtab = W.wtab + (size_t)blockIdx.x * W.wtab_bytes;
+    uint64_t *pend = W.pend + (size_t)blockIdx.x * 2 * W.pend_cap;
+    unsigned long long my_probes = 0;
+    for (;;) {
+        if (tid == 0) {
+            const int idx = atomicAdd(A.queue, 1);
+            sh.key = idx < A.n_list ? A.list[idx] : -1;
+            sh.cmd = 0;
+        }
+        __syncthreads();
+        const int key = sh.key;
+        if (key < 0) break;
+        const KeyMeta mt = A.meta[key];
+        if (!(A.states8 && mt.maxw <= 40)) {      // WIDE keys: k_lin_seq3<false>
+            __syncthreads();
+            continue;
+        }
+        if (wid == 0) {
+            KeyInfo K;
+            K.n_ops = mt.n_ops; K.n_ok = mt.n_ok; K.sumW = mt.pad; K.s0 = 0; K.s1 = 0;
+            long long inserts = 0;
+            uint32_t tmax = 0;
+            const unsigned long long ck0 = __builtin_amdgcn_s_memtime();
+            const int verdict = dfs_acc<MemoW>(W, sh, K, A.tables + mt.off, key, lane, memo, stack, stage, gset,
+                                               work, wtab, pend, inserts, tmax, my_probes);
+            jh_key_verdict v;
+            v.valid = verdict;
+            v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
+            v.explored = inserts;
+            v.fail_entry = verdict == JH_INVALID ? -(int64_t)tmax - 2 : -1;
+            if (lane == 0) { A.out[key] = v; sh.cmd = CMD_DONE; }
+            if (lane == 0 && W.acc_stats) atomicAdd(&W.acc_stats[7], __builtin_amdgcn_s_memtime() - ck0);
+            if (lane == 0 && W.key_prof) {
+                // JH_DEBUG=4: per-key cycles / inserts / verdict for the tail analysis
+                W.key_prof[3 * (size_t)key] = __builtin_amdgcn_s_memtime() - ck0;
+                W.key_prof[3 * (size_t)key + 1] = (unsigned long long)inserts;
+                W.key_prof[3 * (size_t)key + 2] = (unsigned long long)verdict | ((unsigned long long)blockIdx.x << 8);
+            }
+            __syncthreads();                    // releases the helpers
+        } else {
+            for (;;) {
+                __syncthreads();                // wave 0's enumeration request, or the end of the key
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                if (sh.cmd == CMD_DONE) break;
+                wg_enum_work(W, sh, tid, gset, work, memo, pend, my_probes);
+            }
+        }
+        __syncthreads();
+    }
+    for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
+    if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
+}
+
+// ---------------------------------------------------------------------------
 // Heavy keys: parallel breadth-first enumeration of the reachable
 // configuration graph by a whole workgroup. For a key with no terminal
 // configuration (invalid) WGL's cache ends up holding exactly this set, so
@@ -1766,6 +2705,7 @@ struct BfsArgs {
     int32_t init_state;
     int32_t states_ok;      // every interned state < 2^12
     int32_t *claim;         // race with the sequential search (see emit_verdict)
+    int32_t settle_valid;   // 1: also settle valid keys (explored -2: WGL's count unknown; JH_BFS_VALID=1)
 };
 
 struct BfsShared {
@@ -2014,7 +2954,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
         d[0] += __builtin_amdgcn_s_memtime() - b0; d[1] += rounds; d[3] += sh.count; d[4] += 1;
     }
-    if (sh.status || (sh.term && !((long long)sh.count - 1 >= BFS_VALID_MIN &&
+    if (sh.status || (sh.term && !(A.settle_valid && (long long)sh.count - 1 >= BFS_VALID_MIN &&
                                    (long long)sh.count - 1 < A.budget))) {
         if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
     } else if (sh.term) {
@@ -2662,7 +3602,101 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipEventRecord(ctx->ev[9], ctx->aux2));
     }
     int n_unres = 0, n_defer3 = 0;
-    if (n_defer > 0) {
+    const char *wg_env = getenv("JH_WG");
+    // JH_WG=1: the workgroup engine (k_lin_wg, exact DFS with accelerated dead
+    // subtrees) for deferred LEAN keys; default: the BFS / sequential race
+    const bool use_wg = wg_env && atoi(wg_env) != 0;
+    unsigned long long *acc_stats = nullptr;
+    int n_wg = 0;
+    if (n_defer > 0 && use_wg) {
+        // Deferred keys, exact WGL with accelerated dead subtrees: LEAN keys on
+        // k_lin_wg (one workgroup per key, stream st), WIDE keys on the plain
+        // sequential search with the full budget (k_lin_seq3<false>, aux stream).
+        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(q + 18, 0, sizeof(int32_t), st));
+        acc_stats = ctx->ws<unsigned long long>(WS_ACC_STATS, 8);
+        HIP_TRY(hipMemsetAsync(acc_stats, 0, 8 * sizeof(unsigned long long), st));
+        uint32_t cap2 = 1u << 16;
+        while ((int64_t)cap2 < 2 * budget && cap2 < (1u << 30)) cap2 <<= 1;
+        // + slack: keys claimed in the set after the cap is hit are still recorded
+        const uint64_t work_cap = (uint64_t)std::min<int64_t>(budget, (int64_t)1 << 30) + ACC_MAXROOTS + 16384;
+        uint64_t gcap = 1024;
+        while (gcap < 2 * work_cap) gcap <<= 1;
+        const uint32_t mo = (uint32_t)smax;   // >= n_ok of any key
+        const uint64_t wtab_b = (((uint64_t)(mo + 1) * 4 + 255) & ~255ULL) + (((uint64_t)mo * 40 * 4 + 255) & ~255ULL) +
+                                (((uint64_t)mo + 255) & ~255ULL);
+        const uint64_t per_wg = (uint64_t)cap2 * 16 + gcap * 8 + 3 * work_cap * 8 + (uint64_t)stack_cap * sizeof(Frame) +
+                                MemoW::SLOTS * 8 + wtab_b;
+        uint64_t mem_limit = 48ULL << 30;
+        if (const char *e = getenv("JH_WG_MEM_GB")) mem_limit = (uint64_t)std::max(1, atoi(e)) << 30;
+        int per_cu = 1;
+        n_wg = std::min<int64_t>(n_defer, (int64_t)per_cu * ctx->n_cu);
+        n_wg = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)n_wg, mem_limit / per_wg));
+        const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)n_wg * cap2 * 16;
+        uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)n_wg * cap2 * 2, /*zero=*/true);
+        if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
+        // kept all zero between calls by the enumeration's clean-up
+        uint64_t *gset = ctx->ws<uint64_t>(WS_WG_GSET, (size_t)n_wg * gcap, /*zero=*/true);
+        uint64_t *work = ctx->ws<uint64_t>(WS_WG_WORK, (size_t)n_wg * work_cap, /*zero=*/true);
+        WgArgs wa{};
+        wa.d = a;
+        wa.d.list = defer; wa.d.n_list = n_defer; wa.d.n_list_dev = nullptr; wa.d.queue = q; wa.d.defer = 0;
+        wa.d.defer_list = nullptr; wa.d.defer_count = nullptr; wa.d.defer_prog = nullptr;
+        wa.d.memo = memo2; wa.d.memo_cap = cap2;
+        wa.d.stack = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)n_wg * stack_cap);
+        wa.d.scratch = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)n_wg * MemoW::SLOTS * 8);
+        wa.d.scratch_bytes = MemoW::SLOTS * 8;
+        wa.d.budget = budget; wa.d.budget_full = 0; wa.d.claim = nullptr;
+        wa.d.gen_base = ctx->gen_base + (uint32_t)K + 1;
+        wa.d.dbg = nullptr; wa.d.probes = (unsigned long long *)(q + 8);
+        wa.gset = gset; wa.gset_cap = (uint32_t)gcap; wa.work = work; wa.work_cap = (uint32_t)work_cap;
+        wa.wtab = ctx->ws<char>(WS_WG_WTAB, (size_t)n_wg * wtab_b); wa.wtab_bytes = wtab_b;
+        if (dbgenv && atoi(dbgenv) >= 3) {
+            wa.d.dbg = ctx->ws<unsigned long long>(WS_DEBUG, (size_t)n_wg * 256 + 16 * 1024);
+            HIP_TRY(hipMemsetAsync(wa.d.dbg, 0, sizeof(unsigned long long) * n_wg * 256, st));
+        }
+        wa.acc_stats = acc_stats;
+        wa.pend_cap = (uint32_t)work_cap;
+        wa.acc_t = ACC_T;
+        if (const char *e = getenv("JH_ACC_T")) wa.acc_t = (uint32_t)std::max(0, atoi(e));
+        if (dbgenv && atoi(dbgenv) >= 4) {
+            wa.key_prof = ctx->ws<unsigned long long>(WS_STATS_KEYS, 3 * (size_t)K);
+            HIP_TRY(hipMemsetAsync(wa.key_prof, 0, 3 * sizeof(unsigned long long) * K, st));
+        }
+        wa.pend = ctx->ws<uint64_t>(WS_WG_PEND, (size_t)n_wg * 2 * work_cap);
+        if (!ctx->lds_attr_wg) {
+            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_wg, hipFuncAttributeMaxDynamicSharedMemorySize, WG_LDS));
+            ctx->lds_attr_wg = true;
+        }
+        HIP_TRY(hipEventRecord(ctx->ev[6], st));
+        k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, st>>>(wa);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->ev[5], st));
+        {
+            // WIDE deferred keys (windows of 41-64 members or >= 256 states)
+            const int waves3 = std::min(n_defer, 128);
+            const bool fresh3 = ctx->ws_fresh(WS_MEMO_P3) || ctx->bufs[WS_MEMO_P3].bytes < (size_t)waves3 * cap2 * 16;
+            uint64_t *memo3 = ctx->ws<uint64_t>(WS_MEMO_P3, (size_t)waves3 * cap2 * 2, /*zero=*/true);
+            if (clear_memo && !fresh3) HIP_TRY(hipMemsetAsync(memo3, 0, ctx->bufs[WS_MEMO_P3].bytes, st));
+            HIP_TRY(hipEventRecord(ctx->ev[6], st));
+            HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
+            DfsArgs c3 = a;
+            c3.list = defer; c3.n_list = n_defer; c3.n_list_dev = nullptr; c3.queue = q + 18; c3.defer = 0;
+            c3.defer_list = nullptr; c3.defer_count = nullptr; c3.defer_prog = nullptr;
+            c3.memo = memo3; c3.memo_cap = cap2;
+            c3.stack = ctx->ws<Frame>(WS_STACK_P3, (size_t)waves3 * stack_cap);
+            c3.scratch = ctx->ws<char>(WS_SCRATCH_P3, (size_t)waves3 * MemoH::SLOTS * 8);
+            c3.scratch_bytes = MemoH::SLOTS * 8;
+            c3.budget = budget; c3.budget_full = 0; c3.claim = nullptr;
+            c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
+            c3.dbg = nullptr; c3.probes = (unsigned long long *)(q + 22);
+            k_lin_seq3<false><<<waves3, 64, MemoM::LDS, ctx->aux>>>(c3);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
+            HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
+            HIP_TRY(hipStreamWaitEvent(st, ctx->ev[7], 0));
+        }
+    } else if (n_defer > 0) {
         // Heavy keys: two exact searches race per key and the first to settle
         // it writes its verdict (emit_verdict), the other abandons it.
         //  - the workgroup BFS (stream st) settles keys with no reachable
@@ -2696,6 +3730,11 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         c.scratch = bscr; c.scratch_bytes = scr_bytes_bfs; c.budget = budget;
         c.init_state = init_state; c.states_ok = (vmax - vmin + 2) < 4096 ? 1 : 0;
         c.dbg = dbg; c.claim = claim;
+        // By default the BFS settles invalid keys only (their WGL cache is the
+        // whole reachable set, an exact count); every valid key is settled by
+        // the sequential search, so `explored` is WGL's count on every key and
+        // the same on every run.
+        c.settle_valid = getenv("JH_BFS_VALID") && atoi(getenv("JH_BFS_VALID")) ? 1 : 0;
         // per context (= per device; calls on one context are serialised by its mutex)
         if (!ctx->lds_attr) {
             HIP_TRY(hipFuncSetAttribute((const void *)k_lin_bfs, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2828,6 +3867,32 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     if (qh[2] & 1) throw_jh(JH_EUNSUPPORTED, "a key with more than 65535 ops or 2^20 ok returns");
     if (qh[2] & 2) throw_jh(JH_EDEVICE, "per-key table exceeded the scratch reservation");
     if (qh[2] & 4) throw_jh(JH_EDEVICE, "DFS stack overflow");
+    if ((qh[2] & 0x1F0) && acc_stats && ctx->bufs.size() > WS_DEBUG && ctx->bufs[WS_DEBUG].p && n_wg > 0 &&
+        dbgenv && atoi(dbgenv) >= 3) {
+        std::vector<unsigned long long> tr((size_t)n_wg * 256);
+        HIP_TRY(hipMemcpy(tr.data(), ctx->bufs[WS_DEBUG].p, tr.size() * 8, hipMemcpyDeviceToHost));
+        for (int g = 0; g < n_wg; g++) {
+            for (int e = 0; e < 31; e++) {
+                const unsigned long long *d8 = &tr[(size_t)g * 256 + 8 * e];
+                if (!d8[3]) break;
+                fprintf(stderr, "[jh-acc] wg %d key %llu d %llu depth %llu roots %llu cap %llu status %llu tail %llu ins %llu\n",
+                        g, d8[0], d8[1], d8[2], d8[3], d8[4], d8[5], d8[6], d8[7]);
+            }
+            const unsigned long long *w8 = &tr[(size_t)g * 256 + 248];
+            if (w8[6] == 0xDEAD)
+                fprintf(stderr, "[jh-acc] wg %d WATCHDOG head %llu tail %llu active %llu cap_total %llu roots %llu wave %llu\n",
+                        g, w8[0], w8[1], w8[2], w8[3], w8[4], w8[5]);
+            const unsigned long long *l8 = &tr[(size_t)g * 256 + 240];
+            if (l8[3] == 0xBEEF)
+                fprintf(stderr, "[jh-acc] wg %d LOST ITEM pos %llu tail %llu cap_total %llu\n", g, l8[0], l8[1], l8[2]);
+        }
+    }
+    if (qh[2] & 0x1F0) {
+        char m[160];
+        snprintf(m, sizeof m, "search watchdog tripped (flags 0x%x: 16 lost work item, 32 idle enumeration, "
+                 "64 full set, 128 step limit, 256 bad window)", qh[2]);
+        throw_jh(JH_EDEVICE, m);
+    }
     if (sum) {
         sum->valid = sh[0]; sum->n_invalid = sh[1]; sum->n_unknown = sh[2];
         sum->first_fail_entry = sh[3] == LLONG_MAX ? -1 : sh[3];
@@ -2850,6 +3915,54 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             if (n_defer > 0) HIP_TRY(hipEventElapsedTime(&p2, ctx->ev[4], ctx->ev[10]));
             fprintf(stderr, "[jh] keys=%lld prep=%.3f ms phase1=%.3f ms (waves %d) deferred=%d bfs=%.3f ms (gave up %d) seq=%.3f ms (phase 2 %.3f ms, phase 3: %d keys) wide=%d keys %.3f ms\n",
                     (long long)K, a, b, waves1, n_defer, c, n_unres, d, p2, n_defer3, n_x, xw);
+            if (acc_stats && dbgenv && atoi(dbgenv) >= 3 && n_wg > 0) {
+                std::vector<unsigned long long> tr((size_t)n_wg * 256);
+                HIP_TRY(hipMemcpy(tr.data(), ctx->bufs[WS_DEBUG].p, tr.size() * 8, hipMemcpyDeviceToHost));
+                for (int g = 0; g < std::min(n_wg, 8); g++)
+                    for (int e = 0; e < 32; e++) {
+                        const unsigned long long *d8 = &tr[(size_t)g * 256 + 8 * e];
+                        if (!d8[3]) break;
+                        fprintf(stderr, "[jh-acc] wg %d key %llu d %llu depth %llu roots %llu cap %llu status %llu tail %llu ins %llu\n",
+                                g, d8[0], d8[1], d8[2], d8[3], d8[4], d8[5], d8[6], d8[7]);
+                    }
+            }
+            if (acc_stats && dbgenv && atoi(dbgenv) >= 4) {
+                std::vector<unsigned long long> kp(3 * (size_t)K);
+                HIP_TRY(hipMemcpy(kp.data(), ctx->bufs[WS_STATS_KEYS].p, kp.size() * 8, hipMemcpyDeviceToHost));
+                std::vector<int> ix;
+                for (int64_t k = 0; k < K; k++) if (kp[3 * k]) ix.push_back((int)k);
+                std::sort(ix.begin(), ix.end(), [&](int x, int y) { return kp[3 * x] > kp[3 * y]; });
+                for (size_t i = 0; i < std::min<size_t>(12, ix.size()); i++)
+                    fprintf(stderr, "[jh-key] key %d memtime %.3g inserts %llu verdict %llu wg %llu\n", ix[i],
+                            (double)kp[3 * ix[i]], kp[3 * ix[i] + 1], kp[3 * ix[i] + 2] & 255, kp[3 * ix[i] + 2] >> 8);
+            }
+#ifdef JH_ENUM_PROF
+            {
+                unsigned int a4[4]; unsigned long long b3[3];
+                HIP_TRY(hipMemcpyFromSymbol(a4, HIP_SYMBOL(g_prof_hbm), 4));
+                HIP_TRY(hipMemcpyFromSymbol(a4 + 1, HIP_SYMBOL(g_prof_gset), 4));
+                HIP_TRY(hipMemcpyFromSymbol(a4 + 2, HIP_SYMBOL(g_prof_rounds), 4));
+                HIP_TRY(hipMemcpyFromSymbol(a4 + 3, HIP_SYMBOL(g_prof_layers), 4));
+                HIP_TRY(hipMemcpyFromSymbol(b3, HIP_SYMBOL(g_prof_form), 8));
+                HIP_TRY(hipMemcpyFromSymbol(b3 + 1, HIP_SYMBOL(g_prof_close), 8));
+                fprintf(stderr, "[jh-prof] hbm-probes %u gset-inserts %u rounds %u layers %u | memtime formation %.3g closure %.3g\n",
+                        a4[0], a4[1], a4[2], a4[3], (double)b3[0], (double)b3[1]);
+                unsigned int z4[4] = {0, 0, 0, 0}; unsigned long long zb[3] = {0, 0, 0};
+                HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof_hbm), z4, 4));
+                HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof_gset), z4, 4));
+                HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof_rounds), z4, 4));
+                HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof_layers), z4, 4));
+                HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof_form), zb, 8));
+                HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof_close), zb, 8));
+            }
+#endif
+            if (acc_stats) {
+                unsigned long long st8[8];
+                HIP_TRY(hipMemcpy(st8, acc_stats, sizeof st8, hipMemcpyDeviceToHost));
+                fprintf(stderr, "[jh-wg] workgroups=%d enumerations=%llu new-nodes=%llu dead=%llu live=%llu inconclusive=%llu | "
+                        "memtime: keys %.3g, in enumerations %.3g (work loops %.3g)\n",
+                        n_wg, st8[0], st8[1], st8[2], st8[3], st8[4], (double)st8[7], (double)st8[5], (double)st8[6]);
+            }
         }
     }
 }

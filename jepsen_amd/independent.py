@@ -102,7 +102,7 @@ class IndependentChecker(Checker):
                 lin_res = {}
                 for kid, key in enumerate(cols.keys):
                     v = verdicts[kid]
-                    if int(v["explored"]) == -1:      # a key in no tuple (-2: settled by the BFS, valid)
+                    if int(v["explored"]) == -1:      # a key in no tuple: no :results entry
                         continue
                     lin_res[key] = lin_result(int(v["valid"]), int(v["cause"]), int(v["fail_entry"]),
                                               int(v["explored"]), cols)

@@ -17,15 +17,11 @@ pytestmark = pytest.mark.gpu
 
 
 def _same(gpu, cpu):
-    for f in ("valid", "cause", "fail_entry"):
+    """Verdict, cause, failing row and WGL's cache size, key by key (explored
+    is exact and deterministic on every key: include/jh.h)."""
+    for f in ("valid", "cause", "fail_entry", "explored"):
         bad = np.nonzero(gpu[f] != cpu[f])[0]
         assert len(bad) == 0, (f, bad[:10], gpu[bad[:5]], cpu[bad[:5]])
-    # WGL's cache size, key by key; -2 only for a valid key the BFS settled by
-    # its complete reachable set (>= 2^16 configurations, include/jh.h)
-    bfs = (gpu["explored"] == -2) & (cpu["explored"] >= 0)
-    assert (gpu["valid"][bfs] == A.VALID).all() and (cpu["explored"][bfs] >= 1).all()
-    bad = np.nonzero(gpu["explored"][~bfs] != cpu["explored"][~bfs])[0]
-    assert len(bad) == 0, ("explored", bad[:10])
 
 
 def test_perf_test_history(ctx):
@@ -58,10 +54,8 @@ def test_random_histories(ctx, seed):
     g, gs = ctx.check_cas_independent(cols)
     c, cs = oracle.check_cas_independent(cols, threads=8)
     _same(g, c)
-    bfs = (g["explored"] == -2) & (c["explored"] >= 0)      # not in the device's sum
     assert (gs.valid, gs.n_invalid, gs.n_unknown, gs.first_fail_entry, gs.explored) == \
-           (cs.valid, cs.n_invalid, cs.n_unknown, cs.first_fail_entry,
-            cs.explored - int(c["explored"][bfs].sum()))
+           (cs.valid, cs.n_invalid, cs.n_unknown, cs.first_fail_entry, cs.explored)
 
 
 def test_budget_and_deferral(ctx):

@@ -26,32 +26,35 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: 8 TB/s HBM3E (spec)
 BYTES_PER_ENTRY = 56           # 7 x int64 columns read once
 BYTES_PER_PROBE = 16           # one memo entry {mask, t|state|gen}
-# HBM bytes per launch of k_lin_dfs<LEAN> from the rocprofv3 FETCH_SIZE and
-# WRITE_SIZE passes of the same workload (tools/gpu_profile.sh ->
-# tools/pmc_traffic.py); PMC counters cannot be read inside a timed run
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic_k_lin_dfs.json")
+# HBM bytes per launch of a kernel from the rocprofv3 FETCH_SIZE and
+# WRITE_SIZE passes of the same workload (tools/pmc_traffic.py), one file per
+# (workload, kernel) under profiles/: PMC counters cannot be read inside a
+# timed run, and a file of another workload is never used
+TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r02")
 
 
-def pmc_traffic():
+def pmc_traffic(workload, kernel):
+    path = os.path.join(TRAFFIC_DIR, f"traffic_{workload}_{kernel}.json")
     try:
-        with open(TRAFFIC_JSON) as fh:
-            return float(json.load(fh)["traffic_bytes"])
+        with open(path) as fh:
+            d = json.load(fh)
+        return float(d["traffic_bytes"]), os.path.relpath(path, ROOT)
     except (OSError, ValueError, KeyError):
-        return None
+        return None, None
 
 
 # SURVEY.md 8(d) configurations. Each rank checks its own shard (weak scaling).
 WORKLOADS = {
     "c3": dict(desc="C3: independent cas-register, 10000 keys x ~1k entries per GPU", keys=10000,
-               seed=3, cpu_keys=10000,
+               seed=3, cpu_keys=10000, cpu_keys_opt=10000,
                gen=dict(threads_per_key=10, readers=5, n_values=5, process_limit=20, groups=10,
                         init_nil=True, p_info=0.02, p_invalid=0.01, nemesis_every=10000)),
     "c4": dict(desc="C4: independent cas-register, 1M keys over 8 GPUs: a 125000-key shard "
-                    "(~125M entries) per GPU", keys=125000, seed=4, cpu_keys=3000,
+                    "(~125M entries) per GPU", keys=125000, seed=4, cpu_keys=3000, cpu_keys_opt=125000,
                gen=dict(threads_per_key=10, readers=5, n_values=5, process_limit=20, groups=10,
                         init_nil=True, p_info=0.02, p_invalid=0.01, nemesis_every=10000)),
     "c5": dict(desc="C5: independent cas-register, 1000 keys x ~1k entries, 50 threads per key, "
-                    "p_info 0.2 (deep searches, HBM memo stress)", keys=1000, seed=5, cpu_keys=48,
+                    "p_info 0.2 (deep searches, HBM memo stress)", keys=1000, seed=5, cpu_keys=48, cpu_keys_opt=64,
                gen=dict(threads_per_key=50, readers=25, n_values=5, process_limit=100, groups=10,
                         init_nil=True, p_info=0.2, p_invalid=0.01, nemesis_every=10000)),
 }
@@ -137,7 +140,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    dfs_ms, dev_ms, probes = [], [], []
+    dfs_ms, dev_ms, probes, seq_ms, bfs_ms, seq_probes = [], [], [], [], [], []
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -147,6 +150,9 @@ def main():
         dfs_ms.append(s.dfs_ms)
         dev_ms.append(s.device_ms)
         probes.append(s.memo_probes)
+        seq_ms.append(s.seq_ms)
+        bfs_ms.append(s.bfs_ms)
+        seq_probes.append(s.seq_probes)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -162,18 +168,32 @@ def main():
         total_entries = n_entries
     value = total_entries * args.steps / elapsed
 
-    # ---- roofline of the dominant kernel (k_lin_dfs), live HIP events ----
+    # ---- rooflines from live HIP events (jh_summary), per kernel ----------
+    # phase 1 (k_lin_dfs): every key's search under the quick budget; it reads
+    # the whole history (56 B/entry) and probes the HBM memo
     dfs_avg = float(np.mean(dfs_ms)) / 1e3
-    alg_bytes = BYTES_PER_ENTRY * n_entries + BYTES_PER_PROBE * float(np.mean(probes))
-    achieved = alg_bytes / dfs_avg / 1e9 if dfs_avg > 0 else 0.0
+    alg1 = BYTES_PER_ENTRY * n_entries + BYTES_PER_PROBE * float(np.mean(probes))
+    ach1 = alg1 / dfs_avg / 1e9 if dfs_avg > 0 else 0.0
+    # phase 2 (the step's dominant kernel): the sequential search of the keys
+    # phase 1 handed on; its algorithmic bytes are those keys' entries plus its
+    # HBM memo probes. The search is latency-bound (one wave walks one key's DFS)
+    seq_avg = float(np.mean(seq_ms)) / 1e3
+    alg2 = BYTES_PER_ENTRY * float(s.deferred_entries) + BYTES_PER_PROBE * float(np.mean(seq_probes))
+    ach2 = alg2 / seq_avg / 1e9 if seq_avg > 0 else 0.0
+    dominant = seq_avg > dfs_avg
+    tr_kernel = "k_lin_seq" if dominant else "k_lin_dfs"
+    traffic, traffic_src = pmc_traffic(args.workload, tr_kernel) if args.keys is None else (None, None)
 
-    # end-to-end from host columns (H2D copy + check + verdicts D2H): the
-    # boundary's host-buffer entry point, reported beside the HBM-resident value
-    e2e_ms = None
+    # host buffers to host verdicts (H2D copy + check + verdicts D2H), over K
+    # calls: the boundary's host-buffer entry point, beside the HBM-resident value
+    e2e = None
     if args.e2e:
         t1 = time.perf_counter()
-        ctx.check_cas_independent(cols)
-        e2e_ms = (time.perf_counter() - t1) * 1e3
+        for _ in range(args.steps):
+            ctx.check_cas_independent(cols)
+        e2e_s = (time.perf_counter() - t1) / args.steps
+        e2e = {"ms_per_call": e2e_s * 1e3, "entries_per_s_this_rank": n_entries / e2e_s,
+               "calls": args.steps}
 
     out = None
     if rank == 0:
@@ -184,9 +204,10 @@ def main():
             ov, os_ = oracle.check_cas_independent(cols, threads=min(16, len(os.sched_getaffinity(0))))
             # verdict, cause, failing row and WGL's cache size of every key
             parity = bool(all((hv[f] == ov[f]).all() for f in ("valid", "cause", "fail_entry", "explored")))
-        cpu = None
+        cpu = cpu_faithful = None
         if not args.no_cpu and world == 1:
-            cpu = cpu_baseline(cols, args.cpu_sample_keys or wl["cpu_keys"], args.workload.upper())
+            cpu = cpu_baseline(cols, args.cpu_sample_keys or wl["cpu_keys_opt"], args.workload.upper(), mode=0)
+            cpu_faithful = cpu_baseline(cols, args.cpu_sample_keys or wl["cpu_keys"], args.workload.upper(), mode=3)
         out = {
             "metric": "history ops verified/sec (node), independent cas-register 10k keys, 1/2/4/8 GPU",
             "value": value,
@@ -207,14 +228,27 @@ def main():
                        "p_invalid": wl["gen"]["p_invalid"], "budget": A.DEFAULT_BUDGET,
                        "explored_per_step": int(s.explored), "invalid_keys": int(s.n_invalid),
                        "unknown_keys": int(s.n_unknown), "device_ms": float(np.mean(dev_ms)),
-                       "e2e_ms_host_buffers": e2e_ms},
-            "roofline": {"bound": "hbm", "kernel": "k_lin_dfs (phase 1: every key, quick budget)", "achieved": achieved,
-                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                         # the committed PMC passes are of the C3 workload only
-                         "traffic": pmc_traffic() if args.workload == "c3" and args.keys is None else None,
-                         "kernel_ms": dfs_avg * 1e3,
-                         "alg_bytes": alg_bytes},
+                       "deferred_keys": int(s.n_deferred), "deferred_entries": int(s.deferred_entries),
+                       "phase1_ms": dfs_avg * 1e3, "phase2_seq_ms": seq_avg * 1e3,
+                       "phase2_bfs_ms": float(np.mean(bfs_ms))},
+            "value_kind": "history resident in HBM, verdicts left in HBM (kernel pipeline only); "
+                          "host-to-host rate in e2e_host_buffers",
+            "e2e_host_buffers": e2e,
+            "roofline": {"bound": "hbm",
+                         "kernel": ("k_lin_seq (phase 2: the deferred keys' sequential WGL search)" if dominant
+                                    else "k_lin_dfs (phase 1: every key, quick budget)"),
+                         "achieved": ach2 if dominant else ach1, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": (ach2 if dominant else ach1) / PEAK_HBM_GBS,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel_ms": (seq_avg if dominant else dfs_avg) * 1e3,
+                         "alg_bytes": alg2 if dominant else alg1,
+                         "note": "latency-bound tree search: one wave per key, LDS memo; bytes are 56 B per entry "
+                                 "of the keys searched + 16 B per HBM memo probe (SURVEY 8(d))"},
+            "roofline_phase1": {"bound": "hbm", "kernel": "k_lin_dfs", "achieved": ach1, "peak": PEAK_HBM_GBS,
+                                "unit": "GB/s", "frac": ach1 / PEAK_HBM_GBS, "kernel_ms": dfs_avg * 1e3,
+                                "alg_bytes": alg1},
             "cpu_baseline": cpu,
+            "cpu_baseline_faithful": cpu_faithful,
             "parity_vs_oracle": parity,
         }
         print(json.dumps(out), flush=True)
@@ -224,21 +258,26 @@ def main():
     return out
 
 
-def cpu_baseline(cols, sample_keys, name="C3"):
-    """The oracle, reference-faithful mode (independent.clj:234-245's O(K*N)
-    per-key subhistory scan + knossos-style linked-list/BitSet WGL), on the
-    host cores, over a bounded sample of this rank's keys."""
+def cpu_baseline(cols, sample_keys, name="C3", mode=0):
+    """The CPU oracle on every host core this process may use, over a bounded
+    sample of this rank's keys. mode 0 = optimized CPU (one
+    O(N) split, canonical WGL); mode 3 = reference-faithful
+    (independent.clj:234-245's O(K*N) per-key subhistory scan + knossos-style
+    linked-list/BitSet WGL)."""
     from oracle import oracle
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = len(os.sched_getaffinity(0))
     k1 = min(sample_keys, cols.n_keys)
     t0 = time.perf_counter()
-    oracle.check_cas_independent_range(cols, 0, k1, mode=3, threads=threads)
+    oracle.check_cas_independent_range(cols, 0, k1, mode=mode, threads=threads)
     dt = time.perf_counter() - t0
     counts = np.bincount(cols.key[cols.key >= 0], minlength=cols.n_keys)
     ent = int(counts[:k1].sum())
+    what = ("optimized CPU oracle (one O(N) split + canonical WGL)" if mode == 0 else
+            "reference-faithful oracle (O(K*N) subhistory + list WGL)")
     return {"value": ent / dt, "unit": "entries/s", "cores": threads, "kind": "port",
-            "sample": f"keys 0..{k1 - 1} ({ent} entries) of the rank-0 {name} history, "
-                      f"reference-faithful oracle (O(K*N) subhistory + list WGL), {dt:.2f} s"}
+            "nproc_visible": os.cpu_count(),
+            "sample": f"keys 0..{k1 - 1} ({ent} entries) of the rank-0 {name} history, {what}, {dt:.2f} s "
+                      f"on {threads} threads"}
 
 
 if __name__ == "__main__":

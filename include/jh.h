@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define JH_ABI_VERSION 1
+#define JH_ABI_VERSION 2
 
 /* Return codes. Anything non-zero also writes a NUL-terminated message into
  * the caller's err buffer; the JNA shim throws ex-info and check-safe turns
@@ -138,6 +138,12 @@ typedef struct jh_summary {
     int64_t memo_probes;       /* memo slots read by the phase-1 search kernel k_lin_dfs (roofline bytes) */
     double  device_ms;         /* device time of the check (HIP events) */
     double  dfs_ms;            /* of which the phase-1 search kernel k_lin_dfs (all keys, quick budget) */
+    /* phase 2 (keys over the quick budget), for the roofline of its kernels */
+    double  seq_ms;            /* the sequential search of the deferred keys (k_lin_seq / k_lin_wg) */
+    double  bfs_ms;            /* the reachable-set BFS racing it (k_lin_bfs; 0 if not run) */
+    int64_t n_deferred;        /* keys the phase-1 search handed on */
+    int64_t deferred_entries;  /* history entries of those keys */
+    int64_t seq_probes;        /* HBM memo probes of the phase-2 sequential search */
 } jh_summary;
 
 typedef struct jh_ctx jh_ctx;

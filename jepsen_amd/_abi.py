@@ -6,7 +6,7 @@ every struct layout.
 """
 import ctypes as C
 
-JH_ABI_VERSION = 1
+JH_ABI_VERSION = 2
 
 JH_OK, JH_EINVAL, JH_EUNSUPPORTED, JH_EDEVICE, JH_ENOMEM = 0, 1, 2, 3, 4
 TYPE_INVOKE, TYPE_OK, TYPE_FAIL, TYPE_INFO = 0, 1, 2, 3
@@ -64,7 +64,9 @@ class JhSummary(C.Structure):
     _fields_ = [("valid", C.c_int64), ("n_invalid", C.c_int64), ("n_unknown", C.c_int64),
                 ("first_fail_entry", C.c_int64), ("n_keys", C.c_int64),
                 ("explored", C.c_int64), ("memo_probes", C.c_int64),
-                ("device_ms", C.c_double), ("dfs_ms", C.c_double)]
+                ("device_ms", C.c_double), ("dfs_ms", C.c_double),
+                ("seq_ms", C.c_double), ("bfs_ms", C.c_double), ("n_deferred", C.c_int64),
+                ("deferred_entries", C.c_int64), ("seq_probes", C.c_int64)]
 
 
 class JhSetResult(C.Structure):

@@ -3393,6 +3393,18 @@ __global__ void k_summary(const jh_key_verdict *__restrict__ v, int64_t K, long 
     }
 }
 
+// entries of the deferred keys (the phase-2 kernels' share of the history)
+__global__ void k_defer_entries(const int32_t *__restrict__ defer, int n, const uint32_t *__restrict__ off,
+                                unsigned long long *sum) {
+    unsigned long long x = 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int k = defer[i];
+        x += off[k + 1] - off[k];
+    }
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if ((threadIdx.x & 63) == 0 && x) atomicAdd(sum, x);
+}
+
 __global__ void k_iota(int32_t *a, int64_t n) {
     int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i < n) a[i] = (int32_t)i;
@@ -3551,6 +3563,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const int n_defer = qh[1];
+    unsigned long long *defer_entries = (unsigned long long *)(q + 24);
+    HIP_TRY(hipMemsetAsync(defer_entries, 0, sizeof(unsigned long long), st));
+    if (n_defer > 0) k_defer_entries<<<std::min(256, (n_defer + 255) / 256), 256, 0, st>>>(defer, n_defer, off, defer_entries);
     if (n_defer > 1) {
         // heavy keys, least advanced first (the likely longest searches start first)
         std::vector<int32_t> dk(n_defer);
@@ -3668,7 +3683,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             HIP_TRY(hipFuncSetAttribute((const void *)k_lin_wg, hipFuncAttributeMaxDynamicSharedMemorySize, WG_LDS));
             ctx->lds_attr_wg = true;
         }
-        HIP_TRY(hipEventRecord(ctx->ev[6], st));
+        HIP_TRY(hipEventRecord(ctx->ev[11], st));
         k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, st>>>(wa);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
@@ -3902,6 +3917,17 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]));
         HIP_TRY(hipEventElapsedTime(&ms_dfs, ctx->ev[1], ctx->ev[4]));
         sum->device_ms = ms; sum->dfs_ms = ms_dfs;
+        sum->n_deferred = n_defer;
+        sum->deferred_entries = (int64_t)(((uint64_t)(uint32_t)qh[25] << 32) | (uint32_t)qh[24]);
+        sum->seq_probes = (int64_t)(((uint64_t)(uint32_t)qh[9] << 32) | (uint32_t)qh[8]);
+        sum->seq_ms = 0; sum->bfs_ms = 0;
+        if (n_defer > 0) {
+            float a2 = 0, b2 = 0;
+            if (use_wg) HIP_TRY(hipEventElapsedTime(&a2, ctx->ev[11], ctx->ev[5]));
+            else HIP_TRY(hipEventElapsedTime(&a2, ctx->ev[6], ctx->ev[10]));
+            sum->seq_ms = a2;
+            if (!use_wg) { HIP_TRY(hipEventElapsedTime(&b2, ctx->ev[6], ctx->ev[5])); sum->bfs_ms = b2; }
+        }
         if (getenv("JH_DEBUG")) {
             float a = 0, b = 0, c = 0;
             HIP_TRY(hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]));

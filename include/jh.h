@@ -151,7 +151,24 @@ typedef struct jh_ctx jh_ctx;
 int  jh_version(void);
 /* Opens a context on HIP device `device`. */
 int  jh_open(int device, jh_ctx **out);
+/* Opens one context over devices 0..n_gpus-1 (n_gpus <= 0: every visible
+ * device; SURVEY 8(b) "jh_open(n_gpus)"). jh_check_cas_independent on it
+ * splits the keys over the devices by the jh_key_costs estimate (heaviest
+ * first to the least-loaded device), checks every part concurrently, one host
+ * thread per device, and merges the verdicts and the summary on the host:
+ * same result as one device, bit for bit. The other checkers run on device 0.
+ * Host columns only (on_device = 0). jh_close closes every device. */
+int  jh_open_multi(int n_gpus, jh_ctx **out);
+/* The same over an explicit device list; a device may appear more than once
+ * (several contexts share it, each with its own streams and workspace). */
+int  jh_open_devices(const int32_t *devices, int n, jh_ctx **out);
+int  jh_n_devices(const jh_ctx *ctx);
 void jh_close(jh_ctx *ctx);
+
+/* Per-key search-cost estimate used to split keys between devices: the key's
+ * entries plus its window sum (for every client op, the :ok returns inside its
+ * window; a crashed op's window runs to the end). Host columns; no device. */
+int  jh_key_costs(const jh_history *h, int64_t *cost /*[n_keys]*/, char *err, size_t errlen);
 
 /* (independent/checker (checker/linearizable {:model (model/cas-register init)})).
  * out[k] receives the verdict of key k for k in [0, h->n_keys); keys that
@@ -161,6 +178,16 @@ int jh_check_cas_independent(jh_ctx *ctx, const jh_history *h,
                              const jh_lin_opts *opts,
                              jh_key_verdict *out, jh_summary *sum,
                              char *err, size_t errlen);
+
+/* The per-key row index of an independent history, from the device's stable
+ * key partition: rows[key_off[k] .. key_off[k+1]) are key k's rows in history
+ * order, and rows[key_off[n_keys] .. n) the rows in no tuple (nemesis ops).
+ * Key k's subhistory (independent.clj:234-245) is the merge of its rows with
+ * the un-keyed rows, so the shim writes every key's history.edn
+ * (independent.clj:277-284) in one O(N) pass. Only the key column is read.
+ * key_off: n_keys+1 entries; rows: n entries (host buffers). */
+int jh_key_index(jh_ctx *ctx, const jh_history *h, int64_t *key_off, int64_t *rows,
+                 char *err, size_t errlen);
 
 /* (checker/linearizable {:model (model/cas-register init)}) on a history
  * whose values are not tuples (key column ignored). */

@@ -33,6 +33,12 @@ def lib():
             H = C.POINTER(A.JhHistory)
             L.jh_version.restype = C.c_int
             L.jh_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+            L.jh_open_multi.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+            L.jh_open_devices.argtypes = [C.POINTER(C.c_int32), C.c_int, C.POINTER(C.c_void_p)]
+            L.jh_n_devices.argtypes = [C.c_void_p]
+            L.jh_key_index.argtypes = [C.c_void_p, H, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                       C.c_char_p, C.c_size_t]
+            L.jh_key_costs.argtypes = [C.POINTER(A.JhHistory), C.POINTER(C.c_int64), C.c_char_p, C.c_size_t]
             L.jh_close.argtypes = [C.c_void_p]
             L.jh_close.restype = None
             L.jh_check_cas_independent.argtypes = [C.c_void_p, H, C.POINTER(A.JhLinOpts),
@@ -59,7 +65,8 @@ def lib():
     return _lib
 
 
-EXPORTED_SYMBOLS = ["jh_version", "jh_open", "jh_close", "jh_check_cas_independent",
+EXPORTED_SYMBOLS = ["jh_version", "jh_open", "jh_open_multi", "jh_open_devices", "jh_n_devices", "jh_key_costs", "jh_key_index",
+                    "jh_close", "jh_check_cas_independent",
                     "jh_check_cas", "jh_check_cas_independent_device", "jh_check_counter",
                     "jh_check_set", "jh_check_set_full", "jh_check_total_queue", "jh_check_queue"]
 
@@ -73,17 +80,37 @@ def _opts(init, budget, stream=0):
     return A.JhLinOpts(A.NIL if init is None else int(init), int(budget or 0), int(stream))
 
 
-class Context:
-    """One jh_ctx on one HIP device (jh_open / jh_close)."""
+def key_costs(cols):
+    """jh_key_costs: per-key search-cost estimate (entries + window sum), the
+    weight that splits keys between devices. Host-only: needs no GPU."""
+    h = A.make_history(cols)
+    out = np.zeros(max(cols.n_keys, 1), dtype=np.int64)
+    err = C.create_string_buffer(256)
+    rc = lib().jh_key_costs(C.byref(h), out.ctypes.data_as(C.POINTER(C.c_int64)), err, len(err))
+    _raise(rc, err)
+    return out[:cols.n_keys]
 
-    def __init__(self, device=0):
+
+class Context:
+    """One jh_ctx on one HIP device (jh_open / jh_close), or, with n_gpus, one
+    context over devices 0..n_gpus-1 (jh_open_multi: the independent check is
+    split by key over them inside libjh)."""
+
+    def __init__(self, device=0, n_gpus=None, devices=None):
         L = lib()
         h = C.c_void_p()
-        rc = L.jh_open(int(device), C.byref(h))
+        if devices is not None:
+            arr = (C.c_int32 * len(devices))(*devices)
+            rc = L.jh_open_devices(arr, len(devices), C.byref(h))
+        elif n_gpus is None:
+            rc = L.jh_open(int(device), C.byref(h))
+        else:
+            rc = L.jh_open_multi(int(n_gpus), C.byref(h))
         if rc != A.JH_OK:
-            raise JhError(rc, f"jh_open({device}) failed (no usable HIP device?)")
+            raise JhError(rc, f"jh_open({device}, n_gpus={n_gpus}) failed (no usable HIP device?)")
         self._h = h
         self.device = device
+        self.n_devices = L.jh_n_devices(h)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -95,6 +122,20 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def key_index(self, cols):
+        """jh_key_index: (key_off [n_keys+1], rows [n]) -- key k's rows are
+        rows[key_off[k]:key_off[k+1]] in history order, the un-keyed rows
+        rows[key_off[n_keys]:]."""
+        h = A.make_history(cols)
+        off = np.zeros(cols.n_keys + 1, np.int64)
+        rows = np.zeros(max(cols.n, 1), np.int64)
+        err = C.create_string_buffer(512)
+        p64 = C.POINTER(C.c_int64)
+        rc = lib().jh_key_index(self._h, C.byref(h), off.ctypes.data_as(p64), rows.ctypes.data_as(p64),
+                                err, len(err))
+        _raise(rc, err)
+        return off, rows[:cols.n]
 
     # -- linearizability ---------------------------------------------------
     def check_cas_independent(self, cols, init=None, budget=None):

@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build")
-HIP_SOURCES = ["jh_lin.hip", "jh_counter.hip", "jh_set.hip", "jh_setfull.hip", "jh_queue.hip", "jh_api.hip"]
+HIP_SOURCES = ["jh_lin.hip", "jh_counter.hip", "jh_set.hip", "jh_setfull.hip", "jh_queue.hip", "jh_api.hip", "jh_multi.hip"]
 HEADERS = [os.path.join(CSRC, "jh_internal.h"), os.path.join(ROOT, "include", "jh.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -76,8 +76,20 @@ def build_oracle():
     return os.path.join(ROOT, "oracle", "liboracle.so")
 
 
+def build_harness():
+    """tests/c/jh_harness: a plain-C program linked against libjh.so (the
+    boundary as a JNA/cgo caller sees it; tests/test_c_harness.py)."""
+    src = os.path.join(ROOT, "tests", "c", "jh_harness.c")
+    exe = os.path.join(ROOT, "tests", "c", "jh_harness")
+    lib = os.path.join(HERE, "libjh.so")
+    if _newer(exe, [src, lib, os.path.join(ROOT, "include", "jh.h")]):
+        _run(["gcc", "-O2", "-Wall", "-I" + os.path.join(ROOT, "include"), src, "-L" + HERE, "-ljh",
+              "-Wl,-rpath,$ORIGIN/../../jepsen_amd", "-o", exe])
+    return exe
+
+
 def build_all(verbose=False):
-    return [build_libjh(verbose), build_gen(), build_oracle()]
+    return [build_libjh(verbose), build_gen(), build_oracle(), build_harness()]
 
 
 if __name__ == "__main__":

@@ -61,6 +61,13 @@ static void check_hist(const jh_history *h) {
     if (h->n_keys < 0) throw_jh(JH_EINVAL, "negative key count");
 }
 
+// a multi-device context (jh_open_multi) shards the independent checks over
+// its devices; the single-history checkers run on its first device
+static jh_ctx *primary(jh_ctx *c) { return c->members.empty() ? c : c->members[0]; }
+
+int multi_check_cas_independent(jh_ctx *g, const jh_history *h, const jh_lin_opts *opts,
+                                jh_key_verdict *out, jh_summary *sum, char *err, size_t errlen);
+
 extern "C" {
 
 int jh_version(void) { return JH_ABI_VERSION; }
@@ -92,6 +99,11 @@ int jh_open(int device, jh_ctx **out) {
 
 void jh_close(jh_ctx *ctx) {
     if (!ctx) return;
+    if (!ctx->members.empty()) {
+        for (jh_ctx *m : ctx->members) jh_close(m);
+        delete ctx;
+        return;
+    }
     {
         std::lock_guard<std::mutex> g(ctx->mu);
         (void)hipSetDevice(ctx->device);
@@ -108,6 +120,13 @@ void jh_close(jh_ctx *ctx) {
 int jh_check_cas_independent(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts,
                              jh_key_verdict *out, jh_summary *sum, char *err, size_t errlen) {
     if (!ctx || !out) { set_err(err, errlen, "null context or output"); return JH_EINVAL; }
+    if (!ctx->members.empty()) {
+        char e[512] = "";
+        int rc = guarded(e, sizeof e, [&] { check_hist(h); });
+        if (rc == JH_OK) rc = multi_check_cas_independent(ctx, h, opts, out, sum, e, sizeof e);
+        set_err(err, errlen, e);
+        return rc;
+    }
     std::lock_guard<std::mutex> g(ctx->mu);
     return guarded(err, errlen, [&] {
         check_hist(h);
@@ -130,6 +149,7 @@ int jh_check_cas_independent_device(jh_ctx *ctx, const jh_history *h, const jh_l
                                     jh_key_verdict *out_dev, jh_summary *sum, char *err,
                                     size_t errlen) {
     if (!ctx || !out_dev) { set_err(err, errlen, "null context or output"); return JH_EINVAL; }
+    ctx = primary(ctx);   // device pointers live on one device: the first
     std::lock_guard<std::mutex> g(ctx->mu);
     return guarded(err, errlen, [&] {
         check_hist(h);
@@ -144,9 +164,25 @@ int jh_check_cas_independent_device(jh_ctx *ctx, const jh_history *h, const jh_l
     });
 }
 
+int jh_key_index(jh_ctx *ctx, const jh_history *h, int64_t *key_off, int64_t *rows, char *err,
+                 size_t errlen) {
+    if (!ctx || !key_off || (!rows && h && h->n > 0)) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    ctx = primary(ctx);
+    std::lock_guard<std::mutex> g(ctx->mu);
+    return guarded(err, errlen, [&] {
+        if (!h || h->n < 0 || h->n_keys < 0) throw_jh(JH_EINVAL, "bad history");
+        if (h->n > 0 && !h->key) throw_jh(JH_EINVAL, "jh_key_index needs the key column");
+        HIP_TRY(hipSetDevice(ctx->device));
+        jh_history d = *h;
+        if (!h->on_device) d.key = stage_col(ctx, WS_COL_KEY, h->key, h->n, ctx->stream);
+        key_index(ctx, &d, key_off, rows, ctx->stream);
+    });
+}
+
 int jh_check_cas(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts, jh_key_verdict *out,
                  char *err, size_t errlen) {
     if (!ctx || !out) { set_err(err, errlen, "null context or output"); return JH_EINVAL; }
+    ctx = primary(ctx);
     std::lock_guard<std::mutex> g(ctx->mu);
     return guarded(err, errlen, [&] {
         check_hist(h);
@@ -173,6 +209,7 @@ int jh_check_counter(jh_ctx *ctx, const jh_history *h, int64_t *reads_out, int64
         set_err(err, errlen, "null argument");
         return JH_EINVAL;
     }
+    ctx = primary(ctx);
     std::lock_guard<std::mutex> g(ctx->mu);
     return guarded(err, errlen, [&] {
         check_hist(h);
@@ -187,6 +224,7 @@ int jh_check_set(jh_ctx *ctx, const jh_history *h, jh_set_result *res, int64_t *
                  int64_t *runs_lost, int64_t *runs_unexpected, int64_t *runs_recovered,
                  int64_t runs_cap, char *err, size_t errlen) {
     if (!ctx || !res) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    ctx = primary(ctx);
     std::lock_guard<std::mutex> g(ctx->mu);
     return guarded(err, errlen, [&] {
         check_hist(h);
@@ -201,6 +239,7 @@ int jh_check_set_full(jh_ctx *ctx, const jh_history *h, const int64_t *time, int
                       jh_set_full_result *res, int64_t *lost, int64_t *never_read, int64_t *stale,
                       int64_t list_cap, char *err, size_t errlen) {
     if (!ctx || !res) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    ctx = primary(ctx);
     std::lock_guard<std::mutex> g(ctx->mu);
     return guarded(err, errlen, [&] {
         check_hist(h);
@@ -217,6 +256,7 @@ int jh_check_total_queue(jh_ctx *ctx, const jh_history *h, jh_queue_result *res,
                          int64_t *unexpected, int64_t *duplicated, int64_t *recovered, int64_t pairs_cap,
                          char *err, size_t errlen) {
     if (!ctx || !res) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    ctx = primary(ctx);
     std::lock_guard<std::mutex> g(ctx->mu);
     return guarded(err, errlen, [&] {
         check_hist(h);
@@ -230,6 +270,7 @@ int jh_check_total_queue(jh_ctx *ctx, const jh_history *h, jh_queue_result *res,
 int jh_check_queue(jh_ctx *ctx, const jh_history *h, jh_queue_result *res, int64_t *final_queue,
                    int64_t pairs_cap, char *err, size_t errlen) {
     if (!ctx || !res) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    ctx = primary(ctx);
     std::lock_guard<std::mutex> g(ctx->mu);
     return guarded(err, errlen, [&] {
         check_hist(h);

@@ -62,6 +62,7 @@ struct jh_ctx {
     int n_cu = 256;
     void *pinned = nullptr;       // small pinned staging for scalars
     size_t pinned_bytes = 0;
+    std::vector<jh_ctx *> members;  // jh_open_multi: one context per device (jh_multi.hip); empty otherwise
 
     template <class T>
     T *ws(int slot, size_t count, bool zero = false) {
@@ -141,6 +142,8 @@ jh_history stage_history(jh_ctx *ctx, const jh_history *h, bool need_key, bool n
 void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts *opts,
                            bool keyed, jh_key_verdict *out_dev, jh_summary *sum,
                            hipStream_t stream);
+// per-key row CSR of an independent history (jh_lin.hip)
+void key_index(jh_ctx *ctx, const jh_history *dh, int64_t *key_off, int64_t *rows, hipStream_t stream);
 // counter (jh_counter.hip)
 void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_t reads_cap,
                    int64_t *n_reads, int64_t *n_errors, int64_t *first_err, int32_t *valid,

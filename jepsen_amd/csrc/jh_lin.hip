@@ -3410,6 +3410,12 @@ __global__ void k_iota(int32_t *a, int64_t n) {
     if (i < n) a[i] = (int32_t)i;
 }
 
+// widens the sorted row ids / segment offsets for the jh_key_index CSR
+__global__ void k_widen(const uint32_t *__restrict__ a, int64_t n, int64_t *__restrict__ b) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        b[i] = a[i];
+}
+
 inline int bits_for(uint64_t x) {
     int b = 1;
     while ((1ULL << b) <= x) b++;
@@ -3992,3 +3998,35 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         }
     }
 }
+
+// The per-key row index (CSR) of an independent history: the same stable
+// radix partition the check starts with, handed back so a caller can write
+// every key's subhistory (independent.clj:234-245, :277-284) in one O(N) pass
+// instead of K scans of the whole history.
+void key_index(jh_ctx *ctx, const jh_history *dh, int64_t *key_off, int64_t *rows, hipStream_t st) {
+    const int64_t n = dh->n, K = dh->n_keys;
+    if (K >= (1LL << 31) - 2) throw_jh(JH_EUNSUPPORTED, "more than 2^31 keys");
+    if (n >= (1LL << 32) - 1) throw_jh(JH_EUNSUPPORTED, "more than 2^32 entries");
+    uint32_t *kA = ctx->ws<uint32_t>(WS_KEYS_A, n), *kB = ctx->ws<uint32_t>(WS_KEYS_B, n);
+    uint32_t *rA = ctx->ws<uint32_t>(WS_ROWS_A, n), *rB = ctx->ws<uint32_t>(WS_ROWS_B, n);
+    uint32_t *off = ctx->ws<uint32_t>(WS_SEG_OFF, K + 2);
+    RangeOut *ro = ctx->ws<RangeOut>(WS_MISC, 1);
+    int64_t *wide = ctx->ws<int64_t>(WS_C_TMP, std::max<int64_t>(n, K + 1));
+    if (n > 0) {
+        k_keys<<<grid_for(n, 256), 256, 0, st>>>(dh->key, n, K, 1, kA, rA);
+        const int endbit = bits_for((uint64_t)K);
+        size_t tb = 0;
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kA, kB, rA, rB, (int)n, 0, endbit, st));
+        void *tmp = ctx->ws<char>(WS_SORT_TMP, tb);
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kA, kB, rA, rB, (int)n, 0, endbit, st));
+        k_seg_off<<<grid_for(K + 1, 256), 256, 0, st>>>(kB, n, K, off, ro);
+        k_widen<<<grid_for(n, 256), 256, 0, st>>>(rB, n, wide);
+        HIP_TRY(hipMemcpyAsync(rows, wide, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+        k_widen<<<grid_for(K + 1, 256), 256, 0, st>>>(off, K + 1, wide);
+        HIP_TRY(hipMemcpyAsync(key_off, wide, sizeof(int64_t) * (K + 1), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    } else {
+        for (int64_t k = 0; k <= K; ++k) key_off[k] = 0;
+    }
+}
+

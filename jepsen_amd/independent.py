@@ -63,6 +63,30 @@ def subhistories(history, keys=None):
     return out
 
 
+def subhistories_indexed(history, key_off, rows, key_ids):
+    """The same lists as `subhistories`, built from libjh's per-key row index
+    (jh_key_index: the device's stable key partition). Key k's subhistory is
+    its rows merged with the un-keyed rows, both already in history order, so
+    building all of them is one O(N + K*U) pass with no scan per key.
+    key_ids: {key: dense key id of the encoding}."""
+    import numpy as np
+    unkeyed = rows[key_off[-1]:]
+    out = {}
+    for key, kid in key_ids.items():
+        mine = rows[key_off[kid]:key_off[kid + 1]]
+        merged = np.sort(np.concatenate([mine, unkeyed])) if len(unkeyed) else mine
+        lst = []
+        for r in merged.tolist():
+            op = history[r]
+            v = op.get("value")
+            if is_tuple(v):
+                op = dict(op)
+                op["value"] = v.val
+            lst.append(op)
+        out[key] = lst
+    return out
+
+
 def _lin_member(inner):
     if isinstance(inner, Linearizable) and inner.supported():
         return None, inner
@@ -109,7 +133,10 @@ class IndependentChecker(Checker):
                 if name is None:
                     return self._results_map(lin_res)
                 results = {}
-                subs = subhistories(history, list(lin_res))
+                ctx = _ctx()
+                key_off, rows = ctx.key_index(cols)
+                kid_of = {key: kid for kid, key in enumerate(cols.keys) if key in lin_res}
+                subs = subhistories_indexed(history, key_off, rows, kid_of)
                 for key, lr in lin_res.items():
                     sub = subs[key]
                     r = {}

@@ -18,11 +18,13 @@ _FAR = 1 << 62
 
 
 def key_costs(cols):
-    """Estimated search cost per key: its entry count (the DFS does ~6 memo
-    inserts per op on valid keys; crashed ops and invalidity add more, which
-    only the search itself can tell)."""
-    k = cols.key[cols.key >= 0]
-    return np.bincount(k, minlength=cols.n_keys).astype(np.int64)
+    """Estimated search cost per key (libjh's jh_key_costs, the same weight
+    jh_open_multi splits by): entries + the window sum -- for every client op,
+    the :ok returns that fall inside its window, a crashed op's window running
+    to the end. Cost grows with window width and crashes, not entry count
+    (every C3/C4 key has about the same count)."""
+    from . import _native
+    return _native.key_costs(cols)
 
 
 def assign_keys(costs, world):

@@ -29,7 +29,7 @@ def per_launch(d, counter, kernel):
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    kernel = sys.argv[3] if len(sys.argv) > 3 else "k_lin_seq"
+    kernel = sys.argv[3] if len(sys.argv) > 3 else "k_lin_seq<true>"
     workload = sys.argv[4] if len(sys.argv) > 4 else "c3"
     fetch, nf = per_launch(src, "FETCH_SIZE", kernel)
     write, nw = per_launch(src, "WRITE_SIZE", kernel)
@@ -41,7 +41,7 @@ def main():
     # algorithmic bytes, not the bench's
     run = {}
     try:
-        last = open(os.path.join(src, "fetch.log")).read().strip().splitlines()[-1]
+        last = [ln for ln in open(os.path.join(src, "fetch.log")) if ln.startswith("keys=")][-1]
         run = {k: float(v) for k, v in (f.split("=") for f in last.split()) if k}
     except (OSError, IndexError, ValueError):
         pass

@@ -93,6 +93,7 @@ extern "C" {
 #define JH_CAUSE_BAD_F        5  /* op :f the cas-register model does not know */
 #define JH_CAUSE_NIL_VALUE    6  /* nil where the checker does arithmetic     */
 #define JH_CAUSE_OVERFLOW     7  /* long overflow (Clojure + throws)          */
+#define JH_CAUSE_STATES       8  /* more than 65532 distinct values in one key */
 
 #define JH_MAX_WINDOW 256
 

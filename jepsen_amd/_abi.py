@@ -26,6 +26,7 @@ CAUSES = {
     5: "unsupported-f",
     6: "nil-value",
     7: "overflow",
+    8: "states",
 }
 
 MAX_WINDOW = 256

@@ -153,6 +153,7 @@ CAUSE_ERRORS = {
     "orphan-completion": "knossos.history/complete: completion without an outstanding invocation",
     "unsupported-f": "IllegalArgumentException: the cas-register model has no step for this :f",
     "window": "more concurrent operations than the device search window supports",
+    "states": "more distinct register values in one key than the device state encoding holds",
 }
 
 

@@ -478,8 +478,7 @@ __device__ bool key_pass1(const KeySrc &S, int key, int lane, KeyInfo &K, jh_key
         v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
         return false;
     }
-    if (n_ops > 65535 || n_ok >= (int)T_MASK) {
-        if (lane == 0) atomicOr(S.flags, 1);
+    if (n_ok >= (int)T_MASK) {   // beyond every table's t field: this key alone is :unknown
         v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
         return false;
     }
@@ -1561,7 +1560,7 @@ done:
 // bytes of a k_lin_xw key's tables (ops, windows per layer)
 __device__ __forceinline__ uint64_t a16(uint64_t x) { return (x + 15) & ~15ULL; }
 __device__ __forceinline__ uint64_t xw_bytes(int n_ops, int n_ok, long long sumW) {
-    return 3 * a16((uint64_t)n_ops * 4) + a16((uint64_t)(n_ok + 1) * 4) + a16((uint64_t)sumW * 2 + 512);
+    return 3 * a16((uint64_t)n_ops * 4) + a16((uint64_t)(n_ok + 1) * 4) + a16((uint64_t)sumW * 4 + 1024);
 }
 
 struct KeyMeta {
@@ -1584,7 +1583,7 @@ struct TblArgs {
     int32_t *n_list_w;
     int32_t *list_x;            // keys that need a search: windows wider than 64 (k_lin_xw)
     int32_t *n_list_x;
-    int32_t *xw_max;            // the largest k_lin_xw table (bytes)
+    unsigned long long *xw_max; // the largest k_lin_xw table (bytes)
     int32_t states8;            // every interned state < 256
 };
 
@@ -1595,15 +1594,12 @@ __global__ void __launch_bounds__(256) k_key_tables(TblArgs A) {
         KeyInfo K;
         jh_key_verdict v;
         bool need = key_pass1(A.src, (int)key, lane, K, v);
-        if (need && K.n_ok >= COMPACT_MAX_OK) {
-            // beyond the compact encoding (a < 2^14): not on this build's path
-            if (lane == 0) atomicOr(A.src.flags, 1);
-            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW;
-            need = false;
-        }
+        // long keys (beyond the compact encoding: a < 2^14, op ids < 2^16) take
+        // the k_lin_xw path, whose tables are 32-bit
+        const bool long_key = K.n_ok >= COMPACT_MAX_OK || K.n_ops > 65535;
         if (need) {
             int maxw = 65;
-            if (K.sumW <= 64LL * K.n_ok) {
+            if (!long_key && K.sumW <= 64LL * K.n_ok) {
                 unsigned long long off = 0;
                 if (lane == 0) off = atomicAdd(A.bump, (unsigned long long)tblc_bytes(K));
                 off = (unsigned long long)rfl64(__shfl(off, 0));
@@ -1624,7 +1620,7 @@ __global__ void __launch_bounds__(256) k_key_tables(TblArgs A) {
                 m.off = 0; m.n_ops = K.n_ops; m.n_ok = K.n_ok; m.maxw = -1; m.pad = (int32_t)K.sumW;
                 A.meta[key] = m;
                 A.list_x[atomicAdd(A.n_list_x, 1)] = (int32_t)key;
-                atomicMax(A.xw_max, (int32_t)xw_bytes(K.n_ops, K.n_ok, K.sumW));
+                atomicMax(A.xw_max, (unsigned long long)xw_bytes(K.n_ops, K.n_ok, K.sumW));
             }
         }
         if (!need && lane == 0) A.out[key] = v;
@@ -3055,7 +3051,7 @@ struct XwTbl {
     int32_t *rr;      // ok-return rank, -1 crashed
     int32_t *a;       // ok returns before the invocation (the op joins W(a))
     int32_t *woff;    // W(t) = W[woff[t] .. woff[t+1])
-    uint16_t *W;
+    uint32_t *W;      // op ids: 32-bit, long keys come here
 };
 __device__ __forceinline__ XwTbl xw_tbl(char *tb, int n_ops, int n_ok) {
     XwTbl T;
@@ -3064,7 +3060,7 @@ __device__ __forceinline__ XwTbl xw_tbl(char *tb, int n_ops, int n_ok) {
     T.rr = (int32_t *)(tb + o); o += a16((uint64_t)n_ops * 4);
     T.a = (int32_t *)(tb + o); o += a16((uint64_t)n_ops * 4);
     T.woff = (int32_t *)(tb + o); o += a16((uint64_t)(n_ok + 1) * 4);
-    T.W = (uint16_t *)(tb + o);
+    T.W = (uint32_t *)(tb + o);
     return T;
 }
 
@@ -3114,7 +3110,7 @@ __device__ int xw_fill(const KeySrc &S, uint32_t s0, uint32_t s1, int n_ops, int
                 bool keep = false;
                 if (idx < w) { prev = T.W[offp + idx]; keep = T.rr[prev] != t - 1; }
                 const uint64_t bk = ballot(keep);
-                if (keep) T.W[offt + nk + mbcnt(bk)] = (uint16_t)prev;
+                if (keep) T.W[offt + nk + mbcnt(bk)] = (uint32_t)prev;
                 nk += __popcll(bk);
             }
         }
@@ -3124,7 +3120,7 @@ __device__ int xw_fill(const KeySrc &S, uint32_t s0, uint32_t s1, int n_ops, int
             const bool in = j < n_ops && T.a[j] <= t;
             const uint64_t ba = ballot(in);
             const int c = __popcll(ba);             // a is non-decreasing: a prefix
-            if (in && nk + added + lane < JH_MAX_WINDOW) T.W[offt + nk + added + lane] = (uint16_t)j;
+            if (in && nk + added + lane < JH_MAX_WINDOW) T.W[offt + nk + added + lane] = (uint32_t)j;
             added += c; nxt += c;
             if (c < 64) break;
         }
@@ -3410,6 +3406,82 @@ __global__ void k_iota(int32_t *a, int64_t n) {
     if (i < n) a[i] = (int32_t)i;
 }
 
+// Per-key dense interning of register values, for histories whose values
+// span more than one 16-bit state range (unique values, wide ids). Every key
+// numbers its own distinct values: 0 = nil, 1 = the initial value (when not
+// nil), then the key's other values in order. The search compares states
+// only for equality, so any per-key bijection leaves every configuration
+// set, search order and count unchanged. Items are (record, v1|v2) pairs:
+// radix-sorted by value, then stably by key, ranked by a scan of "new
+// distinct value" flags within each key's item range [2*off[k], 2*off[k+1]).
+__global__ void k_ival(const int64_t *__restrict__ v1, const int64_t *__restrict__ v2,
+                       const int64_t *__restrict__ f, const uint32_t *__restrict__ rows, int64_t m,
+                       uint64_t *__restrict__ u, uint32_t *__restrict__ idx) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < 2 * m; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = rows[i >> 1];
+        int64_t raw = (i & 1) ? v2[r] : v1[r];
+        if (f_code(f[r]) > F_CAS) raw = JH_NIL;
+        u[i] = (uint64_t)raw ^ (1ULL << 63);           // signed order; nil -> 0
+        idx[i] = (uint32_t)i;
+    }
+}
+__global__ void k_ikey(const uint32_t *__restrict__ idx, const uint32_t *__restrict__ rkey, int64_t n2,
+                       uint32_t *__restrict__ key_of) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n2; j += (int64_t)gridDim.x * blockDim.x)
+        key_of[j] = rkey[idx[j] >> 1];
+}
+__global__ void k_iflag(const uint32_t *__restrict__ idx, const uint64_t *__restrict__ u,
+                        const uint32_t *__restrict__ rkey, const uint32_t *__restrict__ off, int64_t n2,
+                        uint32_t *__restrict__ flag) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n2; j += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t i = idx[j];
+        const uint64_t x = u[i];
+        const uint32_t k = rkey[i >> 1];
+        const bool first = j == 2 * (int64_t)off[k];
+        flag[j] = (x != 0 && (first || u[idx[j - (first ? 0 : 1)]] != x)) ? 1u : 0u;
+    }
+}
+// rank within the key: 1..n_distinct (0 for nil)
+__device__ __forceinline__ uint32_t ival_rank(const uint32_t *P, const uint32_t *off, uint32_t k, int64_t j) {
+    const int64_t s = 2 * (int64_t)off[k];
+    return P[j] - (s > 0 ? P[s - 1] : 0u);
+}
+__global__ void k_iinit(const uint32_t *__restrict__ idx, const uint64_t *__restrict__ u,
+                        const uint32_t *__restrict__ rkey, const uint32_t *__restrict__ off,
+                        const uint32_t *__restrict__ P, int64_t n2, uint64_t init_u, uint32_t *__restrict__ r_init) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n2; j += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t i = idx[j];
+        if (u[i] == init_u) { const uint32_t k = rkey[i >> 1]; r_init[k] = ival_rank(P, off, k, j); }
+    }
+}
+__global__ void k_iassign(const uint32_t *__restrict__ idx, const uint64_t *__restrict__ u,
+                          const uint32_t *__restrict__ rkey, const uint32_t *__restrict__ off,
+                          const uint32_t *__restrict__ P, int64_t n2, int has_init, uint64_t init_u,
+                          const uint32_t *__restrict__ r_init, Rec *__restrict__ rec,
+                          unsigned long long *__restrict__ viol, unsigned int *__restrict__ maxid) {
+    unsigned int mx = 0;
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n2; j += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t i = idx[j];
+        const uint64_t x = u[i];
+        const uint32_t p = i >> 1, k = rkey[p];
+        uint32_t id = 0;
+        if (x != 0) {
+            const uint32_t r = ival_rank(P, off, k, j);
+            if (!has_init) id = r;
+            else if (x == init_u) id = 1;
+            else id = 1 + r - ((r_init[k] > 0 && r > r_init[k]) ? 1u : 0u);
+        }
+        if (id >= RQ_EMPTY - 1) {      // beyond the 16-bit state encoding: this key alone is :unknown
+            atomicMin(&viol[k], ((unsigned long long)p << 4) | JH_CAUSE_STATES);
+            id = 0;
+        }
+        if (i & 1) rec[p].v2 = (int32_t)id; else rec[p].v1 = (int32_t)id;
+        mx = max(mx, id);
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned int)__shfl_xor((int)mx, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(maxid, mx);
+}
+
 // widens the sorted row ids / segment offsets for the jh_key_index CSR
 __global__ void k_widen(const uint32_t *__restrict__ a, int64_t n, int64_t *__restrict__ b) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -3452,9 +3524,12 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     long long vmin = rh.vmin, vmax = rh.vmax;
     if (init != JH_NIL) { vmin = std::min<long long>(vmin, init); vmax = std::max<long long>(vmax, init); }
     if (vmin > vmax) { vmin = 0; vmax = 0; }
-    if ((unsigned long long)(vmax - vmin) >= (unsigned long long)(RQ_EMPTY - 2))
-        throw_jh(JH_EUNSUPPORTED, "register values span more than 65532 distinct states");
-    const int init_state = init == JH_NIL ? 0 : (int)(init - vmin + 1);
+    // values spanning more than one 16-bit state range are interned per key
+    // (k_ival..k_iassign) instead of as one global offset
+    const bool per_key_values = (unsigned long long)(vmax - vmin) >= (unsigned long long)(RQ_EMPTY - 3) ||
+                                (getenv("JH_INTERN_PER_KEY") && atoi(getenv("JH_INTERN_PER_KEY")) != 0);
+    const int init_state = init == JH_NIL ? 0 : per_key_values ? 1 : (int)(init - vmin + 1);
+    long long n_states = vmax - vmin + 2;      // state ids 0 (nil) .. vmax - vmin + 1
 
     // partition by key
     uint32_t *kA = ctx->ws<uint32_t>(WS_KEYS_A, n), *kB = ctx->ws<uint32_t>(WS_KEYS_B, n);
@@ -3486,6 +3561,41 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                                                    rB, m, vmin, rec);
         k_pair<<<grid_for((m + 63) / 64, 4, 16384), 256, 0, st>>>(rec, kB, off, m, pair, viol);
         k_orphan<<<grid_for(m, 256), 256, 0, st>>>(rec, kB, m, pair, viol);
+    }
+    if (per_key_values && m > 0) {
+        const int64_t n2 = 2 * m;
+        if (n2 >= (1LL << 32) - 1) throw_jh(JH_EUNSUPPORTED, "too many entries for per-key value interning");
+        uint64_t *iu = ctx->ws<uint64_t>(WS_IV_U, 2 * n2);
+        uint32_t *ix = ctx->ws<uint32_t>(WS_IV_IDX, 3 * n2);
+        uint32_t *ik = ctx->ws<uint32_t>(WS_IV_KEY, 2 * n2);
+        uint32_t *rinit = ctx->ws<uint32_t>(WS_IV_RINIT, K + 1);
+        unsigned int *maxid = (unsigned int *)ctx->ws<uint32_t>(WS_IV_MAX, 4);
+        uint32_t *flag = ik + n2;                   // reuses the key buffer's second half
+        k_ival<<<grid_for(n2, 256), 256, 0, st>>>(dh->value, dh->value2, dh->f, rB, m, iu, ix);
+        size_t tb1 = 0, tb2 = 0, tb3 = 0;
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb1, iu, iu + n2, ix, ix + n2, (int)n2, 0, 64, st));
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, ik, ik + n2, ix + n2, ix + 2 * n2, (int)n2, 0, endbit, st));
+        HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb3, flag, flag, (int)n2, st));
+        char *itmp = ctx->ws<char>(WS_IV_TMP, std::max(tb1, std::max(tb2, tb3)));
+        // by value (iu keeps the original values, iu + n2 the sorted ones) ...
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(itmp, tb1, iu, iu + n2, ix, ix + n2, (int)n2, 0, 64, st));
+        // ... then stably by key: each key's items in value order
+        k_ikey<<<grid_for(n2, 256), 256, 0, st>>>(ix + n2, kB, n2, ik);
+        uint32_t *ik2 = (uint32_t *)(iu + n2);      // sorted values no longer needed: key output
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(itmp, tb2, ik, ik2, ix + n2, ix + 2 * n2, (int)n2, 0, endbit, st));
+        const uint32_t *idx2 = ix + 2 * n2;
+        k_iflag<<<grid_for(n2, 256), 256, 0, st>>>(idx2, iu, kB, off, n2, flag);
+        HIP_TRY(hipcub::DeviceScan::InclusiveSum(itmp, tb3, flag, flag, (int)n2, st));
+        const uint64_t init_u = (uint64_t)init ^ (1ULL << 63);
+        HIP_TRY(hipMemsetAsync(rinit, 0, sizeof(uint32_t) * (K + 1), st));
+        HIP_TRY(hipMemsetAsync(maxid, 0, sizeof(unsigned int), st));
+        if (init != JH_NIL) k_iinit<<<grid_for(n2, 256), 256, 0, st>>>(idx2, iu, kB, off, flag, n2, init_u, rinit);
+        k_iassign<<<grid_for(n2, 256), 256, 0, st>>>(idx2, iu, kB, off, flag, n2, init != JH_NIL ? 1 : 0, init_u,
+                                                     rinit, rec, viol, maxid);
+        unsigned int mh = 0;
+        HIP_TRY(hipMemcpyAsync(&mh, maxid, sizeof mh, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        n_states = (long long)std::max<unsigned int>(mh, init != JH_NIL ? 1u : 0u) + 1;
     }
 
     // memo generation tags: distinct per (call, key, pass); wrap -> clear
@@ -3521,8 +3631,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     int32_t *list_w = ctx->ws<int32_t>(WS_LIST_W, K);
     ta.out = out_dev; ta.list = list; ta.n_list = q + 12; ta.list_w = list_w; ta.n_list_w = q + 13;
     int32_t *list_x = ctx->ws<int32_t>(WS_LIST_X, K);
-    ta.list_x = list_x; ta.n_list_x = q + 19; ta.xw_max = q + 20;
-    ta.states8 = (vmax - vmin + 2) <= 256 ? 1 : 0;
+    ta.list_x = list_x; ta.n_list_x = q + 19; ta.xw_max = (unsigned long long *)(q + 26);
+    ta.states8 = n_states <= 256 ? 1 : 0;
     k_key_tables<<<(unsigned)std::min<int64_t>((K + 3) / 4, 8192), 256, 0, st>>>(ta);
 
     int32_t *list1 = list;
@@ -3546,7 +3656,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     a.memo = memo; a.memo_cap = memo_cap1; a.stack = stack; a.stack_cap = stack_cap;
     a.scratch = scr; a.scratch_bytes = scr_bytes; a.budget = quick; a.defer = quick < budget ? 1 : 0;
     a.init_state = init_state; a.gen_base = ctx->gen_base; a.flags = q + 2; a.probes = probes;
-    a.states8 = (vmax - vmin + 2) <= 256 ? 1 : 0;
+    a.states8 = n_states <= 256 ? 1 : 0;
     const char *dbgenv = getenv("JH_DEBUG");
     const bool dbg2 = dbgenv && atoi(dbgenv) >= 2;
     unsigned long long *dbg = nullptr;
@@ -3603,7 +3713,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         uint32_t capx = 1u << 12;
         while ((int64_t)capx < 2 * budget && capx < (1u << 30)) capx <<= 1;
         const int waves_x = std::min(n_x, getenv("JH_XW_WAVES") ? std::max(1, atoi(getenv("JH_XW_WAVES"))) : 128);
-        const uint64_t scr_x = ((uint64_t)qh[20] + 255) & ~255ULL;
+        const uint64_t scr_x = (((uint64_t)(uint32_t)qh[26] | ((uint64_t)(uint32_t)qh[27] << 32)) + 255) & ~255ULL;
         const bool freshx = ctx->ws_fresh(WS_MEMO_X) || ctx->bufs[WS_MEMO_X].bytes < (size_t)waves_x * capx * XW_EW * 8;
         uint64_t *memox = ctx->ws<uint64_t>(WS_MEMO_X, (size_t)waves_x * capx * XW_EW, /*zero=*/true);
         if (clear_memo && !freshx) HIP_TRY(hipMemsetAsync(memox, 0, ctx->bufs[WS_MEMO_X].bytes, st));
@@ -3749,7 +3859,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         c.gset = bset; c.gset_cap = set_cap; c.pend = bq; c.front = bq + (size_t)wg2 * 2 * q_cap;
         c.q_cap = q_cap;
         c.scratch = bscr; c.scratch_bytes = scr_bytes_bfs; c.budget = budget;
-        c.init_state = init_state; c.states_ok = (vmax - vmin + 2) < 4096 ? 1 : 0;
+        c.init_state = init_state; c.states_ok = n_states < 4096 ? 1 : 0;
         c.dbg = dbg; c.claim = claim;
         // By default the BFS settles invalid keys only (their WGL cache is the
         // whole reachable set, an exact count); every valid key is settled by
@@ -3885,7 +3995,6 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipEventRecord(ctx->ev[3], st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (qh[2] & 1) throw_jh(JH_EUNSUPPORTED, "a key with more than 65535 ops or 2^20 ok returns");
     if (qh[2] & 2) throw_jh(JH_EDEVICE, "per-key table exceeded the scratch reservation");
     if (qh[2] & 4) throw_jh(JH_EDEVICE, "DFS stack overflow");
     if ((qh[2] & 0x1F0) && acc_stats && ctx->bufs.size() > WS_DEBUG && ctx->bufs[WS_DEBUG].p && n_wg > 0 &&

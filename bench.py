@@ -203,7 +203,7 @@ def main():
             hv = np.frombuffer(verd.cpu().numpy().tobytes(), dtype=A.VERDICT_DTYPE)
             ov, os_ = oracle.check_cas_independent(cols, threads=min(16, len(os.sched_getaffinity(0))))
             # verdict, cause, failing row and WGL's cache size of every key
-            parity = bool(all((hv[f] == ov[f]).all() for f in ("valid", "cause", "fail_entry", "explored")))
+            parity = bool(all((hv[f] == ov[f]).all() for f in A.VERDICT_FIELDS))
         cpu = cpu_faithful = None
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(cols, args.cpu_sample_keys or wl["cpu_keys_opt"], args.workload.upper(), mode=0)

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define JH_ABI_VERSION 2
+#define JH_ABI_VERSION 3
 
 /* Return codes. Anything non-zero also writes a NUL-terminated message into
  * the caller's err buffer; the JNA shim throws ex-info and check-safe turns
@@ -127,6 +127,15 @@ typedef struct jh_key_verdict {
                                   first op no linearization can get past; else -1 */
     int64_t explored;          /* memo inserts (WGL cache size) for this key, the same
                                   on every run; -1 for a key in no tuple */
+    /* invalid keys, from the search frontier (knossos' :previous-ok / :last-op;
+     * knossos is not vendored, so these definitions are this library's):
+     * last_op     = history row of the :ok completion of the last op the
+     *               furthest configuration got past (RET[tmax-1]), -1 if none;
+     * previous_ok = history row of the last client :ok in the key's
+     *               subhistory before fail_entry, -1 if none.
+     * Both -1 for keys that are not invalid. */
+    int64_t previous_ok;
+    int64_t last_op;
 } jh_key_verdict;
 
 typedef struct jh_summary {

@@ -6,7 +6,7 @@ every struct layout.
 """
 import ctypes as C
 
-JH_ABI_VERSION = 2
+JH_ABI_VERSION = 3
 
 JH_OK, JH_EINVAL, JH_EUNSUPPORTED, JH_EDEVICE, JH_ENOMEM = 0, 1, 2, 3, 4
 TYPE_INVOKE, TYPE_OK, TYPE_FAIL, TYPE_INFO = 0, 1, 2, 3
@@ -56,9 +56,14 @@ class JhLinOpts(C.Structure):
     _fields_ = [("init_value", C.c_int64), ("budget", C.c_int64), ("stream", C.c_int64)]
 
 
+# every field of jh_key_verdict: the parity tests compare all of them
+VERDICT_FIELDS = ("valid", "cause", "fail_entry", "explored", "previous_ok", "last_op")
+
+
 class JhKeyVerdict(C.Structure):
     _fields_ = [("valid", C.c_int32), ("cause", C.c_int32),
-                ("fail_entry", C.c_int64), ("explored", C.c_int64)]
+                ("fail_entry", C.c_int64), ("explored", C.c_int64),
+                ("previous_ok", C.c_int64), ("last_op", C.c_int64)]
 
 
 class JhSummary(C.Structure):
@@ -115,7 +120,8 @@ class JhQueueResult(C.Structure):
 try:
     import numpy as _np
     VERDICT_DTYPE = _np.dtype([("valid", _np.int32), ("cause", _np.int32),
-                               ("fail_entry", _np.int64), ("explored", _np.int64)])
+                               ("fail_entry", _np.int64), ("explored", _np.int64),
+                               ("previous_ok", _np.int64), ("last_op", _np.int64)])
 except Exception:  # pragma: no cover
     VERDICT_DTYPE = None
 

@@ -172,6 +172,16 @@ class Context:
         _raise(rc, err)
         return v.valid, v.cause, v.fail_entry, v.explored
 
+    def check_cas_full(self, cols, init=None, budget=None):
+        """jh_check_cas -> {valid, cause, fail_entry, explored, previous_ok, last_op}."""
+        h = A.make_history(cols)
+        v = A.JhKeyVerdict()
+        err = C.create_string_buffer(1024)
+        rc = lib().jh_check_cas(self._h, C.byref(h), C.byref(_opts(init, budget)), C.byref(v),
+                                err, len(err))
+        _raise(rc, err)
+        return {f: getattr(v, f) for f, _ in A.JhKeyVerdict._fields_}
+
     # -- counter / set -----------------------------------------------------
     def check_counter(self, cols, reads_cap=None, on_device=False):
         """on_device: cols' columns are device pointers (the history already in HBM)."""

@@ -157,8 +157,12 @@ CAUSE_ERRORS = {
 }
 
 
-def lin_result(valid, cause, fail_entry, explored, cols=None):
-    """Per-history result map of checker/linearizable (checker.clj:139-158)."""
+def lin_result(valid, cause, fail_entry, explored, cols=None, previous_ok=-1, last_op=-1):
+    """Per-history result map of checker/linearizable (checker.clj:139-158).
+    An invalid result carries :op (the ok completion no configuration gets
+    past) and, from the search frontier, :previous-ok and :last-op
+    (include/jh.h; knossos is not vendored, so their exact knossos
+    definitions are parity unpinned)."""
     c = A.CAUSES.get(int(cause))
     if valid == A.VALID:
         return {"valid?": True, "analyzer": "wgl", "explored": int(explored)}
@@ -167,6 +171,9 @@ def lin_result(valid, cause, fail_entry, explored, cols=None):
              "fail-entry": int(fail_entry)}
         if cols is not None and 0 <= fail_entry < cols.n:
             r["op"] = H.decode_op(cols, int(fail_entry))
+        if cols is not None:
+            r["previous-ok"] = H.decode_op(cols, int(previous_ok)) if 0 <= previous_ok < cols.n else None
+            r["last-op"] = H.decode_op(cols, int(last_op)) if 0 <= last_op < cols.n else None
         return r
     if c == "budget":
         return {"valid?": UNKNOWN, "analyzer": "wgl", "cause": "budget", "explored": int(explored)}
@@ -194,8 +201,9 @@ class Linearizable(Checker):
         if not isinstance(history, H.Columns):
             history = to_device_ops(self.model, list(history))
         cols = _cols(history, keyed=False)
-        v, c, fe, ex = _ctx().check_cas(cols, init=_init_state(self.model, cols), budget=self.budget)
-        return lin_result(v, c, fe, ex, cols)
+        r = _ctx().check_cas_full(cols, init=_init_state(self.model, cols), budget=self.budget)
+        return lin_result(r["valid"], r["cause"], r["fail_entry"], r["explored"], cols,
+                          r["previous_ok"], r["last_op"])
 
 
 def linearizable(opts):

@@ -3361,6 +3361,41 @@ __global__ void __launch_bounds__(256) k_fail_rows(KeySrc S, jh_key_verdict *out
     }
 }
 
+// The search frontier of every invalid key (include/jh.h): the failing row is
+// the ok completion of RET[t]; last_op = that of RET[t-1], previous_ok = the
+// last client :ok row before it in the key's segment. -1 for other keys.
+__global__ void __launch_bounds__(256) k_frontier(KeySrc S, jh_key_verdict *out, int64_t K) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t key = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); key < K; key += nw) {
+        const jh_key_verdict v = out[key];
+        long long prev = -1, last = -1;
+        if (v.valid == JH_INVALID && v.fail_entry >= 0) {
+            const uint32_t s0 = S.off[key], s1 = S.off[key + 1];
+            int want = 0;     // rank code of RET[t] = -(t + 2); 0 = not found yet
+            for (uint32_t base = s0; base < s1; base += 64) {
+                const uint32_t p = base + lane;
+                const bool in = p < s1;
+                const long long row = in ? (long long)S.rows[p] : -1;
+                const Rec x = in ? S.rec[p] : Rec{-1, 0, 0, 0, 0, 0};
+                if (in && row == v.fail_entry) want = S.rank[p];
+                if (in && row < v.fail_entry && x.proc >= 0 && x.type == T_OK) prev = max(prev, row);
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                prev = max(prev, (long long)__shfl_xor(prev, o));
+                want = min(want, __shfl_xor(want, o));
+            }
+            const int t = -want - 2;
+            if (want <= -3) {   // t >= 1
+                KeyInfo Ki;
+                Ki.s0 = s0; Ki.s1 = s1;
+                last = ret_row(S, Ki, (uint32_t)(t - 1), lane);
+            }
+        }
+        if (lane == 0) { out[key].previous_ok = prev; out[key].last_op = last; }
+    }
+}
+
 __global__ void k_summary(const jh_key_verdict *__restrict__ v, int64_t K, long long *sum) {
     // sum: [0] valid max [1] n_invalid [2] n_unknown [3] first_fail [4] n_keys [5] explored
     long long vmax = 0, ninv = 0, nunk = 0, ff = LLONG_MAX, nk = 0, ex = 0;
@@ -3985,6 +4020,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     ctx->gen_base += gen_span;
 
     k_fail_rows<<<(unsigned)std::min<int64_t>((K + 3) / 4, 4096), 256, 0, st>>>(
+        KeySrc{rec, pair, off, rB, viol, rank, q + 2}, out_dev, K);
+    k_frontier<<<(unsigned)std::min<int64_t>((K + 3) / 4, 4096), 256, 0, st>>>(
         KeySrc{rec, pair, off, rB, viol, rank, q + 2}, out_dev, K);
     long long *sd = ctx->ws<long long>(WS_SUMMARY, 8);
     long long s_init[8] = {0, 0, 0, LLONG_MAX, 0, 0, 0, 0};

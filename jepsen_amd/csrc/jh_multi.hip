@@ -268,6 +268,8 @@ int multi_check_cas_independent(jh_ctx *g, const jh_history *h, const jh_lin_opt
         for (size_t j = 0; j < S.keys.size(); ++j) {
             jh_key_verdict x = v[d][j];
             if (x.fail_entry >= 0) x.fail_entry = S.row[x.fail_entry];
+            if (x.previous_ok >= 0) x.previous_ok = S.row[x.previous_ok];
+            if (x.last_op >= 0) x.last_op = S.row[x.last_op];
             out[S.keys[j]] = x;
         }
         const jh_summary &a = s[d];

@@ -129,7 +129,8 @@ class IndependentChecker(Checker):
                     if int(v["explored"]) == -1:      # a key in no tuple: no :results entry
                         continue
                     lin_res[key] = lin_result(int(v["valid"]), int(v["cause"]), int(v["fail_entry"]),
-                                              int(v["explored"]), cols)
+                                              int(v["explored"]), cols, int(v["previous_ok"]),
+                                              int(v["last_op"]))
                 if name is None:
                     return self._results_map(lin_res)
                 results = {}

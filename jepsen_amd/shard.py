@@ -90,7 +90,8 @@ def check_cas_independent_sharded(cols, rank, world, check_fn, device=None, init
     sub, mine, rows = shard_history(cols, owner, rank)
     v, s = check_fn(sub, init, budget)
     v = v.copy()
-    inv = v["fail_entry"] >= 0
-    v["fail_entry"][inv] = rows[v["fail_entry"][inv]]
+    for f in ("fail_entry", "previous_ok", "last_op"):   # local rows -> global rows
+        hit = v[f] >= 0
+        v[f][hit] = rows[v[f][hit]]
     mx, sm = summary_vector(s, rows)
     return mine, v, all_reduce_summary(mx, sm, device)

@@ -522,6 +522,21 @@ static void check_one(const jh_history *h, const int64_t *sel, int64_t m,
         out->valid = orc_wgl_canonical(&k, init, budget, &out->explored, &out->fail_entry);
         out->cause = out->valid == JH_UNKNOWN ? JH_CAUSE_BUDGET : JH_CAUSE_NONE;
     }
+    /* the search frontier of an invalid key (include/jh.h): last_op = the ok
+     * completion of RET[tmax-1], previous_ok = the last client :ok before
+     * the failing row in the key's subhistory */
+    out->previous_ok = -1; out->last_op = -1;
+    if (out->valid == JH_INVALID && out->fail_entry >= 0) {
+        for (int t = 0; t < k.n_ok; t++)
+            if (k.ops[k.ret_op[t]].ret == out->fail_entry) {
+                if (t > 0) out->last_op = k.ops[k.ret_op[t - 1]].ret;
+                break;
+            }
+        for (int64_t i = 0; i < m; i++) {
+            const int64_t r = sel[i];
+            if (r < out->fail_entry && h->process[r] >= 0 && h->type[r] == JH_TYPE_OK) out->previous_ok = r;
+        }
+    }
     orc_key_free(&k);
 }
 
@@ -571,7 +586,11 @@ static void *indep_worker(void *arg) {
                 else sel[m++] = J->unkeyed[iu++];
             }
         }
-        if (!present) { o->valid = JH_VALID; o->cause = 0; o->fail_entry = -1; o->explored = -1; continue; }
+        if (!present) {
+            o->valid = JH_VALID; o->cause = 0; o->fail_entry = -1; o->explored = -1;
+            o->previous_ok = -1; o->last_op = -1;
+            continue;
+        }
         check_one(h, sel, m, J->init, J->budget, (J->mode >> 1) & 1, o);
     }
     free(sel);

@@ -55,6 +55,13 @@ def check_cas(cols, init=A.NIL, budget=A.DEFAULT_BUDGET):
     return v.valid, v.cause, v.fail_entry, v.explored
 
 
+def check_cas_full(cols, init=A.NIL, budget=A.DEFAULT_BUDGET):
+    h = cols.as_jh()
+    v = A.JhKeyVerdict()
+    lib().orc_check_cas(C.byref(h), init, budget, C.byref(v))
+    return {f: getattr(v, f) for f, _ in A.JhKeyVerdict._fields_}
+
+
 def check_cas_independent(cols, init=A.NIL, budget=A.DEFAULT_BUDGET, mode=0, threads=1):
     """Returns (verdicts structured array [n_keys], summary)."""
     h = cols.as_jh()

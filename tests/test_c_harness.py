@@ -106,7 +106,7 @@ def _check_vs_oracle(tmp_path, cols, devs=None):
     out = _run(*args)
     got = np.fromfile(tmp_path / "v.bin", dtype=A.VERDICT_DTYPE)
     ov, os_ = oracle.check_cas_independent(cols, threads=8)
-    for f in ("valid", "cause", "fail_entry", "explored"):
+    for f in A.VERDICT_FIELDS:
         assert (got[f] == ov[f]).all(), f
     summ = dict(kv.split("=") for kv in out.split("\n")[1].split())
     ff = ov["fail_entry"][ov["valid"] == A.INVALID]

@@ -28,7 +28,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _same(gpu, cpu):
-    for f in ("valid", "cause", "fail_entry", "explored"):
+    for f in A.VERDICT_FIELDS:
         bad = np.nonzero(gpu[f] != cpu[f])[0]
         assert len(bad) == 0, (f, bad[:10], gpu[bad[:5]], cpu[bad[:5]])
 

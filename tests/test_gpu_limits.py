@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _same(v, ov):
-    for f in ("valid", "cause", "fail_entry", "explored"):
+    for f in A.VERDICT_FIELDS:
         assert (v[f] == ov[f]).all(), (f, np.nonzero(v[f] != ov[f])[0][:10])
 
 

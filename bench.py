@@ -49,8 +49,10 @@ WORKLOADS = {
                seed=3, cpu_keys=10000, cpu_keys_opt=10000,
                gen=dict(threads_per_key=10, readers=5, n_values=5, process_limit=20, groups=10,
                         init_nil=True, p_info=0.02, p_invalid=0.01, nemesis_every=10000)),
-    "c4": dict(desc="C4: independent cas-register, 1M keys over 8 GPUs: a 125000-key shard "
-                    "(~125M entries) per GPU", keys=125000, seed=4, cpu_keys=3000, cpu_keys_opt=125000,
+    "c4": dict(desc="C4: independent cas-register, ONE history of 125000 x N keys (1M at N=8) generated "
+                    "identically on every rank and split by key over the N GPUs with the window-sum cost "
+                    "model + LPT (jepsen_amd/shard.py); each GPU checks its shard", keys=125000, seed=4,
+               cpu_keys=3000, cpu_keys_opt=125000, global_history=True,
                gen=dict(threads_per_key=10, readers=5, n_values=5, process_limit=20, groups=10,
                         init_nil=True, p_info=0.02, p_invalid=0.01, nemesis_every=10000)),
     "c5": dict(desc="C5: independent cas-register, 1000 keys x ~1k entries, 50 threads per key, "
@@ -100,8 +102,28 @@ def main():
     # ---- workload: this rank's shard of the C3 configuration -------------
     wl = WORKLOADS[args.workload]
     n_keys = args.keys or wl["keys"]
-    seed = wl["seed"] + 7919 * (rank if args.seed_rank is None else args.seed_rank)
-    cols, truth = synth.cas_register(n_keys=n_keys, ops_per_key=args.ops_per_key, seed=seed, **wl["gen"])
+    shard_info = None
+    if wl.get("global_history"):
+        # C4: one global history (every rank generates the same one, 16 host
+        # threads), weighed by jh_key_costs, dealt out by LPT; this rank keeps
+        # its keys' rows plus the un-keyed rows (shard.shard_history)
+        from jepsen_amd import shard
+        t_g = time.perf_counter()
+        gcols, _ = synth.cas_register(n_keys=n_keys * world, ops_per_key=args.ops_per_key, seed=wl["seed"],
+                                      parts=16, **wl["gen"])
+        t_s = time.perf_counter()
+        costs = shard.key_costs(gcols)
+        owner = shard.assign_keys(costs, world)
+        cols, mine, _rows = shard.shard_history(gcols, owner, rank)
+        loads = np.bincount(owner, weights=costs, minlength=world)
+        shard_info = {"global_keys": int(gcols.n_keys), "global_entries": int(gcols.n),
+                      "generate_s": t_s - t_g, "cost_and_split_s": time.perf_counter() - t_s,
+                      "cost_model": "entries + window sum (jh_key_costs), LPT",
+                      "max_over_mean_load": float(loads.max() / max(loads.mean(), 1.0))}
+        del gcols, _rows
+    else:
+        seed = wl["seed"] + 7919 * (rank if args.seed_rank is None else args.seed_rank)
+        cols, truth = synth.cas_register(n_keys=n_keys, ops_per_key=args.ops_per_key, seed=seed, **wl["gen"])
     n_entries = int(cols.n)
     names = ["process", "type", "f", "key", "value", "value2"]
     dcols = {k: torch.from_numpy(getattr(cols, k)).to(dev) for k in names}
@@ -231,6 +253,7 @@ def main():
                        "deferred_keys": int(s.n_deferred), "deferred_entries": int(s.deferred_entries),
                        "phase1_ms": dfs_avg * 1e3, "phase2_seq_ms": seq_avg * 1e3,
                        "phase2_bfs_ms": float(np.mean(bfs_ms))},
+            "shard": shard_info,
             "value_kind": "history resident in HBM, verdicts left in HBM (kernel pipeline only); "
                           "host-to-host rate in e2e_host_buffers",
             "e2e_host_buffers": e2e,

@@ -32,7 +32,8 @@ def _worker(rank, world, port, q):
             return oracle.check_cas_independent(sub)
 
         mine, v, g = shard.check_cas_independent_sharded(cols, rank, world, check_fn)
-        q.put((rank, mine.tolist(), v.tolist(), g))
+        load = int(shard.key_costs(cols)[mine].sum())      # this rank's share of the window-sum cost
+        q.put((rank, mine.tolist(), v.tolist(), g, load))
     finally:
         dist.destroy_process_group()
 
@@ -54,7 +55,11 @@ def test_sharded_equals_single(built, world):
     cols, _ = synth.cas_register(n_keys=240, ops_per_key=80, p_invalid=0.1, seed=9)
     full, s = oracle.check_cas_independent(cols)
     seen = set()
-    for rank, mine, v, g in res:
+    costs = shard.key_costs(cols)
+    loads = [r[4] for r in res]
+    # LPT on the window-sum estimate: the ranks' loads differ by at most one key's cost
+    assert sum(loads) == int(costs.sum()) and max(loads) - min(loads) <= int(costs.max())
+    for rank, mine, v, g, _ in res:
         v = np.array([tuple(x) for x in v], dtype=A.VERDICT_DTYPE)
         for i, k in enumerate(mine):
             assert tuple(v[i]) == tuple(full[k]), (rank, k)

@@ -28,7 +28,7 @@
 namespace {
 
 constexpr int T_INVOKE = 0, T_OK = 1, T_FAIL = 2, T_INFO = 3;
-constexpr int CHUNK = 4096, HSLOTS = 2048;
+constexpr int CHUNK = 2048, HSLOTS = 1024;
 
 struct CntMeta {
     long long pmin, pmax;          // process range
@@ -62,45 +62,85 @@ __global__ void __launch_bounds__(256) k_cnt_prange(const int64_t *__restrict__ 
 
 // packed row codes + last row of every process (per-chunk LDS hash of
 // (process -> max row), then one global atomicMax per distinct process) +
-// the add-value range for the overflow check
+// the add-value range for the overflow check, and the complete pairing of
+// every invocation whose completion lies in the same chunk.
+//
+// Pairing (util.clj:606-640: an invocation's completion is the next
+// non-:info row of its process): the chunk's first PAIR_PROCS distinct
+// processes get a compact index c, and each 64-row group g of the chunk a
+// bit mask M[g][c] of its non-:info rows of process c (one LDS atomicOr per
+// row). An invocation's completion is then the lowest set bit after its own
+// lane in M[g][c], or in the next group with a non-zero M[g'][c]: O(1) LDS
+// reads per row. Invocations with no completion in the chunk, or of a
+// process beyond the first PAIR_PROCS, go to a spill list (k_cnt_pair_spill).
+constexpr int PAIR_PROCS = 32, PAIR_GROUPS = CHUNK / 64;
 __global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ proc,
                                                   const int64_t *__restrict__ type,
                                                   const int64_t *__restrict__ f,
                                                   const int64_t *__restrict__ val, int64_t n,
                                                   long long pmin, int32_t *__restrict__ last,
-                                                  uint32_t *__restrict__ code, CntMeta *m) {
-    __shared__ long long hk[HSLOTS];
-    __shared__ int hv[HSLOTS];
+                                                  uint32_t *__restrict__ code, int32_t *__restrict__ pair,
+                                                  int32_t *__restrict__ spill, unsigned int *__restrict__ n_spill,
+                                                  CntMeta *m) {
+    __shared__ uint32_t hk[HSLOTS];                 // process - pmin + 1 (0: empty)
+    __shared__ int hv[HSLOTS];                      // its last row
+    __shared__ int8_t hc[HSLOTS];                   // its compact index, -1 beyond PAIR_PROCS
+    __shared__ uint32_t sc[CHUNK];                  // the chunk's row codes
+    __shared__ int8_t rc[CHUNK];                    // each row's compact process index (-1: none)
+    __shared__ unsigned long long M[PAIR_GROUPS][PAIR_PROCS];
+    __shared__ int nd, nls, gbase;
+    __shared__ int32_t ls[CHUNK];                   // this chunk's spilled invocations
     __shared__ long long sh[4];
     const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
-    for (int i = threadIdx.x; i < HSLOTS; i += blockDim.x) { hk[i] = LLONG_MIN; hv[i] = -1; }
+    const int nc = (int)min<int64_t>(CHUNK, n - c0);
+    for (int i = threadIdx.x; i < HSLOTS; i += blockDim.x) { hk[i] = 0; hv[i] = -1; hc[i] = -1; }
+    for (int i = threadIdx.x; i < PAIR_GROUPS * PAIR_PROCS; i += blockDim.x) (&M[0][0])[i] = 0;
+    if (threadIdx.x == 0) { nd = 0; nls = 0; }
     __syncthreads();
     long long am = 0, na = 0;
-    for (int i = threadIdx.x; i < CHUNK; i += blockDim.x) {
+    // all of this thread's rows in flight at once (the loop below waits on LDS)
+    constexpr int PER = CHUNK / 256;
+    long long rp[PER], rt[PER], rf[PER], rv[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int i = k * 256 + threadIdx.x;
+        if (i < nc) { rp[k] = proc[c0 + i]; rt[k] = type[c0 + i]; rf[k] = f[c0 + i]; rv[k] = val[c0 + i]; }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int i = k * 256 + threadIdx.x;
+        if (i >= nc) break;
         const int64_t r = c0 + i;
-        if (r >= n) break;
-        const long long p = proc[r];
-        const int64_t ty = type[r] & 3, ff = f[r];
+        const long long p = rp[k];
+        const int64_t ty = rt[k] & 3, ff = rf[k];
         const uint32_t f2 = ff == JH_F_ADD ? F2_ADD : ff == JH_F_READ ? F2_READ : F2_OTHER;
-        code[r] = ((uint32_t)(p - pmin) << 4) | (f2 << 2) | (uint32_t)ty;   // span < 2^28
+        const uint32_t pk = (uint32_t)(p - pmin);                                  // span < 2^28
+        const uint32_t x = (pk << 4) | (f2 << 2) | (uint32_t)ty;
+        code[r] = x;
+        sc[i] = x;
         if (f2 == F2_ADD && (ty == T_INVOKE || ty == T_OK)) {
-            const long long v = val[r];
+            const long long v = rv[k];
             if (v != JH_NIL) am = max(am, v < 0 ? (v == LLONG_MIN ? LLONG_MAX : -v) : v);
             na++;
         }
         uint32_t h = (uint32_t)jh_mix64((uint64_t)p) & (HSLOTS - 1);
-        bool done = false;
-        for (int probe = 0; probe < 64 && !done; probe++) {
-            long long cur = hk[h];
-            if (cur == LLONG_MIN) {
-                cur = (long long)atomicCAS((unsigned long long *)&hk[h], (unsigned long long)LLONG_MIN,
-                                           (unsigned long long)p);
-                if (cur == LLONG_MIN) cur = p;
+        int slot = -1;
+        for (int probe = 0; probe < 64; probe++) {
+            uint32_t cur = hk[h];
+            if (cur == 0) {
+                cur = atomicCAS(&hk[h], 0u, pk + 1);
+                if (cur == 0) {
+                    const int c = atomicAdd(&nd, 1);
+                    hc[h] = (int8_t)(c < PAIR_PROCS ? c : -1);
+                    cur = pk + 1;
+                }
             }
-            if (cur == p) { atomicMax(&hv[h], (int)r); done = true; }
-            else h = (h + 1) & (HSLOTS - 1);
+            if (cur == pk + 1) { slot = (int)h; break; }
+            h = (h + 1) & (HSLOTS - 1);
         }
-        if (!done) atomicMax(&last[p - pmin], (int)r);
+        if (slot >= 0) atomicMax(&hv[slot], (int)r);
+        else atomicMax(&last[pk], (int)r);
+        rc[i] = slot >= 0 ? (int8_t)-2 : (int8_t)-1;   // -2: in the hash; its index is read below
     }
     am = block_reduce256(am, RedMax(), sh);
     na = block_reduce256(na, RedSum(), sh);
@@ -110,7 +150,70 @@ __global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ pr
     }
     __syncthreads();
     for (int i = threadIdx.x; i < HSLOTS; i += blockDim.x)
-        if (hk[i] != LLONG_MIN) atomicMax(&last[hk[i] - pmin], hv[i]);
+        if (hk[i]) atomicMax(&last[hk[i] - 1], hv[i]);
+    // compact process index of every row (the hash is complete now), and the
+    // group masks of non-:info rows
+    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+        int c = -1;
+        if (rc[i] == -2) {
+            const uint32_t pk = sc[i] >> 4;
+            uint32_t h = (uint32_t)jh_mix64((uint64_t)((long long)pk + pmin)) & (HSLOTS - 1);
+            while (hk[h] != pk + 1) h = (h + 1) & (HSLOTS - 1);
+            c = hc[h];
+        }
+        rc[i] = (int8_t)c;
+        if (c >= 0 && (sc[i] & 3) != T_INFO) atomicOr(&M[i >> 6][c], 1ULL << (i & 63));
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+        const uint32_t x = sc[i];
+        if ((x & 3) != T_INVOKE) continue;
+        const int64_t r = c0 + i;
+        const int c = rc[i];
+        int got = -1;
+        if (c >= 0) {
+            const int g = i >> 6, l = i & 63;
+            const unsigned long long after = l == 63 ? 0ULL : (M[g][c] & (~0ULL << (l + 1)));
+            if (after) got = (g << 6) + __builtin_ctzll(after);
+            else
+                for (int g2 = g + 1; g2 < PAIR_GROUPS && (g2 << 6) < nc; g2++)
+                    if (M[g2][c]) { got = (g2 << 6) + __builtin_ctzll(M[g2][c]); break; }
+        }
+        if (got < 0) {
+            ls[atomicAdd(&nls, 1)] = (int32_t)r;       // spills gather in LDS: one global atomic per chunk
+        } else if ((sc[got] & 3) == T_INVOKE) {
+            atomicMin(&m->viol1, ((unsigned long long)(c0 + got) << 4) | JH_CAUSE_DOUBLE_INVOKE);
+        } else {
+            pair[r] = (int32_t)(c0 + got);
+            pair[c0 + got] = (int32_t)r;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && nls) gbase = (int)atomicAdd(n_spill, (unsigned int)nls);
+    __syncthreads();
+    for (int k = threadIdx.x; k < nls; k += blockDim.x) spill[gbase + k] = ls[k];
+}
+
+// the spilled invocations: one thread each walks the codes forward to the
+// completion, or past its process' last row (no completion: stays open)
+__global__ void __launch_bounds__(256) k_cnt_pair_spill(const uint32_t *__restrict__ code, int64_t n,
+                                                        const int32_t *__restrict__ last,
+                                                        const int32_t *__restrict__ spill,
+                                                        const unsigned int *__restrict__ n_spill,
+                                                        int32_t *__restrict__ pair, CntMeta *m) {
+    const unsigned int ns = *n_spill;
+    for (unsigned int s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
+        const int64_t r = spill[s];
+        const uint32_t p = code[r] >> 4;
+        const int64_t lr = last[p];
+        for (int64_t j = r + 1; j <= lr; j++) {
+            const uint32_t y = code[j];
+            if ((y >> 4) != p || (y & 3) == T_INFO) continue;
+            if ((y & 3) == T_INVOKE) atomicMin(&m->viol1, ((unsigned long long)j << 4) | JH_CAUSE_DOUBLE_INVOKE);
+            else { pair[r] = (int32_t)j; pair[j] = (int32_t)r; }
+            break;
+        }
+    }
 }
 
 // per-row contributions and prefixes of lower / upper / ok reads; flags mark
@@ -279,58 +382,6 @@ __global__ void k_cnt_triples(const int32_t *__restrict__ rd_row, const int64_t 
 
 
 
-// complete pairing: an invocation's completion is the next non-:info row of
-// its process (util.clj:606-640). One wave per 64 consecutive rows: it reads
-// the packed (process, type) words 64 rows at a time and, for each distinct
-// process among its still-open invocations, one ballot over the window gives
-// every candidate row; each open lane takes the first one after its own row.
-// A lane gives up after its process' last row (no completion: stays open).
-__global__ void __launch_bounds__(256) k_cnt_pair(const uint32_t *__restrict__ pt, int64_t n,
-                                                  const int32_t *__restrict__ last,
-                                                  int32_t *__restrict__ pair, CntMeta *m) {
-    const int lane = threadIdx.x & 63;
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    for (int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); wv * 64 < n; wv += nw) {
-        const int64_t base = wv * 64, r = base + lane;
-        const uint32_t x = r < n ? pt[r] : 3u;
-        const uint32_t p = x >> 4;
-        const bool inv = r < n && (x & 3) == T_INVOKE;
-        const int64_t lr = inv ? (int64_t)last[p] : -1;
-        bool open = inv && lr > r;
-        int64_t got = -1;
-        for (int64_t wb = base; wb < n; wb += 64) {
-            if (!__ballot(open)) break;
-            const int64_t j = wb + lane;
-            const uint32_t y = j < n ? pt[j] : 3u;
-            uint64_t todo = __ballot(open);
-            while (todo) {
-                const int l = __builtin_ctzll(todo);
-                const uint32_t pl = (uint32_t)__builtin_amdgcn_readlane((int)p, l);
-                const uint64_t mine = __ballot(open && p == pl);
-                const uint64_t cand = __ballot((y >> 4) == pl && (y & 3) != T_INFO);
-                todo &= ~mine;
-                if ((mine >> lane) & 1) {
-                    // candidates strictly after this lane's row
-                    const int64_t rel = r - wb;          // in [-63.., 63]
-                    const uint64_t after = rel < 0 ? ~0ULL : (rel >= 63 ? 0ULL : (~0ULL << (rel + 1)));
-                    const uint64_t c = cand & after;
-                    if (c) { got = wb + __builtin_ctzll(c); open = false; }
-                }
-            }
-            // past the process' last row: no completion
-            if (open && wb + 63 >= lr) open = false;
-        }
-        if (got >= 0) {
-            if ((pt[got] & 3) == T_INVOKE)
-                atomicMin(&m->viol1, ((unsigned long long)got << 4) | JH_CAUSE_DOUBLE_INVOKE);
-            else { pair[r] = (int32_t)got; pair[got] = (int32_t)r; }
-        }
-    }
-}
-
-
-
-
 }  // namespace
 
 void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_t reads_cap,
@@ -355,10 +406,13 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
     uint32_t *code = ctx->ws<uint32_t>(WS_C_PT, n);
     HIP_TRY(hipMemsetAsync(last, 0xFF, sizeof(int32_t) * (span + 1), st));
     HIP_TRY(hipMemsetAsync(pair, 0xFF, sizeof(int32_t) * n, st));
+    int32_t *spill = ctx->ws<int32_t>(WS_C_IDX, n);          // reused for the read rows below
+    unsigned int *n_spill = (unsigned int *)ctx->ws<int32_t>(WS_C_FLAG, 4);
+    HIP_TRY(hipMemsetAsync(n_spill, 0, sizeof(unsigned int), st));
     k_cnt_pack<<<(int)((n + CHUNK - 1) / CHUNK), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
-                                                              mh.pmin, last, code, m);
+                                                              mh.pmin, last, code, pair, spill, n_spill, m);
+    k_cnt_pair_spill<<<grid_for(n / 64 + 1, 256, 4096), 256, 0, st>>>(code, n, last, spill, n_spill, pair, m);
     HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
-    k_cnt_pair<<<grid_for((n + 63) / 64, 4, 16384), 256, 0, st>>>(code, n, last, pair, m);
     HIP_TRY(hipStreamSynchronize(st));
     // Clojure + throws on long overflow; if no prefix can overflow we need no
     // ordered overflow check (else the shim falls back to the JVM checker).

@@ -71,87 +71,138 @@ __global__ void __launch_bounds__(256) k_set_range(const int64_t *__restrict__ a
     }
 }
 
-// Marking is privatised per workgroup: a chunk of MARK_CH rows (or read
-// elements) whose element range spans at most MARK_LW words is marked with
-// LDS atomics, then merged with one global atomicOr per non-zero word; a
-// chunk spanning more falls back to global atomics per element.
-constexpr int MARK_CH = 16384, MARK_LW = 8192;
+// Marking: each workgroup takes a contiguous chunk of MARK_CH rows (or read
+// elements) and merges its bits in LDS before touching HBM.
+//  * Within a wave, lanes holding the same bitmap word are merged by a
+//    segmented OR scan over lanes (shuffles); only the last lane of each run
+//    writes. Jepsen's set elements are mostly written and read in ascending
+//    order, so a wave's 64 elements fall into two or three words.
+//  * Those few writes go to a direct-mapped LDS cache of words (tag + bits);
+//    a word whose slot holds another word goes straight to HBM.
+//  * At the end the cache is flushed: one global atomicOr per cached word.
+// Any element order stays correct (unmerged lanes just write on their own).
+constexpr int MARK_CH = 16384, MARK_SLOTS = 2048;
+constexpr long long MARK_EMPTY = -1;
 
-__device__ __forceinline__ void block_minmax(long long &lo, long long &hi, long long *sh) {
-    for (int o = 32; o > 0; o >>= 1) { lo = min(lo, __shfl_xor(lo, o)); hi = max(hi, __shfl_xor(hi, o)); }
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { sh[2 * wv] = lo; sh[2 * wv + 1] = hi; }
-    __syncthreads();
-    lo = sh[0]; hi = sh[1];
-    for (int i = 1; i < (int)(blockDim.x >> 6); i++) { lo = min(lo, sh[2 * i]); hi = max(hi, sh[2 * i + 1]); }
-    __syncthreads();
+__device__ __forceinline__ void mark_bits(uint32_t *bm, long long *tag, uint32_t *lb, long long w, uint32_t bits) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long wn = __shfl_up(w, o);
+        const uint32_t bn = (uint32_t)__shfl_up((int)bits, o);
+        if (lane >= o && wn == w) bits |= bn;
+    }
+    const long long wnext = __shfl_down(w, 1);
+    const bool tail = lane == 63 || wnext != w;
+    if (w < 0 || !tail) return;
+    const int sl = (int)(w & (MARK_SLOTS - 1));
+    long long t = tag[sl];
+    if (t == MARK_EMPTY)
+        t = (long long)atomicCAS((unsigned long long *)&tag[sl], (unsigned long long)MARK_EMPTY, (unsigned long long)w);
+    if (t == MARK_EMPTY || t == w) atomicOr(&lb[sl], bits);
+    else atomicOr(&bm[w], bits);
 }
 
+__device__ __forceinline__ void mark_init(long long *tag, uint32_t *lb) {
+    for (int i = threadIdx.x; i < MARK_SLOTS; i += blockDim.x) { tag[i] = MARK_EMPTY; lb[i] = 0; }
+    __syncthreads();
+}
+__device__ __forceinline__ void mark_flush(uint32_t *bm, const long long *tag, const uint32_t *lb) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < MARK_SLOTS; i += blockDim.x)
+        if (tag[i] != MARK_EMPTY && lb[i]) atomicOr(&bm[tag[i]], lb[i]);
+}
+
+// one pass over the rows (24 B each): :invoke :add elements into A, :ok :add
+// elements into D
 __global__ void __launch_bounds__(256) k_set_mark_rows(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
                                                        const int64_t *__restrict__ val, int64_t n, long long vmin,
                                                        uint32_t *__restrict__ A, uint32_t *__restrict__ D) {
-    __shared__ uint32_t la[MARK_LW], ld[MARK_LW];
-    __shared__ long long sh[16];
+    __shared__ long long ta[MARK_SLOTS], td[MARK_SLOTS];
+    __shared__ uint32_t ba[MARK_SLOTS], bd[MARK_SLOTS];
+    mark_init(ta, ba);
+    mark_init(td, bd);
     const int64_t c0 = (int64_t)blockIdx.x * MARK_CH, c1 = min(n, c0 + MARK_CH);
-    long long lo = LLONG_MAX, hi = LLONG_MIN;
-    for (int64_t r = c0 + threadIdx.x; r < c1; r += blockDim.x) {
-        if (f[r] != JH_F_ADD) continue;
-        const int64_t ty = type[r];
-        if (ty != T_INVOKE && ty != T_OK) continue;
-        lo = min(lo, (long long)val[r]); hi = max(hi, (long long)val[r]);
-    }
-    block_minmax(lo, hi, sh);
-    if (lo > hi) return;
-    const int64_t w0 = (lo - vmin) >> 5, nwc = ((hi - vmin) >> 5) - w0 + 1;
-    const bool priv = nwc <= MARK_LW;
-    if (priv) {
-        for (int i = threadIdx.x; i < nwc; i += blockDim.x) { la[i] = 0; ld[i] = 0; }
-        __syncthreads();
-    }
-    for (int64_t r = c0 + threadIdx.x; r < c1; r += blockDim.x) {
-        if (f[r] != JH_F_ADD) continue;
-        const int64_t ty = type[r];
-        if (ty != T_INVOKE && ty != T_OK) continue;
-        const uint64_t b = (uint64_t)(val[r] - vmin);
-        if (priv) atomicOr(&(ty == T_INVOKE ? la : ld)[(b >> 5) - w0], 1u << (b & 31));
-        else atomicOr(&(ty == T_INVOKE ? A : D)[b >> 5], 1u << (b & 31));
-    }
-    if (priv) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < nwc; i += blockDim.x) {
-            if (la[i]) atomicOr(&A[w0 + i], la[i]);
-            if (ld[i]) atomicOr(&D[w0 + i], ld[i]);
+    for (int64_t base = c0; base < c1; base += blockDim.x) {      // same trip count for every lane
+        const int64_t r = base + threadIdx.x;
+        long long wa = -1, wd = -1;
+        uint32_t bit = 0;
+        if (r < c1 && f[r] == JH_F_ADD) {
+            const int64_t ty = type[r];
+            if (ty == T_INVOKE || ty == T_OK) {
+                const uint64_t b = (uint64_t)(val[r] - vmin);
+                bit = 1u << (b & 31);
+                if (ty == T_INVOKE) wa = (long long)(b >> 5); else wd = (long long)(b >> 5);
+            }
         }
+        mark_bits(A, ta, ba, wa, bit);
+        mark_bits(D, td, bd, wd, bit);
+    }
+    mark_flush(A, ta, ba);
+    mark_flush(D, td, bd);
+}
+
+// one pass over the final read's elements (8 B each) into R
+__global__ void __launch_bounds__(256) k_set_mark_read(const int64_t *__restrict__ aux, int64_t off, int64_t cnt,
+                                                       long long vmin, uint32_t *__restrict__ R) {
+    __shared__ long long tr[MARK_SLOTS];
+    __shared__ uint32_t br[MARK_SLOTS];
+    mark_init(tr, br);
+    const int64_t c0 = (int64_t)blockIdx.x * MARK_CH, c1 = min(cnt, c0 + MARK_CH);
+    for (int64_t base = c0; base < c1; base += blockDim.x) {
+        const int64_t i = base + threadIdx.x;
+        long long w = -1;
+        uint32_t bit = 0;
+        if (i < c1) {
+            const uint64_t b = (uint64_t)(aux[off + i] - vmin);
+            w = (long long)(b >> 5);
+            bit = 1u << (b & 31);
+        }
+        mark_bits(R, tr, br, w, bit);
+    }
+    mark_flush(R, tr, br);
+}
+
+// Byte-map marking (element spans up to BYTEMAP_MAX): every element sets
+// its own byte with a plain store -- idempotent, so no atomics and no
+// ordering -- and one streaming pass packs the bytes into the three bitmaps.
+// Final-read elements arrive in any order (hash order on the JVM), which
+// makes bit atomics on a 12 MB bitmap the bottleneck; byte stores are not.
+constexpr unsigned long long BYTEMAP_MAX = 1ULL << 32;
+
+__global__ void __launch_bounds__(256) k_set_bytes_rows(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
+                                                        const int64_t *__restrict__ val, int64_t n, long long vmin,
+                                                        uint8_t *__restrict__ Ab, uint8_t *__restrict__ Db) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        if (f[r] != JH_F_ADD) continue;
+        const int64_t ty = type[r];
+        if (ty == T_INVOKE) Ab[val[r] - vmin] = 1;
+        else if (ty == T_OK) Db[val[r] - vmin] = 1;
     }
 }
 
-__global__ void __launch_bounds__(256) k_set_mark_read(const int64_t *__restrict__ aux, int64_t off, int64_t cnt,
-                                                       long long vmin, uint32_t *__restrict__ R) {
-    __shared__ uint32_t lr[MARK_LW];
-    __shared__ long long sh[16];
-    const int64_t c0 = (int64_t)blockIdx.x * MARK_CH, c1 = min(cnt, c0 + MARK_CH);
-    long long lo = LLONG_MAX, hi = LLONG_MIN;
-    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
-        const long long v = aux[off + i];
-        lo = min(lo, v); hi = max(hi, v);
-    }
-    block_minmax(lo, hi, sh);
-    if (lo > hi) return;
-    const int64_t w0 = (lo - vmin) >> 5, nwc = ((hi - vmin) >> 5) - w0 + 1;
-    const bool priv = nwc <= MARK_LW;
-    if (priv) {
-        for (int i = threadIdx.x; i < nwc; i += blockDim.x) lr[i] = 0;
-        __syncthreads();
-    }
-    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
-        const uint64_t b = (uint64_t)(aux[off + i] - vmin);
-        if (priv) atomicOr(&lr[(b >> 5) - w0], 1u << (b & 31));
-        else atomicOr(&R[b >> 5], 1u << (b & 31));
-    }
-    if (priv) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < nwc; i += blockDim.x)
-            if (lr[i]) atomicOr(&R[w0 + i], lr[i]);
+__global__ void __launch_bounds__(256) k_set_bytes_read(const int64_t *__restrict__ aux, int64_t off, int64_t cnt,
+                                                        long long vmin, uint8_t *__restrict__ Rb) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * blockDim.x)
+        Rb[aux[off + i] - vmin] = 1;
+}
+
+// 32 bytes -> one bitmap word, for each of A, D, R
+__global__ void __launch_bounds__(256) k_set_pack_bits(const uint8_t *__restrict__ bytes, int64_t span_pad, int64_t nw,
+                                                       uint32_t *__restrict__ bits) {
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < 3 * nw; w += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = w / nw, ww = w - s * nw;
+        const uint4 *src = (const uint4 *)(bytes + s * span_pad + ww * 32);
+        const uint4 a = src[0], b = src[1];
+        const uint32_t q[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t out = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            // bytes are 0 or 1: gather bit 0 of each byte
+            const uint32_t v = q[k];
+            out |= ((v & 1u) | ((v >> 7) & 2u) | ((v >> 14) & 4u) | ((v >> 21) & 8u)) << (4 * k);
+        }
+        bits[w] = out;
     }
 }
 
@@ -294,9 +345,21 @@ void set_check(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, int64_t *r
     const int64_t nw = (int64_t)((span + 31) / 32);
     uint32_t *bits = ctx->ws<uint32_t>(WS_S_BITS, 3 * nw);
     uint32_t *A = bits, *D = bits + nw, *R = bits + 2 * nw;
-    HIP_TRY(hipMemsetAsync(bits, 0, sizeof(uint32_t) * 3 * nw, st));
-    if (n > 0) k_set_mark_rows<<<(unsigned)((n + MARK_CH - 1) / MARK_CH), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, A, D);
-    if (cnt > 0) k_set_mark_read<<<(unsigned)((cnt + MARK_CH - 1) / MARK_CH), 256, 0, st>>>(dh->aux, off, cnt, vmin, R);
+    if (span <= BYTEMAP_MAX) {
+        const int64_t span_pad = nw * 32;
+        uint8_t *bytes = ctx->ws<uint8_t>(WS_S_BYTES, 3 * span_pad);
+        HIP_TRY(hipMemsetAsync(bytes, 0, 3 * span_pad, st));
+        if (n > 0)
+            k_set_bytes_rows<<<grid_for(n, 256, 16384), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, bytes,
+                                                                     bytes + span_pad);
+        if (cnt > 0)
+            k_set_bytes_read<<<grid_for(cnt, 256, 16384), 256, 0, st>>>(dh->aux, off, cnt, vmin, bytes + 2 * span_pad);
+        k_set_pack_bits<<<grid_for(3 * nw, 256, 16384), 256, 0, st>>>(bytes, span_pad, nw, bits);
+    } else {
+        HIP_TRY(hipMemsetAsync(bits, 0, sizeof(uint32_t) * 3 * nw, st));
+        if (n > 0) k_set_mark_rows<<<(unsigned)((n + MARK_CH - 1) / MARK_CH), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, A, D);
+        if (cnt > 0) k_set_mark_read<<<(unsigned)((cnt + MARK_CH - 1) / MARK_CH), 256, 0, st>>>(dh->aux, off, cnt, vmin, R);
+    }
     uint32_t *starts = ctx->ws<uint32_t>(WS_S_RUNS, 8 * nw + 8);
     uint32_t *spos = starts + 4 * nw;
     k_set_count<<<grid_for(nw, 256, 2048), 256, 0, st>>>(A, D, R, nw, starts, m);

@@ -101,7 +101,8 @@ enum WsSlot {
     WS_SF_BITS, WS_SF_OUT, WS_SF_FL, WS_SF_SEL, WS_SF_TIME, WS_SF_PART,
     WS_Q_META, WS_Q_PART, WS_Q_HIST, WS_Q_FLAG, WS_Q_ROWS, WS_Q_TMP, WS_Q_MULT, WS_Q_MFLAG, WS_Q_POS,
     WS_Q_OUT, WS_Q_KEYS, WS_Q_MULT2, WS_LCOST, WS_LSORT, WS_LTMP, WS_ACC_STATS, WS_WG_GSET, WS_WG_WORK, WS_WG_WTAB, WS_WG_PEND, WS_STATS_KEYS,
-    WS_S_BYTES, WS_IV_U, WS_IV_IDX, WS_IV_KEY, WS_IV_RINIT, WS_IV_MAX, WS_IV_TMP,
+    WS_BFS_NODES, WS_BFS_LSTART, WS_BFS_HKEY, WS_BFS_HID, WS_BFS_LIVE, WS_BFS_VIS, WS_BFS_TMP,
+    WS_WG_MEMO, WS_WG_STACK, WS_WG_SCR, WS_S_BYTES, WS_IV_U, WS_IV_IDX, WS_IV_KEY, WS_IV_RINIT, WS_IV_MAX, WS_IV_TMP,
     WS_COUNT
 };
 

@@ -2013,6 +2013,9 @@ __device__ __forceinline__ void wg_enum_work(const WgArgs &W, WgShared &sh, int 
         if (tid == 64) {
             sh.t_cur = sh.t_next; sh.t_next = 0xFFFFFFFFu; sh.npend2 = 0;
             sh.head = sh.tail; sh.active = 0;
+            // racing k_lin_bfs: a key it settled ends the enumeration as incomplete
+            if (W.d.claim && __hip_atomic_load(&W.d.claim[sh.key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                sh.status |= ENUM_CAP;
         }
         __syncthreads();
         const uint32_t tc = sh.t_cur, np = sh.npend, sel = sh.pend_sel;
@@ -2372,6 +2375,12 @@ insert:
     {
         if (ins >= chk) {
             if (ins >= budget) { verdict = JH_UNKNOWN; goto done; }
+            if (A.claim) {
+                // racing k_lin_bfs: stop if it settled this key first
+                int c = 0;
+                if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (readlane(c, 0)) { verdict = JH_CANCELLED; goto done; }
+            }
             if (ins >= next_acc) {
                 next_acc = ins + acc_t;
                 // the deepest open node with >= ACC_T/2 inserts below it, not known live
@@ -2637,7 +2646,10 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
             v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
             v.explored = inserts;
             v.fail_entry = verdict == JH_INVALID ? -(int64_t)tmax - 2 : -1;
-            if (lane == 0) { A.out[key] = v; sh.cmd = CMD_DONE; }
+            if (lane == 0) {
+                if (verdict != JH_CANCELLED) emit_verdict(A.out, A.claim, key, v);
+                sh.cmd = CMD_DONE;
+            }
             if (lane == 0 && W.acc_stats) atomicAdd(&W.acc_stats[7], __builtin_amdgcn_s_memtime() - ck0);
             if (lane == 0 && W.key_prof) {
                 // JH_DEBUG=4: per-key cycles / inserts / verdict for the tail analysis
@@ -2665,11 +2677,19 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
 // configuration graph by a whole workgroup. For a key with no terminal
 // configuration (invalid) WGL's cache ends up holding exactly this set, so
 // verdict, explored count and the furthest return rank (fail_entry) are
-// identical to the sequential search. A key where a terminal configuration
-// is reachable (valid) is settled here only if the complete reachable set is
-// at least BFS_VALID_MIN and below the budget (then WGL cannot reach
-// :unknown); otherwise, and when the set outgrows the budget, it is handed to
-// the sequential search (which alone defines where :unknown starts).
+// identical to the sequential search (over the budget: :unknown with the
+// budget as count, where the search stops).
+//
+// A key where a terminal configuration is reachable (valid, or :unknown if
+// WGL runs out of budget first) gets WGL's exact count from the stored set
+// (bfs_wgl_count): a node is live iff a terminal configuration is reachable
+// from it; WGL's DFS goes from the root to the first live child at every
+// step (in candidate order), and before taking it exhausts every earlier
+// (dead) child's whole reachable set. So WGL's cache at the terminal is the
+// path (root excluded, terminal included) plus the closure of those dead
+// children -- computed here in parallel: liveness layer by layer backwards,
+// the path by one wave, the closure by a multi-source BFS. Sets beyond the
+// storage cap are left to the sequential search.
 constexpr int BFS_THREADS = 512;
 constexpr int BFS_HDR = 1024;                      // shared scalars + the layer's window
 constexpr int BFS_TBL = 28672;                     // W-format tables (ops, woff, W) + r[]
@@ -2701,7 +2721,18 @@ struct BfsArgs {
     int32_t init_state;
     int32_t states_ok;      // every interned state < 2^12
     int32_t *claim;         // race with the sequential search (see emit_verdict)
-    int32_t settle_valid;   // 1: also settle valid keys (explored -2: WGL's count unknown; JH_BFS_VALID=1)
+    int64_t reach_cap;      // reachable configurations enumerated at most (>= budget + 1)
+    // per workgroup, for bfs_wgl_count (valid keys): every node of the set in
+    // layer order, its layer offsets, a node -> id hash, liveness / closure marks
+    uint64_t *nodes;        // ncap
+    uint32_t ncap;
+    uint32_t *lstart;       // n_ok + 2 (sized by the longest key)
+    uint32_t lcap;
+    ulonglong2 *ent;        // hcap (power of two) hash entries {configuration, id | LIVE}
+    uint32_t hcap;
+    uint32_t *slot;         // ncap: each node's hash slot
+    uint32_t *vis;          // ncap / 32 + 1
+    uint32_t *tmp;          // ncap
 };
 
 struct BfsShared {
@@ -2709,7 +2740,8 @@ struct BfsShared {
     jh_key_verdict v;
     int key, need, maxw, status, mode, gclear, ovf, term;
     unsigned npend, npend2, nfront, nnext, tmax, lcount, r;
-    unsigned long long count;
+    unsigned nnodes, nostore, dlen, clen, cnext, ok;
+    unsigned long long count, ccount, plen;
     uint32_t win_vv[64];    // the current layer's window: v1 | v2 << 16
     uint32_t win_f[64];     // f, or 3 for no member
 };
@@ -2725,6 +2757,284 @@ __device__ __forceinline__ uint32_t lset_hash(uint64_t k) {
     h ^= h >> 16;
     h *= 0x7FEB352Du;
     return (h >> 11) & (LSET - 1);
+}
+
+// child j of configuration (t, s, mask) in the canonical coordinates of the
+// BFS: 0 none (member linearized or the model refuses it), 1 same layer,
+// 2 a later layer, 3 a terminal configuration; *ck = the child's packed key
+__device__ __forceinline__ int bfs_child(const Op *ops, const int32_t *woff, const uint16_t *W, const uint8_t *rpos,
+                                         uint32_t n_ok, uint32_t t, uint32_t s, uint32_t mask, int j,
+                                         uint64_t *ck) {
+    const int wo = woff[t], w = woff[t + 1] - wo;
+    if (j >= w || ((mask >> j) & 1)) return 0;
+    const Op o = ops[W[wo + j]];
+    int s2;
+    if (!cas_step(o.fa & 3, o.v1, o.v2, (int)s, &s2)) return 0;
+    const uint32_t r = rpos[t];
+    if ((uint32_t)j != r) { *ck = bfs_pack(t, (uint32_t)s2, mask | (1u << j)); return 1; }
+    uint64_t nm = mask | (1u << j);
+    uint32_t u = t, ru = r;
+    for (;;) {
+        nm = drop_bit(nm, ru);
+        u++;
+        if (u >= n_ok) return 3;
+        ru = rpos[u];
+        if (!((nm >> ru) & 1)) break;
+    }
+    *ck = bfs_pack(u, (uint32_t)s2, (uint32_t)nm);
+    return 2;
+}
+
+// The stored set's hash: 16-byte entries {packed configuration, id | LIVE},
+// so that one load answers "which node, and is it live" for a child.
+constexpr uint64_t BFS_LIVE = 1ULL << 40;
+
+__device__ __forceinline__ ulonglong2 bfs_ent(const ulonglong2 *ent, uint32_t h) { return ent[h]; }
+
+// slot of key k, or -1 (the table is at most half full)
+__device__ __forceinline__ int64_t bfs_slot(const ulonglong2 *ent, uint32_t hmask, uint64_t k) {
+    uint32_t h = (uint32_t)jh_mix64(k) & hmask;
+    for (;;) {
+        const uint64_t e = ent[h].x;
+        if (e == k) return h;
+        if (e == BFS_EMPTY) return -1;
+        h = (h + 1) & hmask;
+    }
+}
+
+// a batch of child keys (k[i] = 0: none): slot and info word of each, the
+// first probes all in flight together; slot -1 for a key not in the set
+template <int B>
+__device__ __forceinline__ void bfs_lookup_batch(const ulonglong2 *ent, uint32_t hmask, const uint64_t (&k)[B],
+                                                 int64_t (&slot)[B], uint64_t (&info)[B]) {
+    uint32_t h[B];
+    ulonglong2 e[B];
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+        h[i] = (uint32_t)jh_mix64(k[i]) & hmask;
+        e[i] = k[i] ? ent[h[i]] : make_ulonglong2(BFS_EMPTY, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+        slot[i] = -1; info[i] = 0;
+        if (!k[i]) continue;
+        if (e[i].x == k[i]) { slot[i] = h[i]; info[i] = e[i].y; }
+        else if (e[i].x != BFS_EMPTY) {
+            slot[i] = bfs_slot(ent, hmask, k[i]);
+            if (slot[i] >= 0) info[i] = ent[slot[i]].y;
+        }
+    }
+}
+
+// bfs_child for layer t with its window in LDS (sh.win_vv / sh.win_f, r = RET's position)
+__device__ __forceinline__ int bfs_child_w(const BfsShared &sh, const uint8_t *rpos, uint32_t n_ok, uint32_t t,
+                                           uint32_t r, int w, uint32_t s, uint32_t mask, int j, uint64_t *ck) {
+    if (j >= w || ((mask >> j) & 1)) return 0;
+    const uint32_t vv = sh.win_vv[j];
+    int s2;
+    if (!cas_step((int)sh.win_f[j], (int)(vv & 0xFFFF), (int)(vv >> 16), (int)s, &s2)) return 0;
+    if ((uint32_t)j != r) { *ck = bfs_pack(t, (uint32_t)s2, mask | (1u << j)); return 1; }
+    uint64_t nm = mask | (1u << j);
+    uint32_t u = t, ru = r;
+    for (;;) {
+        nm = drop_bit(nm, ru);
+        u++;
+        if (u >= n_ok) return 3;
+        ru = rpos[u];
+        if (!((nm >> ru) & 1)) break;
+    }
+    *ck = bfs_pack(u, (uint32_t)s2, (uint32_t)nm);
+    return 2;
+}
+
+// live if any child among members j0 .. j0+7 is terminal or live
+__device__ __forceinline__ bool bfs_any_live8(const ulonglong2 *ent, uint32_t hmask, const BfsShared &sh,
+                                              const uint8_t *rpos, uint32_t n_ok, uint32_t t, uint32_t r, int w,
+                                              uint32_t s0, uint32_t m0, int j0) {
+    uint64_t k[8];
+    int64_t sl[8];
+    uint64_t inf[8];
+    bool term = false;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint64_t ck = 0;
+        const int c = bfs_child_w(sh, rpos, n_ok, t, r, w, s0, m0, j0 + i, &ck);
+        term |= c == 3;
+        k[i] = (c == 1 || c == 2) ? ck : 0;
+    }
+    if (term) return true;
+    bfs_lookup_batch<8>(ent, hmask, k, sl, inf);
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < 8; i++) any |= (inf[i] & BFS_LIVE) != 0;
+    return any;
+}
+
+// WGL's cache size for a key whose whole reachable set the BFS has stored
+// (see above). Sets sh.ok, sh.plen (path: root excluded, terminal included)
+// and sh.ccount (closure of the dead children left of the path).
+__device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key, const Op *ops,
+                              const int32_t *woff, const uint16_t *W, const uint8_t *rpos, uint32_t n_ok) {
+    const int lane = tid & 63;
+    if (sh.nostore) return;
+    const uint32_t N = sh.nnodes;
+    if ((uint64_t)N * 2 > A.hcap) return;
+    const uint32_t hmask = A.hcap - 1;
+    ulonglong2 *ent = A.ent;
+    uint32_t *slot_of = A.slot;
+    unsigned long long *dq = A.dbg ? A.dbg + 16 * (size_t)blockIdx.x : nullptr;   // JH_DEBUG=2 phase cycles
+    unsigned long long tq = __builtin_amdgcn_s_memtime();
+    auto stamp = [&](int idx) {
+        const unsigned long long n = __builtin_amdgcn_s_memtime();
+        if (dq && tid == 0) dq[idx] += n - tq;
+        tq = n;
+    };
+    // ---- node -> slot hash ----------------------------------------------------
+    for (uint32_t i = tid; i < A.hcap; i += BFS_THREADS) ent[i] = make_ulonglong2(BFS_EMPTY, 0);
+    for (uint32_t i = tid; i < N / 32 + 1; i += BFS_THREADS) A.vis[i] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < N; i += BFS_THREADS) {
+        const uint64_t k = A.nodes[i];
+        uint32_t h = (uint32_t)jh_mix64(k) & hmask;
+        while (atomicCAS((unsigned long long *)&ent[h].x, BFS_EMPTY, k) != BFS_EMPTY) h = (h + 1) & hmask;
+        ent[h].y = i;
+        slot_of[i] = h;
+    }
+    __syncthreads();
+    stamp(5);
+    // ---- liveness, layer by layer backwards; within a layer by mask size
+    // descending (same-layer edges add one member) ------------------------------
+    uint32_t *hist = (uint32_t *)(jh_lds + BFS_HDR + BFS_TBL);     // the layer set's LDS, free now
+    for (int t = (int)n_ok - 1; t >= 0; t--) {
+        if (A.claim && tid == 0 &&
+            __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            sh.status |= 4;
+        const uint32_t a = A.lstart[t], b = A.lstart[t + 1];
+        __syncthreads();
+        if (sh.status) return;
+        if (a == b) continue;
+        if (tid < 66) hist[tid] = 0;
+        const int w = woff[t + 1] - woff[t];
+        if (tid < 64) {       // the layer's window into LDS, as in the forward pass
+            if (tid < w) {
+                const Op o = ops[W[woff[t] + tid]];
+                sh.win_vv[tid] = (uint32_t)o.v1 | ((uint32_t)o.v2 << 16);
+                sh.win_f[tid] = (uint32_t)(o.fa & 3);
+            } else sh.win_f[tid] = 3;
+        }
+        const uint32_t rt = rpos[t];
+        __syncthreads();
+        for (uint32_t i = a + tid; i < b; i += BFS_THREADS)
+            atomicAdd(&hist[__popc((uint32_t)A.nodes[i])], 1u);
+        __syncthreads();
+        if (tid == 0) {   // bucket starts, largest masks first
+            uint32_t acc = 0;
+            for (int p = 32; p >= 0; p--) { const uint32_t c = hist[p]; hist[33 + p] = acc; hist[p] = acc; acc += c; }
+        }
+        __syncthreads();
+        for (uint32_t i = a + tid; i < b; i += BFS_THREADS)
+            A.tmp[atomicAdd(&hist[__popc((uint32_t)A.nodes[i])], 1u)] = slot_of[i];
+        __syncthreads();
+        for (int p = 32; p >= 0; p--) {
+            const uint32_t bs = hist[33 + p], be = p > 0 ? hist[33 + p - 1] : b - a;
+            if (bs == be) continue;
+            for (uint32_t q = bs + tid; q < be; q += BFS_THREADS) {
+                const uint32_t sl = A.tmp[q];
+                const uint64_t x = ent[sl].x;
+                const uint32_t s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
+                bool lv = false;
+                for (int j0 = 0; j0 < w && !lv; j0 += 8)
+                    lv = bfs_any_live8(ent, hmask, sh, rpos, n_ok, (uint32_t)t, rt, w, s0, m0, j0);
+                if (lv) atomicOr((unsigned long long *)&ent[sl].y, BFS_LIVE);
+            }
+            __syncthreads();
+        }
+    }
+    stamp(6);
+    // ---- the path: from the root, the first live child each step; the dead
+    // children before it seed the closure (one wave) -------------------------------
+    uint32_t *dl = A.tmp;                                    // dead children (slots), then closure frontiers
+    if (tid < 64) {
+        uint64_t x = A.nodes[0];                             // the root (layer 0's first entry)
+        unsigned long long plen = 0;
+        uint32_t dn = 0;
+        bool done = false;
+        while (!done && dn + 64 < A.ncap / 2) {
+            const uint32_t t = (uint32_t)(x >> 44), s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
+            uint64_t ck = 0;
+            const int c = bfs_child(ops, woff, W, rpos, n_ok, t, s0, m0, lane, &ck);
+            int64_t sl = -1;
+            uint64_t inf = 0;
+            if (c == 1 || c == 2) { sl = bfs_slot(ent, hmask, ck); if (sl >= 0) inf = ent[sl].y; }
+            const bool lv = c == 3 || (inf & BFS_LIVE);
+            const uint64_t lm = ballot(lv);
+            if (!lm) break;                                   // cannot happen on a live node
+            const int jl = __builtin_ctzll(lm);
+            const bool dead = sl >= 0 && lane < jl;
+            const uint64_t dm = ballot(dead);
+            if (dead) dl[dn + mbcnt(dm)] = (uint32_t)sl;
+            dn += (uint32_t)__popcll(dm);
+            plen++;
+            if (readlane(c, jl) == 3) done = true;
+            else x = readlane64(ck, jl);
+        }
+        if (lane == 0) { sh.plen = plen; sh.dlen = dn; sh.ok = done ? 1u : 0u; }
+    }
+    __syncthreads();
+    stamp(7);
+    if (!sh.ok) return;
+    // ---- closure of the dead children: a multi-source BFS over stored slots ----
+    if (tid == 0) { sh.ccount = 0; sh.clen = 0; }
+    __syncthreads();
+    uint32_t *fa = dl, *fb = dl + A.ncap / 2;
+    uint32_t nf = 0;
+    auto visit = [&](uint32_t sl, uint64_t info) -> bool {
+        const uint32_t id = (uint32_t)info & 0xFFFFFFFFu;
+        const uint32_t old = atomicOr(&A.vis[id >> 5], 1u << (id & 31));
+        return !(old & (1u << (id & 31)));
+    };
+    for (uint32_t i = tid; i < sh.dlen; i += BFS_THREADS) {
+        const uint32_t sl = dl[i];
+        if (visit(sl, ent[sl].y)) fb[atomicAdd(&sh.clen, 1u)] = sl;
+    }
+    __syncthreads();
+    for (;;) {
+        nf = sh.clen;
+        if (tid == 0) { sh.ccount += nf; sh.cnext = 0; }
+        if (nf == 0 || nf > A.ncap / 2) break;
+        { uint32_t *tp = fa; fa = fb; fb = tp; }
+        __syncthreads();
+        for (uint32_t q = tid; q < nf; q += BFS_THREADS) {
+            const uint64_t x = ent[fa[q]].x;
+            const uint32_t t = (uint32_t)(x >> 44), s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
+            const int w = woff[t + 1] - woff[t];
+            for (int j0 = 0; j0 < w; j0 += 8) {
+                uint64_t k[8];
+                int64_t sl[8];
+                uint64_t inf[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    uint64_t ck = 0;
+                    const int c = bfs_child(ops, woff, W, rpos, n_ok, t, s0, m0, j0 + i, &ck);
+                    k[i] = (c == 1 || c == 2) ? ck : 0;
+                }
+                bfs_lookup_batch<8>(ent, hmask, k, sl, inf);
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    if (sl[i] < 0 || !visit((uint32_t)sl[i], inf[i])) continue;
+                    const uint32_t pos = atomicAdd(&sh.cnext, 1u);
+                    if (pos < A.ncap / 2) fb[pos] = (uint32_t)sl[i];
+                }
+            }
+        }
+        __syncthreads();
+        if (tid == 0) sh.clen = sh.cnext;
+        __syncthreads();
+    }
+    __syncthreads();
+    stamp(8);
+    if (tid == 0 && nf > A.ncap / 2) sh.ok = 0;
+    __syncthreads();
 }
 
 // Heavy keys, one workgroup each: the reachable configuration set layer by
@@ -2784,6 +3094,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
     if (tid == 0) {
         pend[0] = bfs_pack(0, (uint32_t)A.init_state, 0);
         sh.npend = 1; sh.tmax = 0; sh.count = 0; sh.status = 0; sh.gclear = 0; sh.term = 0;
+        sh.nnodes = 0; sh.nostore = n_ok + 2 > A.lcap ? 1u : 0u;
     }
     __syncthreads();
     const unsigned long long b0 = __builtin_amdgcn_s_memtime();
@@ -2802,6 +3113,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             } else sh.win_f[tid] = 3;
         }
         if (tid == 0) {
+            if (t < A.lcap) A.lstart[t] = sh.nnodes;
             sh.nfront = 0; sh.lcount = 0; sh.mode = 0; sh.ovf = 0; sh.r = rpos[t];
             // the sequential search settled this key first
             if (A.claim && __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
@@ -2855,7 +3167,9 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                 }
             }
             const unsigned long long n = atomicAdd(&sh.count, 1ULL);
-            if ((long long)n >= A.budget + 1) atomicOr(&sh.status, 2);
+            if ((long long)n >= A.reach_cap) atomicOr(&sh.status, 2);
+            const unsigned id = atomicAdd(&sh.nnodes, 1u);
+            if (id < A.ncap) A.nodes[id] = bfs_pack(t, cs, cm); else sh.nostore = 1;
             return true;
         };
         // An insert refused for LDS load (ovf) re-runs the pass against the
@@ -2950,17 +3264,30 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
         d[0] += __builtin_amdgcn_s_memtime() - b0; d[1] += rounds; d[3] += sh.count; d[4] += 1;
     }
-    if (sh.status || (sh.term && !(A.settle_valid && (long long)sh.count - 1 >= BFS_VALID_MIN &&
-                                   (long long)sh.count - 1 < A.budget))) {
-        if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
+    if (sh.status) {
+        if (tid == 0 && !(sh.status & 4)) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
     } else if (sh.term) {
-        // Valid, and WGL could not have reached :unknown: its cache only ever
-        // holds reachable non-terminal configurations (count - 1 of them, the
-        // initial one is not cached), fewer than the budget. The insert count
-        // of the DFS itself is not known here: explored = -2.
+        // valid, or :unknown if WGL's count passes the budget: WGL's exact count
+        if (tid == 0) { if (n_ok < A.lcap) A.lstart[n_ok] = sh.nnodes; sh.ok = 0; }
+        __syncthreads();
+        bfs_wgl_count(A, sh, tid, key, ops, woff, W, rpos, n_ok);
+        if (tid == 0) {
+            if (!sh.ok) {
+                A.unres_list[atomicAdd(A.unres_count, 1)] = key;
+            } else {
+                jh_key_verdict v;
+                v.cause = 0; v.fail_entry = -1;
+                const unsigned long long cnt = sh.plen + sh.ccount;
+                if ((long long)cnt <= A.budget) { v.valid = JH_VALID; v.explored = (int64_t)cnt; }
+                else { v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_BUDGET; v.explored = A.budget; }
+                emit_verdict(A.out, A.claim, key, v);
+            }
+        }
+    } else if ((long long)sh.count - 1 > A.budget) {
+        // no terminal, more reachable configurations than the budget: WGL stops at it
         if (tid == 0) {
             jh_key_verdict v;
-            v.valid = JH_VALID; v.cause = 0; v.fail_entry = -1; v.explored = -2;
+            v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_BUDGET; v.fail_entry = -1; v.explored = A.budget;
             emit_verdict(A.out, A.claim, key, v);
         }
     } else if (wid == 0) {
@@ -2973,8 +3300,15 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A) {
+__global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A0) {
     BfsShared &sh = *(BfsShared *)jh_lds;
+    BfsArgs A = A0;                      // this workgroup's slices of the count buffers
+    A.nodes += (size_t)blockIdx.x * A.ncap;
+    A.lstart += (size_t)blockIdx.x * A.lcap;
+    A.ent += (size_t)blockIdx.x * A.hcap;
+    A.slot += (size_t)blockIdx.x * A.ncap;
+    A.vis += (size_t)blockIdx.x * (A.ncap / 32 + 1);
+    A.tmp += (size_t)blockIdx.x * A.ncap;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     uint64_t *gset = A.gset + (size_t)blockIdx.x * A.gset_cap;
     uint64_t *pend = A.pend + (size_t)blockIdx.x * 2 * A.q_cap;
@@ -3767,19 +4101,12 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[9], ctx->aux2));
     }
-    int n_unres = 0, n_defer3 = 0;
-    const char *wg_env = getenv("JH_WG");
-    // JH_WG=1: the workgroup engine (k_lin_wg, exact DFS with accelerated dead
-    // subtrees) for deferred LEAN keys; default: the BFS / sequential race
-    const bool use_wg = wg_env && atoi(wg_env) != 0;
     unsigned long long *acc_stats = nullptr;
     int n_wg = 0;
-    if (n_defer > 0 && use_wg) {
-        // Deferred keys, exact WGL with accelerated dead subtrees: LEAN keys on
-        // k_lin_wg (one workgroup per key, stream st), WIDE keys on the plain
-        // sequential search with the full budget (k_lin_seq3<false>, aux stream).
-        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
-        HIP_TRY(hipMemsetAsync(q + 18, 0, sizeof(int32_t), st));
+    // the workgroup engine (k_lin_wg): exact WGL, dead subtrees enumerated by
+    // the workgroup's helper waves; built for wg_cus CUs, racing the BFS when
+    // wg_claim is set
+    auto build_wg = [&](int wg_cus, int32_t *wg_claim, int32_t *wg_queue) -> WgArgs {
         acc_stats = ctx->ws<unsigned long long>(WS_ACC_STATS, 8);
         HIP_TRY(hipMemsetAsync(acc_stats, 0, 8 * sizeof(unsigned long long), st));
         uint32_t cap2 = 1u << 16;
@@ -3796,23 +4123,23 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         uint64_t mem_limit = 48ULL << 30;
         if (const char *e = getenv("JH_WG_MEM_GB")) mem_limit = (uint64_t)std::max(1, atoi(e)) << 30;
         int per_cu = 1;
-        n_wg = std::min<int64_t>(n_defer, (int64_t)per_cu * ctx->n_cu);
+        n_wg = std::min<int64_t>(n_defer, (int64_t)per_cu * wg_cus);
         n_wg = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)n_wg, mem_limit / per_wg));
-        const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)n_wg * cap2 * 16;
-        uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)n_wg * cap2 * 2, /*zero=*/true);
-        if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
+        const bool fresh2 = ctx->ws_fresh(WS_WG_MEMO) || ctx->bufs[WS_WG_MEMO].bytes < (size_t)n_wg * cap2 * 16;
+        uint64_t *memo2 = ctx->ws<uint64_t>(WS_WG_MEMO, (size_t)n_wg * cap2 * 2, /*zero=*/true);
+        if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_WG_MEMO].bytes, st));
         // kept all zero between calls by the enumeration's clean-up
         uint64_t *gset = ctx->ws<uint64_t>(WS_WG_GSET, (size_t)n_wg * gcap, /*zero=*/true);
         uint64_t *work = ctx->ws<uint64_t>(WS_WG_WORK, (size_t)n_wg * work_cap, /*zero=*/true);
         WgArgs wa{};
         wa.d = a;
-        wa.d.list = defer; wa.d.n_list = n_defer; wa.d.n_list_dev = nullptr; wa.d.queue = q; wa.d.defer = 0;
+        wa.d.list = defer; wa.d.n_list = n_defer; wa.d.n_list_dev = nullptr; wa.d.queue = wg_queue; wa.d.defer = 0;
         wa.d.defer_list = nullptr; wa.d.defer_count = nullptr; wa.d.defer_prog = nullptr;
         wa.d.memo = memo2; wa.d.memo_cap = cap2;
-        wa.d.stack = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)n_wg * stack_cap);
-        wa.d.scratch = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)n_wg * MemoW::SLOTS * 8);
+        wa.d.stack = ctx->ws<Frame>(WS_WG_STACK, (size_t)n_wg * stack_cap);
+        wa.d.scratch = ctx->ws<char>(WS_WG_SCR, (size_t)n_wg * MemoW::SLOTS * 8);
         wa.d.scratch_bytes = MemoW::SLOTS * 8;
-        wa.d.budget = budget; wa.d.budget_full = 0; wa.d.claim = nullptr;
+        wa.d.budget = budget; wa.d.budget_full = 0; wa.d.claim = wg_claim;
         wa.d.gen_base = ctx->gen_base + (uint32_t)K + 1;
         wa.d.dbg = nullptr; wa.d.probes = (unsigned long long *)(q + 8);
         wa.gset = gset; wa.gset_cap = (uint32_t)gcap; wa.work = work; wa.work_cap = (uint32_t)work_cap;
@@ -3834,6 +4161,23 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             HIP_TRY(hipFuncSetAttribute((const void *)k_lin_wg, hipFuncAttributeMaxDynamicSharedMemorySize, WG_LDS));
             ctx->lds_attr_wg = true;
         }
+        return wa;
+    };
+    int n_unres = 0, n_defer3 = 0;
+    const char *wg_env = getenv("JH_WG");
+    // JH_WG=1: the workgroup engine (k_lin_wg, exact DFS with accelerated dead
+    // subtrees) for deferred LEAN keys; default: the BFS / sequential race
+    const bool use_wg = wg_env && atoi(wg_env) == 1;
+    // JH_WG=2: the workgroup engine races the BFS in place of the sequential search
+    const bool wg_race = wg_env && atoi(wg_env) == 2;
+    if (n_defer > 0 && use_wg) {
+        // Deferred keys, exact WGL with accelerated dead subtrees: LEAN keys on
+        // k_lin_wg (one workgroup per key, stream st), WIDE keys on the plain
+        // sequential search with the full budget (k_lin_seq3<false>, aux stream).
+        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(q + 18, 0, sizeof(int32_t), st));
+        WgArgs wa = build_wg(ctx->n_cu, nullptr, q);
+        const uint32_t cap2 = wa.d.memo_cap;
         HIP_TRY(hipEventRecord(ctx->ev[11], st));
         k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, st>>>(wa);
         HIP_TRY(hipGetLastError());
@@ -3875,9 +4219,14 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipMemsetAsync(q + 3, 0, sizeof(int32_t), st));
         HIP_TRY(hipMemsetAsync(q + 6, 0, sizeof(int32_t), st));
 
+        // the BFS enumerates up to reach_cap configurations and keeps up to
+        // ncap of them for WGL's exact count of valid keys (bfs_wgl_count)
+        uint32_t ncap = 1u << 22;
+        if (const char *e = getenv("JH_BFS_NODES")) ncap = (uint32_t)std::max(1 << 16, std::min(1 << 26, atoi(e)));
+        const int64_t reach_cap = std::max<int64_t>(budget + 1, ncap);
         uint32_t set_cap = 1u << 12;
-        while ((int64_t)set_cap < 2 * budget && set_cap < (1u << 30)) set_cap <<= 1;
-        const uint32_t q_cap = (uint32_t)std::min<int64_t>(budget + 64, (int64_t)1 << 30);
+        while ((int64_t)set_cap < 2 * reach_cap && set_cap < (1u << 30)) set_cap <<= 1;
+        const uint32_t q_cap = (uint32_t)std::min<int64_t>(reach_cap + 64, (int64_t)1 << 30);
         // CU split of the heavy-key pass (one BFS workgroup or one sequential
         // wave per CU, by LDS): invalid keys are few, the sequential searches
         // many (every valid deferred key), so most CUs go to the latter
@@ -3896,11 +4245,19 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         c.scratch = bscr; c.scratch_bytes = scr_bytes_bfs; c.budget = budget;
         c.init_state = init_state; c.states_ok = n_states < 4096 ? 1 : 0;
         c.dbg = dbg; c.claim = claim;
-        // By default the BFS settles invalid keys only (their WGL cache is the
-        // whole reachable set, an exact count); every valid key is settled by
-        // the sequential search, so `explored` is WGL's count on every key and
-        // the same on every run.
-        c.settle_valid = getenv("JH_BFS_VALID") && atoi(getenv("JH_BFS_VALID")) ? 1 : 0;
+        // every key the BFS settles carries WGL's exact count (the whole set for
+        // an invalid key; path + dead closure for a valid one, bfs_wgl_count)
+        c.reach_cap = reach_cap;
+        uint32_t hcap = 1u << 16;
+        while (hcap < 2 * (uint64_t)ncap) hcap <<= 1;
+        const uint32_t lcap = (uint32_t)smax + 2;
+        c.ncap = ncap; c.hcap = hcap; c.lcap = lcap;
+        c.nodes = ctx->ws<uint64_t>(WS_BFS_NODES, (size_t)wg2 * ncap);
+        c.lstart = ctx->ws<uint32_t>(WS_BFS_LSTART, (size_t)wg2 * lcap);
+        c.ent = ctx->ws<ulonglong2>(WS_BFS_HKEY, (size_t)wg2 * hcap);
+        c.slot = ctx->ws<uint32_t>(WS_BFS_LIVE, (size_t)wg2 * ncap);
+        c.vis = ctx->ws<uint32_t>(WS_BFS_VIS, (size_t)wg2 * (ncap / 32 + 1));
+        c.tmp = ctx->ws<uint32_t>(WS_BFS_TMP, (size_t)wg2 * ncap);
         // per context (= per device; calls on one context are serialised by its mutex)
         if (!ctx->lds_attr) {
             HIP_TRY(hipFuncSetAttribute((const void *)k_lin_bfs, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3920,6 +4277,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;
         uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
         if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
+        WgArgs wr{};
+        if (wg_race) wr = build_wg(std::max(1, ctx->n_cu - wg2), claim, q + 6);
         // the fork point: everything the phase-2 searches read (claims, queue
         // counters, the cleared memo on a generation wrap) is ordered before it
         HIP_TRY(hipEventRecord(ctx->ev[6], st));
@@ -3950,7 +4309,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             bw.queue = q + 7;
             k_lin_seq<false><<<std::min(waves2, 32), 64, MemoH::LDS, ctx->aux>>>(bw);
         }
-        k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
+        if (wg_race) k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux>>>(wr);
+        else k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
         if (split3) {
@@ -3999,9 +4359,11 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             HIP_TRY(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
             for (int w = 0; w < wg2; w++)
                 if (h[16 * w + 4])
-                    fprintf(stderr, "[jh-bfs] wg %d keys=%llu cycles=%llu rounds=%llu configs=%llu cyc/round=%.0f\n",
+                    fprintf(stderr, "[jh-bfs] wg %d keys=%llu cycles=%llu rounds=%llu configs=%llu cyc/round=%.0f | "
+                            "count: hash=%llu live=%llu path=%llu closure=%llu cyc\n",
                             w, h[16 * w + 4], h[16 * w], h[16 * w + 1], h[16 * w + 3],
-                            (double)h[16 * w] / std::max(1ULL, h[16 * w + 1]));
+                            (double)h[16 * w] / std::max(1ULL, h[16 * w + 1]), h[16 * w + 5], h[16 * w + 6],
+                            h[16 * w + 7], h[16 * w + 8]);
             std::vector<unsigned long long> g((size_t)waves2 * 16);
             HIP_TRY(hipMemcpy(g.data(), dbg + 16 * 256, g.size() * 8, hipMemcpyDeviceToHost));
             for (int w = 0; w < waves2; w++)

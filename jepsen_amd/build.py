@@ -21,10 +21,12 @@ HEADERS = [os.path.join(CSRC, "jh_internal.h"), os.path.join(ROOT, "include", "j
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 HIPFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
-            "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable",
-            # keep uniform (scalar) branches of the DFS loop unstructurized: fewer
-            # copies and exec-mask moves per step (-5..8% per DFS step, measured)
-            "-mllvm", "-structurizecfg-skip-uniform-regions=1"]
+            "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+# Not used: -mllvm -structurizecfg-skip-uniform-regions=1. It made the DFS step
+# 5-8% faster, but it miscompiles a divergent loop with data-dependent exits in
+# the BFS (the cross-layer RET-drop loop of k_lin_bfs): some lanes' edges were
+# dropped and a reachable set came out 11 configurations short (found by the
+# exact-count test of a valid key; tools/dbg_bfs_only.py reproduces it).
 HIPFLAGS += os.environ.get("JH_HIPFLAGS", "").split()   # e.g. -DJH_STEP_PROF (profiling builds)
 
 

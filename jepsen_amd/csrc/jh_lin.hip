@@ -2722,6 +2722,7 @@ struct BfsArgs {
     int32_t states_ok;      // every interned state < 2^12
     int32_t *claim;         // race with the sequential search (see emit_verdict)
     int64_t reach_cap;      // reachable configurations enumerated at most (>= budget + 1)
+    int32_t dbg_plen;       // JH_BFS_ONLY=1 (debugging): the BFS alone settles, fail_entry = path length
     // per workgroup, for bfs_wgl_count (valid keys): every node of the set in
     // layer order, its layer offsets, a node -> id hash, liveness / closure marks
     uint64_t *nodes;        // ncap
@@ -2789,13 +2790,22 @@ __device__ __forceinline__ int bfs_child(const Op *ops, const int32_t *woff, con
 // so that one load answers "which node, and is it live" for a child.
 constexpr uint64_t BFS_LIVE = 1ULL << 40;
 
-__device__ __forceinline__ ulonglong2 bfs_ent(const ulonglong2 *ent, uint32_t h) { return ent[h]; }
+// The LIVE bit is set with a global atomic, which is performed in L2 and does
+// not update the CU's L1 copy of the line: its readers load the info word with
+// an L1-bypassing (agent-scope) atomic load, never a plain load.
+__device__ __forceinline__ uint64_t bfs_info(const ulonglong2 *ent, uint32_t h) {
+    return __hip_atomic_load(&ent[h].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the keys are placed with a global CAS as well: read the same way
+__device__ __forceinline__ uint64_t bfs_keyat(const ulonglong2 *ent, uint32_t h) {
+    return __hip_atomic_load(&ent[h].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // slot of key k, or -1 (the table is at most half full)
 __device__ __forceinline__ int64_t bfs_slot(const ulonglong2 *ent, uint32_t hmask, uint64_t k) {
     uint32_t h = (uint32_t)jh_mix64(k) & hmask;
     for (;;) {
-        const uint64_t e = ent[h].x;
+        const uint64_t e = bfs_keyat(ent, h);
         if (e == k) return h;
         if (e == BFS_EMPTY) return -1;
         h = (h + 1) & hmask;
@@ -2808,20 +2818,21 @@ template <int B>
 __device__ __forceinline__ void bfs_lookup_batch(const ulonglong2 *ent, uint32_t hmask, const uint64_t (&k)[B],
                                                  int64_t (&slot)[B], uint64_t (&info)[B]) {
     uint32_t h[B];
-    ulonglong2 e[B];
+    uint64_t e[B], y[B];
 #pragma unroll
     for (int i = 0; i < B; i++) {
         h[i] = (uint32_t)jh_mix64(k[i]) & hmask;
-        e[i] = k[i] ? ent[h[i]] : make_ulonglong2(BFS_EMPTY, 0);
+        e[i] = k[i] ? bfs_keyat(ent, h[i]) : BFS_EMPTY;
+        y[i] = k[i] ? bfs_info(ent, h[i]) : 0;
     }
 #pragma unroll
     for (int i = 0; i < B; i++) {
         slot[i] = -1; info[i] = 0;
         if (!k[i]) continue;
-        if (e[i].x == k[i]) { slot[i] = h[i]; info[i] = e[i].y; }
-        else if (e[i].x != BFS_EMPTY) {
+        if (e[i] == k[i]) { slot[i] = h[i]; info[i] = y[i]; }
+        else if (e[i] != BFS_EMPTY) {
             slot[i] = bfs_slot(ent, hmask, k[i]);
-            if (slot[i] >= 0) info[i] = ent[slot[i]].y;
+            if (slot[i] >= 0) info[i] = bfs_info(ent, (uint32_t)slot[i]);
         }
     }
 }
@@ -2940,7 +2951,7 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
             if (bs == be) continue;
             for (uint32_t q = bs + tid; q < be; q += BFS_THREADS) {
                 const uint32_t sl = A.tmp[q];
-                const uint64_t x = ent[sl].x;
+                const uint64_t x = bfs_keyat(ent, sl);
                 const uint32_t s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
                 bool lv = false;
                 for (int j0 = 0; j0 < w && !lv; j0 += 8)
@@ -2965,7 +2976,7 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
             const int c = bfs_child(ops, woff, W, rpos, n_ok, t, s0, m0, lane, &ck);
             int64_t sl = -1;
             uint64_t inf = 0;
-            if (c == 1 || c == 2) { sl = bfs_slot(ent, hmask, ck); if (sl >= 0) inf = ent[sl].y; }
+            if (c == 1 || c == 2) { sl = bfs_slot(ent, hmask, ck); if (sl >= 0) inf = bfs_info(ent, (uint32_t)sl); }
             const bool lv = c == 3 || (inf & BFS_LIVE);
             const uint64_t lm = ballot(lv);
             if (!lm) break;                                   // cannot happen on a live node
@@ -3005,7 +3016,7 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
         { uint32_t *tp = fa; fa = fb; fb = tp; }
         __syncthreads();
         for (uint32_t q = tid; q < nf; q += BFS_THREADS) {
-            const uint64_t x = ent[fa[q]].x;
+            const uint64_t x = bfs_keyat(ent, fa[q]);
             const uint32_t t = (uint32_t)(x >> 44), s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
             const int w = woff[t + 1] - woff[t];
             for (int j0 = 0; j0 < w; j0 += 8) {
@@ -3280,6 +3291,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                 const unsigned long long cnt = sh.plen + sh.ccount;
                 if ((long long)cnt <= A.budget) { v.valid = JH_VALID; v.explored = (int64_t)cnt; }
                 else { v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_BUDGET; v.explored = A.budget; }
+                if (A.dbg_plen) { v.fail_entry = (int64_t)sh.plen; v.cause = (int32_t)sh.nnodes; v.explored = (int64_t)cnt; }   // debugging
                 emit_verdict(A.out, A.claim, key, v);
             }
         }
@@ -4248,6 +4260,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // every key the BFS settles carries WGL's exact count (the whole set for
         // an invalid key; path + dead closure for a valid one, bfs_wgl_count)
         c.reach_cap = reach_cap;
+        const bool bfs_only = getenv("JH_BFS_ONLY") && atoi(getenv("JH_BFS_ONLY"));
+        c.dbg_plen = bfs_only || (getenv("JH_BFS_DBGV") && atoi(getenv("JH_BFS_DBGV"))) ? 1 : 0;
         uint32_t hcap = 1u << 16;
         while (hcap < 2 * (uint64_t)ncap) hcap <<= 1;
         const uint32_t lcap = (uint32_t)smax + 2;
@@ -4309,7 +4323,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             bw.queue = q + 7;
             k_lin_seq<false><<<std::min(waves2, 32), 64, MemoH::LDS, ctx->aux>>>(bw);
         }
-        if (wg_race) k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux>>>(wr);
+        if (bfs_only) {}
+        else if (wg_race) k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux>>>(wr);
         else k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
@@ -4351,6 +4366,13 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         }
         HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
         HIP_TRY(hipStreamWaitEvent(st, ctx->ev[7], 0));
+        if (const char *dp = getenv("JH_BFS_DUMP")) {
+            // debugging: workgroup 0's stored configurations (t:20 | s:12 | mask:32)
+            HIP_TRY(hipStreamSynchronize(st));
+            std::vector<uint64_t> nd(c.ncap);
+            HIP_TRY(hipMemcpy(nd.data(), c.nodes, nd.size() * 8, hipMemcpyDeviceToHost));
+            if (FILE *fp = fopen(dp, "wb")) { fwrite(nd.data(), 8, nd.size(), fp); fclose(fp); }
+        }
         if (dbg2) {
             HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));

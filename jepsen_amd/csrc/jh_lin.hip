@@ -4261,7 +4261,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // an invalid key; path + dead closure for a valid one, bfs_wgl_count)
         c.reach_cap = reach_cap;
         const bool bfs_only = getenv("JH_BFS_ONLY") && atoi(getenv("JH_BFS_ONLY"));
-        c.dbg_plen = bfs_only || (getenv("JH_BFS_DBGV") && atoi(getenv("JH_BFS_DBGV"))) ? 1 : 0;
+        // JH_BFS_ONLY=1 (tests, debugging): no sequential search, the BFS settles every
+        // key it can (the others stay unsettled); JH_BFS_DBGV=1: its valid verdicts carry
+        // fail_entry = path length, cause = stored configurations, explored = count
+        c.dbg_plen = getenv("JH_BFS_DBGV") && atoi(getenv("JH_BFS_DBGV")) ? 1 : 0;
         uint32_t hcap = 1u << 16;
         while (hcap < 2 * (uint64_t)ncap) hcap <<= 1;
         const uint32_t lcap = (uint32_t)smax + 2;

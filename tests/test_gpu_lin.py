@@ -266,3 +266,23 @@ def test_mutex_and_register_models(ctx):
     assert reg.check(None, w, {})["valid?"] is True
     r = CK.check_safe(reg, None, w + [{"process": 2, "type": "invoke", "f": "cas", "value": [1, 2]}], {})
     assert r["valid?"] == CK.UNKNOWN
+
+
+@pytest.mark.parametrize("seed,init", [(21, None), (22, 0), (23, None)])
+def test_bfs_exact_counts(ctx, seed, init):
+    """The BFS alone (JH_BFS_ONLY=1: no sequential search in the race) settles
+    every deferred key -- invalid ones by their whole reachable set, valid ones
+    by liveness + first-live-child path + closure of the dead children
+    (bfs_wgl_count) -- with WGL's exact cache size, equal to the oracle's."""
+    import os
+    cols, _ = synth.cas_register(n_keys=150, ops_per_key=300, threads_per_key=12, readers=6, groups=10,
+                                 p_info=0.0, p_invalid=0.05, nemesis_every=0, init_nil=init is None, seed=seed)
+    os.environ["JH_BFS_ONLY"] = "1"
+    try:
+        v, s = ctx.check_cas_independent(cols, init=init)
+    finally:
+        del os.environ["JH_BFS_ONLY"]
+    ov, _ = oracle.check_cas_independent(cols, init=A.NIL if init is None else init, threads=8)
+    deferred = ov["explored"] > 4096
+    assert deferred.sum() >= 5 and (ov["valid"][deferred] == A.VALID).sum() >= 3
+    _same(v, ov)

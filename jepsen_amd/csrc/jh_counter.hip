@@ -12,16 +12,21 @@
 // HBM-bound streaming passes (bytes per row read / written):
 //   k_cnt_prange  process range                                        8 / 0
 //   k_cnt_pack    packed row code (process - pmin) << 4 | f2 << 2 | type,
-//                 last row per process (LDS-privatised), add-value range   32 / 4
-//   k_cnt_pair    complete pairing over the codes (64-row ballot windows)  ~8 / 4
-//   scan          ONE decoupled look-back inclusive scan (rocprim) of
-//                 {lower, upper, reads, flags-of-this-row} over a transform
-//                 of (code, pair, value): per-row contributions, :fails?,
-//                 orphans and nil checks fused in; its output iterator
+//                 last row per process (LDS-privatised), add-value range,
+//                 and the complete pairing of every invocation whose
+//                 completion lies in its 2048-row chunk                     32 / 8
+//   k_cnt_pair_spill  pairing of the few invocations the chunk could not
+//                 pair (thread per spill, walks its process' rows)          ~0
+//   k_cnt_tile_sums / hipcub scan / k_cnt_tile_scan
+//                 reduce-then-scan of {lower, upper, reads} over 2048-row
+//                 tiles, per-row :fails?, orphan and nil checks fused in;
 //                 writes only at read rows (the ok read's row and upper,
-//                 the invoke read's lower)                                  16 / ~0
-//   k_cnt_reads   the triples, in history order, errors, first failing row
+//                 the invoke read's lower)                                2 x 16 / ~0
+//   k_cnt_triples the triples, in history order, errors, first failing row
 //                 (over the ~1% read rows only)
+// (A single-pass decoupled look-back scan over the 49 K tiles was measured
+// at 20.8 ms on MI355X: the tile-to-tile look-back chain is serial latency
+// across XCDs. Reduce-then-scan costs one extra 16 B/row read and is ~1 ms.)
 #include "jh_internal.h"
 #include <hipcub/hipcub.hpp>
 

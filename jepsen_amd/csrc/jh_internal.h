@@ -53,9 +53,10 @@ struct jh_ctx {
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;     // second stream for racing searches (jh_lin.hip)
     hipStream_t aux2 = nullptr;    // third stream: windows wider than 64 (jh_lin.hip)
+    hipStream_t aux3 = nullptr;    // fourth stream: phase-2 late helpers (jh_lin.hip)
     std::mutex mu;
     std::vector<Buf> bufs;
-    hipEvent_t ev[12] = {};
+    hipEvent_t ev[14] = {};
     uint32_t gen_base = 0;        // memo generation tags (see jh_lin.hip)
     bool lds_attr = false;        // >64 KB dynamic-LDS attributes set for this device's kernels
     bool lds_attr_wg = false;
@@ -103,6 +104,7 @@ enum WsSlot {
     WS_Q_OUT, WS_Q_KEYS, WS_Q_MULT2, WS_LCOST, WS_LSORT, WS_LTMP, WS_ACC_STATS, WS_WG_GSET, WS_WG_WORK, WS_WG_WTAB, WS_WG_PEND, WS_STATS_KEYS,
     WS_BFS_NODES, WS_BFS_LSTART, WS_BFS_HKEY, WS_BFS_HID, WS_BFS_LIVE, WS_BFS_VIS, WS_BFS_TMP,
     WS_WG_MEMO, WS_WG_STACK, WS_WG_SCR, WS_S_BYTES, WS_IV_U, WS_IV_IDX, WS_IV_KEY, WS_IV_RINIT, WS_IV_MAX, WS_IV_TMP,
+    WS_HELP_START, WS_HELP_TAKEN,
     WS_COUNT
 };
 

@@ -299,7 +299,13 @@ struct DfsArgs {
     const int32_t *n_list_dev;  // if set: the list length, on the device
     int64_t budget_full;        // defer mode: past `budget` a search keeps going up to this
                                 // budget once the queue has no key left for its wave
+    // phase 2 with late helpers (k_lin_wg in helper mode): per key, the
+    // s_memrealtime at which a wave took it (0 not yet, SEQ_HANDED: gone to
+    // phase 3), and the number of waves that have left the queue
+    unsigned long long *seq_start;
+    int32_t *exit_count;
 };
+constexpr unsigned long long SEQ_HANDED = ~0ULL;
 
 constexpr int JH_CANCELLED = 3; // internal: the other search settled the key first
 
@@ -326,11 +332,16 @@ __device__ __forceinline__ bool extend_budget(const DfsArgs &A, uint32_t &budget
     return true;
 }
 constexpr int64_t P2_BUDGET = 1 << 16;  // phase-2 inserts before a key moves to phase 3
+constexpr int64_t QUICK_BUDGET = 8192;  // phase-1 inserts before a key is deferred
+constexpr int HELPERS = 16;             // phase-2 late helpers (workgroups, one per CU)
+constexpr uint64_t HELPER_LATE_US = 2000;   // a key must have run this long in the sequential search
 
 // write a key's verdict; in a race only the first finisher writes
-__device__ __forceinline__ void emit_verdict(jh_key_verdict *out, int32_t *claim, int key,
+__device__ __forceinline__ bool emit_verdict(jh_key_verdict *out, int32_t *claim, int key,
                                              const jh_key_verdict &v) {
-    if (!claim || atomicCAS(&claim[key], 0, 1) == 0) out[key] = v;
+    if (claim && atomicCAS(&claim[key], 0, 1) != 0) return false;
+    out[key] = v;
+    return true;
 }
 
 __device__ __forceinline__ uint64_t ballot(bool b) { return __ballot(b); }
@@ -1654,6 +1665,9 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         // the HBM table only (WIDE). One mode per kernel: the two searches do
         // not share a register allocation.
         if ((A.states8 && mt.maxw <= 40) != LEAN) continue;
+        if (A.seq_start && lane == 0)
+            __hip_atomic_store(&A.seq_start[key], __builtin_amdgcn_s_memrealtime() | 1ULL, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         int verdict;
         if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
@@ -1667,6 +1681,8 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
                 // progress of the quick search (deepest layer / layers): the
                 // heavy-key pass starts with the least advanced keys
                 if (A.defer_prog) A.defer_prog[d] = (uint32_t)((uint64_t)tmax * 1000000u / (uint64_t)max(1, K.n_ok));
+                if (A.seq_start)
+                    __hip_atomic_store(&A.seq_start[key], SEQ_HANDED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             continue;
         }
@@ -1683,6 +1699,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
     if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 15] = my_probes;
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
+    if (lane == 0 && A.exit_count) atomicAdd(A.exit_count, 1);
 }
 
 // Phase 1 hands keys out in list order and ends when its slowest wave ends;
@@ -1777,6 +1794,7 @@ struct WgShared {
     uint32_t npend, npend2, pend_sel, gset_used;
     uint32_t w_cur, r_cur;    // the current layer's window size and RET position
     uint32_t nchild;          // children of the staged chunk
+    unsigned long long pick;  // helper mode: (longest running, lowest list index) candidate
     uint32_t win[64];         // the current layer's window: need | becomes << 16 per member
     const uint32_t *woff;     // the key's window table (wtab_build)
     const uint32_t *wrq;
@@ -1805,6 +1823,14 @@ struct WgArgs {
     unsigned long long *key_prof;    // JH_DEBUG=4: per key {cycles, inserts, verdict | workgroup << 8}
     uint32_t acc_t;            // inserts between acceleration attempts (ACC_T; 0: plain DFS)
     unsigned long long *acc_stats;   // [0] enumerations [1] their new nodes [2] dead [3] live [4] inconclusive
+    // helper mode (late helpers of phase 2, see wg_helper_pick): the
+    // sequential search's per-key start times and exit count, a per-key
+    // taken flag, and how long (s_memrealtime ticks) a key must have run
+    const unsigned long long *seq_start;
+    const int32_t *seq_exit;
+    int32_t seq_waves;
+    int32_t *taken;
+    uint64_t late_ticks;
 };
 
 __device__ __forceinline__ uint64_t lk_make(uint32_t t, uint32_t s, uint64_t m) {
@@ -2229,7 +2255,9 @@ __device__ int dfs_acc(const WgArgs &W, WgShared &sh, const KeyInfo &K, const ch
     const uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
     const uint32_t acc_t = W.acc_t ? W.acc_t : 0x7FFFFFFFu;
     uint32_t next_acc = acc_t;
-    uint32_t chk = min(budget, acc_t);
+    // a late helper checks its key more often: it races a search that may be about to finish
+    const uint32_t chk_step = W.seq_start ? 128u : 1024u;
+    uint32_t chk = min(budget, min(acc_t, chk_step));
     uint32_t cur_seq = 0xFFFFFFFFu, cur_inc = 0;      // the root: seq -1
     int l_live = -1;                                   // deepest node known to be live
     uint32_t acc_lo = 1, acc_hi = 0;                   // layers holding merged (HBM) entries
@@ -2376,9 +2404,16 @@ insert:
         if (ins >= chk) {
             if (ins >= budget) { verdict = JH_UNKNOWN; goto done; }
             if (A.claim) {
-                // racing k_lin_bfs: stop if it settled this key first
+                // racing k_lin_bfs: stop if it settled this key first; a late
+                // helper also stops once the sequential search has handed the
+                // key to phase 3 (which settles it)
                 int c = 0;
-                if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) {
+                    c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (W.seq_start && __hip_atomic_load(&W.seq_start[key], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) == SEQ_HANDED)
+                        c = 1;
+                }
                 if (readlane(c, 0)) { verdict = JH_CANCELLED; goto done; }
             }
             if (ins >= next_acc) {
@@ -2424,7 +2459,7 @@ insert:
                     }
                 }
             }
-            chk = min(budget, min(ins + 1024, next_acc));
+            chk = min(budget, min(ins + chk_step, next_acc));
         }
         const int i = __builtin_ctzll(absent);
         const uint32_t myseq = ins;
@@ -2573,7 +2608,7 @@ pop:
                     acc_hi = max(acc_hi, acc_tmax);
                 }
                 next_acc = ins + acc_t;
-                chk = min(budget, min(ins + 1024, next_acc));
+                chk = min(budget, min(ins + chk_step, next_acc));
                 climb = true;
                 climb_jump = min(climb_jump * 2, 64u);
                 depth = dt;
@@ -2590,7 +2625,7 @@ pop:
             climb_jump = 1;
             break;
         }
-        chk = min(budget, min(ins + 1024, next_acc));
+        chk = min(budget, min(ins + chk_step, next_acc));
     }
     if (!absent) goto pop;
     child_keys();
@@ -2607,6 +2642,51 @@ done:
     return verdict;
 }
 
+// Late helpers of phase 2 (k_lin_wg in helper mode, a few CUs beside the
+// sequential search and the BFS): a workgroup takes the unclaimed LEAN key the
+// sequential search has been on longest, once that is more than late_ticks,
+// and races it with the workgroup engine (exact, so whoever settles first
+// writes the same verdict). That is the valid key with a huge reachable set
+// (too large for the BFS) and a long backtracking DFS, which otherwise holds
+// the whole step on one wave. Sets sh.key (-1: the sequential search has
+// left its queue, or the helper has waited HELPER_MAX_TICKS: done).
+constexpr unsigned long long HELPER_MAX_TICKS = 500000000ULL;   // 5 s of s_memrealtime (100 MHz)
+__device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned long long t_enter) {
+    const DfsArgs &A = W.d;
+    for (;;) {
+        if (tid == 0) {
+            sh.pick = ~0ULL;
+            sh.cmd = 0;
+            const bool over = __hip_atomic_load(W.seq_exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= W.seq_waves ||
+                              __builtin_amdgcn_s_memrealtime() - t_enter > HELPER_MAX_TICKS;
+            sh.key = over ? -1 : -2;
+        }
+        __syncthreads();
+        if (sh.key == -1) return;
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        for (int i = tid; i < A.n_list; i += WG_THREADS) {
+            const int key = A.list[i];
+            const unsigned long long s = __hip_atomic_load(&W.seq_start[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (s == 0 || s == SEQ_HANDED || s > now || now - s < W.late_ticks) continue;
+            if (__hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                __hip_atomic_load(&W.taken[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                continue;
+            const unsigned long long run = min(now - s, (1ULL << 40) - 1);
+            atomicMin(&sh.pick, (((1ULL << 40) - 1 - run) << 24) | (unsigned long long)i);
+        }
+        __syncthreads();
+        if (tid == 0 && sh.pick != ~0ULL) {
+            const int key = A.list[(int)(sh.pick & ((1u << 24) - 1))];
+            sh.key = atomicCAS(&W.taken[key], 0, 1) == 0 ? key : -3;
+        }
+        __syncthreads();
+        if (sh.key >= 0) return;
+        if (sh.key == -2)
+            for (int k = 0; k < 16; k++) __builtin_amdgcn_s_sleep(127);   // ~50 us between scans
+        __syncthreads();
+    }
+}
+
 __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
     WgShared &sh = *(WgShared *)(jh_lds + WG_SH_OFF);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -2619,8 +2699,11 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
     char *wtab = W.wtab + (size_t)blockIdx.x * W.wtab_bytes;
     uint64_t *pend = W.pend + (size_t)blockIdx.x * 2 * W.pend_cap;
     unsigned long long my_probes = 0;
+    const unsigned long long t_enter = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        if (tid == 0) {
+        if (W.seq_start) {
+            wg_helper_pick(W, sh, tid, t_enter);
+        } else if (tid == 0) {
             const int idx = atomicAdd(A.queue, 1);
             sh.key = idx < A.n_list ? A.list[idx] : -1;
             sh.cmd = 0;
@@ -2646,16 +2729,20 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
             v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
             v.explored = inserts;
             v.fail_entry = verdict == JH_INVALID ? -(int64_t)tmax - 2 : -1;
+            bool won = false;
             if (lane == 0) {
-                if (verdict != JH_CANCELLED) emit_verdict(A.out, A.claim, key, v);
+                if (verdict != JH_CANCELLED) won = emit_verdict(A.out, A.claim, key, v);
                 sh.cmd = CMD_DONE;
             }
             if (lane == 0 && W.acc_stats) atomicAdd(&W.acc_stats[7], __builtin_amdgcn_s_memtime() - ck0);
             if (lane == 0 && W.key_prof) {
-                // JH_DEBUG=4: per-key cycles / inserts / verdict for the tail analysis
+                // JH_DEBUG=4: per-key cycles / inserts / verdict | workgroup << 8 | won << 20 |
+                // start (us after the kernel's start) << 32, for the tail analysis
+                const unsigned long long t_us = (__builtin_amdgcn_s_memrealtime() - t_enter) / 100;
                 W.key_prof[3 * (size_t)key] = __builtin_amdgcn_s_memtime() - ck0;
                 W.key_prof[3 * (size_t)key + 1] = (unsigned long long)inserts;
-                W.key_prof[3 * (size_t)key + 2] = (unsigned long long)verdict | ((unsigned long long)blockIdx.x << 8);
+                W.key_prof[3 * (size_t)key + 2] = (unsigned long long)verdict | ((unsigned long long)blockIdx.x << 8) |
+                                                  ((unsigned long long)won << 20) | (t_us << 32);
             }
             __syncthreads();                    // releases the helpers
         } else {
@@ -3986,8 +4073,12 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
 
     // phase 1: every key, quick budget, persistent grid
     const uint32_t memo_cap1 = 1u << 16;
-    int64_t quick = std::min<int64_t>(budget, 4096);
-    if (const char *e = getenv("JH_QUICK_BUDGET")) quick = std::max<int64_t>(1, std::min<int64_t>(quick, atoll(e)));
+    // 8192: measured against 4096 (C3 rank 0 50.7 -> 42.4 ms, C4 635 -> 430 ms, C5 and ranks 3/4/6
+    // unchanged): phase 1 runs 15 waves per CU, phase 2 one, and phase 2 restarts a deferred
+    // key from scratch, so every key phase 1 can finish is cheaper there
+    int64_t quick = std::min<int64_t>(budget, QUICK_BUDGET);
+    if (const char *e = getenv("JH_QUICK_BUDGET"))
+        quick = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(budget, memo_cap1 / 2), atoll(e)));
     const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * (163840 / MemoQ::LDS));
     uint64_t *memo = ctx->ws<uint64_t>(WS_MEMO, (size_t)waves1 * memo_cap1 * 2, /*zero=*/true);
     if (clear_memo) HIP_TRY(hipMemsetAsync(memo, 0, ctx->bufs[WS_MEMO].bytes, st));
@@ -4289,13 +4380,33 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         uint32_t cap2 = 1u << 16;
         while ((int64_t)cap2 < 2 * budget && cap2 < (1u << 30)) cap2 <<= 1;
         if (const char *e = getenv("JH_MEMO_CAP_SHIFT")) cap2 <<= std::max(0, std::min(3, atoi(e)));   // experiments
-        const int waves2 = std::min(n_defer, std::max(1, ctx->n_cu - wg2));
+        // late helpers (k_lin_wg in helper mode, wg_helper_pick): a few CUs
+        // taken from the sequential search; JH_HELPERS=0 turns them off
+        int n_help = bfs_only || wg_race ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 16));
+        if (const char *e = getenv("JH_HELPERS")) n_help = std::max(0, std::min(64, atoi(e)));
+        if (n_help > 0 && ctx->n_cu - wg2 - n_help < 16) n_help = 0;
+        // JH_P2_M=1 (experiment): phase 2 with four waves per CU and the 32 KB memo
+        const bool p2_m = getenv("JH_P2_M") && atoi(getenv("JH_P2_M"));
+        const int waves2 = std::min(n_defer, std::max(1, (ctx->n_cu - wg2 - n_help) * (p2_m ? 4 : 1)));
         // generation-tagged: zeroed once when allocated (and on wrap), not per call
         const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;
         uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
         if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
         WgArgs wr{};
         if (wg_race) wr = build_wg(std::max(1, ctx->n_cu - wg2), claim, q + 6);
+        WgArgs wh{};
+        unsigned long long *seq_start = nullptr;
+        if (n_help > 0) {
+            wh = build_wg(n_help, claim, nullptr);
+            seq_start = ctx->ws<unsigned long long>(WS_HELP_START, K);
+            int32_t *taken = ctx->ws<int32_t>(WS_HELP_TAKEN, K);
+            HIP_TRY(hipMemsetAsync(seq_start, 0, (size_t)K * sizeof(unsigned long long), st));
+            HIP_TRY(hipMemsetAsync(taken, 0, (size_t)K * sizeof(int32_t), st));
+            wh.seq_start = seq_start; wh.seq_exit = q + 28; wh.seq_waves = waves2; wh.taken = taken;
+            uint64_t late_us = HELPER_LATE_US;
+            if (const char *e = getenv("JH_HELPER_LATE_US")) late_us = (uint64_t)std::max(0, atoi(e));
+            wh.late_ticks = late_us * 100;     // s_memrealtime: 100 MHz
+        }
         // the fork point: everything the phase-2 searches read (claims, queue
         // counters, the cleared memo on a generation wrap) is ordered before it
         HIP_TRY(hipEventRecord(ctx->ev[6], st));
@@ -4315,6 +4426,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         b.gen_base = ctx->gen_base + (uint32_t)K + 1;
         b.dbg = dbg ? dbg + 16 * 256 : nullptr; b.claim = claim;
         b.probes = (unsigned long long *)(q + 8);
+        b.seq_start = seq_start; b.exit_count = seq_start ? q + 28 : nullptr;
 
         // fork: the BFS on st, the sequential search on the aux stream
         HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
@@ -4324,13 +4436,23 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         {
             DfsArgs bw = b;
             bw.queue = q + 7;
+            bw.seq_start = nullptr; bw.exit_count = nullptr;
             k_lin_seq<false><<<std::min(waves2, 32), 64, MemoH::LDS, ctx->aux>>>(bw);
         }
         if (bfs_only) {}
         else if (wg_race) k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux>>>(wr);
+        else if (p2_m) k_lin_seq3<true><<<waves2, 64, MemoM::LDS, ctx->aux>>>(b);
         else k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
+        if (n_help > 0) {
+            // every helper leaves once the sequential search has left its
+            // queue (or after HELPER_MAX_TICKS): joined before the verdicts are read
+            HIP_TRY(hipStreamWaitEvent(ctx->aux3, ctx->ev[6], 0));
+            k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux3>>>(wh);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(ctx->ev[12], ctx->aux3));
+        }
         if (split3) {
             // phase 3: the keys phase 2 handed over, full budget, 4 waves per CU
             int32_t q16 = 0;
@@ -4348,6 +4470,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             char *scr3 = ctx->ws<char>(WS_SCRATCH_P3, (size_t)waves3 * MemoH::SLOTS * 8);
             DfsArgs c3 = b;
             c3.list = defer3; c3.n_list = n_defer3; c3.queue = q + 17; c3.defer = 0;
+            c3.seq_start = nullptr; c3.exit_count = nullptr;
             c3.memo = memo3; c3.stack = stack3; c3.scratch = scr3; c3.scratch_bytes = MemoH::SLOTS * 8;
             c3.budget = budget;
             // a fresh generation range: phase 2's table entries of these keys are not reused
@@ -4369,6 +4492,18 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         }
         HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
         HIP_TRY(hipStreamWaitEvent(st, ctx->ev[7], 0));
+        if (n_help > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[12], 0));
+        if (n_help > 0 && wh.key_prof) {
+            // JH_DEBUG=4: what the late helpers took (end time in us after their start)
+            HIP_TRY(hipStreamSynchronize(st));
+            std::vector<unsigned long long> kp(3 * (size_t)K);
+            HIP_TRY(hipMemcpy(kp.data(), wh.key_prof, kp.size() * 8, hipMemcpyDeviceToHost));
+            for (int64_t k = 0; k < K; k++)
+                if (kp[3 * k])
+                    fprintf(stderr, "[jh-help] key %lld wg %llu verdict %llu won %llu inserts %llu cycles %llu end_us %llu\n",
+                            (long long)k, (kp[3 * k + 2] >> 8) & 0xFFF, kp[3 * k + 2] & 0xFF, (kp[3 * k + 2] >> 20) & 1,
+                            kp[3 * k + 1], kp[3 * k], kp[3 * k + 2] >> 32);
+        }
         if (const char *dp = getenv("JH_BFS_DUMP")) {
             // debugging: workgroup 0's stored configurations (t:20 | s:12 | mask:32)
             HIP_TRY(hipStreamSynchronize(st));

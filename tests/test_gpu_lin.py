@@ -84,6 +84,29 @@ def test_heavy_key_paths(ctx, quick, monkeypatch):
     _same(g, c)
 
 
+@pytest.mark.parametrize("env", [
+    {"JH_HELPER_LATE_US": "0", "JH_QUICK_BUDGET": "40"},
+    {"JH_HELPER_LATE_US": "0", "JH_QUICK_BUDGET": "40", "JH_HELPERS": "48"},
+    {"JH_HELPER_LATE_US": "0", "JH_QUICK_BUDGET": "40", "JH_P2_BUDGET": "300"},
+    {"JH_HELPER_LATE_US": "0", "JH_QUICK_BUDGET": "40", "JH_P2_M": "1"},
+    {"JH_HELPERS": "0", "JH_QUICK_BUDGET": "40"},
+])
+def test_late_helpers(ctx, env, monkeypatch):
+    """Phase-2 late helpers (the workgroup engine racing the sequential search
+    and the BFS on long-running keys): with no delay every deferred key gets a
+    helper, which settles some of them first, hands others back when phase 3
+    takes the key (small phase-2 budget), or loses the race. Every verdict,
+    cause, failing row and WGL count must equal the oracle's, at the full
+    budget and at a budget the helpers run into."""
+    cols, _ = synth.cas_register(n_keys=400, ops_per_key=200, p_invalid=0.1, p_info=0.05, seed=95)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for budget in (None, 3000):
+        g, _ = ctx.check_cas_independent(cols, budget=budget)
+        c, _ = oracle.check_cas_independent(cols, budget=budget or A.DEFAULT_BUDGET, threads=8)
+        _same(g, c)
+
+
 @pytest.mark.parametrize("p2", ["4097", "9000"])
 def test_phase3_handover(ctx, p2, monkeypatch):
     """Keys past the phase-2 budget restart in phase 3 (4 waves per CU, HBM

@@ -1,7 +1,7 @@
 """One independent cas-register check of a bench.py workload's rank-0 history
 on cuda:0, for profilers (rocprofv3 --pmc / --kernel-trace wrap this).
 
-    python tools/run_once.py c3|c4|c5 [reps]
+    python tools/run_once.py c3|c4|c5 [reps] [seed-rank]
 """
 import os
 import sys
@@ -13,7 +13,8 @@ from jepsen_amd import _native, synth  # noqa: E402
 
 wl = WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "c3"]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-cols, _ = synth.cas_register(n_keys=wl["keys"], ops_per_key=500, seed=wl["seed"], **wl["gen"])
+rank = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+cols, _ = synth.cas_register(n_keys=wl["keys"], ops_per_key=500, seed=wl["seed"] + 7919 * rank, **wl["gen"])
 ctx = _native.Context(0)
 for _ in range(reps):
     v, s = ctx.check_cas_independent(cols)

@@ -59,6 +59,22 @@ def lib():
                                                C.c_int64, C.c_char_p, C.c_size_t]
             L.jh_check_queue.argtypes = [C.c_void_p, H, C.POINTER(A.JhQueueResult), p64, C.c_int64,
                                          C.c_char_p, C.c_size_t]
+            # history ingest (include/jh_io.h), host code in the same library
+            pp = C.POINTER(C.c_void_p)
+            L.jh_ingest_file.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, pp, C.c_char_p, C.c_size_t]
+            L.jh_ingest_buffer.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.c_int, pp,
+                                           C.c_char_p, C.c_size_t]
+            L.jh_ingest_history.argtypes = [C.c_void_p, H]
+            L.jh_ingest_history.restype = None
+            L.jh_ingest_time.argtypes = [C.c_void_p]
+            L.jh_ingest_time.restype = p64
+            L.jh_ingest_values_interned.argtypes = [C.c_void_p]
+            L.jh_ingest_table_size.argtypes = [C.c_void_p, C.c_int]
+            L.jh_ingest_table_size.restype = C.c_int64
+            L.jh_ingest_table_entry.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_char_p, C.c_size_t]
+            L.jh_ingest_table_entry.restype = C.c_int64
+            L.jh_ingest_free.argtypes = [C.c_void_p]
+            L.jh_ingest_free.restype = None
             if L.jh_version() != A.JH_ABI_VERSION:
                 raise RuntimeError("libjh.so ABI version mismatch")
             _lib = L
@@ -68,7 +84,10 @@ def lib():
 EXPORTED_SYMBOLS = ["jh_version", "jh_open", "jh_open_multi", "jh_open_devices", "jh_n_devices", "jh_key_costs", "jh_key_index",
                     "jh_close", "jh_check_cas_independent",
                     "jh_check_cas", "jh_check_cas_independent_device", "jh_check_counter",
-                    "jh_check_set", "jh_check_set_full", "jh_check_total_queue", "jh_check_queue"]
+                    "jh_check_set", "jh_check_set_full", "jh_check_total_queue", "jh_check_queue",
+                    # include/jh_io.h
+                    "jh_ingest_file", "jh_ingest_buffer", "jh_ingest_history", "jh_ingest_time",
+                    "jh_ingest_values_interned", "jh_ingest_table_size", "jh_ingest_table_entry", "jh_ingest_free"]
 
 
 def _raise(rc, err):

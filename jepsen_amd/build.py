@@ -17,7 +17,9 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build")
 HIP_SOURCES = ["jh_lin.hip", "jh_counter.hip", "jh_set.hip", "jh_setfull.hip", "jh_queue.hip", "jh_api.hip", "jh_multi.hip"]
+HOST_SOURCES = ["jh_io.cpp"]
 HEADERS = [os.path.join(CSRC, "jh_internal.h"), os.path.join(ROOT, "include", "jh.h")]
+HOST_HEADERS = [os.path.join(ROOT, "include", "jh.h"), os.path.join(ROOT, "include", "jh_io.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 HIPFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
@@ -54,13 +56,20 @@ def build_libjh(verbose=False):
         objs.append(obj)
         if _newer(obj, [src] + HEADERS):
             jobs.append([HIPCC] + HIPFLAGS + ["-c", src, "-o", obj])
+    # host-only sources (history ingest, include/jh_io.h): g++, linked into libjh.so
+    for s in HOST_SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(OBJ, s.replace(".cpp", ".o"))
+        objs.append(obj)
+        if _newer(obj, [src] + HOST_HEADERS):
+            jobs.append(["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-pthread", "-c", src, "-o", obj])
     with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         for out in ex.map(_run, jobs):
             if verbose and out.strip():
                 print(out)
     lib = os.path.join(HERE, "libjh.so")
     if _newer(lib, objs):
-        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs)
+        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-pthread", "-o", lib] + objs)
     return lib
 
 

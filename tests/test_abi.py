@@ -1,5 +1,6 @@
-"""The drop-in boundary: libjh.so loads and exports every symbol include/jh.h
-declares, and the ctypes mirror has the C layout (no GPU, no compute calls)."""
+"""The drop-in boundary: libjh.so loads and exports every symbol include/*.h
+(jh.h, jh_io.h) declares, and the ctypes mirror has the C layout (no GPU, no
+compute calls)."""
 import ctypes as C
 import os
 import re
@@ -9,11 +10,12 @@ from conftest import ROOT
 from jepsen_amd import _abi as A
 
 HEADER = os.path.join(ROOT, "include", "jh.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "jh_io.h")]
 
 
 def declared_symbols():
-    src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void)\s+\*?(jh_\w+)\s*\(", src, re.M)))
+    src = "".join(open(h).read() for h in HEADERS)
+    return sorted(set(re.findall(r"^\s*(?:int|void|int64_t|const int64_t)\s+\*?(jh_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_the_abi():

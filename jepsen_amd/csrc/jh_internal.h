@@ -104,7 +104,7 @@ enum WsSlot {
     WS_Q_OUT, WS_Q_KEYS, WS_Q_MULT2, WS_LCOST, WS_LSORT, WS_LTMP, WS_ACC_STATS, WS_WG_GSET, WS_WG_WORK, WS_WG_WTAB, WS_WG_PEND, WS_STATS_KEYS,
     WS_BFS_NODES, WS_BFS_LSTART, WS_BFS_HKEY, WS_BFS_HID, WS_BFS_LIVE, WS_BFS_VIS, WS_BFS_TMP,
     WS_WG_MEMO, WS_WG_STACK, WS_WG_SCR, WS_S_BYTES, WS_IV_U, WS_IV_IDX, WS_IV_KEY, WS_IV_RINIT, WS_IV_MAX, WS_IV_TMP,
-    WS_HELP_START, WS_HELP_TAKEN,
+    WS_HELP_START, WS_HELP_TAKEN, WS_DEFER_TIME, WS_BFS_TMPK,
     WS_COUNT
 };
 

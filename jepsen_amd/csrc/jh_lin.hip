@@ -304,6 +304,9 @@ struct DfsArgs {
     // phase 3), and the number of waves that have left the queue
     unsigned long long *seq_start;
     int32_t *exit_count;
+    // JH_DEFER_TIMES=1 (timeline study): [0] first wave start, [1] last wave
+    // end (s_memrealtime), [2 + key] the time the key was handed on
+    unsigned long long *defer_time;
 };
 constexpr unsigned long long SEQ_HANDED = ~0ULL;
 
@@ -1647,6 +1650,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     unsigned long long my_probes = 0;
     const int n_list = A.n_list_dev ? *A.n_list_dev : A.n_list;
     const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
+    if (A.defer_time && lane == 0) atomicMin(&A.defer_time[0], __builtin_amdgcn_s_memrealtime());
     for (;;) {
         int idx = 0;
         if (lane == 0) idx = atomicAdd(A.queue, 1);
@@ -1681,6 +1685,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
                 // progress of the quick search (deepest layer / layers): the
                 // heavy-key pass starts with the least advanced keys
                 if (A.defer_prog) A.defer_prog[d] = (uint32_t)((uint64_t)tmax * 1000000u / (uint64_t)max(1, K.n_ok));
+                if (A.defer_time) A.defer_time[2 + key] = __builtin_amdgcn_s_memrealtime();
                 if (A.seq_start)
                     __hip_atomic_store(&A.seq_start[key], SEQ_HANDED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -1700,6 +1705,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 15] = my_probes;
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
     if (lane == 0 && A.exit_count) atomicAdd(A.exit_count, 1);
+    if (A.defer_time && lane == 0) atomicMax(&A.defer_time[1], __builtin_amdgcn_s_memrealtime());
 }
 
 // Phase 1 hands keys out in list order and ends when its slowest wave ends;
@@ -2780,8 +2786,13 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
 constexpr int BFS_THREADS = 512;
 constexpr int BFS_HDR = 1024;                      // shared scalars + the layer's window
 constexpr int BFS_TBL = 28672;                     // W-format tables (ops, woff, W) + r[]
-constexpr int LSET = 8192;                         // layer set slots (8 B keys)
-constexpr int BFS_LDS_BYTES = BFS_HDR + BFS_TBL + LSET * 8;   // ~94 KB: one workgroup per CU
+constexpr int LSET = 16384;                        // layer set slots (8 B keys)
+constexpr int BFS_LDS_BYTES = BFS_HDR + BFS_TBL + LSET * 8;   // 157 KB: one workgroup per CU
+// the count pass's LDS-resident liveness of one layer (over the free layer set):
+// keys, global slots, a key -> local index hash, live flags
+constexpr int LV_CAP = 4096, LV_H = 8192;
+static_assert(LV_CAP * 8 + LV_CAP * 4 + LV_H * 4 + LV_CAP + LV_CAP * 2 + 512 <= LSET * 8, "liveness LDS");
+__device__ __forceinline__ uint32_t lv_hash(uint64_t k) { return (uint32_t)jh_mix64(k) & (LV_H - 1); }
 constexpr uint64_t BFS_EMPTY = ~0ULL;
 // A valid key is settled by the BFS (instead of waiting for the sequential
 // search) when its whole reachable set is complete and smaller than the
@@ -2821,6 +2832,7 @@ struct BfsArgs {
     uint32_t *slot;         // ncap: each node's hash slot
     uint32_t *vis;          // ncap / 32 + 1
     uint32_t *tmp;          // ncap
+    uint64_t *tmpk;         // ncap: the liveness pass's node keys, beside their slots in tmp
 };
 
 struct BfsShared {
@@ -2977,7 +2989,11 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
     if (sh.nostore) return;
     const uint32_t N = sh.nnodes;
     if ((uint64_t)N * 2 > A.hcap) return;
-    const uint32_t hmask = A.hcap - 1;
+    // the hash sized to this key: load <= 1/4 where it fits (short probe
+    // chains: every liveness / closure lookup is an HBM round trip)
+    uint32_t hc = 1u << 12;
+    while (hc < A.hcap && (uint64_t)hc < 4ull * N) hc <<= 1;
+    const uint32_t hmask = hc - 1;
     ulonglong2 *ent = A.ent;
     uint32_t *slot_of = A.slot;
     unsigned long long *dq = A.dbg ? A.dbg + 16 * (size_t)blockIdx.x : nullptr;   // JH_DEBUG=2 phase cycles
@@ -2988,15 +3004,37 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
         tq = n;
     };
     // ---- node -> slot hash ----------------------------------------------------
-    for (uint32_t i = tid; i < A.hcap; i += BFS_THREADS) ent[i] = make_ulonglong2(BFS_EMPTY, 0);
+    for (uint32_t i = tid; i < hc; i += BFS_THREADS) ent[i] = make_ulonglong2(BFS_EMPTY, 0);
     for (uint32_t i = tid; i < N / 32 + 1; i += BFS_THREADS) A.vis[i] = 0;
     __syncthreads();
-    for (uint32_t i = tid; i < N; i += BFS_THREADS) {
-        const uint64_t k = A.nodes[i];
-        uint32_t h = (uint32_t)jh_mix64(k) & hmask;
-        while (atomicCAS((unsigned long long *)&ent[h].x, BFS_EMPTY, k) != BFS_EMPTY) h = (h + 1) & hmask;
-        ent[h].y = i;
-        slot_of[i] = h;
+    // four nodes per thread per pass, their first CAS in flight together
+    for (uint32_t i0 = tid; i0 < N; i0 += 4 * BFS_THREADS) {
+        uint64_t k[4];
+        uint32_t h[4];
+        unsigned long long pv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + (uint32_t)u * BFS_THREADS;
+            k[u] = i < N ? A.nodes[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + (uint32_t)u * BFS_THREADS;
+            h[u] = (uint32_t)jh_mix64(k[u]) & hmask;
+            pv[u] = i < N ? atomicCAS((unsigned long long *)&ent[h[u]].x, BFS_EMPTY, k[u]) : BFS_EMPTY;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + (uint32_t)u * BFS_THREADS;
+            if (i >= N) continue;
+            uint32_t hh = h[u];
+            while (pv[u] != BFS_EMPTY) {
+                hh = (hh + 1) & hmask;
+                pv[u] = atomicCAS((unsigned long long *)&ent[hh].x, BFS_EMPTY, k[u]);
+            }
+            ent[hh].y = i;
+            slot_of[i] = hh;
+        }
     }
     __syncthreads();
     stamp(5);
@@ -3004,6 +3042,7 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
     // descending (same-layer edges add one member) ------------------------------
     uint32_t *hist = (uint32_t *)(jh_lds + BFS_HDR + BFS_TBL);     // the layer set's LDS, free now
     for (int t = (int)n_ok - 1; t >= 0; t--) {
+        const unsigned long long lt0 = __builtin_amdgcn_s_memtime();
         if (A.claim && tid == 0 &&
             __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
             sh.status |= 4;
@@ -3011,6 +3050,7 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
         __syncthreads();
         if (sh.status) return;
         if (a == b) continue;
+        if (dq && tid == 0) { dq[14] += 1; dq[15] += __builtin_amdgcn_s_memtime() - lt0; }
         if (tid < 66) hist[tid] = 0;
         const int w = woff[t + 1] - woff[t];
         if (tid < 64) {       // the layer's window into LDS, as in the forward pass
@@ -3022,6 +3062,104 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
         }
         const uint32_t rt = rpos[t];
         __syncthreads();
+        if (b - a <= (uint32_t)LV_CAP) {
+            // The layer in LDS. A node's children are one cross-layer child
+            // (member RET[t], into a later layer whose liveness is final) and
+            // same-layer children (one member more, so one popcount higher):
+            // the cross-layer lookups of the whole layer go out together (one
+            // HBM round trip), then the same-layer liveness runs by popcount
+            // descending on LDS only, and the live marks go back in one pass.
+            const uint32_t n = b - a;
+            uint64_t *lk = (uint64_t *)(jh_lds + BFS_HDR + BFS_TBL + 512);
+            uint32_t *ls = (uint32_t *)(lk + LV_CAP);
+            uint32_t *lh = ls + LV_CAP;
+            uint8_t *lv = (uint8_t *)(lh + LV_H);
+            uint16_t *ord = (uint16_t *)(lv + LV_CAP);            // nodes by popcount, descending
+            for (uint32_t i = tid; i < LV_H; i += BFS_THREADS) lh[i] = 0;
+            if (tid < 2) hist[tid] = tid ? 0u : 32u;               // [0] min popcount, [1] max
+            if (tid >= 2 && tid < 2 + 2 * 33) hist[tid] = 0;      // [2+p] count, [35+p] fill
+            __syncthreads();
+            for (uint32_t i = tid; i < n; i += BFS_THREADS) {
+                const uint64_t x = A.nodes[a + i];
+                const uint32_t sl = slot_of[a + i];
+                lk[i] = x;
+                ls[i] = sl;
+                const uint32_t pc = (uint32_t)__popc((uint32_t)x);
+                atomicMin(&hist[0], pc);
+                atomicMax(&hist[1], pc);
+                atomicAdd(&hist[2 + pc], 1u);
+                uint32_t h = lv_hash(x);
+                while (atomicCAS(&lh[h], 0u, i + 1) != 0u) h = (h + 1) & (LV_H - 1);
+                // the cross-layer child (or a terminal one)
+                uint64_t ck = 0;
+                const int c = bfs_child_w(sh, rpos, n_ok, (uint32_t)t, rt, w, (uint32_t)(x >> 32) & 0xFFF, (uint32_t)x,
+                                          (int)rt, &ck);
+                bool live = c == 3;
+                if (c == 2) {
+                    const int64_t cs = bfs_slot(ent, hmask, ck);
+                    live = cs >= 0 && (bfs_info(ent, (uint32_t)cs) & BFS_LIVE);
+                }
+                lv[i] = live ? 1 : 0;
+            }
+            __syncthreads();
+            if (tid == 0) {                                         // bucket starts, largest first
+                uint32_t acc = 0;
+                for (int p = 32; p >= 0; p--) { hist[35 + p] = acc; acc += hist[2 + p]; }
+            }
+            __syncthreads();
+            for (uint32_t i = tid; i < n; i += BFS_THREADS)
+                ord[atomicAdd(&hist[35 + __popc((uint32_t)lk[i])], 1u)] = (uint16_t)i;
+            __syncthreads();
+            const int pmin = (int)hist[0], pmax = (int)hist[1];
+            const uint32_t nb = (uint32_t)(w + 7) / 8;
+            for (int p = pmax; p >= pmin; p--) {
+                // one item per (node, 8 members): the 8 children's LDS probes issue together
+                const uint32_t cnt = hist[2 + p], b0 = hist[35 + p] - cnt;
+                for (uint32_t q = tid; q < cnt * nb; q += BFS_THREADS) {
+                    const uint32_t i = ord[b0 + q / nb];
+                    const int j0 = (int)(q % nb) * 8;
+                    if (lv[i]) continue;
+                    const uint64_t x = lk[i];
+                    const uint32_t s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
+                    uint64_t ck[8];
+                    uint32_t h[8], e[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        ck[u] = 0;
+                        const int j = j0 + u;
+                        if ((uint32_t)j != rt && bfs_child_w(sh, rpos, n_ok, (uint32_t)t, rt, w, s0, m0, j, &ck[u]) != 1)
+                            ck[u] = 0;
+                        if ((uint32_t)j == rt) ck[u] = 0;
+                        h[u] = lv_hash(ck[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; u++) e[u] = ck[u] ? lh[h[u]] : 0u;
+                    uint64_t kk[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) kk[u] = e[u] ? lk[e[u] - 1] : 0;
+                    bool live = false;
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        if (!ck[u] || !e[u]) continue;
+                        uint32_t idx = 0;
+                        if (kk[u] == ck[u]) idx = e[u];
+                        else
+                            for (uint32_t hh = (h[u] + 1) & (LV_H - 1);; hh = (hh + 1) & (LV_H - 1)) {
+                                const uint32_t ee = lh[hh];
+                                if (ee == 0) break;
+                                if (lk[ee - 1] == ck[u]) { idx = ee; break; }
+                            }
+                        if (idx && lv[idx - 1]) live = true;
+                    }
+                    if (live) lv[i] = 1;
+                }
+                __syncthreads();
+            }
+            for (uint32_t i = tid; i < n; i += BFS_THREADS)
+                if (lv[i]) atomicOr((unsigned long long *)&ent[ls[i]].y, BFS_LIVE);
+            if (dq && tid == 0) { dq[2] += __builtin_amdgcn_s_memtime() - lt0; dq[14] += 1ULL << 32; }
+            continue;                                              // (the loop head syncs)
+        }
         for (uint32_t i = a + tid; i < b; i += BFS_THREADS)
             atomicAdd(&hist[__popc((uint32_t)A.nodes[i])], 1u);
         __syncthreads();
@@ -3030,20 +3168,27 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
             for (int p = 32; p >= 0; p--) { const uint32_t c = hist[p]; hist[33 + p] = acc; hist[p] = acc; acc += c; }
         }
         __syncthreads();
-        for (uint32_t i = a + tid; i < b; i += BFS_THREADS)
-            A.tmp[atomicAdd(&hist[__popc((uint32_t)A.nodes[i])], 1u)] = slot_of[i];
+        for (uint32_t i = a + tid; i < b; i += BFS_THREADS) {
+            const uint64_t x = A.nodes[i];
+            const uint32_t pos = atomicAdd(&hist[__popc((uint32_t)x)], 1u);
+            A.tmp[pos] = slot_of[i];
+            A.tmpk[pos] = x;
+        }
         __syncthreads();
+        // one work item per (node, 8 members): the children's lookups of a
+        // bucket all in flight at once, instead of a node's batches in series
+        const uint32_t nb = (uint32_t)(w + 7) / 8;
         for (int p = 32; p >= 0; p--) {
             const uint32_t bs = hist[33 + p], be = p > 0 ? hist[33 + p - 1] : b - a;
             if (bs == be) continue;
-            for (uint32_t q = bs + tid; q < be; q += BFS_THREADS) {
-                const uint32_t sl = A.tmp[q];
-                const uint64_t x = bfs_keyat(ent, sl);
+            const uint32_t items = (be - bs) * nb;
+            for (uint32_t q = tid; q < items; q += BFS_THREADS) {
+                const uint32_t sl = A.tmp[bs + q / nb];
+                const int j0 = (int)(q % nb) * 8;
+                const uint64_t x = A.tmpk[bs + q / nb];
                 const uint32_t s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
-                bool lv = false;
-                for (int j0 = 0; j0 < w && !lv; j0 += 8)
-                    lv = bfs_any_live8(ent, hmask, sh, rpos, n_ok, (uint32_t)t, rt, w, s0, m0, j0);
-                if (lv) atomicOr((unsigned long long *)&ent[sl].y, BFS_LIVE);
+                if (bfs_any_live8(ent, hmask, sh, rpos, n_ok, (uint32_t)t, rt, w, s0, m0, j0))
+                    atomicOr((unsigned long long *)&ent[sl].y, BFS_LIVE);
             }
             __syncthreads();
         }
@@ -3102,11 +3247,15 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
         if (nf == 0 || nf > A.ncap / 2) break;
         { uint32_t *tp = fa; fa = fb; fb = tp; }
         __syncthreads();
-        for (uint32_t q = tid; q < nf; q += BFS_THREADS) {
-            const uint64_t x = bfs_keyat(ent, fa[q]);
+        // one work item per (node, 8 members), as in the liveness pass
+        const uint32_t nbc = (uint32_t)(sh.maxw + 7) / 8;
+        for (uint32_t qq = tid; qq < nf * nbc; qq += BFS_THREADS) {
+            const uint64_t x = bfs_keyat(ent, fa[qq / nbc]);
             const uint32_t t = (uint32_t)(x >> 44), s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
             const int w = woff[t + 1] - woff[t];
-            for (int j0 = 0; j0 < w; j0 += 8) {
+            {
+                const int j0 = (int)(qq % nbc) * 8;
+                if (j0 >= w) continue;
                 uint64_t k[8];
                 int64_t sl[8];
                 uint64_t inf[8];
@@ -3238,8 +3387,16 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             if (tid == 0) { sh.mode = 1; sh.ovf = 0; }
             __syncthreads();
         };
-        // insert (s, mask) of layer t; returns true if new
-        auto insert = [&](uint32_t cs, uint32_t cm) -> bool {
+        // a configuration new to the set: count it, store it for the WGL count
+        auto added = [&](uint32_t cs, uint32_t cm) -> bool {
+            const unsigned long long n = atomicAdd(&sh.count, 1ULL);
+            if ((long long)n >= A.reach_cap) atomicOr(&sh.status, 2);
+            const unsigned id = atomicAdd(&sh.nnodes, 1u);
+            if (id < A.ncap) A.nodes[id] = bfs_pack(t, cs, cm); else sh.nostore = 1;
+            return true;
+        };
+        // insert (s, mask) of layer t into the set; true if new (not counted yet)
+        auto insert_raw = [&](uint32_t cs, uint32_t cm) -> bool {
             if (sh.status & 2) return false;
             if (sh.mode == 0) {
                 // keep the LDS set under 3/4 load (+ at most one insert per thread in flight)
@@ -3264,11 +3421,79 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                     h = (h + 1) & gmask;
                 }
             }
-            const unsigned long long n = atomicAdd(&sh.count, 1ULL);
-            if ((long long)n >= A.reach_cap) atomicOr(&sh.status, 2);
-            const unsigned id = atomicAdd(&sh.nnodes, 1u);
-            if (id < A.ncap) A.nodes[id] = bfs_pack(t, cs, cm); else sh.nostore = 1;
             return true;
+        };
+        auto insert = [&](uint32_t cs, uint32_t cm) -> bool { return insert_raw(cs, cm) && added(cs, cm); };
+        // the global set's inserts of up to 8 children, their first probes all
+        // in flight together (a lone CAS per child was one HBM round trip each,
+        // serial per thread: the forward pass's bound once a layer is global)
+        auto insert8 = [&](const uint64_t (&ck)[8], bool (&nw)[8]) {
+            if (sh.mode == 0) {
+#pragma unroll
+                for (int q = 0; q < 8; q++) nw[q] = ck[q] ? insert_raw((uint32_t)(ck[q] >> 32), (uint32_t)ck[q]) : false;
+                return;
+            }
+            uint64_t g[8];
+            uint32_t h[8];
+            unsigned long long prev[8];
+            const bool off = (sh.status & 2) != 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                nw[q] = false;
+                g[q] = bfs_pack(t, (uint32_t)(ck[q] >> 32), (uint32_t)ck[q]);
+                h[q] = (uint32_t)jh_mix64(g[q]) & gmask;
+                prev[q] = (ck[q] && !off) ? atomicCAS((unsigned long long *)&gset[h[q]], BFS_EMPTY, g[q]) : (unsigned long long)g[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                if (!ck[q] || off) continue;
+                if (prev[q] == g[q]) continue;
+                if (prev[q] != BFS_EMPTY) {
+                    uint32_t hh = h[q];
+                    bool dup = false;
+                    for (uint32_t probe = 1;; probe++) {
+                        if (probe > gmask) { atomicOr(&sh.status, 2); dup = true; break; }
+                        hh = (hh + 1) & gmask;
+                        const unsigned long long pv = atomicCAS((unsigned long long *)&gset[hh], BFS_EMPTY, g[q]);
+                        if (pv == BFS_EMPTY) break;
+                        if (pv == g[q]) { dup = true; break; }
+                    }
+                    if (dup) continue;
+                }
+                nw[q] = true;
+            }
+        };
+        // the new children of a batch, counted once per wave: one LDS atomic
+        // per counter per wave instead of three per configuration (same-address
+        // LDS atomics serialise lane by lane); wave-uniform control flow
+        auto record8 = [&](const uint64_t (&ck)[8], const bool (&nw)[8]) {
+            uint32_t below[8], tot = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint64_t bq = ballot(nw[q]);
+                below[q] = tot + mbcnt(bq);
+                tot += (uint32_t)__popcll(bq);
+            }
+            if (tot == 0) return;
+            unsigned nb0 = 0, fb0 = 0;
+            if (lane == 0) {
+                const unsigned long long c0 = atomicAdd(&sh.count, (unsigned long long)tot);
+                if ((long long)(c0 + tot) > A.reach_cap) atomicOr(&sh.status, 2);
+                nb0 = atomicAdd(&sh.nnodes, tot);
+                fb0 = atomicAdd(&sh.nnext, tot);
+            }
+            nb0 = readlane(nb0, 0);
+            fb0 = readlane(fb0, 0);
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                if (!nw[q]) continue;
+                const unsigned id = nb0 + below[q];
+                if (id < A.ncap) A.nodes[id] = bfs_pack(t, (uint32_t)(ck[q] >> 32), (uint32_t)ck[q]);
+                else sh.nostore = 1;
+                const unsigned pos = fb0 + below[q];
+                if (pos < A.q_cap) fnxt[pos] = ck[q];
+                else atomicOr(&sh.status, 2);
+            }
         };
         // An insert refused for LDS load (ovf) re-runs the pass against the
         // global set: configurations already inserted stay (and are already on
@@ -3303,6 +3528,8 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         while (sh.nfront > 0 && !sh.status) {
             rounds++;
             const unsigned nf = sh.nfront;
+            const unsigned long long rt0 = __builtin_amdgcn_s_memtime();
+            const int mode_at = sh.mode;
             if (tid == 0) {
                 sh.nnext = 0;
                 // the sequential search settled this key: stop at the next round
@@ -3312,38 +3539,43 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             __syncthreads();
             if (sh.status & 4) break;
             for (;;) {
-            for (unsigned i = tid; i < nf; i += BFS_THREADS) {
-                const uint64_t c = fcur[i];
+            for (unsigned i0 = tid - lane; i0 < nf; i0 += BFS_THREADS) {
+                const unsigned i = i0 + lane;
+                const uint64_t c = i < nf ? fcur[i] : 0xFFFFFFFFull;    // past the end: every member taken
                 const uint32_t s = (uint32_t)(c >> 32), mask = (uint32_t)c;
-                for (int j = 0; j < w; j++) {
-                    if ((mask >> j) & 1) continue;
-                    const uint32_t f = sh.win_f[j], vv = sh.win_vv[j];
-                    const int v1 = (int)(vv & 0xFFFF), v2 = (int)(vv >> 16);
-                    int s2;
-                    if (!cas_step((int)f, v1, v2, (int)s, &s2)) continue;
-                    if ((uint32_t)j == r) {
-                        // cross-layer edge: drop RET members until one is not linearized
-                        uint64_t nm = mask | (1u << j);
-                        uint32_t u = t, ru = r;
-                        for (;;) {
-                            nm = drop_bit(nm, ru);
-                            u++;
-                            if (u >= n_ok) break;
-                            ru = rpos[u];
-                            if (!((nm >> ru) & 1)) break;
-                        }
-                        if (u >= n_ok) { sh.term = 1; continue; }   // a terminal configuration
-                        const unsigned pos = atomicAdd(&sh.npend, 1u);
-                        if (pos < A.q_cap) pcur[pos] = bfs_pack(u, (uint32_t)s2, (uint32_t)nm);
-                        else atomicOr(&sh.status, 2);
-                    } else {
-                        const uint32_t cm = mask | (1u << j);
-                        if (insert((uint32_t)s2, cm)) {
-                            const unsigned pos = atomicAdd(&sh.nnext, 1u);
-                            if (pos < A.q_cap) fnxt[pos] = ((uint64_t)(uint32_t)s2 << 32) | cm;
+                for (int j0 = 0; j0 < w; j0 += 8) {
+                    uint64_t ck[8];       // same-layer children of members j0..j0+7: s2 << 32 | mask'
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        ck[q] = 0;
+                        const int j = j0 + q;
+                        if (j >= w || ((mask >> j) & 1)) continue;
+                        const uint32_t f = sh.win_f[j], vv = sh.win_vv[j];
+                        const int v1 = (int)(vv & 0xFFFF), v2 = (int)(vv >> 16);
+                        int s2;
+                        if (!cas_step((int)f, v1, v2, (int)s, &s2)) continue;
+                        if ((uint32_t)j == r) {
+                            // cross-layer edge: drop RET members until one is not linearized
+                            uint64_t nm = mask | (1u << j);
+                            uint32_t u = t, ru = r;
+                            for (;;) {
+                                nm = drop_bit(nm, ru);
+                                u++;
+                                if (u >= n_ok) break;
+                                ru = rpos[u];
+                                if (!((nm >> ru) & 1)) break;
+                            }
+                            if (u >= n_ok) { sh.term = 1; continue; }   // a terminal configuration
+                            const unsigned pos = atomicAdd(&sh.npend, 1u);
+                            if (pos < A.q_cap) pcur[pos] = bfs_pack(u, (uint32_t)s2, (uint32_t)nm);
                             else atomicOr(&sh.status, 2);
+                        } else {
+                            ck[q] = ((uint64_t)(uint32_t)s2 << 32) | (mask | (1u << j));
                         }
                     }
+                    bool nw[8];
+                    insert8(ck, nw);
+                    record8(ck, nw);
                 }
             }
             __syncthreads();
@@ -3353,6 +3585,12 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             { uint64_t *tp = fcur; fcur = fnxt; fnxt = tp; }
             if (sh.mode == 0 && sh.lcount > LSET / 2 && !sh.status) migrate();
             if (tid == 0) sh.nfront = sh.nnext;
+            if (A.dbg && tid == 0) {
+                // JH_DEBUG=2: rounds and cycles with the layer in the global set (mode 1)
+                unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
+                if (mode_at) { d[9] += __builtin_amdgcn_s_memtime() - rt0; d[10] += 1; d[11] += nf; }
+                else { d[12] += __builtin_amdgcn_s_memtime() - rt0; d[13] += nf; }
+            }
             __syncthreads();
         }
         if (sh.status) break;
@@ -3408,6 +3646,7 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A0) {
     A.slot += (size_t)blockIdx.x * A.ncap;
     A.vis += (size_t)blockIdx.x * (A.ncap / 32 + 1);
     A.tmp += (size_t)blockIdx.x * A.ncap;
+    A.tmpk += (size_t)blockIdx.x * A.ncap;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     uint64_t *gset = A.gset + (size_t)blockIdx.x * A.gset_cap;
     uint64_t *pend = A.pend + (size_t)blockIdx.x * 2 * A.q_cap;
@@ -4137,6 +4376,12 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 512) * 16, st));
         a.dbg = dbg;
     }
+    const bool defer_times = getenv("JH_DEFER_TIMES") && atoi(getenv("JH_DEFER_TIMES"));
+    if (defer_times) {
+        a.defer_time = ctx->ws<unsigned long long>(WS_DEFER_TIME, (size_t)K + 2);
+        HIP_TRY(hipMemsetAsync(a.defer_time, 0, sizeof(unsigned long long) * (K + 2), st));
+        HIP_TRY(hipMemsetAsync(a.defer_time, 0xFF, sizeof(unsigned long long), st));
+    }
     HIP_TRY(hipEventRecord(ctx->ev[1], st));
     k_lin_dfs<true><<<waves1, 64, MemoQ::LDS, st>>>(a);
     HIP_TRY(hipGetLastError());
@@ -4366,6 +4611,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         c.slot = ctx->ws<uint32_t>(WS_BFS_LIVE, (size_t)wg2 * ncap);
         c.vis = ctx->ws<uint32_t>(WS_BFS_VIS, (size_t)wg2 * (ncap / 32 + 1));
         c.tmp = ctx->ws<uint32_t>(WS_BFS_TMP, (size_t)wg2 * ncap);
+        c.tmpk = ctx->ws<uint64_t>(WS_BFS_TMPK, (size_t)wg2 * ncap);
         // per context (= per device; calls on one context are serialised by its mutex)
         if (!ctx->lds_attr) {
             HIP_TRY(hipFuncSetAttribute((const void *)k_lin_bfs, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -4520,10 +4766,12 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             for (int w = 0; w < wg2; w++)
                 if (h[16 * w + 4])
                     fprintf(stderr, "[jh-bfs] wg %d keys=%llu cycles=%llu rounds=%llu configs=%llu cyc/round=%.0f | "
-                            "count: hash=%llu live=%llu path=%llu closure=%llu cyc\n",
+                            "count: hash=%llu live=%llu path=%llu closure=%llu cyc | global-set rounds=%llu cyc=%llu "
+                            "configs=%llu, LDS-set rounds cyc=%llu configs=%llu | live: layers=%llu (LDS %llu) head-cyc=%llu LDS-layers-cyc=%llu\n",
                             w, h[16 * w + 4], h[16 * w], h[16 * w + 1], h[16 * w + 3],
                             (double)h[16 * w] / std::max(1ULL, h[16 * w + 1]), h[16 * w + 5], h[16 * w + 6],
-                            h[16 * w + 7], h[16 * w + 8]);
+                            h[16 * w + 7], h[16 * w + 8], h[16 * w + 10], h[16 * w + 9], h[16 * w + 11],
+                            h[16 * w + 12], h[16 * w + 13], h[16 * w + 14] & 0xFFFFFFFF, h[16 * w + 14] >> 32, h[16 * w + 15], h[16 * w + 2]);
             std::vector<unsigned long long> g((size_t)waves2 * 16);
             HIP_TRY(hipMemcpy(g.data(), dbg + 16 * 256, g.size() * 8, hipMemcpyDeviceToHost));
             for (int w = 0; w < waves2; w++)
@@ -4539,6 +4787,39 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     }
     if (n_x > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[9], 0));
     HIP_TRY(hipEventRecord(ctx->ev[2], st));
+    if (defer_times && n_defer > 0) {
+        // timeline: when each deferred key was handed on (us after phase 1's
+        // first wave), when phase 1 ended, when the sequential search took the
+        // key (if helpers ran), and the key's final insert count
+        HIP_TRY(hipStreamSynchronize(st));
+        std::vector<unsigned long long> dt((size_t)K + 2);
+        HIP_TRY(hipMemcpy(dt.data(), a.defer_time, dt.size() * 8, hipMemcpyDeviceToHost));
+        std::vector<int32_t> dk(n_defer);
+        HIP_TRY(hipMemcpy(dk.data(), defer, sizeof(int32_t) * n_defer, hipMemcpyDeviceToHost));
+        std::vector<jh_key_verdict> vv(K);
+        HIP_TRY(hipMemcpy(vv.data(), out_dev, sizeof(jh_key_verdict) * K, hipMemcpyDeviceToHost));
+        std::vector<unsigned long long> ss;
+        if (ctx->bufs.size() > WS_HELP_START && ctx->bufs[WS_HELP_START].p) {
+            ss.resize(K);
+            HIP_TRY(hipMemcpy(ss.data(), ctx->bufs[WS_HELP_START].p, 8 * K, hipMemcpyDeviceToHost));
+        }
+        fprintf(stderr, "[jh-defer] phase 1: %.1f us (first wave start to last wave end)\n", (dt[1] - dt[0]) / 100.0);
+        std::vector<std::pair<double, int>> ev;
+        for (int d = 0; d < n_defer; d++) ev.push_back({(dt[2 + dk[d]] - dt[0]) / 100.0, dk[d]});
+        std::vector<std::pair<long long, int>> heavy;
+        for (int d = 0; d < n_defer; d++) heavy.push_back({vv[dk[d]].explored, dk[d]});
+        std::sort(heavy.rbegin(), heavy.rend());
+        for (int i = 0; i < std::min(n_defer, 12); i++) {
+            const int k = heavy[i].second;
+            double st_us = -1;
+            if (!ss.empty() && ss[k] && ss[k] != SEQ_HANDED) st_us = ((ss[k] & ~1ULL) - dt[0]) / 100.0;
+            fprintf(stderr, "[jh-defer] key %d explored %lld valid %d deferred %.1f us seq-start %.1f us\n", k,
+                    heavy[i].first, vv[k].valid, (dt[2 + k] - dt[0]) / 100.0, st_us);
+        }
+        int q[5] = {0, 0, 0, 0, 0};
+        for (auto &e2 : ev) q[std::min(4, (int)(e2.first / (std::max(1.0, (dt[1] - dt[0]) / 100.0) / 5)))]++;
+        fprintf(stderr, "[jh-defer] deferrals by fifth of phase 1: %d %d %d %d %d\n", q[0], q[1], q[2], q[3], q[4]);
+    }
     ctx->gen_base += gen_span;
 
     k_fail_rows<<<(unsigned)std::min<int64_t>((K + 3) / 4, 4096), 256, 0, st>>>(

@@ -2783,7 +2783,13 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
 // children -- computed here in parallel: liveness layer by layer backwards,
 // the path by one wave, the closure by a multi-source BFS. Sets beyond the
 // storage cap are left to the sequential search.
-constexpr int BFS_THREADS = 512;
+// 1024 threads (16 waves on the BFS's CU): the closure rounds and the count
+// pass are latency-bound, and twice the waves in flight took the heavy valid
+// keys of C3 ranks 3 / 6 from 104 / 111 to 82 / 88 ms per step (512 before)
+#ifndef JH_BFS_THREADS
+#define JH_BFS_THREADS 1024
+#endif
+constexpr int BFS_THREADS = JH_BFS_THREADS;
 constexpr int BFS_HDR = 1024;                      // shared scalars + the layer's window
 constexpr int BFS_TBL = 28672;                     // W-format tables (ops, woff, W) + r[]
 constexpr int LSET = 16384;                        // layer set slots (8 B keys)

@@ -59,7 +59,11 @@ struct MemoCfg {
     static constexpr int OFF_CNT = OFF_BLOOM + BLOOM / 8;
     static constexpr int LDS = OFF_CNT + BKT;
 };
-using MemoQ = MemoCfg<8, 14>;    // phase 1: 8 KB memo + 2 KB Bloom = 10.25 KB -> 15 waves/CU
+#ifndef JH_MEMOQ_LG
+#define JH_MEMOQ_LG 8
+#define JH_MEMOQ_BLOOM 14
+#endif
+using MemoQ = MemoCfg<JH_MEMOQ_LG, JH_MEMOQ_BLOOM>;   // phase 1: 8 KB memo + 2 KB Bloom = 10.25 KB -> 15 waves/CU
 #ifndef JH_MEMOH_BLOOM
 #define JH_MEMOH_BLOOM 17
 #endif
@@ -336,8 +340,12 @@ __device__ __forceinline__ bool extend_budget(const DfsArgs &A, uint32_t &budget
 }
 constexpr int64_t P2_BUDGET = 1 << 16;  // phase-2 inserts before a key moves to phase 3
 constexpr int64_t QUICK_BUDGET = 8192;  // phase-1 inserts before a key is deferred
-constexpr int HELPERS = 16;             // phase-2 late helpers (workgroups, one per CU)
-constexpr uint64_t HELPER_LATE_US = 2000;   // a key must have run this long in the sequential search
+// phase-2 late helpers (workgroups, one per CU) and how long a key must have run
+// in the sequential search before one takes it: 32 and 250 us measured against
+// 16 and 2 000 us (C3 rank 0 43.2 -> 40.9 ms, ranks 3 / 6 unchanged; the sweep
+// of tools/gpu_env_sweep.sh is flat from 24 to 48 helpers and 0 to 250 us)
+constexpr int HELPERS = 32;
+constexpr uint64_t HELPER_LATE_US = 250;
 
 // write a key's verdict; in a race only the first finisher writes
 __device__ __forceinline__ bool emit_verdict(jh_key_verdict *out, int32_t *claim, int key,
@@ -4634,7 +4642,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         if (const char *e = getenv("JH_MEMO_CAP_SHIFT")) cap2 <<= std::max(0, std::min(3, atoi(e)));   // experiments
         // late helpers (k_lin_wg in helper mode, wg_helper_pick): a few CUs
         // taken from the sequential search; JH_HELPERS=0 turns them off
-        int n_help = bfs_only || wg_race ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 16));
+        int n_help = bfs_only || wg_race ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 8));
         if (const char *e = getenv("JH_HELPERS")) n_help = std::max(0, std::min(64, atoi(e)));
         if (n_help > 0 && ctx->n_cu - wg2 - n_help < 16) n_help = 0;
         // JH_P2_M=1 (experiment): phase 2 with four waves per CU and the 32 KB memo

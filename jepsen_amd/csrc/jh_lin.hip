@@ -59,11 +59,14 @@ struct MemoCfg {
     static constexpr int OFF_CNT = OFF_BLOOM + BLOOM / 8;
     static constexpr int LDS = OFF_CNT + BKT;
 };
+// phase 1: 4 KB memo + 2 KB Bloom = 6.1 KB -> 26 waves/CU. Measured against the
+// 8 KB memo (15 waves/CU): C3 40.8 -> 40.2 ms, C4 shard 283 -> 268 ms (phase 1
+// 108 -> 93 ms), C5 flat (tools/gpu_ab_workloads.sh); 2 KB memos lose again
 #ifndef JH_MEMOQ_LG
-#define JH_MEMOQ_LG 8
+#define JH_MEMOQ_LG 7
 #define JH_MEMOQ_BLOOM 14
 #endif
-using MemoQ = MemoCfg<JH_MEMOQ_LG, JH_MEMOQ_BLOOM>;   // phase 1: 8 KB memo + 2 KB Bloom = 10.25 KB -> 15 waves/CU
+using MemoQ = MemoCfg<JH_MEMOQ_LG, JH_MEMOQ_BLOOM>;
 #ifndef JH_MEMOH_BLOOM
 #define JH_MEMOH_BLOOM 17
 #endif

@@ -4325,7 +4325,15 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     // memo generation tags: distinct per (call, key, pass); wrap -> clear
     const uint32_t gen_span = (uint32_t)(3 * K + 3);
     bool clear_memo = false;
-    if ((uint64_t)ctx->gen_base + gen_span >= (1u << GEN_BITS) - 1) { ctx->gen_base = 0; clear_memo = true; }
+    // JH_GEN_JUMP=1 (tests): start this call at the top of the generation range,
+    // so it wraps and must clear every memo table before its searches read them
+    if (const char *e = getenv("JH_GEN_JUMP"); e && atoi(e)) ctx->gen_base = (1u << GEN_BITS) - 2;
+    if ((uint64_t)ctx->gen_base + gen_span >= (1u << GEN_BITS) - 1) {
+        ctx->gen_base = 0;
+#ifndef JH_NO_WRAP_CLEAR          // (a test build that leaves the tables stale: the wrap test must fail)
+        clear_memo = true;
+#endif
+    }
 
     // phase 1: every key, quick budget, persistent grid
     const uint32_t memo_cap1 = 1u << 16;

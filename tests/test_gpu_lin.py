@@ -309,3 +309,24 @@ def test_bfs_exact_counts(ctx, seed, init):
     deferred = ov["explored"] > 4096
     assert deferred.sum() >= 5 and (ov["valid"][deferred] == A.VALID).sum() >= 3
     _same(v, ov)
+
+
+def test_memo_generation_wrap(monkeypatch):
+    """the memo tables are generation-tagged and cleared only
+    when the 24-bit generation range wraps. A first call leaves entries tagged
+    with generations from 0; the second call is forced to wrap (JH_GEN_JUMP),
+    restarts at generation 0 and must clear every table (phase 1, phase 2's
+    sequential search, the helpers, phase 3) before its searches read them,
+    or the first call's configurations would look visited (C3-sized keys: the
+    phase-1 searches evict to the HBM table past a few hundred inserts; a
+    build without the clear fails here)."""
+    from jepsen_amd import _native
+    ctx = _native.Context(0)
+    cols, _ = synth.cas_register(n_keys=400, ops_per_key=500, p_invalid=0.02, p_info=0.02, seed=97)
+    c, _ = oracle.check_cas_independent(cols, threads=8)
+    g1, _ = ctx.check_cas_independent(cols)
+    _same(g1, c)
+    monkeypatch.setenv("JH_GEN_JUMP", "1")
+    g2, _ = ctx.check_cas_independent(cols)
+    _same(g2, c)
+    ctx.close()

@@ -208,7 +208,7 @@ def main():
     alg2 = BYTES_PER_ENTRY * float(s.deferred_entries) + BYTES_PER_PROBE * float(np.mean(seq_probes))
     ach2 = alg2 / seq_avg / 1e9 if seq_avg > 0 else 0.0
     dominant = seq_avg > dfs_avg
-    tr_kernel = "k_lin_seq" if dominant else "k_lin_dfs"
+    tr_kernel = "k_lin_seq3" if dominant else "k_lin_dfs"
     traffic, traffic_src = pmc_traffic(args.workload, tr_kernel) if args.keys is None else (None, None)
 
     # host buffers to host verdicts (H2D copy + check + verdicts D2H), over K
@@ -263,7 +263,7 @@ def main():
                           "host-to-host rate in e2e_host_buffers",
             "e2e_host_buffers": e2e,
             "roofline": {"bound": "hbm",
-                         "kernel": ("k_lin_seq (phase 2: the deferred keys' sequential WGL search)" if dominant
+                         "kernel": ("k_lin_seq3<true> (phase 2: the deferred keys' sequential WGL search, four waves per CU)" if dominant
                                     else "k_lin_dfs (phase 1: every key, quick budget)"),
                          "achieved": ach2 if dominant else ach1, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (ach2 if dominant else ach1) / PEAK_HBM_GBS,

@@ -4656,8 +4656,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         int n_help = bfs_only || wg_race ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 8));
         if (const char *e = getenv("JH_HELPERS")) n_help = std::max(0, std::min(64, atoi(e)));
         if (n_help > 0 && ctx->n_cu - wg2 - n_help < 16) n_help = 0;
-        // JH_P2_M=1 (experiment): phase 2 with four waves per CU and the 32 KB memo
-        const bool p2_m = getenv("JH_P2_M") && atoi(getenv("JH_P2_M"));
+        // phase 2's sequential search with four waves per CU and the 32 KB memo
+        // (k_lin_seq3), JH_P2_M=0 for one wave per CU and the 128 KB memo
+        // (k_lin_seq): measured C4 shard 268 -> 228 ms, C3 / ranks 3, 6 / C5 flat
+        const bool p2_m = !(getenv("JH_P2_M") && atoi(getenv("JH_P2_M")) == 0);
         const int waves2 = std::min(n_defer, std::max(1, (ctx->n_cu - wg2 - n_help) * (p2_m ? 4 : 1)));
         // generation-tagged: zeroed once when allocated (and on wrap), not per call
         const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;

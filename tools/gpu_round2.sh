@@ -16,6 +16,6 @@ timeout -k 10 300 python -u bench.py --workload c5 --steps 2 --warmup 1 --no-cpu
 timeout -k 10 300 python -u tools/bench_c2.py --no-cpu > $O/bench_c2.log 2>&1 || exit 1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/kt -o run -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu --no-parity --e2e 0 > $R/$O/kt.log 2>&1 || exit 1
-bash $R/tools/gpu_pmc.sh c3 "k_lin_seq<" $O/pmc_c3 || exit 1
+bash $R/tools/gpu_pmc.sh c3 "k_lin_seq3<" $O/pmc_c3 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum --kernel-include-regex "k_lin_seq3" -d $R/$O/pmc_c5 -o tcc --output-format csv -- python3 $R/tools/run_once.py c5 1 > $R/$O/pmc_c5_tcc.log 2>&1
 exit 0

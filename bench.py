@@ -93,10 +93,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    # JH_BENCH_REHEARSE=1: every rank on cuda:0 over gloo, to rehearse the
+    # N-rank launch, barrier / max-over-ranks timing and the report on a
+    # one-GPU box (RCCL refuses two ranks on one device); never a bench number
+    rehearse = world > 1 and os.environ.get("JH_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -279,6 +288,8 @@ def main():
             "cpu_baseline_faithful": cpu_faithful,
             "parity_vs_oracle": parity,
         }
+        if rehearse:
+            out["rehearsal"] = "JH_BENCH_REHEARSE: every rank on cuda:0 over gloo; not a bench number"
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:

@@ -4603,7 +4603,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // CU split of the heavy-key pass (one BFS workgroup or one sequential
         // wave per CU, by LDS): invalid keys are few, the sequential searches
         // many (every valid deferred key), so most CUs go to the latter
-        const int bfs_cus = std::max(1, std::min(64, ctx->n_cu / 4));
+        // 96 of 256 (round 2, with phase 2 at four waves per CU): C4 shard
+        // 230 -> 223 ms, C3 ranks 0 / 3 / 6 flat (32: C4 +9 %, 128: no better)
+        const int bfs_cus = std::max(1, std::min(96, ctx->n_cu * 3 / 8));
         const int wg2 = std::min(n_defer, getenv("JH_BFS_CUS") ? std::max(1, atoi(getenv("JH_BFS_CUS"))) : bfs_cus);
         uint64_t *bset = ctx->ws<uint64_t>(WS_BFS_SET, (size_t)wg2 * set_cap);
         uint64_t *bq = ctx->ws<uint64_t>(WS_BFS_Q, (size_t)wg2 * 4 * q_cap);

@@ -177,6 +177,7 @@ def main():
     for _ in range(args.warmup):
         step()
     dfs_ms, dev_ms, probes, seq_ms, bfs_ms, seq_probes = [], [], [], [], [], []
+    sums = []
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -189,6 +190,7 @@ def main():
         seq_ms.append(s.seq_ms)
         bfs_ms.append(s.bfs_ms)
         seq_probes.append(s.seq_probes)
+        sums.append({f: (list(getattr(s, f)) if f == "waves" else getattr(s, f)) for f, _ in A.JhSummary._fields_})
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -266,7 +268,8 @@ def main():
                        "unknown_keys": int(s.n_unknown), "device_ms": float(np.mean(dev_ms)),
                        "deferred_keys": int(s.n_deferred), "deferred_entries": int(s.deferred_entries),
                        "phase1_ms": dfs_avg * 1e3, "phase2_seq_ms": seq_avg * 1e3,
-                       "phase2_bfs_ms": float(np.mean(bfs_ms))},
+                       "phase2_bfs_ms": float(np.mean(bfs_ms)),
+                       "phases": phase_table(sums)},
             "shard": shard_info,
             "value_kind": "history resident in HBM, verdicts left in HBM (kernel pipeline only); "
                           "host-to-host rate in e2e_host_buffers",
@@ -295,6 +298,24 @@ def main():
     if dist is not None:
         dist.destroy_process_group()
     return out
+
+
+def phase_table(sums):
+    """Per-phase times, probes, entries and waves of the timed steps (jh_summary,
+    ABI 4): each search kernel's own HIP events and probe counter."""
+    if not sums:
+        return None
+    mean = lambda f: float(np.mean([x[f] for x in sums]))
+    last = sums[-1]
+    return {"phase1": {"ms": mean("dfs_ms"), "probes": mean("memo_probes")},
+            "phase2_lean": {"ms": mean("seq_ms"), "probes": mean("seq_probes"), "keys": last["n_deferred"] - last["n_deferred_wide"],
+                            "entries": last["lean_entries"], "waves": last["waves"][0], "helper_probes": mean("helper_probes")},
+            "phase3_lean": {"ms": mean("p3_ms"), "probes": mean("p3_probes"), "keys": last["n_phase3"], "waves": last["waves"][2]},
+            "bfs": {"ms": mean("bfs_ms")},
+            "wide": {"ms": mean("wide_ms"), "probes": mean("wide_probes"), "keys": last["n_deferred_wide"],
+                     "entries": last["wide_entries"], "waves": last["waves"][1], "phase3_keys": last["n_phase3_wide"]},
+            "xw": {"ms": mean("xw_ms"), "probes": mean("xw_probes"), "keys": last["n_xw"], "entries": last["xw_entries"],
+                   "waves": last["waves"][3]}}
 
 
 def cpu_quota_cores():

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define JH_ABI_VERSION 3
+#define JH_ABI_VERSION 4
 
 /* Return codes. Anything non-zero also writes a NUL-terminated message into
  * the caller's err buffer; the JNA shim throws ex-info and check-safe turns
@@ -112,10 +112,38 @@ typedef struct jh_history {
     int32_t reserved;
 } jh_history;
 
+/* :algorithm of (checker/linearizable {:model m :algorithm a}), checker.clj:141-145.
+ * Every algorithm decides the same :valid? (all are complete decision
+ * procedures); the choice selects which analysis is reported (:analyzer) and,
+ * for an invalid key, which search's frontier :configs come from. */
+#define JH_ALGO_COMPETITION 0       /* knossos.competition (the default): :wgl and :linear race */
+#define JH_ALGO_WGL         1       /* knossos.wgl */
+#define JH_ALGO_LINEAR      2       /* knossos.linear (JIT-linearization configuration sets) */
+
+/* jh_lin_opts.flags: test hooks, 0 in production */
+#define JH_LIN_BFS_ONLY        1    /* heavy keys: the reachable-set BFS alone (no DFS race) */
+#define JH_LIN_GEN_JUMP        2    /* start at the top of the memo generation range (wrap test) */
+#define JH_LIN_INTERN_PER_KEY  4    /* intern values per key even when one global range fits */
+#define JH_LIN_NO_HELPERS      8    /* no late helper workgroups in phase 2 */
+#define JH_LIN_HELPERS_NOW    16    /* late helpers take a key at once (helper_late_us = 0) */
+
 typedef struct jh_lin_opts {
     int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */
     int64_t budget;            /* max memo inserts per key before :unknown; <=0: default */
     int64_t stream;            /* hipStream_t to run on (0 = the ctx stream) */
+    int32_t algorithm;         /* JH_ALGO_*; 0 = competition, the reference's default */
+    int32_t flags;             /* JH_LIN_* test hooks */
+    int64_t quick_budget;      /* phase-1 inserts before a key is deferred; <=0: 8192 */
+    int64_t phase2_budget;     /* phase-2 inserts before a key restarts in phase 3; <=0: 65536 */
+    /* scheduling of the heavy-key pass (every value decides the same verdicts;
+     * the parity tests run the less common paths through these): */
+    int32_t helpers;           /* phase-2 late helper workgroups; <=0: 32 (JH_LIN_NO_HELPERS: none) */
+    int32_t helper_late_us;    /* run time before a helper takes a key; <=0: 250 (JH_LIN_HELPERS_NOW: 0) */
+    int32_t xw_waves;          /* waves of the 65-256-member search; <=0: one per key, up to 4 per CU */
+    int32_t p2_waves_per_cu;   /* 1: phase 2 at one wave per CU with the 128 KB LDS memo; else 4 */
+    int32_t lean_waves;        /* at most this many phase-2 waves for LEAN keys; <=0: no cap */
+    int32_t wide_waves;        /* at most this many waves for WIDE keys; <=0: no cap */
+    int64_t reserved;          /* zero */
 } jh_lin_opts;
 
 #define JH_DEFAULT_BUDGET (1 << 20)
@@ -153,7 +181,25 @@ typedef struct jh_summary {
     double  bfs_ms;            /* the reachable-set BFS racing it (k_lin_bfs; 0 if not run) */
     int64_t n_deferred;        /* keys the phase-1 search handed on */
     int64_t deferred_entries;  /* history entries of those keys */
-    int64_t seq_probes;        /* HBM memo probes of the phase-2 sequential search */
+    int64_t seq_probes;        /* HBM memo probes of the phase-2 sequential search (LEAN keys) */
+    /* ABI 4: per-phase accounting. Each search kernel has its own probe counter
+     * and its own HIP events (on the stream it runs on), so each phase's
+     * roofline is (56 B x its keys' entries + 16 B x its probes) / its time. */
+    double  p3_ms;             /* phase 3, LEAN keys (restarted past phase2_budget) */
+    double  wide_ms;           /* WIDE keys (window 41-64 or >= 256 states), phases 2 + 3 */
+    double  xw_ms;             /* windows of 65-256 members (k_lin_xw) */
+    int64_t p3_probes;
+    int64_t wide_probes;
+    int64_t xw_probes;
+    int64_t helper_probes;     /* phase-2 late helper workgroups */
+    int64_t n_deferred_wide;   /* WIDE keys among n_deferred */
+    int64_t n_phase3;          /* LEAN keys restarted in phase 3 */
+    int64_t n_phase3_wide;     /* WIDE keys restarted in phase 3 */
+    int64_t n_xw;              /* keys searched by k_lin_xw */
+    int64_t lean_entries;      /* entries of the deferred LEAN keys */
+    int64_t wide_entries;      /* entries of the deferred WIDE keys */
+    int64_t xw_entries;        /* entries of the k_lin_xw keys */
+    int64_t waves[4];          /* launched waves: phase-2 LEAN, WIDE, phase-3 LEAN, xw */
 } jh_summary;
 
 typedef struct jh_ctx jh_ctx;

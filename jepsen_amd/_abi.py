@@ -6,7 +6,7 @@ every struct layout.
 """
 import ctypes as C
 
-JH_ABI_VERSION = 3
+JH_ABI_VERSION = 4
 
 JH_OK, JH_EINVAL, JH_EUNSUPPORTED, JH_EDEVICE, JH_ENOMEM = 0, 1, 2, 3, 4
 TYPE_INVOKE, TYPE_OK, TYPE_FAIL, TYPE_INFO = 0, 1, 2, 3
@@ -52,8 +52,19 @@ class JhHistory(C.Structure):
     ]
 
 
+ALGO_COMPETITION, ALGO_WGL, ALGO_LINEAR = 0, 1, 2
+ALGORITHMS = {"competition": ALGO_COMPETITION, "wgl": ALGO_WGL, "linear": ALGO_LINEAR}
+# jh_lin_opts.flags (test hooks)
+LIN_BFS_ONLY, LIN_GEN_JUMP, LIN_INTERN_PER_KEY, LIN_NO_HELPERS, LIN_HELPERS_NOW = 1, 2, 4, 8, 16
+
+
 class JhLinOpts(C.Structure):
-    _fields_ = [("init_value", C.c_int64), ("budget", C.c_int64), ("stream", C.c_int64)]
+    _fields_ = [("init_value", C.c_int64), ("budget", C.c_int64), ("stream", C.c_int64),
+                ("algorithm", C.c_int32), ("flags", C.c_int32),
+                ("quick_budget", C.c_int64), ("phase2_budget", C.c_int64),
+                ("helpers", C.c_int32), ("helper_late_us", C.c_int32),
+                ("xw_waves", C.c_int32), ("p2_waves_per_cu", C.c_int32),
+                ("lean_waves", C.c_int32), ("wide_waves", C.c_int32), ("reserved", C.c_int64)]
 
 
 # every field of jh_key_verdict: the parity tests compare all of them
@@ -72,7 +83,13 @@ class JhSummary(C.Structure):
                 ("explored", C.c_int64), ("memo_probes", C.c_int64),
                 ("device_ms", C.c_double), ("dfs_ms", C.c_double),
                 ("seq_ms", C.c_double), ("bfs_ms", C.c_double), ("n_deferred", C.c_int64),
-                ("deferred_entries", C.c_int64), ("seq_probes", C.c_int64)]
+                ("deferred_entries", C.c_int64), ("seq_probes", C.c_int64),
+                # ABI 4: per-phase accounting
+                ("p3_ms", C.c_double), ("wide_ms", C.c_double), ("xw_ms", C.c_double),
+                ("p3_probes", C.c_int64), ("wide_probes", C.c_int64), ("xw_probes", C.c_int64),
+                ("helper_probes", C.c_int64), ("n_deferred_wide", C.c_int64), ("n_phase3", C.c_int64),
+                ("n_phase3_wide", C.c_int64), ("n_xw", C.c_int64), ("lean_entries", C.c_int64),
+                ("wide_entries", C.c_int64), ("xw_entries", C.c_int64), ("waves", C.c_int64 * 4)]
 
 
 class JhSetResult(C.Structure):

@@ -95,8 +95,22 @@ def _raise(rc, err):
         raise JhError(rc, err.value.decode(errors="replace"))
 
 
-def _opts(init, budget, stream=0):
-    return A.JhLinOpts(A.NIL if init is None else int(init), int(budget or 0), int(stream))
+def _opts(init, budget, stream=0, algorithm=None, **tune):
+    """jh_lin_opts. tune: flags, quick_budget, phase2_budget, helpers,
+    helper_late_us, xw_waves, p2_waves_per_cu (jh.h; all decide the same
+    verdicts, the tests use them to reach the less common search paths)."""
+    o = A.JhLinOpts()
+    o.init_value = A.NIL if init is None else int(init)
+    o.budget = int(budget or 0)
+    o.stream = int(stream)
+    if isinstance(algorithm, str):
+        algorithm = A.ALGORITHMS[algorithm]
+    o.algorithm = int(algorithm or 0)
+    for k, v in tune.items():
+        if k not in dict(A.JhLinOpts._fields_) or k in ("init_value", "budget", "stream", "algorithm", "reserved"):
+            raise TypeError(f"unknown jh_lin_opts field {k}")
+        setattr(o, k, int(v))
+    return o
 
 
 def key_costs(cols):
@@ -157,46 +171,46 @@ class Context:
         return off, rows[:cols.n]
 
     # -- linearizability ---------------------------------------------------
-    def check_cas_independent(self, cols, init=None, budget=None):
+    def check_cas_independent(self, cols, init=None, budget=None, **tune):
         """Returns (verdicts: structured array [n_keys] of VERDICT_DTYPE, JhSummary)."""
         h = A.make_history(cols)
         out = np.zeros(max(cols.n_keys, 1), dtype=A.VERDICT_DTYPE)
         s = A.JhSummary()
         err = C.create_string_buffer(1024)
-        rc = lib().jh_check_cas_independent(self._h, C.byref(h), C.byref(_opts(init, budget)),
+        rc = lib().jh_check_cas_independent(self._h, C.byref(h), C.byref(_opts(init, budget, **tune)),
                                             out.ctypes.data_as(C.POINTER(A.JhKeyVerdict)),
                                             C.byref(s), err, len(err))
         _raise(rc, err)
         return out[:cols.n_keys], s
 
     def check_cas_independent_device(self, dcols, verdicts_dev_ptr, init=None, budget=None,
-                                     stream=0):
+                                     stream=0, **tune):
         """dcols: object whose column attributes are device pointers (ints)."""
         h = A.make_history(dcols, on_device=True)
         s = A.JhSummary()
         err = C.create_string_buffer(1024)
         rc = lib().jh_check_cas_independent_device(
-            self._h, C.byref(h), C.byref(_opts(init, budget, stream)),
+            self._h, C.byref(h), C.byref(_opts(init, budget, stream, **tune)),
             C.cast(C.c_void_p(int(verdicts_dev_ptr)), C.POINTER(A.JhKeyVerdict)),
             C.byref(s), err, len(err))
         _raise(rc, err)
         return s
 
-    def check_cas(self, cols, init=None, budget=None):
+    def check_cas(self, cols, init=None, budget=None, **tune):
         h = A.make_history(cols)
         v = A.JhKeyVerdict()
         err = C.create_string_buffer(1024)
-        rc = lib().jh_check_cas(self._h, C.byref(h), C.byref(_opts(init, budget)), C.byref(v),
+        rc = lib().jh_check_cas(self._h, C.byref(h), C.byref(_opts(init, budget, **tune)), C.byref(v),
                                 err, len(err))
         _raise(rc, err)
         return v.valid, v.cause, v.fail_entry, v.explored
 
-    def check_cas_full(self, cols, init=None, budget=None):
+    def check_cas_full(self, cols, init=None, budget=None, **tune):
         """jh_check_cas -> {valid, cause, fail_entry, explored, previous_ok, last_op}."""
         h = A.make_history(cols)
         v = A.JhKeyVerdict()
         err = C.create_string_buffer(1024)
-        rc = lib().jh_check_cas(self._h, C.byref(h), C.byref(_opts(init, budget)), C.byref(v),
+        rc = lib().jh_check_cas(self._h, C.byref(h), C.byref(_opts(init, budget, **tune)), C.byref(v),
                                 err, len(err))
         _raise(rc, err)
         return {f: getattr(v, f) for f, _ in A.JhKeyVerdict._fields_}

@@ -54,9 +54,10 @@ struct jh_ctx {
     hipStream_t aux = nullptr;     // second stream for racing searches (jh_lin.hip)
     hipStream_t aux2 = nullptr;    // third stream: windows wider than 64 (jh_lin.hip)
     hipStream_t aux3 = nullptr;    // fourth stream: phase-2 late helpers (jh_lin.hip)
+    hipStream_t aux4 = nullptr;    // fifth stream: the deferred WIDE keys (jh_lin.hip)
     std::mutex mu;
     std::vector<Buf> bufs;
-    hipEvent_t ev[14] = {};
+    hipEvent_t ev[24] = {};
     uint32_t gen_base = 0;        // memo generation tags (see jh_lin.hip)
     bool lds_attr = false;        // >64 KB dynamic-LDS attributes set for this device's kernels
     bool lds_attr_wg = false;
@@ -105,6 +106,7 @@ enum WsSlot {
     WS_BFS_NODES, WS_BFS_LSTART, WS_BFS_HKEY, WS_BFS_HID, WS_BFS_LIVE, WS_BFS_VIS, WS_BFS_TMP,
     WS_WG_MEMO, WS_WG_STACK, WS_WG_SCR, WS_S_BYTES, WS_IV_U, WS_IV_IDX, WS_IV_KEY, WS_IV_RINIT, WS_IV_MAX, WS_IV_TMP,
     WS_HELP_START, WS_HELP_TAKEN, WS_DEFER_TIME, WS_BFS_TMPK,
+    WS_DEFER64, WS_DEFER64_T, WS_MEMO_WIDE, WS_STACK_WIDE, WS_SCRATCH_WIDE,
     WS_COUNT
 };
 

@@ -73,6 +73,11 @@ using MemoQ = MemoCfg<JH_MEMOQ_LG, JH_MEMOQ_BLOOM>;
 using MemoH = MemoCfg<12, JH_MEMOH_BLOOM>;   // heavy keys: 128 KB memo + 16 KB Bloom = 152 KB -> 1 wave/CU
                                               // (16 KB Bloom vs 8 KB: -4..7% on the heaviest C3 keys)
 using MemoM = MemoCfg<10, 15>;   // very heavy keys: 32 KB memo + 4 KB Bloom = 37 KB -> 4 waves/CU
+// WIDE deferred keys (dfs_search<.., LEAN=false>): the search keeps every
+// configuration in the wave's HBM table and uses the LDS only for the Bloom
+// filter in front of it, so the memo part is a token 16 slots: 16.5 KB per
+// wave, up to 9 waves per CU
+using MemoX = MemoCfg<2, 17>;
 constexpr int STATE_BITS = 20, T_BITS = 20, GEN_BITS = 24;
 constexpr uint32_t STATE_MASK = (1u << STATE_BITS) - 1, T_MASK = (1u << T_BITS) - 1;
 
@@ -283,9 +288,14 @@ struct DfsArgs {
     int32_t n_list;
     int32_t *queue;             // work counter
     jh_key_verdict *out;
-    int32_t *defer_list;        // phase 1: keys over the quick budget
+    int32_t *defer_list;        // phase 2: keys over its budget (to phase 3)
     int32_t *defer_count;
-    uint32_t *defer_prog;       // phase 1: progress of each deferred key (ordering of the heavy pass)
+    // phase 1: keys over the quick budget as (progress << 32 | key), progress =
+    // deepest layer / layers (k_sort_defer orders the heavy pass by it): every
+    // deferred key in defer64, and this kernel's mode (LEAN / WIDE) in defer_kind
+    uint64_t *defer64;
+    uint64_t *defer_kind;
+    int32_t *defer_kind_count;
     uint64_t *memo;             // per wave: memo_cap entries x 2 words
     uint32_t memo_cap;          // power of two
     Frame *stack;               // per wave: stack_cap frames
@@ -314,6 +324,9 @@ struct DfsArgs {
     // JH_DEFER_TIMES=1 (timeline study): [0] first wave start, [1] last wave
     // end (s_memrealtime), [2 + key] the time the key was handed on
     unsigned long long *defer_time;
+    // run only when the list length (read on the device) is in [n_min, n_max]
+    // (n_max 0: no upper bound): phase 3 picks one of two launched kernels
+    int32_t n_min, n_max;
 };
 constexpr unsigned long long SEQ_HANDED = ~0ULL;
 
@@ -1660,6 +1673,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     uint64_t *stage = (uint64_t *)(A.scratch + (size_t)blockIdx.x * A.scratch_bytes);
     unsigned long long my_probes = 0;
     const int n_list = A.n_list_dev ? *A.n_list_dev : A.n_list;
+    if (n_list < A.n_min || (A.n_max > 0 && n_list > A.n_max)) return;
     const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
     if (A.defer_time && lane == 0) atomicMin(&A.defer_time[0], __builtin_amdgcn_s_memrealtime());
     for (;;) {
@@ -1692,10 +1706,13 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
             (A.budget_full == 0 || inserts < A.budget_full)) {
             if (lane == 0) {
                 const int d = atomicAdd(A.defer_count, 1);
-                A.defer_list[d] = key;
+                if (A.defer_list) A.defer_list[d] = key;
                 // progress of the quick search (deepest layer / layers): the
                 // heavy-key pass starts with the least advanced keys
-                if (A.defer_prog) A.defer_prog[d] = (uint32_t)((uint64_t)tmax * 1000000u / (uint64_t)max(1, K.n_ok));
+                const uint64_t pk = ((uint64_t)((uint64_t)tmax * 1000000u / (uint64_t)max(1, K.n_ok)) << 32) |
+                                    (uint32_t)key;
+                if (A.defer64) A.defer64[d] = pk;
+                if (A.defer_kind) A.defer_kind[atomicAdd(A.defer_kind_count, 1)] = pk;
                 if (A.defer_time) A.defer_time[2 + key] = __builtin_amdgcn_s_memrealtime();
                 if (A.seq_start)
                     __hip_atomic_store(&A.seq_start[key], SEQ_HANDED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1754,6 +1771,48 @@ __global__ void __launch_bounds__(64) k_lin_seq(DfsArgs A) { lin_dfs_waves<MemoH
 // four times as many of those searches in flight
 template <bool LEAN>
 __global__ void __launch_bounds__(64) k_lin_seq3(DfsArgs A) { lin_dfs_waves<MemoM, LEAN>(A); }
+// the deferred WIDE keys (phases 2 and 3): their own list, stream and waves,
+// as many as there are keys (up to 4 per CU, bounded by free HBM), beside the
+// LEAN pipeline instead of behind it
+__global__ void __launch_bounds__(64) k_lin_seqw(DfsArgs A) { lin_dfs_waves<MemoX, false>(A); }
+
+// Deferred keys, least advanced first (phase 1's progress, ties by key: the
+// likely longest searches start first), then the key ids alone: one workgroup
+// per list, a bitonic sort of (progress << 32 | key) in LDS. Lists longer than
+// SORT_SMALL are sorted by hipcub on the host side of the call.
+constexpr int SORT_SMALL = 4096;
+struct SortLists {
+    const uint64_t *in[3];
+    int32_t *out[3];
+    int n[3];
+};
+__global__ void __launch_bounds__(1024) k_sort_defer(SortLists L) {
+    __shared__ uint64_t s[SORT_SMALL];
+    const int n = L.n[blockIdx.x];
+    if (n <= 0 || n > SORT_SMALL) return;
+    const uint64_t *in = L.in[blockIdx.x];
+    int32_t *out = L.out[blockIdx.x];
+    int P = 2;
+    while (P < n) P <<= 1;
+    for (int i = threadIdx.x; i < P; i += blockDim.x) s[i] = i < n ? in[i] : ~0ULL;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t a = s[i], b = s[ixj];
+                    if ((a > b) == ((i & k) == 0)) { s[i] = b; s[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = (int32_t)(uint32_t)s[i];
+}
+__global__ void k_unpack_keys(const uint64_t *__restrict__ in, int n, int32_t *__restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (int32_t)(uint32_t)in[i];
+}
 
 // ---------------------------------------------------------------------------
 // Phase 2 (deferred LEAN keys): one workgroup per key. Wave 0 runs the WGL
@@ -4113,16 +4172,24 @@ __global__ void k_summary(const jh_key_verdict *__restrict__ v, int64_t K, long 
     }
 }
 
-// entries of the deferred keys (the phase-2 kernels' share of the history)
-__global__ void k_defer_entries(const int32_t *__restrict__ defer, int n, const uint32_t *__restrict__ off,
-                                unsigned long long *sum) {
+// history entries of the keys in each of four lists (the deferred keys, LEAN,
+// WIDE, the k_lin_xw keys): each phase's roofline bytes
+struct EntryLists {
+    const int32_t *list[4];
+    int n[4];
+    unsigned long long *sum[4];
+    const uint32_t *off;
+};
+__global__ void __launch_bounds__(256) k_list_entries(EntryLists L) {
+    const int y = blockIdx.y, n = L.n[y];
+    const int32_t *list = L.list[y];
     unsigned long long x = 0;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int k = defer[i];
-        x += off[k + 1] - off[k];
+        const int k = list[i];
+        x += L.off[k + 1] - L.off[k];
     }
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    if ((threadIdx.x & 63) == 0 && x) atomicAdd(sum, x);
+    if ((threadIdx.x & 63) == 0 && x) atomicAdd(L.sum[y], x);
 }
 
 __global__ void k_iota(int32_t *a, int64_t n) {
@@ -4221,6 +4288,49 @@ inline int bits_for(uint64_t x) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
+// Tuning and diagnostics knobs (JH_* environment variables) are read only by a
+// build with -DJH_TUNING (tools/build_variants.sh): the release library ignores
+// the environment. Options that change what a call does are jh_lin_opts fields.
+static inline const char *tune_env(const char *name) {
+#ifdef JH_TUNING
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
+// Units (waves or workgroups) of per_unit bytes each that fit in HBM: at most
+// `want`, at least 1. The buffers of `slots` count as free (they are what the
+// units' tables replace); a reserve stays free, and no one kind of search
+// table takes more than a quarter of the device. No query in the steady state
+// (the slots already hold `want` units).
+static int fit_units(jh_ctx *ctx, int want, uint64_t per_unit, std::initializer_list<int> slots) {
+    if (want <= 1 || per_unit == 0) return std::max(want, 1);
+    uint64_t held = 0;
+    for (int sl : slots)
+        if ((int)ctx->bufs.size() > sl) held += ctx->bufs[sl].bytes;
+    if ((uint64_t)want * per_unit <= held) return want;
+    size_t fr = 0, tot = 0;
+    HIP_TRY(hipMemGetInfo(&fr, &tot));
+    const uint64_t reserve = std::max<uint64_t>(2ULL << 30, tot / 32);
+    uint64_t room = fr + held;
+    room = room > reserve ? room - reserve : 0;
+    room = std::min<uint64_t>(room, tot / 4);
+    const uint64_t fit = room / (per_unit + per_unit / 8);    // ws() allocates 1/8 over
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)want, fit));
+}
+
+// words of the per-call counter block q (device): queues, list lengths, probe
+// and entry counters of the phases
+constexpr int Q_WORDS = 64;
+constexpr int Q_ENT_ALL = 24, Q_DEFER_L = 29, Q_DEFER_W = 30, Q_DEFER3W = 31;
+constexpr int Q_PROBES_HELP = 32, Q_PROBES_P3 = 34, Q_PROBES_WIDE = 36;
+constexpr int Q_ENT_LEAN = 40, Q_ENT_WIDE = 42, Q_ENT_XW = 44;
+static inline int64_t q64(const int32_t *qh, int i) {
+    return (int64_t)(((uint64_t)(uint32_t)qh[i + 1] << 32) | (uint32_t)qh[i]);
+}
+
 void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts *opts,
                            bool keyed, jh_key_verdict *out_dev, jh_summary *sum,
                            hipStream_t st) {
@@ -4230,6 +4340,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     if (n >= (1LL << 31)) throw_jh(JH_EUNSUPPORTED, "more than 2^31 entries in one call");
     const int64_t budget = opts && opts->budget > 0 ? opts->budget : JH_DEFAULT_BUDGET;
     const int64_t init = opts ? opts->init_value : JH_NIL;
+    const int32_t lflags = opts ? opts->flags : 0;
     HIP_TRY(hipEventRecord(ctx->ev[0], st));
 
     // ranges
@@ -4251,7 +4362,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     // values spanning more than one 16-bit state range are interned per key
     // (k_ival..k_iassign) instead of as one global offset
     const bool per_key_values = (unsigned long long)(vmax - vmin) >= (unsigned long long)(RQ_EMPTY - 3) ||
-                                (getenv("JH_INTERN_PER_KEY") && atoi(getenv("JH_INTERN_PER_KEY")) != 0);
+                                (lflags & JH_LIN_INTERN_PER_KEY) != 0;
     const int init_state = init == JH_NIL ? 0 : per_key_values ? 1 : (int)(init - vmin + 1);
     long long n_states = vmax - vmin + 2;      // state ids 0 (nil) .. vmax - vmin + 1
 
@@ -4325,9 +4436,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     // memo generation tags: distinct per (call, key, pass); wrap -> clear
     const uint32_t gen_span = (uint32_t)(3 * K + 3);
     bool clear_memo = false;
-    // JH_GEN_JUMP=1 (tests): start this call at the top of the generation range,
+    // JH_LIN_GEN_JUMP (tests): start this call at the top of the generation range,
     // so it wraps and must clear every memo table before its searches read them
-    if (const char *e = getenv("JH_GEN_JUMP"); e && atoi(e)) ctx->gen_base = (1u << GEN_BITS) - 2;
+    if (lflags & JH_LIN_GEN_JUMP) ctx->gen_base = (1u << GEN_BITS) - 2;
     if ((uint64_t)ctx->gen_base + gen_span >= (1u << GEN_BITS) - 1) {
         ctx->gen_base = 0;
 #ifndef JH_NO_WRAP_CLEAR          // (a test build that leaves the tables stale: the wrap test must fail)
@@ -4341,8 +4452,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     // unchanged): phase 1 runs 15 waves per CU, phase 2 one, and phase 2 restarts a deferred
     // key from scratch, so every key phase 1 can finish is cheaper there
     int64_t quick = std::min<int64_t>(budget, QUICK_BUDGET);
-    if (const char *e = getenv("JH_QUICK_BUDGET"))
-        quick = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(budget, memo_cap1 / 2), atoll(e)));
+    if (opts && opts->quick_budget > 0)
+        quick = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(budget, memo_cap1 / 2), opts->quick_budget));
     const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * (163840 / MemoQ::LDS));
     uint64_t *memo = ctx->ws<uint64_t>(WS_MEMO, (size_t)waves1 * memo_cap1 * 2, /*zero=*/true);
     if (clear_memo) HIP_TRY(hipMemsetAsync(memo, 0, ctx->bufs[WS_MEMO].bytes, st));
@@ -4352,11 +4463,15 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const uint64_t scr_bytes_h = MemoH::SLOTS * 8;
     const uint64_t scr_bytes_bfs = (((uint64_t)smax * 84 + 4096) + 255) & ~255ULL;
     char *scr = ctx->ws<char>(WS_SCRATCH, (size_t)waves1 * scr_bytes);
-    int32_t *q = ctx->ws<int32_t>(WS_QUEUE, 32);
+    int32_t *q = ctx->ws<int32_t>(WS_QUEUE, Q_WORDS);
     int32_t *list = ctx->ws<int32_t>(WS_STATS, K);
-    int32_t *defer = ctx->ws<int32_t>(WS_DEFER, K + 1);
+    // the deferred keys, ordered for the heavy pass (k_sort_defer): every one
+    // (the BFS's list), the LEAN ones and the WIDE ones (each mode's own searches)
+    int32_t *defer = ctx->ws<int32_t>(WS_DEFER, 3 * (size_t)(K + 1));
+    int32_t *defer_l = defer + (K + 1), *defer_w = defer + 2 * (K + 1);
+    uint64_t *d64 = ctx->ws<uint64_t>(WS_DEFER64, 3 * (size_t)(K + 1));
     unsigned long long *probes = (unsigned long long *)(q + 4);
-    HIP_TRY(hipMemsetAsync(q, 0, 32 * sizeof(int32_t), st));
+    HIP_TRY(hipMemsetAsync(q, 0, Q_WORDS * sizeof(int32_t), st));
 
     // per-key search tables for every key (<= 8 B per entry + 32 B per key)
     KeyMeta *meta = ctx->ws<KeyMeta>(WS_META, K);
@@ -4372,7 +4487,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     k_key_tables<<<(unsigned)std::min<int64_t>((K + 3) / 4, 8192), 256, 0, st>>>(ta);
 
     int32_t *list1 = list;
-    if (!getenv("JH_NO_LPT") && K > 1) {
+    if (!tune_env("JH_NO_LPT") && K > 1) {
         uint32_t *cost = ctx->ws<uint32_t>(WS_LCOST, 2 * K);
         int32_t *lv = ctx->ws<int32_t>(WS_LSORT, 2 * K);
         k_list_cost<<<grid_for(K, 256, 4096), 256, 0, st>>>(list, q + 12, meta, K, cost, lv);
@@ -4387,13 +4502,13 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     a.rec = rec; a.pair = pair; a.off = off; a.rows = rB; a.viol = viol; a.rank = rank;
     a.list = list1; a.n_list = 0; a.n_list_dev = q + 12; a.queue = q; a.out = out_dev;
     a.meta = meta; a.tables = arena;
-    uint32_t *defer_prog = ctx->ws<uint32_t>(WS_DEFER_PROG, K + 1);
-    a.defer_list = defer; a.defer_count = q + 1; a.defer_prog = defer_prog;
+    a.defer_list = nullptr; a.defer_count = q + 1;
+    a.defer64 = d64; a.defer_kind = d64 + (K + 1); a.defer_kind_count = q + Q_DEFER_L;
     a.memo = memo; a.memo_cap = memo_cap1; a.stack = stack; a.stack_cap = stack_cap;
     a.scratch = scr; a.scratch_bytes = scr_bytes; a.budget = quick; a.defer = quick < budget ? 1 : 0;
     a.init_state = init_state; a.gen_base = ctx->gen_base; a.flags = q + 2; a.probes = probes;
     a.states8 = n_states <= 256 ? 1 : 0;
-    const char *dbgenv = getenv("JH_DEBUG");
+    const char *dbgenv = tune_env("JH_DEBUG");
     const bool dbg2 = dbgenv && atoi(dbgenv) >= 2;
     unsigned long long *dbg = nullptr;
     if (dbg2) {
@@ -4401,7 +4516,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 512) * 16, st));
         a.dbg = dbg;
     }
-    const bool defer_times = getenv("JH_DEFER_TIMES") && atoi(getenv("JH_DEFER_TIMES"));
+    const bool defer_times = tune_env("JH_DEFER_TIMES") && atoi(tune_env("JH_DEFER_TIMES"));
     if (defer_times) {
         a.defer_time = ctx->ws<unsigned long long>(WS_DEFER_TIME, (size_t)K + 2);
         HIP_TRY(hipMemsetAsync(a.defer_time, 0, sizeof(unsigned long long) * (K + 2), st));
@@ -4413,31 +4528,43 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     {
         DfsArgs aw = a;
         aw.list = list_w; aw.n_list_dev = q + 13; aw.queue = q + 14;
+        aw.defer_kind = d64 + 2 * (K + 1); aw.defer_kind_count = q + Q_DEFER_W;
         k_lin_dfs<false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[4], st));
-    int32_t qh[32];
+    int32_t qh[Q_WORDS];
     HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    const int n_defer = qh[1];
-    unsigned long long *defer_entries = (unsigned long long *)(q + 24);
-    HIP_TRY(hipMemsetAsync(defer_entries, 0, sizeof(unsigned long long), st));
-    if (n_defer > 0) k_defer_entries<<<std::min(256, (n_defer + 255) / 256), 256, 0, st>>>(defer, n_defer, off, defer_entries);
-    if (n_defer > 1) {
-        // heavy keys, least advanced first (the likely longest searches start first)
-        std::vector<int32_t> dk(n_defer);
-        std::vector<uint32_t> dp(n_defer);
-        HIP_TRY(hipMemcpyAsync(dk.data(), defer, sizeof(int32_t) * n_defer, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(dp.data(), defer_prog, sizeof(uint32_t) * n_defer, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        std::vector<int> ix(n_defer);
-        for (int i = 0; i < n_defer; i++) ix[i] = i;
-        std::stable_sort(ix.begin(), ix.end(), [&](int x, int y) { return dp[x] < dp[y]; });
-        std::vector<int32_t> sk(n_defer);
-        for (int i = 0; i < n_defer; i++) sk[i] = dk[ix[i]];
-        HIP_TRY(hipMemcpyAsync(defer, sk.data(), sizeof(int32_t) * n_defer, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipStreamSynchronize(st));
+    const int n_defer = qh[1], n_def_l = qh[Q_DEFER_L], n_def_w = qh[Q_DEFER_W];
+    const int n_x = qh[19];
+    if (n_def_l + n_def_w != n_defer) throw_jh(JH_EDEVICE, "deferred-key lists disagree");
+    if (n_defer > 0) {
+        // heavy keys, least advanced first (the likely longest searches start
+        // first), sorted on the device: no host round trip between the phases
+        SortLists sl{};
+        const int nn[3] = {n_defer, n_def_l, n_def_w};
+        int32_t *outs[3] = {defer, defer_l, defer_w};
+        for (int i = 0; i < 3; i++) { sl.in[i] = d64 + (size_t)i * (K + 1); sl.out[i] = outs[i]; sl.n[i] = nn[i]; }
+        k_sort_defer<<<3, 1024, 0, st>>>(sl);
+        for (int i = 0; i < 3; i++) {
+            if (nn[i] <= SORT_SMALL) continue;
+            uint64_t *tk = ctx->ws<uint64_t>(WS_DEFER64_T, (size_t)K + 1);
+            size_t tbs = 0;
+            HIP_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, tbs, sl.in[i], tk, nn[i], 0, 64, st));
+            HIP_TRY(hipcub::DeviceRadixSort::SortKeys(ctx->ws<char>(WS_LTMP, tbs), tbs, sl.in[i], tk, nn[i], 0, 64, st));
+            k_unpack_keys<<<grid_for(nn[i], 256), 256, 0, st>>>(tk, nn[i], outs[i]);
+        }
+    }
+    if (n_defer > 0 || n_x > 0) {
+        // entries per list: the phases' rooflines (56 B per entry of the keys they search)
+        EntryLists el{};
+        el.list[0] = defer; el.n[0] = n_defer; el.sum[0] = (unsigned long long *)(q + Q_ENT_ALL);
+        el.list[1] = defer_l; el.n[1] = n_def_l; el.sum[1] = (unsigned long long *)(q + Q_ENT_LEAN);
+        el.list[2] = defer_w; el.n[2] = n_def_w; el.sum[2] = (unsigned long long *)(q + Q_ENT_WIDE);
+        el.list[3] = list_x; el.n[3] = n_x; el.sum[3] = (unsigned long long *)(q + Q_ENT_XW);
+        el.off = off;
+        k_list_entries<<<dim3(16, 4), 256, 0, st>>>(el);
     }
     if (dbg2) {
         std::vector<unsigned long long> h((size_t)waves1 * 16);
@@ -4449,13 +4576,17 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 tot[11], tot[12], tot[13], tot[14], (double)tot[2] / std::max(1ULL, tot[4]), (double)tot[9] / waves1, mx9);
         HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 512) * 16, st));
     }
+    int waves_x = 0;
     // windows wider than 64: k_lin_xw on the third stream, alongside phases 2 and 3
-    const int n_x = qh[19];
     if (n_x > 0) {
         uint32_t capx = 1u << 12;
         while ((int64_t)capx < 2 * budget && capx < (1u << 30)) capx <<= 1;
-        const int waves_x = std::min(n_x, getenv("JH_XW_WAVES") ? std::max(1, atoi(getenv("JH_XW_WAVES"))) : 128);
         const uint64_t scr_x = (((uint64_t)(uint32_t)qh[26] | ((uint64_t)(uint32_t)qh[27] << 32)) + 255) & ~255ULL;
+        // one wave per key, up to four per CU (round 2 capped this at 128 waves)
+        int want_x = std::min(n_x, 4 * ctx->n_cu);
+        if (opts && opts->xw_waves > 0) want_x = std::min(n_x, opts->xw_waves);
+        const uint64_t per_x = (uint64_t)capx * XW_EW * 8 + (uint64_t)stack_cap * XW_EW * 8 + scr_x;
+        waves_x = fit_units(ctx, want_x, per_x, {WS_MEMO_X, WS_STACK_X, WS_SCRATCH_X});
         const bool freshx = ctx->ws_fresh(WS_MEMO_X) || ctx->bufs[WS_MEMO_X].bytes < (size_t)waves_x * capx * XW_EW * 8;
         uint64_t *memox = ctx->ws<uint64_t>(WS_MEMO_X, (size_t)waves_x * capx * XW_EW, /*zero=*/true);
         if (clear_memo && !freshx) HIP_TRY(hipMemsetAsync(memox, 0, ctx->bufs[WS_MEMO_X].bytes, st));
@@ -4474,6 +4605,71 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[9], ctx->aux2));
     }
+
+    // phase 2 hands a key that reaches P2_BUDGET inserts to phase 3 (when the
+    // phase has fewer waves than keys)
+    int64_t p2 = P2_BUDGET;
+    if (opts && opts->phase2_budget > 0) p2 = std::max<int64_t>(quick + 1, opts->phase2_budget);
+    uint32_t cap2 = 1u << 16;
+    while ((int64_t)cap2 < 2 * budget && cap2 < (1u << 30)) cap2 <<= 1;
+    if (const char *e = tune_env("JH_MEMO_CAP_SHIFT")) cap2 <<= std::max(0, std::min(3, atoi(e)));   // experiments
+    int32_t *defer3 = ctx->ws<int32_t>(WS_DEFER3, 2 * (size_t)(n_defer + 1));
+    int32_t *defer3w = defer3 + (n_defer + 1);
+    int32_t *claim = nullptr;
+    int waves_w = 0, waves2 = 0;
+    bool split3 = false, split3w = false;
+
+    // ---- the deferred WIDE keys (windows of 41-64 members or >= 256 states):
+    // their own pipeline on the fourth stream, beside the LEAN one. As many
+    // waves as keys, up to four per CU and bounded by free HBM (round 2: 32
+    // waves in phase 2 and 128 in phase 3, queued behind the LEAN kernels on
+    // one stream). With a wave per key there is one pass at the full budget;
+    // with fewer, phase 2 stops a key at P2_BUDGET and phase 3 restarts it
+    // (same waves and tables, a fresh generation range), the count of phase
+    // 3's keys read on the device: no host round trip.
+    DfsArgs bw{};
+    auto prep_wide = [&]() {
+        if (n_def_w == 0) return;
+        const uint64_t per_w = (uint64_t)cap2 * 16 + (uint64_t)stack_cap * sizeof(Frame) + MemoX::SLOTS * 8;
+        int want_w = std::min(n_def_w, 4 * ctx->n_cu);
+        if (opts && opts->wide_waves > 0) want_w = std::min(want_w, opts->wide_waves);
+        waves_w = fit_units(ctx, want_w, per_w, {WS_MEMO_WIDE, WS_STACK_WIDE, WS_SCRATCH_WIDE});
+        const bool freshw = ctx->ws_fresh(WS_MEMO_WIDE) || ctx->bufs[WS_MEMO_WIDE].bytes < (size_t)waves_w * cap2 * 16;
+        uint64_t *memow = ctx->ws<uint64_t>(WS_MEMO_WIDE, (size_t)waves_w * cap2 * 2, /*zero=*/true);
+        if (clear_memo && !freshw) HIP_TRY(hipMemsetAsync(memow, 0, ctx->bufs[WS_MEMO_WIDE].bytes, st));
+        bw = a;
+        bw.list = defer_w; bw.n_list = n_def_w; bw.n_list_dev = nullptr; bw.queue = q + 7;
+        bw.defer64 = nullptr; bw.defer_kind = nullptr; bw.defer_kind_count = nullptr;
+        split3w = waves_w < n_def_w && budget > p2;
+        bw.defer = split3w ? 1 : 0; bw.defer_list = defer3w; bw.defer_count = q + Q_DEFER3W;
+        bw.budget = split3w ? p2 : budget; bw.budget_full = split3w ? budget : 0;
+        bw.memo = memow; bw.memo_cap = cap2;
+        bw.stack = ctx->ws<Frame>(WS_STACK_WIDE, (size_t)waves_w * stack_cap);
+        bw.scratch = ctx->ws<char>(WS_SCRATCH_WIDE, (size_t)waves_w * MemoX::SLOTS * 8);
+        bw.scratch_bytes = MemoX::SLOTS * 8;
+        bw.gen_base = ctx->gen_base + (uint32_t)K + 1;
+        bw.claim = claim;                    // the BFS may settle a WIDE key with a narrow window
+        bw.probes = (unsigned long long *)(q + Q_PROBES_WIDE);
+        bw.seq_start = nullptr; bw.exit_count = nullptr; bw.dbg = nullptr; bw.defer_time = nullptr;
+    };
+    auto launch_wide = [&]() {
+        if (waves_w == 0) return;
+        HIP_TRY(hipStreamWaitEvent(ctx->aux4, ctx->ev[6], 0));
+        HIP_TRY(hipEventRecord(ctx->ev[14], ctx->aux4));
+        k_lin_seqw<<<waves_w, 64, MemoX::LDS, ctx->aux4>>>(bw);
+        HIP_TRY(hipGetLastError());
+        if (split3w) {
+            DfsArgs c3 = bw;
+            c3.list = defer3w; c3.n_list = 0; c3.n_list_dev = q + Q_DEFER3W; c3.queue = q + 20; c3.defer = 0;
+            c3.defer_list = nullptr; c3.defer_count = nullptr;
+            c3.budget = budget; c3.budget_full = 0;
+            c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
+            k_lin_seqw<<<waves_w, 64, MemoX::LDS, ctx->aux4>>>(c3);
+            HIP_TRY(hipGetLastError());
+        }
+        HIP_TRY(hipEventRecord(ctx->ev[15], ctx->aux4));
+    };
+
     unsigned long long *acc_stats = nullptr;
     int n_wg = 0;
     // the workgroup engine (k_lin_wg): exact WGL, dead subtrees enumerated by
@@ -4482,8 +4678,6 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     auto build_wg = [&](int wg_cus, int32_t *wg_claim, int32_t *wg_queue) -> WgArgs {
         acc_stats = ctx->ws<unsigned long long>(WS_ACC_STATS, 8);
         HIP_TRY(hipMemsetAsync(acc_stats, 0, 8 * sizeof(unsigned long long), st));
-        uint32_t cap2 = 1u << 16;
-        while ((int64_t)cap2 < 2 * budget && cap2 < (1u << 30)) cap2 <<= 1;
         // + slack: keys claimed in the set after the cap is hit are still recorded
         const uint64_t work_cap = (uint64_t)std::min<int64_t>(budget, (int64_t)1 << 30) + ACC_MAXROOTS + 16384;
         uint64_t gcap = 1024;
@@ -4494,10 +4688,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         const uint64_t per_wg = (uint64_t)cap2 * 16 + gcap * 8 + 3 * work_cap * 8 + (uint64_t)stack_cap * sizeof(Frame) +
                                 MemoW::SLOTS * 8 + wtab_b;
         uint64_t mem_limit = 48ULL << 30;
-        if (const char *e = getenv("JH_WG_MEM_GB")) mem_limit = (uint64_t)std::max(1, atoi(e)) << 30;
-        int per_cu = 1;
-        n_wg = std::min<int64_t>(n_defer, (int64_t)per_cu * wg_cus);
+        if (const char *e = tune_env("JH_WG_MEM_GB")) mem_limit = (uint64_t)std::max(1, atoi(e)) << 30;
+        n_wg = (int)std::min<int64_t>(n_def_l, (int64_t)wg_cus);
         n_wg = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)n_wg, mem_limit / per_wg));
+        n_wg = fit_units(ctx, n_wg, per_wg, {WS_WG_MEMO, WS_WG_GSET, WS_WG_WORK, WS_WG_PEND});
         const bool fresh2 = ctx->ws_fresh(WS_WG_MEMO) || ctx->bufs[WS_WG_MEMO].bytes < (size_t)n_wg * cap2 * 16;
         uint64_t *memo2 = ctx->ws<uint64_t>(WS_WG_MEMO, (size_t)n_wg * cap2 * 2, /*zero=*/true);
         if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_WG_MEMO].bytes, st));
@@ -4506,15 +4700,16 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         uint64_t *work = ctx->ws<uint64_t>(WS_WG_WORK, (size_t)n_wg * work_cap, /*zero=*/true);
         WgArgs wa{};
         wa.d = a;
-        wa.d.list = defer; wa.d.n_list = n_defer; wa.d.n_list_dev = nullptr; wa.d.queue = wg_queue; wa.d.defer = 0;
-        wa.d.defer_list = nullptr; wa.d.defer_count = nullptr; wa.d.defer_prog = nullptr;
+        wa.d.list = defer_l; wa.d.n_list = n_def_l; wa.d.n_list_dev = nullptr; wa.d.queue = wg_queue; wa.d.defer = 0;
+        wa.d.defer_list = nullptr; wa.d.defer_count = nullptr;
+        wa.d.defer64 = nullptr; wa.d.defer_kind = nullptr; wa.d.defer_kind_count = nullptr;
         wa.d.memo = memo2; wa.d.memo_cap = cap2;
         wa.d.stack = ctx->ws<Frame>(WS_WG_STACK, (size_t)n_wg * stack_cap);
         wa.d.scratch = ctx->ws<char>(WS_WG_SCR, (size_t)n_wg * MemoW::SLOTS * 8);
         wa.d.scratch_bytes = MemoW::SLOTS * 8;
         wa.d.budget = budget; wa.d.budget_full = 0; wa.d.claim = wg_claim;
         wa.d.gen_base = ctx->gen_base + (uint32_t)K + 1;
-        wa.d.dbg = nullptr; wa.d.probes = (unsigned long long *)(q + 8);
+        wa.d.dbg = nullptr; wa.d.probes = (unsigned long long *)(q + Q_PROBES_HELP);
         wa.gset = gset; wa.gset_cap = (uint32_t)gcap; wa.work = work; wa.work_cap = (uint32_t)work_cap;
         wa.wtab = ctx->ws<char>(WS_WG_WTAB, (size_t)n_wg * wtab_b); wa.wtab_bytes = wtab_b;
         if (dbgenv && atoi(dbgenv) >= 3) {
@@ -4524,7 +4719,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         wa.acc_stats = acc_stats;
         wa.pend_cap = (uint32_t)work_cap;
         wa.acc_t = ACC_T;
-        if (const char *e = getenv("JH_ACC_T")) wa.acc_t = (uint32_t)std::max(0, atoi(e));
+        if (const char *e = tune_env("JH_ACC_T")) wa.acc_t = (uint32_t)std::max(0, atoi(e));
         if (dbgenv && atoi(dbgenv) >= 4) {
             wa.key_prof = ctx->ws<unsigned long long>(WS_STATS_KEYS, 3 * (size_t)K);
             HIP_TRY(hipMemsetAsync(wa.key_prof, 0, 3 * sizeof(unsigned long long) * K, st));
@@ -4536,77 +4731,65 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         }
         return wa;
     };
-    int n_unres = 0, n_defer3 = 0;
-    const char *wg_env = getenv("JH_WG");
-    // JH_WG=1: the workgroup engine (k_lin_wg, exact DFS with accelerated dead
-    // subtrees) for deferred LEAN keys; default: the BFS / sequential race
+    int n_unres = 0;
+    const char *wg_env = tune_env("JH_WG");
+    // JH_WG=1 (tuning builds): the workgroup engine (k_lin_wg, exact DFS with
+    // accelerated dead subtrees) for deferred LEAN keys; default: the BFS /
+    // sequential race
     const bool use_wg = wg_env && atoi(wg_env) == 1;
     // JH_WG=2: the workgroup engine races the BFS in place of the sequential search
     const bool wg_race = wg_env && atoi(wg_env) == 2;
+    int wg2 = 0, n_help = 0;
     if (n_defer > 0 && use_wg) {
-        // Deferred keys, exact WGL with accelerated dead subtrees: LEAN keys on
-        // k_lin_wg (one workgroup per key, stream st), WIDE keys on the plain
-        // sequential search with the full budget (k_lin_seq3<false>, aux stream).
-        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
-        HIP_TRY(hipMemsetAsync(q + 18, 0, sizeof(int32_t), st));
-        WgArgs wa = build_wg(ctx->n_cu, nullptr, q);
-        const uint32_t cap2 = wa.d.memo_cap;
+        // Deferred LEAN keys on k_lin_wg (one workgroup per key, stream st),
+        // WIDE keys on their own pipeline (aux4)
+        WgArgs wa{};
+        if (n_def_l > 0) wa = build_wg(ctx->n_cu, nullptr, q);
+        prep_wide();
+        HIP_TRY(hipEventRecord(ctx->ev[6], st));
         HIP_TRY(hipEventRecord(ctx->ev[11], st));
-        k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, st>>>(wa);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        {
-            // WIDE deferred keys (windows of 41-64 members or >= 256 states)
-            const int waves3 = std::min(n_defer, 128);
-            const bool fresh3 = ctx->ws_fresh(WS_MEMO_P3) || ctx->bufs[WS_MEMO_P3].bytes < (size_t)waves3 * cap2 * 16;
-            uint64_t *memo3 = ctx->ws<uint64_t>(WS_MEMO_P3, (size_t)waves3 * cap2 * 2, /*zero=*/true);
-            if (clear_memo && !fresh3) HIP_TRY(hipMemsetAsync(memo3, 0, ctx->bufs[WS_MEMO_P3].bytes, st));
-            HIP_TRY(hipEventRecord(ctx->ev[6], st));
-            HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
-            DfsArgs c3 = a;
-            c3.list = defer; c3.n_list = n_defer; c3.n_list_dev = nullptr; c3.queue = q + 18; c3.defer = 0;
-            c3.defer_list = nullptr; c3.defer_count = nullptr; c3.defer_prog = nullptr;
-            c3.memo = memo3; c3.memo_cap = cap2;
-            c3.stack = ctx->ws<Frame>(WS_STACK_P3, (size_t)waves3 * stack_cap);
-            c3.scratch = ctx->ws<char>(WS_SCRATCH_P3, (size_t)waves3 * MemoH::SLOTS * 8);
-            c3.scratch_bytes = MemoH::SLOTS * 8;
-            c3.budget = budget; c3.budget_full = 0; c3.claim = nullptr;
-            c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
-            c3.dbg = nullptr; c3.probes = (unsigned long long *)(q + 22);
-            k_lin_seq3<false><<<waves3, 64, MemoM::LDS, ctx->aux>>>(c3);
+        if (n_def_l > 0) {
+            k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, st>>>(wa);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
-            HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
-            HIP_TRY(hipStreamWaitEvent(st, ctx->ev[7], 0));
         }
+        HIP_TRY(hipEventRecord(ctx->ev[5], st));
+        HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
+        HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
+        HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
+        launch_wide();
     } else if (n_defer > 0) {
         // Heavy keys: two exact searches race per key and the first to settle
         // it writes its verdict (emit_verdict), the other abandons it.
         //  - the workgroup BFS (stream st) settles keys with no reachable
-        //    terminal configuration (invalid) within the budget;
-        //  - the sequential search with the full budget (aux stream) settles
-        //    every key, and alone decides valid / :unknown.
-        int32_t *claim = ctx->ws<int32_t>(WS_CLAIM, K);
+        //    terminal configuration (invalid) within the budget, and valid
+        //    keys whose reachable set it can store (WGL's exact count);
+        //  - the sequential search with the full budget (aux stream: LEAN
+        //    keys; aux4: WIDE keys) settles every key.
+        claim = ctx->ws<int32_t>(WS_CLAIM, K);
         HIP_TRY(hipMemsetAsync(claim, 0, (size_t)K * sizeof(int32_t), st));
-        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
-        HIP_TRY(hipMemsetAsync(q + 3, 0, sizeof(int32_t), st));
-        HIP_TRY(hipMemsetAsync(q + 6, 0, sizeof(int32_t), st));
 
         // the BFS enumerates up to reach_cap configurations and keeps up to
         // ncap of them for WGL's exact count of valid keys (bfs_wgl_count)
         uint32_t ncap = 1u << 22;
-        if (const char *e = getenv("JH_BFS_NODES")) ncap = (uint32_t)std::max(1 << 16, std::min(1 << 26, atoi(e)));
+        if (const char *e = tune_env("JH_BFS_NODES")) ncap = (uint32_t)std::max(1 << 16, std::min(1 << 26, atoi(e)));
         const int64_t reach_cap = std::max<int64_t>(budget + 1, ncap);
         uint32_t set_cap = 1u << 12;
         while ((int64_t)set_cap < 2 * reach_cap && set_cap < (1u << 30)) set_cap <<= 1;
         const uint32_t q_cap = (uint32_t)std::min<int64_t>(reach_cap + 64, (int64_t)1 << 30);
+        uint32_t hcap = 1u << 16;
+        while (hcap < 2 * (uint64_t)ncap) hcap <<= 1;
+        const uint32_t lcap = (uint32_t)smax + 2;
         // CU split of the heavy-key pass (one BFS workgroup or one sequential
         // wave per CU, by LDS): invalid keys are few, the sequential searches
         // many (every valid deferred key), so most CUs go to the latter
         // 96 of 256 (round 2, with phase 2 at four waves per CU): C4 shard
         // 230 -> 223 ms, C3 ranks 0 / 3 / 6 flat (32: C4 +9 %, 128: no better)
         const int bfs_cus = std::max(1, std::min(96, ctx->n_cu * 3 / 8));
-        const int wg2 = std::min(n_defer, getenv("JH_BFS_CUS") ? std::max(1, atoi(getenv("JH_BFS_CUS"))) : bfs_cus);
+        wg2 = std::min(n_defer, tune_env("JH_BFS_CUS") ? std::max(1, atoi(tune_env("JH_BFS_CUS"))) : bfs_cus);
+        const uint64_t per_bfs = (uint64_t)set_cap * 8 + 4ULL * q_cap * 8 + scr_bytes_bfs + (uint64_t)ncap * 8 +
+                                 (uint64_t)lcap * 4 + (uint64_t)hcap * 16 + (uint64_t)ncap * 4 + ((uint64_t)ncap / 32 + 1) * 4 +
+                                 (uint64_t)ncap * 4 + (uint64_t)ncap * 8;
+        wg2 = fit_units(ctx, wg2, per_bfs, {WS_BFS_SET, WS_BFS_Q, WS_BFS_NODES, WS_BFS_HKEY, WS_BFS_TMPK});
         uint64_t *bset = ctx->ws<uint64_t>(WS_BFS_SET, (size_t)wg2 * set_cap);
         uint64_t *bq = ctx->ws<uint64_t>(WS_BFS_Q, (size_t)wg2 * 4 * q_cap);
         char *bscr = ctx->ws<char>(WS_SCRATCH_BFS, (size_t)wg2 * scr_bytes_bfs);
@@ -4623,14 +4806,12 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // every key the BFS settles carries WGL's exact count (the whole set for
         // an invalid key; path + dead closure for a valid one, bfs_wgl_count)
         c.reach_cap = reach_cap;
-        const bool bfs_only = getenv("JH_BFS_ONLY") && atoi(getenv("JH_BFS_ONLY"));
-        // JH_BFS_ONLY=1 (tests, debugging): no sequential search, the BFS settles every
-        // key it can (the others stay unsettled); JH_BFS_DBGV=1: its valid verdicts carry
-        // fail_entry = path length, cause = stored configurations, explored = count
-        c.dbg_plen = getenv("JH_BFS_DBGV") && atoi(getenv("JH_BFS_DBGV")) ? 1 : 0;
-        uint32_t hcap = 1u << 16;
-        while (hcap < 2 * (uint64_t)ncap) hcap <<= 1;
-        const uint32_t lcap = (uint32_t)smax + 2;
+        // JH_LIN_BFS_ONLY (tests): no sequential search, the BFS settles every
+        // key it can (the others stay unsettled); JH_BFS_DBGV=1 (tuning builds):
+        // its valid verdicts carry fail_entry = path length, cause = stored
+        // configurations, explored = count
+        const bool bfs_only = (lflags & JH_LIN_BFS_ONLY) != 0;
+        c.dbg_plen = tune_env("JH_BFS_DBGV") && atoi(tune_env("JH_BFS_DBGV")) ? 1 : 0;
         c.ncap = ncap; c.hcap = hcap; c.lcap = lcap;
         c.nodes = ctx->ws<uint64_t>(WS_BFS_NODES, (size_t)wg2 * ncap);
         c.lstart = ctx->ws<uint32_t>(WS_BFS_LSTART, (size_t)wg2 * lcap);
@@ -4650,25 +4831,31 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             ctx->lds_attr = true;
         }
 
-        uint32_t cap2 = 1u << 16;
-        while ((int64_t)cap2 < 2 * budget && cap2 < (1u << 30)) cap2 <<= 1;
-        if (const char *e = getenv("JH_MEMO_CAP_SHIFT")) cap2 <<= std::max(0, std::min(3, atoi(e)));   // experiments
         // late helpers (k_lin_wg in helper mode, wg_helper_pick): a few CUs
-        // taken from the sequential search; JH_HELPERS=0 turns them off
-        int n_help = bfs_only || wg_race ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 8));
-        if (const char *e = getenv("JH_HELPERS")) n_help = std::max(0, std::min(64, atoi(e)));
+        // taken from the sequential search of the LEAN keys
+        n_help = bfs_only || wg_race || n_def_l == 0 ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 8));
+        if (opts && opts->helpers > 0) n_help = std::min(64, opts->helpers);
+        if (lflags & JH_LIN_NO_HELPERS) n_help = 0;
         if (n_help > 0 && ctx->n_cu - wg2 - n_help < 16) n_help = 0;
         // phase 2's sequential search with four waves per CU and the 32 KB memo
-        // (k_lin_seq3), JH_P2_M=0 for one wave per CU and the 128 KB memo
-        // (k_lin_seq): measured C4 shard 268 -> 228 ms, C3 / ranks 3, 6 / C5 flat
-        const bool p2_m = !(getenv("JH_P2_M") && atoi(getenv("JH_P2_M")) == 0);
-        const int waves2 = std::min(n_defer, std::max(1, (ctx->n_cu - wg2 - n_help) * (p2_m ? 4 : 1)));
+        // (k_lin_seq3), p2_waves_per_cu = 1 for one wave per CU and the 128 KB
+        // memo (k_lin_seq): measured C4 shard 268 -> 228 ms, C3 / ranks 3, 6 / C5 flat
+        const bool p2_m = !(opts && opts->p2_waves_per_cu == 1);
+        if (n_def_l > 0) {
+            int want2 = std::min(n_def_l, std::max(1, (ctx->n_cu - wg2 - n_help) * (p2_m ? 4 : 1)));
+            if (opts && opts->lean_waves > 0) want2 = std::min(want2, opts->lean_waves);
+            const uint64_t per2 = (uint64_t)cap2 * 16 + (uint64_t)stack_cap * sizeof(Frame) + scr_bytes_h;
+            waves2 = fit_units(ctx, want2, per2, {WS_MEMO_DEEP, WS_STACK_DEEP, WS_SCRATCH_DEEP});
+        }
         // generation-tagged: zeroed once when allocated (and on wrap), not per call
-        const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;
-        uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
-        if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
+        uint64_t *memo2 = nullptr;
+        if (waves2 > 0) {
+            const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;
+            memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
+            if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
+        }
         WgArgs wr{};
-        if (wg_race) wr = build_wg(std::max(1, ctx->n_cu - wg2), claim, q + 6);
+        if (wg_race && n_def_l > 0) wr = build_wg(std::max(1, ctx->n_cu - wg2), claim, q + 6);
         WgArgs wh{};
         unsigned long long *seq_start = nullptr;
         if (n_help > 0) {
@@ -4679,22 +4866,19 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             HIP_TRY(hipMemsetAsync(taken, 0, (size_t)K * sizeof(int32_t), st));
             wh.seq_start = seq_start; wh.seq_exit = q + 28; wh.seq_waves = waves2; wh.taken = taken;
             uint64_t late_us = HELPER_LATE_US;
-            if (const char *e = getenv("JH_HELPER_LATE_US")) late_us = (uint64_t)std::max(0, atoi(e));
+            if (opts && opts->helper_late_us > 0) late_us = (uint64_t)opts->helper_late_us;
+            if (lflags & JH_LIN_HELPERS_NOW) late_us = 0;
             wh.late_ticks = late_us * 100;     // s_memrealtime: 100 MHz
         }
-        // the fork point: everything the phase-2 searches read (claims, queue
-        // counters, the cleared memo on a generation wrap) is ordered before it
-        HIP_TRY(hipEventRecord(ctx->ev[6], st));
-        Frame *stack2 = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap);
-        char *scr2 = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes_h);
-        // phase 2 stops at P2_BUDGET inserts and hands the key to phase 3
-        int64_t p2 = P2_BUDGET;
-        if (const char *e = getenv("JH_P2_BUDGET")) p2 = std::max<int64_t>(quick + 1, atoll(e));
-        const bool split3 = budget > p2;
-        int32_t *defer3 = ctx->ws<int32_t>(WS_DEFER3, n_defer + 1);
+        Frame *stack2 = waves2 > 0 ? ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap) : nullptr;
+        char *scr2 = waves2 > 0 ? ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes_h) : nullptr;
+        // a wave per key: one pass at the full budget; fewer waves than keys:
+        // phase 2 stops at p2 inserts and phase 3 restarts those keys
+        split3 = waves2 < n_def_l && budget > p2;
         DfsArgs b = a;
-        b.list = defer; b.n_list = n_defer; b.n_list_dev = nullptr; b.queue = q + 6; b.defer = split3 ? 1 : 0;
-        b.defer_list = defer3; b.defer_count = q + 16; b.defer_prog = nullptr;
+        b.list = defer_l; b.n_list = n_def_l; b.n_list_dev = nullptr; b.queue = q + 6; b.defer = split3 ? 1 : 0;
+        b.defer_list = defer3; b.defer_count = q + 16;
+        b.defer64 = nullptr; b.defer_kind = nullptr; b.defer_kind_count = nullptr;
         b.memo = memo2; b.memo_cap = cap2; b.stack = stack2; b.scratch = scr2; b.scratch_bytes = scr_bytes_h;
         b.budget = split3 ? p2 : budget;
         b.budget_full = split3 ? budget : 0;
@@ -4702,24 +4886,26 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         b.dbg = dbg ? dbg + 16 * 256 : nullptr; b.claim = claim;
         b.probes = (unsigned long long *)(q + 8);
         b.seq_start = seq_start; b.exit_count = seq_start ? q + 28 : nullptr;
+        b.defer_time = nullptr;
 
-        // fork: the BFS on st, the sequential search on the aux stream
+        // the fork point: everything the phase-2 searches read (claims, queue
+        // counters, sorted lists, the cleared memo on a generation wrap) is
+        // ordered before it; every table of phases 2 and 3 is allocated above
+        // (an allocation after the fork would synchronise the device)
+        prep_wide();
+        HIP_TRY(hipEventRecord(ctx->ev[6], st));
+        // fork: the BFS on st, the LEAN sequential search on aux, WIDE on aux4, helpers on aux3
         HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
         k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        {
-            DfsArgs bw = b;
-            bw.queue = q + 7;
-            bw.seq_start = nullptr; bw.exit_count = nullptr;
-            k_lin_seq<false><<<std::min(waves2, 32), 64, MemoH::LDS, ctx->aux>>>(bw);
-        }
-        if (bfs_only) {}
+        if (bfs_only || waves2 == 0) {}
         else if (wg_race) k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux>>>(wr);
         else if (p2_m) k_lin_seq3<true><<<waves2, 64, MemoM::LDS, ctx->aux>>>(b);
         else k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
+        if (!bfs_only) launch_wide();
         if (n_help > 0) {
             // every helper leaves once the sequential search has left its
             // queue (or after HELPER_MAX_TICKS): joined before the verdicts are read
@@ -4728,41 +4914,28 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ctx->ev[12], ctx->aux3));
         }
-        if (split3) {
-            // phase 3: the keys phase 2 handed over, full budget, 4 waves per CU
-            int32_t q16 = 0;
-            HIP_TRY(hipMemcpyAsync(&q16, q + 16, sizeof q16, hipMemcpyDeviceToHost, ctx->aux));
-            HIP_TRY(hipStreamSynchronize(ctx->aux));
-            n_defer3 = q16;
-        }
-        if (n_defer3 > 0) {
-            int waves3 = std::min(n_defer3, 4 * ctx->n_cu);
-            if (const char *e = getenv("JH_P3_WAVES")) waves3 = std::max(1, std::min(waves3, atoi(e)));
-            const bool fresh3 = ctx->ws_fresh(WS_MEMO_P3) || ctx->bufs[WS_MEMO_P3].bytes < (size_t)waves3 * cap2 * 16;
-            uint64_t *memo3 = ctx->ws<uint64_t>(WS_MEMO_P3, (size_t)waves3 * cap2 * 2, /*zero=*/true);
-            if (clear_memo && !fresh3) HIP_TRY(hipMemsetAsync(memo3, 0, ctx->bufs[WS_MEMO_P3].bytes, ctx->aux));
-            Frame *stack3 = ctx->ws<Frame>(WS_STACK_P3, (size_t)waves3 * stack_cap);
-            char *scr3 = ctx->ws<char>(WS_SCRATCH_P3, (size_t)waves3 * MemoH::SLOTS * 8);
+        if (split3 && !bfs_only && !wg_race) {
+            // phase 3: the LEAN keys phase 2 handed over, full budget, on phase 2's
+            // tables (same stream, phase 2 has ended; a fresh generation range).
+            // Few of them (no more than phase 2's CUs): a lone wave and the 128 KB
+            // LDS memo each, as in phase 2; more: four waves per CU. Both kernels
+            // are launched and the count phase 2 left on the device picks one.
             DfsArgs c3 = b;
-            c3.list = defer3; c3.n_list = n_defer3; c3.queue = q + 17; c3.defer = 0;
+            c3.list = defer3; c3.n_list = 0; c3.n_list_dev = q + 16; c3.defer = 0;
+            c3.defer_list = nullptr; c3.defer_count = nullptr;
             c3.seq_start = nullptr; c3.exit_count = nullptr;
-            c3.memo = memo3; c3.stack = stack3; c3.scratch = scr3; c3.scratch_bytes = MemoH::SLOTS * 8;
-            c3.budget = budget;
-            // a fresh generation range: phase 2's table entries of these keys are not reused
+            c3.budget = budget; c3.budget_full = 0;
             c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
             c3.dbg = nullptr;
-            {
-                DfsArgs cw = c3;
-                cw.queue = q + 18;
-                k_lin_seq3<false><<<std::min(waves3, 128), 64, MemoM::LDS, ctx->aux>>>(cw);
-            }
-            if (n_defer3 <= ctx->n_cu - wg2) {
-                // few of them (no more than phase 2's CUs): a lone wave and
-                // the 128 KB LDS memo each, as in phase 2
-                k_lin_seq<true><<<waves3, 64, MemoH::LDS, ctx->aux>>>(c3);
-            } else {
-                k_lin_seq3<true><<<waves3, 64, MemoM::LDS, ctx->aux>>>(c3);
-            }
+            c3.probes = (unsigned long long *)(q + Q_PROBES_P3);
+            const int few = std::max(1, ctx->n_cu - wg2);
+            DfsArgs c3a = c3;
+            c3a.queue = q + 17; c3a.n_max = few;
+            k_lin_seq<true><<<std::min(waves2, few), 64, MemoH::LDS, ctx->aux>>>(c3a);
+            HIP_TRY(hipGetLastError());
+            DfsArgs c3b = c3;
+            c3b.queue = q + 18; c3b.n_min = few + 1;
+            k_lin_seq3<true><<<waves2, 64, MemoM::LDS, ctx->aux>>>(c3b);
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
@@ -4779,7 +4952,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                             (long long)k, (kp[3 * k + 2] >> 8) & 0xFFF, kp[3 * k + 2] & 0xFF, (kp[3 * k + 2] >> 20) & 1,
                             kp[3 * k + 1], kp[3 * k], kp[3 * k + 2] >> 32);
         }
-        if (const char *dp = getenv("JH_BFS_DUMP")) {
+        if (const char *dp = tune_env("JH_BFS_DUMP")) {
             // debugging: workgroup 0's stored configurations (t:20 | s:12 | mask:32)
             HIP_TRY(hipStreamSynchronize(st));
             std::vector<uint64_t> nd(c.ncap);
@@ -4811,10 +4984,13 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                             (double)g[16 * w + 2] / std::max(1ULL, g[16 * w + 4]));
         }
     } else {
+        HIP_TRY(hipEventRecord(ctx->ev[6], st));
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
+        HIP_TRY(hipEventRecord(ctx->ev[10], st));
         HIP_TRY(hipEventRecord(ctx->ev[7], st));
     }
     if (n_x > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[9], 0));
+    if (waves_w > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[15], 0));
     HIP_TRY(hipEventRecord(ctx->ev[2], st));
     if (defer_times && n_defer > 0) {
         // timeline: when each deferred key was handed on (us after phase 1's
@@ -4845,9 +5021,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             fprintf(stderr, "[jh-defer] key %d explored %lld valid %d deferred %.1f us seq-start %.1f us\n", k,
                     heavy[i].first, vv[k].valid, (dt[2 + k] - dt[0]) / 100.0, st_us);
         }
-        int q[5] = {0, 0, 0, 0, 0};
-        for (auto &e2 : ev) q[std::min(4, (int)(e2.first / (std::max(1.0, (dt[1] - dt[0]) / 100.0) / 5)))]++;
-        fprintf(stderr, "[jh-defer] deferrals by fifth of phase 1: %d %d %d %d %d\n", q[0], q[1], q[2], q[3], q[4]);
+        int q5[5] = {0, 0, 0, 0, 0};
+        for (auto &e2 : ev) q5[std::min(4, (int)(e2.first / (std::max(1.0, (dt[1] - dt[0]) / 100.0) / 5)))]++;
+        fprintf(stderr, "[jh-defer] deferrals by fifth of phase 1: %d %d %d %d %d\n", q5[0], q5[1], q5[2], q5[3], q5[4]);
     }
     ctx->gen_base += gen_span;
 
@@ -4896,35 +5072,49 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         sum->valid = sh[0]; sum->n_invalid = sh[1]; sum->n_unknown = sh[2];
         sum->first_fail_entry = sh[3] == LLONG_MAX ? -1 : sh[3];
         sum->n_keys = sh[4]; sum->explored = sh[5];
-        sum->memo_probes = (int64_t)(((uint64_t)(uint32_t)qh[5] << 32) | (uint32_t)qh[4]);
+        sum->memo_probes = q64(qh, 4);
         float ms = 0, ms_dfs = 0;
         HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]));
         HIP_TRY(hipEventElapsedTime(&ms_dfs, ctx->ev[1], ctx->ev[4]));
         sum->device_ms = ms; sum->dfs_ms = ms_dfs;
         sum->n_deferred = n_defer;
-        sum->deferred_entries = (int64_t)(((uint64_t)(uint32_t)qh[25] << 32) | (uint32_t)qh[24]);
-        sum->seq_probes = (int64_t)(((uint64_t)(uint32_t)qh[9] << 32) | (uint32_t)qh[8]);
-        sum->seq_ms = 0; sum->bfs_ms = 0;
+        sum->deferred_entries = q64(qh, Q_ENT_ALL);
+        sum->seq_probes = q64(qh, 8);
+        sum->seq_ms = 0; sum->bfs_ms = 0; sum->p3_ms = 0; sum->wide_ms = 0; sum->xw_ms = 0;
         if (n_defer > 0) {
             float a2 = 0, b2 = 0;
             if (use_wg) HIP_TRY(hipEventElapsedTime(&a2, ctx->ev[11], ctx->ev[5]));
             else HIP_TRY(hipEventElapsedTime(&a2, ctx->ev[6], ctx->ev[10]));
             sum->seq_ms = a2;
             if (!use_wg) { HIP_TRY(hipEventElapsedTime(&b2, ctx->ev[6], ctx->ev[5])); sum->bfs_ms = b2; }
+            if (split3) { float c2 = 0; HIP_TRY(hipEventElapsedTime(&c2, ctx->ev[10], ctx->ev[7])); sum->p3_ms = c2; }
+            if (waves_w > 0) { float d2 = 0; HIP_TRY(hipEventElapsedTime(&d2, ctx->ev[14], ctx->ev[15])); sum->wide_ms = d2; }
         }
-        if (getenv("JH_DEBUG")) {
+        if (n_x > 0) { float e2 = 0; HIP_TRY(hipEventElapsedTime(&e2, ctx->ev[8], ctx->ev[9])); sum->xw_ms = e2; }
+        sum->p3_probes = q64(qh, Q_PROBES_P3);
+        sum->wide_probes = q64(qh, Q_PROBES_WIDE);
+        sum->xw_probes = q64(qh, 22);
+        sum->helper_probes = q64(qh, Q_PROBES_HELP);
+        sum->n_deferred_wide = n_def_w;
+        sum->n_phase3 = split3 ? qh[16] : 0;
+        sum->n_phase3_wide = split3w ? qh[Q_DEFER3W] : 0;
+        sum->n_xw = n_x;
+        sum->lean_entries = q64(qh, Q_ENT_LEAN);
+        sum->wide_entries = q64(qh, Q_ENT_WIDE);
+        sum->xw_entries = q64(qh, Q_ENT_XW);
+        sum->waves[0] = waves2; sum->waves[1] = waves_w; sum->waves[2] = split3 ? waves2 : 0; sum->waves[3] = waves_x;
+        if (dbgenv) {
             float a = 0, b = 0, c = 0;
             HIP_TRY(hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]));
             HIP_TRY(hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[4]));
-            HIP_TRY(hipEventElapsedTime(&c, ctx->ev[4], ctx->ev[2]));
             float d = 0;
             HIP_TRY(hipEventElapsedTime(&d, ctx->ev[4], ctx->ev[7]));
             HIP_TRY(hipEventElapsedTime(&c, ctx->ev[4], ctx->ev[5]));
-            float xw = 0, p2 = 0;
-            if (n_x > 0) HIP_TRY(hipEventElapsedTime(&xw, ctx->ev[8], ctx->ev[9]));
-            if (n_defer > 0) HIP_TRY(hipEventElapsedTime(&p2, ctx->ev[4], ctx->ev[10]));
-            fprintf(stderr, "[jh] keys=%lld prep=%.3f ms phase1=%.3f ms (waves %d) deferred=%d bfs=%.3f ms (gave up %d) seq=%.3f ms (phase 2 %.3f ms, phase 3: %d keys) wide=%d keys %.3f ms\n",
-                    (long long)K, a, b, waves1, n_defer, c, n_unres, d, p2, n_defer3, n_x, xw);
+            fprintf(stderr, "[jh] keys=%lld prep=%.3f ms phase1=%.3f ms (waves %d) deferred=%d (wide %d) bfs=%.3f ms (gave up %d) "
+                    "seq=%.3f ms (phase 2 %.3f ms, phase 3 %lld keys %.3f ms) wide %.3f ms (%d waves, phase 3 %lld keys) "
+                    "xw %d keys %.3f ms (%d waves)\n",
+                    (long long)K, a, b, waves1, n_defer, n_def_w, c, n_unres, d, sum->seq_ms, (long long)sum->n_phase3,
+                    sum->p3_ms, sum->wide_ms, waves_w, (long long)sum->n_phase3_wide, n_x, sum->xw_ms, waves_x);
             if (acc_stats && dbgenv && atoi(dbgenv) >= 3 && n_wg > 0) {
                 std::vector<unsigned long long> tr((size_t)n_wg * 256);
                 HIP_TRY(hipMemcpy(tr.data(), ctx->bufs[WS_DEBUG].p, tr.size() * 8, hipMemcpyDeviceToHost));

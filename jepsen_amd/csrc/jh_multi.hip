@@ -286,6 +286,14 @@ int multi_check_cas_independent(jh_ctx *g, const jh_history *h, const jh_lin_opt
         m.dfs_ms = std::max(m.dfs_ms, a.dfs_ms);
         m.seq_ms = std::max(m.seq_ms, a.seq_ms);
         m.bfs_ms = std::max(m.bfs_ms, a.bfs_ms);
+        m.p3_ms = std::max(m.p3_ms, a.p3_ms);
+        m.wide_ms = std::max(m.wide_ms, a.wide_ms);
+        m.xw_ms = std::max(m.xw_ms, a.xw_ms);
+        m.p3_probes += a.p3_probes; m.wide_probes += a.wide_probes; m.xw_probes += a.xw_probes;
+        m.helper_probes += a.helper_probes; m.n_deferred_wide += a.n_deferred_wide;
+        m.n_phase3 += a.n_phase3; m.n_phase3_wide += a.n_phase3_wide; m.n_xw += a.n_xw;
+        m.lean_entries += a.lean_entries; m.wide_entries += a.wide_entries; m.xw_entries += a.xw_entries;
+        for (int i = 0; i < 4; i++) m.waves[i] = std::max(m.waves[i], a.waves[i]);
     }
     if (sum) *sum = m;
     if (err && errlen) err[0] = 0;

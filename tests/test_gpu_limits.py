@@ -68,15 +68,11 @@ def test_unique_values(ctx, init):
 
 
 def test_per_key_interning_forced(ctx):
-    """JH_INTERN_PER_KEY=1 takes the per-key path on an ordinary C3 slice:
+    """JH_LIN_INTERN_PER_KEY takes the per-key path on an ordinary C3 slice:
     same verdicts and counts as the global numbering and the oracle."""
     cols, _ = synth.cas_register(n_keys=1000, ops_per_key=500, p_invalid=0.02, seed=13)
     v0, s0 = ctx.check_cas_independent(cols)
-    os.environ["JH_INTERN_PER_KEY"] = "1"
-    try:
-        v1, s1 = ctx.check_cas_independent(cols)
-    finally:
-        del os.environ["JH_INTERN_PER_KEY"]
+    v1, s1 = ctx.check_cas_independent(cols, flags=A.LIN_INTERN_PER_KEY)
     assert (v0 == v1).all()
     ov, _ = oracle.check_cas_independent(cols, threads=8)
     _same(v1, ov)
@@ -100,3 +96,22 @@ def test_too_many_states_is_per_key(ctx):
     assert int(v["valid"][0]) == A.UNKNOWN and A.CAUSES[int(v["cause"][0])] == "states"
     ov, _ = oracle.check_cas_independent(cols, threads=8)
     _same(v[1:], ov[1:])
+
+
+def test_huge_budget_fits_memory():
+    """the phase-2/3 memo tables, the WIDE pipeline and
+    the BFS workgroups are sized for the full budget, so at 2^24 they would
+    ask for more than the device holds; every such table is clamped by free
+    HBM (fit_units), and the call still returns every verdict, equal to the
+    oracle's. A private context: its tables are freed afterwards."""
+    from jepsen_amd import _native
+    cols, _ = synth.cas_register(n_keys=300, ops_per_key=600, p_invalid=0.05, p_info=0.03, seed=131)
+    c, _ = oracle.check_cas_independent(cols, budget=1 << 24, threads=16)
+    ctx = _native.Context(0)
+    try:
+        g, s = ctx.check_cas_independent(cols, budget=1 << 24, quick_budget=200)
+    finally:
+        ctx.close()
+    for f in A.VERDICT_FIELDS:
+        assert (g[f] == c[f]).all(), f
+    assert s.n_deferred > 0

@@ -70,28 +70,30 @@ def test_budget_and_deferral(ctx):
         _same(g, c)
 
 
-@pytest.mark.parametrize("quick", ["1", "40", "700"])
-def test_heavy_key_paths(ctx, quick, monkeypatch):
+@pytest.mark.parametrize("quick", [1, 40, 700])
+def test_heavy_key_paths(ctx, quick):
     """Force keys through the deferral -> workgroup BFS -> sequential DFS
     cascade with a tiny quick budget: results must not change."""
     cols, _ = synth.cas_register(n_keys=400, ops_per_key=150, p_invalid=0.2, p_info=0.05, seed=88)
     c, _ = oracle.check_cas_independent(cols, threads=8)
-    monkeypatch.setenv("JH_QUICK_BUDGET", quick)
-    g, _ = ctx.check_cas_independent(cols)
+    g, _ = ctx.check_cas_independent(cols, quick_budget=quick)
     _same(g, c)
-    g, _ = ctx.check_cas_independent(cols, budget=2000)
+    g, _ = ctx.check_cas_independent(cols, budget=2000, quick_budget=quick)
     c, _ = oracle.check_cas_independent(cols, budget=2000, threads=8)
     _same(g, c)
 
 
-@pytest.mark.parametrize("env", [
-    {"JH_HELPER_LATE_US": "0", "JH_QUICK_BUDGET": "40"},
-    {"JH_HELPER_LATE_US": "0", "JH_QUICK_BUDGET": "40", "JH_HELPERS": "48"},
-    {"JH_HELPER_LATE_US": "0", "JH_QUICK_BUDGET": "40", "JH_P2_BUDGET": "300"},
-    {"JH_HELPER_LATE_US": "0", "JH_QUICK_BUDGET": "40", "JH_P2_M": "1"},
-    {"JH_HELPERS": "0", "JH_QUICK_BUDGET": "40"},
+NOW = A.LIN_HELPERS_NOW
+
+
+@pytest.mark.parametrize("tune", [
+    dict(flags=NOW, quick_budget=40),
+    dict(flags=NOW, quick_budget=40, helpers=48),
+    dict(flags=NOW, quick_budget=40, phase2_budget=300, lean_waves=8),
+    dict(flags=NOW, quick_budget=40, p2_waves_per_cu=1),
+    dict(flags=A.LIN_NO_HELPERS, quick_budget=40),
 ])
-def test_late_helpers(ctx, env, monkeypatch):
+def test_late_helpers(ctx, tune):
     """Phase-2 late helpers (the workgroup engine racing the sequential search
     and the BFS on long-running keys): with no delay every deferred key gets a
     helper, which settles some of them first, hands others back when phase 3
@@ -99,40 +101,40 @@ def test_late_helpers(ctx, env, monkeypatch):
     cause, failing row and WGL count must equal the oracle's, at the full
     budget and at a budget the helpers run into."""
     cols, _ = synth.cas_register(n_keys=400, ops_per_key=200, p_invalid=0.1, p_info=0.05, seed=95)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     for budget in (None, 3000):
-        g, _ = ctx.check_cas_independent(cols, budget=budget)
+        g, _ = ctx.check_cas_independent(cols, budget=budget, **tune)
         c, _ = oracle.check_cas_independent(cols, budget=budget or A.DEFAULT_BUDGET, threads=8)
         _same(g, c)
 
 
-@pytest.mark.parametrize("p2", ["4097", "9000"])
-def test_phase3_handover(ctx, p2, monkeypatch):
-    """Keys past the phase-2 budget restart in phase 3 (4 waves per CU, HBM
-    memo): forcing a small phase-2 budget must not change any result, with
-    the full budget or a budget in between."""
+@pytest.mark.parametrize("p2,waves", [(4097, 1), (4097, 6), (9000, 3)])
+def test_phase3_handover(ctx, p2, waves):
+    """With fewer phase-2 waves than deferred keys, keys past the phase-2
+    budget restart in phase 3 (on phase 2's tables, the kernel picked on the
+    device by phase 3's key count: one wave per CU for few keys, four for
+    many): a small phase-2 budget and few waves must not change any result,
+    with the full budget or a budget in between."""
     cols, _ = synth.cas_register(n_keys=300, ops_per_key=400, p_invalid=0.1, p_info=0.05, seed=91)
-    monkeypatch.setenv("JH_P2_BUDGET", p2)
     for budget in (None, 20000):
-        g, _ = ctx.check_cas_independent(cols, budget=budget)
+        g, s = ctx.check_cas_independent(cols, budget=budget, phase2_budget=p2, lean_waves=waves, quick_budget=500)
         c, _ = oracle.check_cas_independent(cols, budget=budget or A.DEFAULT_BUDGET, threads=8)
         _same(g, c)
+        assert s.waves[0] == min(waves, s.n_deferred - s.n_deferred_wide)
+    assert s.n_phase3 > 0
 
 
-@pytest.mark.parametrize("waves", [None, "1"])
-def test_windows_wider_than_64(ctx, waves, monkeypatch):
+@pytest.mark.parametrize("waves", [None, 1])
+def test_windows_wider_than_64(ctx, waves):
     """Windows of 65..256 members (k_lin_xw, 4-word masks) and wider than
     256 (:unknown, cause window): verdict, cause, failing row and WGL cache
-    size equal the oracle's at several budgets; one wave (JH_XW_WAVES=1)
+    size equal the oracle's at several budgets; one wave (xw_waves=1)
     checks every wide key in turn with the same HBM table."""
-    if waves:
-        monkeypatch.setenv("JH_XW_WAVES", waves)
+    tune = {"xw_waves": waves} if waves else {}
     cols, _ = synth.cas_register(n_keys=24, ops_per_key=260, threads_per_key=120, readers=20,
                                  groups=120, process_limit=10 ** 6, p_info=0.08, p_invalid=0.2,
                                  seed=61)
     for budget in (3000, 40000) if waves else (3000, 40000, None):
-        g, _ = ctx.check_cas_independent(cols, budget=budget)
+        g, _ = ctx.check_cas_independent(cols, budget=budget, **tune)
         c, _ = oracle.check_cas_independent(cols, budget=budget or A.DEFAULT_BUDGET, threads=16)
         _same(g, c)
     assert (c["cause"] != 2).sum() > 0
@@ -148,6 +150,25 @@ def test_c5_shape(ctx):
     c, cs = oracle.check_cas_independent(cols, threads=16)
     _same(g, c)
     assert gs.n_unknown == cs.n_unknown and gs.n_unknown > 0
+
+
+@pytest.mark.parametrize("tune", [dict(), dict(wide_waves=2, phase2_budget=3000), dict(wide_waves=5)])
+def test_wide_pipeline(ctx, tune):
+    """The deferred WIDE keys (windows of 41-64 members) on their own stream:
+    a wave per key and one pass at the full budget (default), or fewer waves
+    than keys -- phase 2 to phase2_budget, then phase 3 restarts the keys past
+    it on the same tables, its key count read on the device. Verdicts, causes,
+    failing rows and WGL counts equal the oracle's at two budgets."""
+    cols, _ = synth.cas_register(n_keys=40, ops_per_key=300, threads_per_key=50, readers=25,
+                                 process_limit=100, p_info=0.1, p_invalid=0.1, seed=71)
+    for budget in (40000, 200000):
+        g, gs = ctx.check_cas_independent(cols, budget=budget, quick_budget=300, **tune)
+        c, _ = oracle.check_cas_independent(cols, budget=budget, threads=16)
+        _same(g, c)
+        assert gs.n_deferred_wide > 0 and gs.waves[1] == min(gs.n_deferred_wide, tune.get("wide_waves", 1 << 30))
+        assert gs.wide_entries > 0 and gs.wide_ms > 0
+    if "phase2_budget" in tune:
+        assert gs.n_phase3_wide > 0
 
 
 def test_c3_scale_properties(ctx):
@@ -293,28 +314,23 @@ def test_mutex_and_register_models(ctx):
 
 @pytest.mark.parametrize("seed,init", [(21, None), (22, 0), (23, None)])
 def test_bfs_exact_counts(ctx, seed, init):
-    """The BFS alone (JH_BFS_ONLY=1: no sequential search in the race) settles
+    """The BFS alone (JH_LIN_BFS_ONLY: no sequential search in the race) settles
     every deferred key -- invalid ones by their whole reachable set, valid ones
     by liveness + first-live-child path + closure of the dead children
     (bfs_wgl_count) -- with WGL's exact cache size, equal to the oracle's."""
-    import os
     cols, _ = synth.cas_register(n_keys=150, ops_per_key=300, threads_per_key=12, readers=6, groups=10,
                                  p_info=0.0, p_invalid=0.05, nemesis_every=0, init_nil=init is None, seed=seed)
-    os.environ["JH_BFS_ONLY"] = "1"
-    try:
-        v, s = ctx.check_cas_independent(cols, init=init)
-    finally:
-        del os.environ["JH_BFS_ONLY"]
+    v, s = ctx.check_cas_independent(cols, init=init, flags=A.LIN_BFS_ONLY)
     ov, _ = oracle.check_cas_independent(cols, init=A.NIL if init is None else init, threads=8)
     deferred = ov["explored"] > 4096
     assert deferred.sum() >= 5 and (ov["valid"][deferred] == A.VALID).sum() >= 3
     _same(v, ov)
 
 
-def test_memo_generation_wrap(monkeypatch):
+def test_memo_generation_wrap():
     """the memo tables are generation-tagged and cleared only
     when the 24-bit generation range wraps. A first call leaves entries tagged
-    with generations from 0; the second call is forced to wrap (JH_GEN_JUMP),
+    with generations from 0; the second call is forced to wrap (JH_LIN_GEN_JUMP),
     restarts at generation 0 and must clear every table (phase 1, phase 2's
     sequential search, the helpers, phase 3) before its searches read them,
     or the first call's configurations would look visited (C3-sized keys: the
@@ -326,7 +342,6 @@ def test_memo_generation_wrap(monkeypatch):
     c, _ = oracle.check_cas_independent(cols, threads=8)
     g1, _ = ctx.check_cas_independent(cols)
     _same(g1, c)
-    monkeypatch.setenv("JH_GEN_JUMP", "1")
-    g2, _ = ctx.check_cas_independent(cols)
+    g2, _ = ctx.check_cas_independent(cols, flags=A.LIN_GEN_JUMP)
     _same(g2, c)
     ctx.close()

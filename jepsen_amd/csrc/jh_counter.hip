@@ -11,22 +11,25 @@
 //
 // HBM-bound streaming passes (bytes per row read / written):
 //   k_cnt_prange  process range                                        8 / 0
-//   k_cnt_pack    packed row code (process - pmin) << 4 | f2 << 2 | type,
-//                 last row per process (LDS-privatised), add-value range,
-//                 and the complete pairing of every invocation whose
-//                 completion lies in its 2048-row chunk                     32 / 8
-//   k_cnt_pair_spill  pairing of the few invocations the chunk could not
-//                 pair (thread per spill, walks its process' rows)          ~0
+//   k_cnt_pack    one pass over the four columns the checker reads: the
+//                 complete pairing of every invocation whose completion lies
+//                 in its 2048-row chunk, and each row's contribution word
+//                 (kind | value) -- after (remove :fails?) / (remove op/fail?)
+//                 and (or inv ok), with the nil checks -- plus the last row
+//                 of every process (LDS-privatised) and the add-value range  32 / 4
+//   k_cnt_pair_spill  the few invocations the chunk could not pair (thread
+//                 per spill, walks its process' rows): completes their words ~0
 //   k_cnt_tile_sums / hipcub scan / k_cnt_tile_scan
 //                 reduce-then-scan of {lower, upper, reads} over 2048-row
-//                 tiles, per-row :fails?, orphan and nil checks fused in;
-//                 writes only at read rows (the ok read's row and upper,
-//                 the invoke read's lower)                                2 x 16 / ~0
+//                 tiles of contribution words; writes only at read rows (the
+//                 ok read's row and upper, the invoke read's lower)       2 x 4 / ~0
 //   k_cnt_triples the triples, in history order, errors, first failing row
 //                 (over the ~1% read rows only)
+// Round 2 packed a 4-byte row code and re-read code, pair and value (16 B per
+// row) in both scan passes; the contribution word carries what they need.
 // (A single-pass decoupled look-back scan over the 49 K tiles was measured
 // at 20.8 ms on MI355X: the tile-to-tile look-back chain is serial latency
-// across XCDs. Reduce-then-scan costs one extra 16 B/row read and is ~1 ms.)
+// across XCDs. Reduce-then-scan costs one extra 4 B/row read.)
 #include "jh_internal.h"
 #include <hipcub/hipcub.hpp>
 
@@ -48,7 +51,29 @@ struct CntMeta {
 };
 
 constexpr uint32_t F2_OTHER = 0, F2_ADD = 1, F2_READ = 2;
-constexpr int RF_OKREAD = 1, RF_INVREAD = 2;
+
+// A row's contribution word (checker.clj:709-727 after history/complete,
+// (remove :fails?) and (remove op/fail?)):
+//   bits 0-2  kind: what the row feeds
+//   bit  3    U: a completion no invocation has claimed yet (an orphan unless
+//             a spilled invocation of an earlier chunk claims it)
+//   bit  4    X: the value does not fit the word: read it from the value
+//             column (own row, or the completion's for (or inv ok))
+//   bits 5-31 the value, 27-bit signed (adds of 1 in the C2 workload)
+constexpr uint32_t CW_NONE = 0, CW_LO = 1, CW_HI = 2, CW_OKREAD = 3, CW_INVREAD = 4, CW_PEND = 5;
+constexpr uint32_t CW_U = 8, CW_X = 16;
+constexpr long long CW_VMAX = (1LL << 26) - 1, CW_VMIN = -(1LL << 26);
+__device__ __forceinline__ uint32_t cw_make(uint32_t kind, long long v) {
+    if (v < CW_VMIN || v > CW_VMAX) return kind | CW_X;
+    return kind | ((uint32_t)(int32_t)v << 5);
+}
+__device__ __forceinline__ long long cw_val(uint32_t w, const int64_t *__restrict__ val,
+                                            const int32_t *__restrict__ pair, int64_t r) {
+    if (!(w & CW_X)) return (long long)((int32_t)w >> 5);
+    long long v = val[r];
+    if (v == JH_NIL) v = val[pair[r]];        // (or inv ok): pair[r] is written for these rows
+    return v;
+}
 
 __global__ void __launch_bounds__(256) k_cnt_prange(const int64_t *__restrict__ proc, int64_t n, CntMeta *m) {
     long long lo = LLONG_MAX, hi = LLONG_MIN;
@@ -65,10 +90,11 @@ __global__ void __launch_bounds__(256) k_cnt_prange(const int64_t *__restrict__ 
     if (threadIdx.x == 0) { atomicMin(&m->pmin, lo); atomicMax(&m->pmax, hi); }
 }
 
-// packed row codes + last row of every process (per-chunk LDS hash of
-// (process -> max row), then one global atomicMax per distinct process) +
-// the add-value range for the overflow check, and the complete pairing of
-// every invocation whose completion lies in the same chunk.
+// One chunk of CHUNK rows per block: contribution words, the last row of
+// every process (per-chunk LDS hash of (process -> max row), then one global
+// atomicMax per distinct process), the add-value range for the overflow
+// check, and the complete pairing of every invocation whose completion lies
+// in the same chunk.
 //
 // Pairing (util.clj:606-640: an invocation's completion is the next
 // non-:info row of its process): the chunk's first PAIR_PROCS distinct
@@ -77,21 +103,24 @@ __global__ void __launch_bounds__(256) k_cnt_prange(const int64_t *__restrict__ 
 // row). An invocation's completion is then the lowest set bit after its own
 // lane in M[g][c], or in the next group with a non-zero M[g'][c]: O(1) LDS
 // reads per row. Invocations with no completion in the chunk, or of a
-// process beyond the first PAIR_PROCS, go to a spill list (k_cnt_pair_spill).
+// process beyond the first PAIR_PROCS, go to a spill list (k_cnt_pair_spill)
+// and their words stay CW_PEND until it completes them.
 constexpr int PAIR_PROCS = 32, PAIR_GROUPS = CHUNK / 64;
 __global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ proc,
                                                   const int64_t *__restrict__ type,
                                                   const int64_t *__restrict__ f,
                                                   const int64_t *__restrict__ val, int64_t n,
                                                   long long pmin, int32_t *__restrict__ last,
-                                                  uint32_t *__restrict__ code, int32_t *__restrict__ pair,
+                                                  uint32_t *__restrict__ cw, int32_t *__restrict__ pair,
                                                   int32_t *__restrict__ spill, unsigned int *__restrict__ n_spill,
                                                   CntMeta *m) {
     __shared__ uint32_t hk[HSLOTS];                 // process - pmin + 1 (0: empty)
     __shared__ int hv[HSLOTS];                      // its last row
     __shared__ int8_t hc[HSLOTS];                   // its compact index, -1 beyond PAIR_PROCS
-    __shared__ uint32_t sc[CHUNK];                  // the chunk's row codes
+    __shared__ uint8_t sc[CHUNK];                   // the chunk's rows: f2 << 2 | type
+    __shared__ int16_t sp[CHUNK];                   // each row's partner in the chunk (-1: none)
     __shared__ int8_t rc[CHUNK];                    // each row's compact process index (-1: none)
+    __shared__ long long sv[CHUNK];                 // the chunk's values
     __shared__ unsigned long long M[PAIR_GROUPS][PAIR_PROCS];
     __shared__ int nd, nls, gbase;
     __shared__ int32_t ls[CHUNK];                   // this chunk's spilled invocations
@@ -120,9 +149,9 @@ __global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ pr
         const int64_t ty = rt[k] & 3, ff = rf[k];
         const uint32_t f2 = ff == JH_F_ADD ? F2_ADD : ff == JH_F_READ ? F2_READ : F2_OTHER;
         const uint32_t pk = (uint32_t)(p - pmin);                                  // span < 2^28
-        const uint32_t x = (pk << 4) | (f2 << 2) | (uint32_t)ty;
-        code[r] = x;
-        sc[i] = x;
+        sc[i] = (uint8_t)((f2 << 2) | (uint32_t)ty);
+        sv[i] = rv[k];
+        sp[i] = -1;
         if (f2 == F2_ADD && (ty == T_INVOKE || ty == T_OK)) {
             const long long v = rv[k];
             if (v != JH_NIL) am = max(am, v < 0 ? (v == LLONG_MIN ? LLONG_MAX : -v) : v);
@@ -145,7 +174,8 @@ __global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ pr
         }
         if (slot >= 0) atomicMax(&hv[slot], (int)r);
         else atomicMax(&last[pk], (int)r);
-        rc[i] = slot >= 0 ? (int8_t)-2 : (int8_t)-1;   // -2: in the hash; its index is read below
+        rc[i] = slot >= 0 ? (int8_t)slot : (int8_t)-1;   // provisional: low byte of the hash slot
+        ls[i] = slot;                                     // (the full slot, until the spill list needs ls)
     }
     am = block_reduce256(am, RedMax(), sh);
     na = block_reduce256(na, RedSum(), sh);
@@ -159,13 +189,8 @@ __global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ pr
     // compact process index of every row (the hash is complete now), and the
     // group masks of non-:info rows
     for (int i = threadIdx.x; i < nc; i += blockDim.x) {
-        int c = -1;
-        if (rc[i] == -2) {
-            const uint32_t pk = sc[i] >> 4;
-            uint32_t h = (uint32_t)jh_mix64((uint64_t)((long long)pk + pmin)) & (HSLOTS - 1);
-            while (hk[h] != pk + 1) h = (h + 1) & (HSLOTS - 1);
-            c = hc[h];
-        }
+        const int slot = ls[i];
+        const int c = slot >= 0 ? hc[slot] : -1;
         rc[i] = (int8_t)c;
         if (c >= 0 && (sc[i] & 3) != T_INFO) atomicOr(&M[i >> 6][c], 1ULL << (i & 63));
     }
@@ -173,7 +198,6 @@ __global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ pr
     for (int i = threadIdx.x; i < nc; i += blockDim.x) {
         const uint32_t x = sc[i];
         if ((x & 3) != T_INVOKE) continue;
-        const int64_t r = c0 + i;
         const int c = rc[i];
         int got = -1;
         if (c >= 0) {
@@ -184,14 +208,57 @@ __global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ pr
                 for (int g2 = g + 1; g2 < PAIR_GROUPS && (g2 << 6) < nc; g2++)
                     if (M[g2][c]) { got = (g2 << 6) + __builtin_ctzll(M[g2][c]); break; }
         }
-        if (got < 0) {
-            ls[atomicAdd(&nls, 1)] = (int32_t)r;       // spills gather in LDS: one global atomic per chunk
-        } else if ((sc[got] & 3) == T_INVOKE) {
+        if (got >= 0 && (sc[got] & 3) == T_INVOKE) {
             atomicMin(&m->viol1, ((unsigned long long)(c0 + got) << 4) | JH_CAUSE_DOUBLE_INVOKE);
-        } else {
-            pair[r] = (int32_t)(c0 + got);
-            pair[c0 + got] = (int32_t)r;
+            got = -2;
         }
+        sp[i] = (int16_t)got;                      // -1: spill (no completion in the chunk)
+        if (got >= 0) sp[got] = (int16_t)i;
+    }
+    if (threadIdx.x == 0) nls = 0;
+    __syncthreads();
+    // the contribution words
+    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+        const uint32_t x = sc[i];
+        const uint32_t ty = x & 3, f2 = x >> 2;
+        const int64_t r = c0 + i;
+        const int c = sp[i];
+        uint32_t w = CW_NONE;
+        if (ty == T_INVOKE) {
+            if (c == -1) {
+                ls[atomicAdd(&nls, 1)] = (int32_t)r;   // spills gather in LDS: one global atomic per chunk
+                w = f2 == F2_READ ? CW_INVREAD : f2 == F2_ADD ? CW_PEND : CW_NONE;
+            } else if (f2 == F2_READ) {
+                w = CW_INVREAD;
+            } else if (f2 == F2_ADD && c >= 0 && (sc[c] & 3) != T_FAIL) {
+                // (remove :fails?) keeps it: upper += (or inv ok)
+                long long v = sv[i];
+                bool own = true;
+                if (v == JH_NIL) { v = sv[c]; own = false; }
+                if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
+                else {
+                    w = cw_make(CW_HI, v);
+                    if ((w & CW_X) && !own) pair[r] = (int32_t)(c0 + c);
+                }
+            }
+        } else if (ty == T_OK || ty == T_FAIL) {
+            const uint32_t u = c < 0 ? CW_U : 0u;      // no invocation in the chunk (yet)
+            if (ty == T_OK && f2 == F2_ADD) {
+                const long long v = sv[i];
+                if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
+                else w = cw_make(CW_LO, v);
+            } else if (ty == T_OK && f2 == F2_READ) {
+                // its pending read must come from an [:invoke :read] (checker.clj:713-716)
+                if (c >= 0 && (sc[c] >> 2) != F2_READ)
+                    atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_ORPHAN);
+                else {
+                    w = CW_OKREAD;
+                    if (c >= 0) pair[r] = (int32_t)(c0 + c);
+                }
+            }
+            w |= u;
+        }
+        cw[r] = w;
     }
     __syncthreads();
     if (threadIdx.x == 0 && nls) gbase = (int)atomicAdd(n_spill, (unsigned int)nls);
@@ -199,128 +266,131 @@ __global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ pr
     for (int k = threadIdx.x; k < nls; k += blockDim.x) spill[gbase + k] = ls[k];
 }
 
-// the spilled invocations: one thread each walks the codes forward to the
-// completion, or past its process' last row (no completion: stays open)
-__global__ void __launch_bounds__(256) k_cnt_pair_spill(const uint32_t *__restrict__ code, int64_t n,
-                                                        const int32_t *__restrict__ last,
+// the spilled invocations: one thread each walks its process' rows forward
+// to the completion, or past the process' last row (no completion: a crashed
+// op, which stays in), and completes the invocation's word (and claims the
+// completion's)
+__global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restrict__ proc,
+                                                        const int64_t *__restrict__ type,
+                                                        const int64_t *__restrict__ f,
+                                                        const int64_t *__restrict__ val, int64_t n,
+                                                        long long pmin, const int32_t *__restrict__ last,
                                                         const int32_t *__restrict__ spill,
                                                         const unsigned int *__restrict__ n_spill,
-                                                        int32_t *__restrict__ pair, CntMeta *m) {
+                                                        uint32_t *__restrict__ cw, int32_t *__restrict__ pair,
+                                                        CntMeta *m) {
     const unsigned int ns = *n_spill;
     for (unsigned int s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
         const int64_t r = spill[s];
-        const uint32_t p = code[r] >> 4;
-        const int64_t lr = last[p];
+        const long long p = proc[r];
+        const int64_t ff = f[r];
+        const int64_t lr = last[p - pmin];
+        int64_t got = -1;
         for (int64_t j = r + 1; j <= lr; j++) {
-            const uint32_t y = code[j];
-            if ((y >> 4) != p || (y & 3) == T_INFO) continue;
-            if ((y & 3) == T_INVOKE) atomicMin(&m->viol1, ((unsigned long long)j << 4) | JH_CAUSE_DOUBLE_INVOKE);
-            else { pair[r] = (int32_t)j; pair[j] = (int32_t)r; }
+            if (proc[j] != p) continue;
+            const int64_t ty = type[j] & 3;
+            if (ty == T_INFO) continue;
+            if (ty == T_INVOKE) { atomicMin(&m->viol1, ((unsigned long long)j << 4) | JH_CAUSE_DOUBLE_INVOKE); got = -2; }
+            else got = j;
             break;
+        }
+        if (got >= 0) atomicAnd(&cw[got], ~CW_U);
+        if (ff == JH_F_ADD) {
+            uint32_t w = CW_NONE;
+            const bool failed = got >= 0 && (type[got] & 3) == T_FAIL;
+            if (got != -2 && !failed) {
+                long long v = val[r];
+                bool own = true;
+                if (v == JH_NIL && got >= 0) { v = val[got]; own = false; }
+                if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
+                else {
+                    w = cw_make(CW_HI, v);
+                    if ((w & CW_X) && !own) pair[r] = (int32_t)got;
+                }
+            }
+            cw[r] = w;
+        } else if (ff == JH_F_READ && got >= 0 && (type[got] & 3) == T_OK) {
+            pair[got] = (int32_t)r;
+        } else if (got >= 0 && (type[got] & 3) == T_OK && f[got] == JH_F_READ) {
+            // an :ok :read completing an invocation that is not a read
+            atomicMin(&m->viol2, ((unsigned long long)got << 4) | JH_CAUSE_ORPHAN);
+            atomicAnd(&cw[got], ~7u);
         }
     }
 }
 
-// per-row contributions and prefixes of lower / upper / ok reads; flags mark
-// the read rows
+// per-row contributions and prefixes of lower / upper / ok reads (an :ok
+// :read still marked U has no invocation: an orphan, never a read row, so
+// pair is only ever read where it was written)
 struct CntAcc {
     long long lo, hi;
     int nr, flags;
 };
 
-// per-row contribution (checker.clj:709-727 after complete / remove :fails?);
-// orphans, :fails? and nil checks fused in
-__device__ __forceinline__ CntAcc cnt_row(const uint32_t *__restrict__ code, const int32_t *__restrict__ pair,
-                                          const int64_t *__restrict__ val, CntMeta *m, int64_t r) {
-    const uint32_t x = code[r];
-    const uint32_t ty = x & 3, f2 = (x >> 2) & 3;
-    const int32_t c = pair[r];
-    CntAcc a{0, 0, 0, 0};
-    if ((ty == T_OK || ty == T_FAIL) && c < 0)
-        atomicMin(&m->viol1, ((unsigned long long)r << 4) | JH_CAUSE_ORPHAN);
-    if (f2 == F2_ADD) {
-        if (ty == T_INVOKE) {
-            const bool failed = c >= 0 && (code[c] & 3) == T_FAIL;
-            if (!failed) {
-                long long v = val[r];
-                if (v == JH_NIL && c >= 0) v = val[c];          // (or inv ok)
-                if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
-                else a.hi = v;
-            }
-        } else if (ty == T_OK) {
-            const long long v = val[r];
-            if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
-            else a.lo = v;
-        }
-    } else if (f2 == F2_READ) {
-        if (ty == T_OK) {
-            // its pending read must come from an [:invoke :read] (checker.clj:713-716)
-            if (c < 0 || ((code[c] >> 2) & 3) != F2_READ)
-                atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_ORPHAN);
-            else { a.nr = 1; a.flags = RF_OKREAD; }
-        } else if (ty == T_INVOKE) {
-            a.flags = RF_INVREAD;
-        }
-    }
-    return a;
-}
-
-// Reduce-then-scan over tiles of CNT_TILE rows (the rows of a tile are read
-// twice, 16 B each time: 32 B/row in all, coalesced).
+// Reduce-then-scan over tiles of CNT_TILE rows (each tile's words are read
+// twice, 4 B each time).
 constexpr int CNT_TILE = 2048, CNT_PER = CNT_TILE / 256;
 
-__global__ void __launch_bounds__(256) k_cnt_tile_sums(const uint32_t *__restrict__ code,
+__global__ void __launch_bounds__(256) k_cnt_tile_sums(const uint32_t *__restrict__ cw,
                                                        const int32_t *__restrict__ pair,
                                                        const int64_t *__restrict__ val, int64_t n,
                                                        CntMeta *m, CntAcc *__restrict__ agg) {
     __shared__ long long sh[4];
     const int64_t base = (int64_t)blockIdx.x * CNT_TILE;
     long long lo = 0, hi = 0, nr = 0;
+    unsigned long long orphan = ~0ULL;
+    // 8 consecutive words per thread, two 16-byte loads
+    const int64_t r0 = base + (int64_t)threadIdx.x * CNT_PER;
+    uint32_t w[CNT_PER];
+    if (r0 + CNT_PER <= n) {
+        const uint4 a = *(const uint4 *)(cw + r0), b = *(const uint4 *)(cw + r0 + 4);
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    } else {
 #pragma unroll
-    for (int k = 0; k < CNT_PER; k++) {
-        const int64_t r = base + k * 256 + threadIdx.x;
-        if (r < n) { const CntAcc a = cnt_row(code, pair, val, m, r); lo += a.lo; hi += a.hi; nr += a.nr; }
+        for (int j = 0; j < CNT_PER; j++) w[j] = r0 + j < n ? cw[r0 + j] : 0u;
     }
+#pragma unroll
+    for (int j = 0; j < CNT_PER; j++) {
+        const uint32_t k = w[j] & 7;
+        if (w[j] & CW_U) orphan = min(orphan, (unsigned long long)(r0 + j));
+        if (k == CW_LO) lo += cw_val(w[j], val, pair, r0 + j);
+        else if (k == CW_HI) hi += cw_val(w[j], val, pair, r0 + j);
+        else if (k == CW_OKREAD && !(w[j] & CW_U)) nr++;
+    }
+    if (orphan != ~0ULL) atomicMin(&m->viol1, (orphan << 4) | JH_CAUSE_ORPHAN);
     lo = block_reduce256(lo, RedSum(), sh);
     hi = block_reduce256(hi, RedSum(), sh);
     nr = block_reduce256(nr, RedSum(), sh);
     if (threadIdx.x == 0) agg[blockIdx.x] = CntAcc{lo, hi, (int)nr, 0};
 }
 
-// rows in order within the tile (LDS transpose: thread t takes rows
-// CNT_PER*t ..), from the tile's exclusive prefix; writes only at read rows
-__global__ void __launch_bounds__(256) k_cnt_tile_scan(const uint32_t *__restrict__ code,
+// thread t takes rows CNT_PER*t .. of the tile in order, from the tile's
+// exclusive prefix; writes only at read rows
+__global__ void __launch_bounds__(256) k_cnt_tile_scan(const uint32_t *__restrict__ cw,
                                                        const int32_t *__restrict__ pair,
                                                        const int64_t *__restrict__ val, int64_t n,
-                                                       CntMeta *m, const CntAcc *__restrict__ pre,
+                                                       const CntAcc *__restrict__ pre,
                                                        int32_t *__restrict__ rd_row, int64_t *__restrict__ rd_hi,
                                                        int64_t *__restrict__ lo_at, CntAcc *total) {
-    // a row feeds at most one of lower / upper / reads: LDS holds its value
-    // and a kind byte (20 KB per block: occupancy hides the HBM latency)
-    constexpr int PAD = CNT_TILE + CNT_TILE / CNT_PER;
-    __shared__ long long s_v[PAD];
-    __shared__ uint8_t s_k[PAD];
     __shared__ long long sc[3][4];
     const int tid = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * CNT_TILE;
+    const int64_t r0 = base + (int64_t)tid * CNT_PER;
+    uint32_t w[CNT_PER];
+    if (r0 + CNT_PER <= n) {
+        const uint4 a = *(const uint4 *)(cw + r0), b = *(const uint4 *)(cw + r0 + 4);
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    } else {
 #pragma unroll
-    for (int k = 0; k < CNT_PER; k++) {
-        const int j = k * 256 + tid;
-        const int64_t r = base + j;
-        CntAcc a{0, 0, 0, 0};
-        if (r < n) a = cnt_row(code, pair, val, m, r);
-        const int q = j + j / CNT_PER;
-        s_v[q] = a.lo ? a.lo : a.hi;
-        s_k[q] = (uint8_t)(a.lo ? 1 : a.hi ? 2 : a.flags == RF_OKREAD ? 3 : a.flags == RF_INVREAD ? 4 : 0);
+        for (int j = 0; j < CNT_PER; j++) w[j] = r0 + j < n ? cw[r0 + j] : 0u;
     }
-    __syncthreads();
     long long lo = 0, hi = 0, nr = 0;
-    const int q0 = tid * (CNT_PER + 1);
 #pragma unroll
     for (int j = 0; j < CNT_PER; j++) {
-        const int kd = s_k[q0 + j];
-        const long long v = s_v[q0 + j];
-        lo += kd == 1 ? v : 0; hi += kd == 2 ? v : 0; nr += kd == 3;
+        const uint32_t k = w[j] & 7;
+        if (k == CW_LO) lo += cw_val(w[j], val, pair, r0 + j);
+        else if (k == CW_HI) hi += cw_val(w[j], val, pair, r0 + j);
+        else if (k == CW_OKREAD && !(w[j] & CW_U)) nr++;
     }
     // block exclusive scan of the per-thread sums: wave shuffles, then the
     // totals of the waves before
@@ -333,17 +403,17 @@ __global__ void __launch_bounds__(256) k_cnt_tile_scan(const uint32_t *__restric
     }
     if (lane == 63) { sc[0][wv] = il; sc[1][wv] = ih; sc[2][wv] = in; }
     __syncthreads();
-    for (int w = 0; w < wv; w++) { il += sc[0][w]; ih += sc[1][w]; in += sc[2][w]; }
+    for (int v = 0; v < wv; v++) { il += sc[0][v]; ih += sc[1][v]; in += sc[2][v]; }
     const CntAcc p = pre[blockIdx.x];
     long long rl = p.lo + il - lo, rh = p.hi + ih - hi, rn = p.nr + in - nr;
 #pragma unroll
     for (int j = 0; j < CNT_PER; j++) {
-        const int kd = s_k[q0 + j];
-        const long long v = s_v[q0 + j];
-        rl += kd == 1 ? v : 0; rh += kd == 2 ? v : 0; rn += kd == 3;
-        const int64_t r = base + (int64_t)tid * CNT_PER + j;
-        if (kd == 3) { rd_row[rn - 1] = (int32_t)r; rd_hi[rn - 1] = rh; }
-        else if (kd == 4) lo_at[r] = rl;
+        const uint32_t k = w[j] & 7;
+        const int64_t r = r0 + j;
+        if (k == CW_LO) rl += cw_val(w[j], val, pair, r);
+        else if (k == CW_HI) rh += cw_val(w[j], val, pair, r);
+        else if (k == CW_OKREAD && !(w[j] & CW_U)) { rn++; rd_row[rn - 1] = (int32_t)r; rd_hi[rn - 1] = rh; }
+        else if (k == CW_INVREAD) lo_at[r] = rl;
         if (r == n - 1) *total = CntAcc{rl, rh, (int)rn, 0};
     }
 }
@@ -356,8 +426,9 @@ struct CntSumOp {
 
 __global__ void k_cnt_triples(const int32_t *__restrict__ rd_row, const int64_t *__restrict__ rd_hi,
                               const int64_t *__restrict__ lo_at, const int32_t *__restrict__ pair,
-                              const int64_t *__restrict__ val, int64_t nr, int64_t *__restrict__ out,
-                              int64_t cap, CntMeta *m) {
+                              const int64_t *__restrict__ val, const CntAcc *__restrict__ total,
+                              int64_t *__restrict__ out, int64_t cap, CntMeta *m) {
+    const int64_t nr = total->nr;
     long long nerr = 0;
     unsigned long long ferr = ~0ULL;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nr;
@@ -407,24 +478,20 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
     if (span >= (1ULL << 28)) throw_jh(JH_EUNSUPPORTED, "process ids span more than 2^28");
 
     int32_t *last = ctx->ws<int32_t>(WS_C_LAST, span + 1);
+    // pair: written (and read) only at :ok :read rows and at the rare rows
+    // whose value word escapes to the column
     int32_t *pair = ctx->ws<int32_t>(WS_C_PAIR, n);
-    uint32_t *code = ctx->ws<uint32_t>(WS_C_PT, n);
+    uint32_t *cw = ctx->ws<uint32_t>(WS_C_PT, n + 8);
     HIP_TRY(hipMemsetAsync(last, 0xFF, sizeof(int32_t) * (span + 1), st));
-    HIP_TRY(hipMemsetAsync(pair, 0xFF, sizeof(int32_t) * n, st));
     int32_t *spill = ctx->ws<int32_t>(WS_C_IDX, n);          // reused for the read rows below
     unsigned int *n_spill = (unsigned int *)ctx->ws<int32_t>(WS_C_FLAG, 4);
     HIP_TRY(hipMemsetAsync(n_spill, 0, sizeof(unsigned int), st));
     k_cnt_pack<<<(int)((n + CHUNK - 1) / CHUNK), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
-                                                              mh.pmin, last, code, pair, spill, n_spill, m);
-    k_cnt_pair_spill<<<grid_for(n / 64 + 1, 256, 4096), 256, 0, st>>>(code, n, last, spill, n_spill, pair, m);
-    HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    // Clojure + throws on long overflow; if no prefix can overflow we need no
-    // ordered overflow check (else the shim falls back to the JVM checker).
-    if (mh.amax_abs > 0 && (unsigned long long)mh.amax_abs > (unsigned long long)(LLONG_MAX / std::max(1LL, mh.n_add)))
-        throw_jh(JH_EUNSUPPORTED, "add values large enough to overflow a long");
+                                                              mh.pmin, last, cw, pair, spill, n_spill, m);
+    k_cnt_pair_spill<<<grid_for(n / 64 + 1, 256, 4096), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
+                                                                      mh.pmin, last, spill, n_spill, cw, pair, m);
 
-    // reduce-then-scan over tiles of rows
+    // reduce-then-scan over tiles of contribution words
     int32_t *rd_row = ctx->ws<int32_t>(WS_C_IDX, n);
     int64_t *rd_hi = ctx->ws<int64_t>(WS_C_HI, n);
     int64_t *lo_at = ctx->ws<int64_t>(WS_C_LO, n);
@@ -432,25 +499,32 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
     CntAcc *agg = ctx->ws<CntAcc>(WS_C_OUT2, 2 * n_tiles + 1);
     CntAcc *pre = agg + n_tiles;
     CntAcc *total = pre + n_tiles;
-    k_cnt_tile_sums<<<(unsigned)n_tiles, 256, 0, st>>>(code, pair, dh->value, n, m, agg);
+    k_cnt_tile_sums<<<(unsigned)n_tiles, 256, 0, st>>>(cw, pair, dh->value, n, m, agg);
     size_t tb = 0;
     HIP_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, tb, agg, pre, CntSumOp(), CntAcc{0, 0, 0, 0}, (int)n_tiles, st));
     void *tmp = ctx->ws<char>(WS_S_TMP, tb);
     HIP_TRY(hipcub::DeviceScan::ExclusiveScan(tmp, tb, agg, pre, CntSumOp(), CntAcc{0, 0, 0, 0}, (int)n_tiles, st));
-    k_cnt_tile_scan<<<(unsigned)n_tiles, 256, 0, st>>>(code, pair, dh->value, n, m, pre, rd_row, rd_hi, lo_at, total);
+    k_cnt_tile_scan<<<(unsigned)n_tiles, 256, 0, st>>>(cw, pair, dh->value, n, pre, rd_row, rd_hi, lo_at, total);
+    // the triples of every :ok :read (their count stays on the device: the
+    // kernel reads it), then one host round trip for the verdict
+    const int64_t cap = std::min(n, reads_cap);
+    int64_t *out = ctx->ws<int64_t>(WS_C_OUT, 3 * std::max<int64_t>(cap, 1));
+    k_cnt_triples<<<grid_for(n / 64 + 1, 256, 4096), 256, 0, st>>>(rd_row, rd_hi, lo_at, pair, dh->value, total,
+                                                                  out, cap, m);
     CntAcc th;
     HIP_TRY(hipMemcpyAsync(&th, total, sizeof th, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    const int64_t nr = th.nr;
-    const int64_t cap = std::min(nr, reads_cap);
-    int64_t *out = ctx->ws<int64_t>(WS_C_OUT, 3 * std::max<int64_t>(cap, 1));
-    if (nr > 0)
-        k_cnt_triples<<<grid_for(nr, 256, 4096), 256, 0, st>>>(rd_row, rd_hi, lo_at, pair, dh->value, nr,
-                                                              out, cap, m);
     HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
-    if (cap > 0 && reads_out)
-        HIP_TRY(hipMemcpyAsync(reads_out, out, sizeof(int64_t) * 3 * cap, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    // Clojure + throws on long overflow; if no prefix can overflow we need no
+    // ordered overflow check (else the shim falls back to the JVM checker).
+    if (mh.amax_abs > 0 && (unsigned long long)mh.amax_abs > (unsigned long long)(LLONG_MAX / std::max(1LL, mh.n_add)))
+        throw_jh(JH_EUNSUPPORTED, "add values large enough to overflow a long");
+    const int64_t nr = th.nr;
+    const int64_t got = std::min(nr, cap);
+    if (got > 0 && reads_out) {
+        HIP_TRY(hipMemcpyAsync(reads_out, out, sizeof(int64_t) * 3 * got, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     *n_reads = nr;
     if (mh.viol1 != ~0ULL) { *valid = JH_UNKNOWN; *cause = (int)(mh.viol1 & 15); *n_reads = 0; return; }
     if (mh.viol2 != ~0ULL) { *valid = JH_UNKNOWN; *cause = (int)(mh.viol2 & 15); *n_reads = 0; return; }

@@ -288,6 +288,17 @@ int jh_check_set(jh_ctx *ctx, const jh_history *h, jh_set_result *res,
                  int64_t *runs_recovered, int64_t runs_cap,
                  char *err, size_t errlen);
 
+/* (checker/set) with the four result sets as bitmaps instead of runs: bit i
+ * of word w of a set is element *base + 32 w + i, for w < *n_words (at most
+ * words_cap words are written per set; *n_words is always the full count).
+ * Same counts, first_fail_entry and n_runs as jh_check_set. The D2H is 4
+ * bytes per 32 elements of span, whatever the run structure; the shim
+ * formats integer-interval-set-str (util.clj:536-575) from the bits. */
+int jh_check_set_bitmaps(jh_ctx *ctx, const jh_history *h, jh_set_result *res,
+                         uint32_t *ok, uint32_t *lost, uint32_t *unexpected, uint32_t *recovered,
+                         int64_t words_cap, int64_t *base, int64_t *n_words,
+                         char *err, size_t errlen);
+
 /* (checker/set-full {:linearizable? linearizable}), checker.clj:236-534.
  * Elements are the :value of every :invoke :add by an integer process; a
  * set :read's :value is its CSR range in aux (value = offset, value2 =

@@ -53,6 +53,9 @@ def lib():
                                            C.c_char_p, C.c_size_t]
             L.jh_check_set.argtypes = [C.c_void_p, H, C.POINTER(A.JhSetResult), p64, p64, p64, p64,
                                        C.c_int64, C.c_char_p, C.c_size_t]
+            p32 = C.POINTER(C.c_uint32)
+            L.jh_check_set_bitmaps.argtypes = [C.c_void_p, H, C.POINTER(A.JhSetResult), p32, p32, p32, p32,
+                                               C.c_int64, p64, p64, C.c_char_p, C.c_size_t]
             L.jh_check_set_full.argtypes = [C.c_void_p, H, p64, C.c_int32, C.POINTER(A.JhSetFullResult),
                                             p64, p64, p64, C.c_int64, C.c_char_p, C.c_size_t]
             L.jh_check_total_queue.argtypes = [C.c_void_p, H, C.POINTER(A.JhQueueResult), p64, p64, p64, p64,
@@ -84,7 +87,7 @@ def lib():
 EXPORTED_SYMBOLS = ["jh_version", "jh_open", "jh_open_multi", "jh_open_devices", "jh_n_devices", "jh_key_costs", "jh_key_index",
                     "jh_close", "jh_check_cas_independent",
                     "jh_check_cas", "jh_check_cas_independent_device", "jh_check_counter",
-                    "jh_check_set", "jh_check_set_full", "jh_check_total_queue", "jh_check_queue",
+                    "jh_check_set", "jh_check_set_bitmaps", "jh_check_set_full", "jh_check_total_queue", "jh_check_queue",
                     # include/jh_io.h
                     "jh_ingest_file", "jh_ingest_buffer", "jh_ingest_history", "jh_ingest_time",
                     "jh_ingest_values_interned", "jh_ingest_table_size", "jh_ingest_table_entry", "jh_ingest_free"]
@@ -247,6 +250,34 @@ class Context:
         out["n_runs"] = list(r.n_runs)
         return out
 
+    def check_set_bitmaps(self, cols, words_cap=None, on_device=False):
+        """jh_check_set_bitmaps: the counts plus the four result sets (ok,
+        lost, unexpected, recovered) as uint32 bitmaps over [base, base + 32 *
+        n_words); bits_to_runs turns one into sorted [lo hi] runs."""
+        h = A.make_history(cols, on_device=on_device)
+        r = A.JhSetResult()
+        err = C.create_string_buffer(1024)
+        p32 = C.POINTER(C.c_uint32)
+        base, nw = C.c_int64(), C.c_int64()
+        cap = 0 if words_cap is None else int(words_cap)
+        if words_cap is None:
+            # size from a first call's n_words would cost a second device pass:
+            # the span is bounded by the history's own values
+            cap = 1 << 16
+        for _ in range(2):
+            bits = [np.zeros(max(cap, 1), np.uint32) for _ in range(4)]
+            rc = lib().jh_check_set_bitmaps(self._h, C.byref(h), C.byref(r), *[b.ctypes.data_as(p32) for b in bits],
+                                            cap, C.byref(base), C.byref(nw), err, len(err))
+            _raise(rc, err)
+            if nw.value <= cap or words_cap is not None:
+                break
+            cap = int(nw.value)
+        out = {name: getattr(r, name) for name, _ in A.JhSetResult._fields_ if name != "n_runs"}
+        out["n_runs"] = list(r.n_runs)
+        out["base"], out["n_words"] = base.value, nw.value
+        out["bits"] = [b[:min(nw.value, cap)] for b in bits]
+        return out
+
     def check_set_full(self, cols, time, linearizable=False, list_cap=None, on_device=False):
         """(checker/set-full {:linearizable? linearizable}). `time` is the :time
         column (numpy int64, or a device pointer when on_device)."""
@@ -298,6 +329,19 @@ class Context:
         rc = lib().jh_check_queue(self._h, C.byref(h), C.byref(r), A.ptr64(pairs[0]), cap, err, len(err))
         _raise(rc, err)
         return self._queue_out(r, pairs, ["final_queue"])
+
+
+def bits_to_runs(words, base):
+    """Sorted [lo hi] runs of the elements base + i for the set bits i of a
+    uint32 bitmap (bit b of word w is element base + 32 w + b)."""
+    words = np.ascontiguousarray(words, dtype=np.uint32)
+    if words.size == 0:
+        return np.zeros((0, 2), np.int64)
+    b = np.unpackbits(words.view(np.uint8), bitorder="little").astype(np.int8)
+    d = np.diff(np.concatenate(([0], b, [0])))
+    lo = np.nonzero(d == 1)[0]
+    hi = np.nonzero(d == -1)[0] - 1
+    return np.stack([lo + base, hi + base], axis=1).astype(np.int64)
 
 
 _default = {}

@@ -235,8 +235,9 @@ class SetChecker(Checker):
     """checker.clj:182-233."""
 
     def check(self, test, history, opts):
+        from ._native import bits_to_runs
         cols = _cols(history, keyed=False)
-        r = _ctx().check_set(cols)
+        r = _ctx().check_set_bitmaps(cols)
         if r["valid"] == A.UNKNOWN:
             return {"valid?": UNKNOWN, "error": "Set was never read"}
         names = ["ok", "lost", "unexpected", "recovered"]
@@ -248,7 +249,7 @@ class SetChecker(Checker):
                "recovered-count": int(r["recovered_count"]),
                "unexpected-count": int(r["unexpected_count"])}
         for i, nm in enumerate(names):
-            out[nm] = _runs_str(r["runs"][i].tolist())
+            out[nm] = _runs_str(bits_to_runs(r["bits"][i], r["base"]).tolist())
         return out
 
 

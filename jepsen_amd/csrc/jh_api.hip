@@ -239,6 +239,21 @@ int jh_check_set(jh_ctx *ctx, const jh_history *h, jh_set_result *res, int64_t *
     });
 }
 
+int jh_check_set_bitmaps(jh_ctx *ctx, const jh_history *h, jh_set_result *res, uint32_t *ok, uint32_t *lost,
+                         uint32_t *unexpected, uint32_t *recovered, int64_t words_cap, int64_t *base,
+                         int64_t *n_words, char *err, size_t errlen) {
+    if (!ctx || !res || !base || !n_words) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    ctx = primary(ctx);
+    std::lock_guard<std::mutex> g(ctx->mu);
+    return guarded(err, errlen, [&] {
+        check_hist(h);
+        HIP_TRY(hipSetDevice(ctx->device));
+        jh_history d = stage_history(ctx, h, false, true);
+        uint32_t *bits[4] = {ok, lost, unexpected, recovered};
+        set_check_bitmaps(ctx, &d, res, bits, words_cap < 0 ? 0 : words_cap, base, n_words, ctx->stream);
+    });
+}
+
 int jh_check_set_full(jh_ctx *ctx, const jh_history *h, const int64_t *time, int32_t linearizable,
                       jh_set_full_result *res, int64_t *lost, int64_t *never_read, int64_t *stale,
                       int64_t list_cap, char *err, size_t errlen) {

@@ -157,6 +157,8 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
 // set (jh_set.hip)
 void set_check(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, int64_t *runs[4],
                int64_t runs_cap, hipStream_t stream);
+void set_check_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, uint32_t *bits_out[4],
+                       int64_t words_cap, int64_t *base, int64_t *n_words, hipStream_t stream);
 // set-full (jh_setfull.hip); lists_out = {lost, never-read, stale}
 void set_full_check(jh_ctx *ctx, const jh_history *dh, const int64_t *time_dev, bool linearizable,
                     jh_set_full_result *res, int64_t *lists_out[3], int64_t list_cap, hipStream_t stream);

@@ -4743,6 +4743,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     if (n_defer > 0 && use_wg) {
         // Deferred LEAN keys on k_lin_wg (one workgroup per key, stream st),
         // WIDE keys on their own pipeline (aux4)
+        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
         WgArgs wa{};
         if (n_def_l > 0) wa = build_wg(ctx->n_cu, nullptr, q);
         prep_wide();
@@ -4767,6 +4768,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         //    keys; aux4: WIDE keys) settles every key.
         claim = ctx->ws<int32_t>(WS_CLAIM, K);
         HIP_TRY(hipMemsetAsync(claim, 0, (size_t)K * sizeof(int32_t), st));
+        // q[0] (phase 1's queue) becomes the BFS's; q[3] its give-up count; q[6] phase 2's queue
+        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(q + 3, 0, sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(q + 6, 0, sizeof(int32_t), st));
 
         // the BFS enumerates up to reach_cap configurations and keeps up to
         // ncap of them for WGL's exact count of valid keys (bfs_wgl_count)

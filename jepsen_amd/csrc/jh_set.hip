@@ -22,7 +22,7 @@ struct SetMeta {
     long long vmin, vmax;
     long long final_row;
     int nil_attempt, nil_add;
-    long long cnt[6];          // attempt, ack, ok, lost, recovered, unexpected
+    long long cnt[10];         // attempt, ack, ok, lost, recovered, unexpected; runs of ok, lost, unexpected, recovered
     unsigned long long first_lost_row;
 };
 
@@ -170,15 +170,26 @@ __global__ void __launch_bounds__(256) k_set_mark_read(const int64_t *__restrict
 // makes bit atomics on a 12 MB bitmap the bottleneck; byte stores are not.
 constexpr unsigned long long BYTEMAP_MAX = 1ULL << 32;
 
+// The final read is marked first (k_set_bytes_read), so the pass over the
+// rows also finds the first lost row: the lowest :ok :add whose element the
+// read lacks (lost = adds - R, checker.clj:214-215)
 __global__ void __launch_bounds__(256) k_set_bytes_rows(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
                                                         const int64_t *__restrict__ val, int64_t n, long long vmin,
-                                                        uint8_t *__restrict__ Ab, uint8_t *__restrict__ Db) {
+                                                        uint8_t *__restrict__ Ab, uint8_t *__restrict__ Db,
+                                                        const uint8_t *__restrict__ Rb, SetMeta *m) {
+    unsigned long long best = ~0ULL;
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
         if (f[r] != JH_F_ADD) continue;
         const int64_t ty = type[r];
         if (ty == T_INVOKE) Ab[val[r] - vmin] = 1;
-        else if (ty == T_OK) Db[val[r] - vmin] = 1;
+        else if (ty == T_OK) {
+            const int64_t b = val[r] - vmin;
+            Db[b] = 1;
+            if (!Rb[b]) best = min(best, (unsigned long long)r);
+        }
     }
+    for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o));
+    if ((threadIdx.x & 63) == 0 && best != ~0ULL) atomicMin(&m->first_lost_row, best);
 }
 
 __global__ void __launch_bounds__(256) k_set_bytes_read(const int64_t *__restrict__ aux, int64_t off, int64_t cnt,
@@ -216,11 +227,15 @@ __device__ __forceinline__ void set_words(const uint32_t *A, const uint32_t *D, 
     out[3] = ok & ~d;     // recovered
 }
 
-// per word: population counts and run-start counts of the four result sets
+// per word: population counts and run-start counts of the four result sets;
+// either the per-word run starts (starts != null: the runs output numbers
+// them by a scan) or the four result bitmaps themselves (outb != null) and
+// the run totals
 __global__ void k_set_count(const uint32_t *__restrict__ A, const uint32_t *__restrict__ D,
                             const uint32_t *__restrict__ R, int64_t nw,
-                            uint32_t *__restrict__ starts /* 4 x nw */, SetMeta *m) {
-    long long c[6] = {0, 0, 0, 0, 0, 0};
+                            uint32_t *__restrict__ starts /* 4 x nw */, uint32_t *__restrict__ outb /* 4 x nw */,
+                            SetMeta *m) {
+    long long c[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw;
          w += (int64_t)gridDim.x * blockDim.x) {
         uint32_t x[4], px[4] = {0, 0, 0, 0};
@@ -230,19 +245,21 @@ __global__ void k_set_count(const uint32_t *__restrict__ A, const uint32_t *__re
         c[2] += __popc(x[0]); c[3] += __popc(x[1]); c[4] += __popc(x[3]); c[5] += __popc(x[2]);
         for (int s = 0; s < 4; s++) {
             const uint32_t st = x[s] & ~((x[s] << 1) | (px[s] >> 31));
-            starts[s * nw + w] = __popc(st);
+            if (starts) starts[s * nw + w] = __popc(st);
+            c[6 + s] += __popc(st);
+            if (outb) outb[s * nw + w] = x[s];
         }
     }
     // one atomic per counter per workgroup (per wave, 48K waves would
     // serialise on six L2 lines)
-    __shared__ long long sc[4][6];
-    for (int i = 0; i < 6; i++) {
+    __shared__ long long sc[4][10];
+    for (int i = 0; i < 10; i++) {
         long long v = c[i];
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         if ((threadIdx.x & 63) == 0) sc[threadIdx.x >> 6][i] = v;
     }
     __syncthreads();
-    if (threadIdx.x < 6) {
+    if (threadIdx.x < 10) {
         long long v = 0;
         for (int k = 0; k < (int)(blockDim.x >> 6); k++) v += sc[k][threadIdx.x];
         if (v) atomicAdd((unsigned long long *)&m->cnt[threadIdx.x], (unsigned long long)v);
@@ -309,27 +326,28 @@ __global__ void k_set_first_lost(const int64_t *__restrict__ type, const int64_t
 }
 }  // namespace
 
-void set_check(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, int64_t *runs_out[4],
-               int64_t runs_cap, hipStream_t st) {
+// The front half of both outputs: the attempts / acknowledged / final-read
+// bitmaps over [vmin, vmin + 32 nw), the counts and the first lost row.
+// Returns false when the result is already final (no :ok :read, nil read).
+static bool set_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, SetMeta *m, SetMeta &mh,
+                        uint32_t *&A, uint32_t *&D, uint32_t *&R, int64_t &nw, long long &vmin, hipStream_t st) {
     memset(res, 0, sizeof(*res));
     res->first_fail_entry = -1; res->final_read_entry = -1;
     const int64_t n = dh->n;
-    SetMeta *m = ctx->ws<SetMeta>(WS_S_CNT, 1);
     SetMeta mi;
     memset(&mi, 0, sizeof mi);
     mi.vmin = LLONG_MAX; mi.vmax = LLONG_MIN; mi.final_row = -1; mi.first_lost_row = ~0ULL;
     HIP_TRY(hipMemcpyAsync(m, &mi, sizeof mi, hipMemcpyHostToDevice, st));
     if (n > 0) k_set_scan<<<grid_for(n, 256, 4096), 256, 0, st>>>(dh->type, dh->f, dh->value, n, m);
-    SetMeta mh;
     HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     res->final_read_entry = mh.final_row;
-    if (mh.final_row < 0) { res->valid = JH_UNKNOWN; res->cause = JH_CAUSE_NIL_VALUE; return; }
+    if (mh.final_row < 0) { res->valid = JH_UNKNOWN; res->cause = JH_CAUSE_NIL_VALUE; return false; }
     int64_t rd[2];
     HIP_TRY(hipMemcpyAsync(rd, dh->value + mh.final_row, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(rd + 1, dh->value2 + mh.final_row, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (rd[0] == JH_NIL) { res->valid = JH_UNKNOWN; res->cause = JH_CAUSE_NIL_VALUE; return; }
+    if (rd[0] == JH_NIL) { res->valid = JH_UNKNOWN; res->cause = JH_CAUSE_NIL_VALUE; return false; }
     if (mh.nil_attempt || mh.nil_add)
         throw_jh(JH_EUNSUPPORTED, "nil set elements (integer-interval-set-str prints those in hash order)");
     if (!dh->aux && rd[1] > 0) throw_jh(JH_EINVAL, "set read without an aux element array");
@@ -338,63 +356,99 @@ void set_check(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, int64_t *r
         k_set_range<<<grid_for(cnt, 256, 4096), 256, 0, st>>>(dh->aux, off, cnt, m);
     HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    long long vmin = mh.vmin, vmax = mh.vmax;
+    vmin = mh.vmin;
+    long long vmax = mh.vmax;
     if (vmin > vmax) { vmin = 0; vmax = 0; }
     const unsigned long long span = (unsigned long long)(vmax - vmin) + 1;
     if (span > (1ULL << 34)) throw_jh(JH_EUNSUPPORTED, "set elements span more than 2^34");
-    const int64_t nw = (int64_t)((span + 31) / 32);
+    nw = (int64_t)((span + 31) / 32);
     uint32_t *bits = ctx->ws<uint32_t>(WS_S_BITS, 3 * nw);
-    uint32_t *A = bits, *D = bits + nw, *R = bits + 2 * nw;
-    if (span <= BYTEMAP_MAX) {
+    A = bits; D = bits + nw; R = bits + 2 * nw;
+    // byte maps (plain idempotent stores, then one packing pass) when the span
+    // is dense enough for 3 bytes per element of span to be cheap next to the
+    // history; sparse or huge spans mark the bitmaps directly (a
+    // sparse set over a wide range no longer allocates 3 x span bytes)
+    if (span <= BYTEMAP_MAX && span <= 8ULL * (unsigned long long)(n + cnt) + 4096) {
         const int64_t span_pad = nw * 32;
         uint8_t *bytes = ctx->ws<uint8_t>(WS_S_BYTES, 3 * span_pad);
         HIP_TRY(hipMemsetAsync(bytes, 0, 3 * span_pad, st));
-        if (n > 0)
-            k_set_bytes_rows<<<grid_for(n, 256, 16384), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, bytes,
-                                                                     bytes + span_pad);
         if (cnt > 0)
             k_set_bytes_read<<<grid_for(cnt, 256, 16384), 256, 0, st>>>(dh->aux, off, cnt, vmin, bytes + 2 * span_pad);
+        if (n > 0)
+            k_set_bytes_rows<<<grid_for(n, 256, 16384), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, bytes,
+                                                                     bytes + span_pad, bytes + 2 * span_pad, m);
         k_set_pack_bits<<<grid_for(3 * nw, 256, 16384), 256, 0, st>>>(bytes, span_pad, nw, bits);
     } else {
         HIP_TRY(hipMemsetAsync(bits, 0, sizeof(uint32_t) * 3 * nw, st));
         if (n > 0) k_set_mark_rows<<<(unsigned)((n + MARK_CH - 1) / MARK_CH), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, A, D);
         if (cnt > 0) k_set_mark_read<<<(unsigned)((cnt + MARK_CH - 1) / MARK_CH), 256, 0, st>>>(dh->aux, off, cnt, vmin, R);
+        if (n > 0)
+            k_set_first_lost<<<grid_for(n, 256), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, D, R, m);
     }
-    uint32_t *starts = ctx->ws<uint32_t>(WS_S_RUNS, 8 * nw + 8);
-    uint32_t *spos = starts + 4 * nw;
-    k_set_count<<<grid_for(nw, 256, 2048), 256, 0, st>>>(A, D, R, nw, starts, m);
-    size_t tb = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, starts, spos, (int)nw, st));
-    void *tmp = ctx->ws<char>(WS_S_TMP, tb);
-    for (int s = 0; s < 4; s++)   // per-set run numbering starts at 0
-        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, starts + s * nw, spos + s * nw, (int)nw, st));
-    uint32_t lastpos[4], lastc[4];
-    for (int s = 0; s < 4; s++) {
-        HIP_TRY(hipMemcpyAsync(&lastpos[s], spos + s * nw + nw - 1, 4, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(&lastc[s], starts + s * nw + nw - 1, 4, hipMemcpyDeviceToHost, st));
-    }
-    if (n > 0)
-        k_set_first_lost<<<grid_for(n, 256), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, D, R, m);
-    HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    int64_t nruns[4];
-    for (int s = 0; s < 4; s++) nruns[s] = (int64_t)lastpos[s] + lastc[s];
-    const int64_t cap = runs_cap;
-    int64_t *runs = ctx->ws<int64_t>(WS_C_OUT, 8 * std::max<int64_t>(cap, 1));
-    k_set_emit<<<grid_for(nw, 256), 256, 0, st>>>(A, D, R, nw, vmin, spos, runs, cap);
+    return true;
+}
+
+static void set_finish(jh_set_result *res, const SetMeta &mh) {
     res->attempt_count = mh.cnt[0]; res->acknowledged_count = mh.cnt[1];
     res->ok_count = mh.cnt[2]; res->lost_count = mh.cnt[3];
     res->recovered_count = mh.cnt[4]; res->unexpected_count = mh.cnt[5];
     res->valid = (mh.cnt[3] == 0 && mh.cnt[5] == 0) ? JH_VALID : JH_INVALID;
     if (mh.cnt[3]) res->first_fail_entry = mh.first_lost_row == ~0ULL ? -1 : (int64_t)mh.first_lost_row;
     else if (mh.cnt[5]) res->first_fail_entry = mh.final_row;
-    for (int s = 0; s < 4; s++) res->n_runs[s] = nruns[s];
+    for (int s = 0; s < 4; s++) res->n_runs[s] = mh.cnt[6 + s];
+}
+
+void set_check(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, int64_t *runs_out[4],
+               int64_t runs_cap, hipStream_t st) {
+    SetMeta *m = ctx->ws<SetMeta>(WS_S_CNT, 1);
+    SetMeta mh;
+    uint32_t *A, *D, *R;
+    int64_t nw;
+    long long vmin;
+    if (!set_bitmaps(ctx, dh, res, m, mh, A, D, R, nw, vmin, st)) return;
+    uint32_t *starts = ctx->ws<uint32_t>(WS_S_RUNS, 8 * nw + 8);
+    uint32_t *spos = starts + 4 * nw;
+    k_set_count<<<grid_for(nw, 256, 2048), 256, 0, st>>>(A, D, R, nw, starts, nullptr, m);
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, starts, spos, (int)nw, st));
+    void *tmp = ctx->ws<char>(WS_S_TMP, tb);
+    for (int s = 0; s < 4; s++)   // per-set run numbering starts at 0
+        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, starts + s * nw, spos + s * nw, (int)nw, st));
+    const int64_t cap = runs_cap;
+    int64_t *runs = ctx->ws<int64_t>(WS_C_OUT, 8 * std::max<int64_t>(cap, 1));
+    k_set_emit<<<grid_for(nw, 256), 256, 0, st>>>(A, D, R, nw, vmin, spos, runs, cap);
+    HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    set_finish(res, mh);
     for (int s = 0; s < 4; s++) {
-        const int64_t k = std::min<int64_t>(nruns[s], cap);
+        const int64_t k = std::min<int64_t>(res->n_runs[s], cap);
         if (k > 0 && runs_out[s])
             HIP_TRY(hipMemcpyAsync(runs_out[s], runs + (int64_t)s * 2 * cap, sizeof(int64_t) * 2 * k,
                                    hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(hipStreamSynchronize(st));
+}
+
+// The four result sets as bitmaps over [*base, *base + 32 * words): 4 bytes
+// per 32 elements of span whatever the run structure (23 M runs of the C2
+// workload are 370 MB as [lo hi] pairs, 25 MB as bitmaps)
+void set_check_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, uint32_t *bits_out[4],
+                       int64_t words_cap, int64_t *base, int64_t *n_words, hipStream_t st) {
+    SetMeta *m = ctx->ws<SetMeta>(WS_S_CNT, 1);
+    SetMeta mh;
+    uint32_t *A, *D, *R;
+    int64_t nw;
+    long long vmin;
+    *base = 0; *n_words = 0;
+    if (!set_bitmaps(ctx, dh, res, m, mh, A, D, R, nw, vmin, st)) return;
+    uint32_t *outb = ctx->ws<uint32_t>(WS_S_RUNS, 4 * nw + 8);
+    k_set_count<<<grid_for(nw, 256, 2048), 256, 0, st>>>(A, D, R, nw, nullptr, outb, m);
+    HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
+    const int64_t k = std::min<int64_t>(nw, words_cap);
+    for (int s = 0; s < 4; s++)
+        if (k > 0 && bits_out[s])
+            HIP_TRY(hipMemcpyAsync(bits_out[s], outb + (int64_t)s * nw, sizeof(uint32_t) * k, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    set_finish(res, mh);
+    *base = vmin; *n_words = nw;
 }

@@ -143,6 +143,25 @@ def test_c2_set_100m(ctx):
     assert not _in_runs(read, runs[1]).any()
 
 
+def test_c2_set_bitmaps_100m(ctx):
+    """The bitmap output (jh_check_set_bitmaps, the product path of the set
+    checker: 4 bytes per 32 elements of span instead of 16 bytes per run) on
+    the C2 set history: counts, first failing row and every run equal the
+    runs output's."""
+    from jepsen_amd._native import bits_to_runs
+    cols = synth.set_history(n_adds=50_000_000, n_procs=10, p_fail=0.05, p_info=0.02,
+                             n_lost=100, n_unexpected=10, seed=2)
+    b = ctx.check_set_bitmaps(cols)
+    g = ctx.check_set(cols, runs_cap=40_000_000)
+    for k in ("valid", "cause", "attempt_count", "acknowledged_count", "ok_count", "lost_count",
+              "recovered_count", "unexpected_count", "first_fail_entry", "final_read_entry"):
+        assert b[k] == g[k], k
+    assert b["n_runs"] == g["n_runs"]
+    for i in range(4):
+        r = bits_to_runs(b["bits"][i], b["base"])
+        assert len(r) == g["n_runs"][i] and (r == g["runs"][i]).all(), i
+
+
 def test_c2_set_slice_vs_oracle(ctx):
     """The same generator at 10M entries: identical to the oracle."""
     cols = synth.set_history(n_adds=5_000_000, n_procs=10, p_fail=0.05, p_info=0.02,

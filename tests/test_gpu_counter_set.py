@@ -78,7 +78,23 @@ def _set_same(g, c):
 def test_set_random(ctx, seed):
     cols = synth.set_history(n_adds=300000, n_procs=10, p_fail=0.05, p_info=0.03,
                              n_lost=seed * 7, n_unexpected=seed, seed=seed)
-    _set_same(ctx.check_set(cols), oracle.check_set(cols))
+    c = oracle.check_set(cols)
+    _set_same(ctx.check_set(cols), c)
+    _bits_same(ctx.check_set_bitmaps(cols), c)
+
+
+def _bits_same(b, c):
+    """jh_check_set_bitmaps against the oracle: counts, rows, and every run."""
+    from jepsen_amd._native import bits_to_runs
+    for k in ("valid", "cause", "attempt_count", "acknowledged_count", "ok_count", "lost_count",
+              "recovered_count", "unexpected_count", "first_fail_entry", "final_read_entry"):
+        assert b[k] == c[k], k
+    if b["valid"] == A.UNKNOWN:
+        return
+    for i in range(4):
+        r = bits_to_runs(b["bits"][i], b["base"])
+        assert b["n_runs"][i] == c["n_runs"][i] and len(r) == c["n_runs"][i], i
+        assert (r == np.asarray(c["runs"][i]).reshape(-1, 2)).all(), i
 
 
 def test_set_golden_and_map(ctx):
@@ -105,4 +121,6 @@ def test_set_edge_cases(ctx):
     assert r["valid?"] is False and r["unexpected"] == "#{9}" and r["ok"] == "#{1..2}"
     assert r["lost"] == "#{}" and r["recovered-count"] == 0
     cols = H.encode(h, keyed=False)
-    _set_same(ctx.check_set(cols), oracle.check_set(cols))
+    c = oracle.check_set(cols)
+    _set_same(ctx.check_set(cols), c)
+    _bits_same(ctx.check_set_bitmaps(cols), c)

@@ -6,7 +6,8 @@ timed region (columns copied once); a step is one jh_check_counter /
 jh_check_set call, including its D2H of the result (the :reads triples or the
 run-length sets). `roofline` is whole-call algorithmic bytes (SURVEY 8(d):
 56 B per entry read once, +24 B per :reads triple, +16 B per run of the four
-result sets) over the call's time, against the 8 TB/s HBM peak; the
+result sets; the set's bitmaps 16 B per word of the four) over the call's
+time, against the 8 TB/s HBM peak; the
 per-kernel split is in the rocprofv3 --stats summary (profiles/).
 
     python tools/bench_c2.py [--entries 100000000] [--steps 5] [--warmup 1]
@@ -105,9 +106,12 @@ def main():
     cols = synth.set_history(n_adds=half, n_procs=10, p_fail=0.05, p_info=0.02, n_lost=100,
                              n_unexpected=10, seed=2)
     d = DevCols(cols, dev)
-    r, sec = timed(lambda: ctx.check_set(d, runs_cap=1 << 20, on_device=True), args.steps, args.warmup)
+    # the product path: the four result sets come back as bitmaps (4 B per 32
+    # elements of span); the runs output (16 B per run) is timed beside it
+    r, sec = timed(lambda: ctx.check_set_bitmaps(d, words_cap=1 << 22, on_device=True), args.steps, args.warmup)
+    _, sec_runs = timed(lambda: ctx.check_set(d, runs_cap=1 << 25, on_device=True), 2, 1)
     n = int(cols.n)
-    alg = 56.0 * n + 8.0 * d.n_aux + 16.0 * sum(r["n_runs"])
+    alg = 56.0 * n + 8.0 * d.n_aux + 16.0 * r["n_words"]
     cpu = None
     if not args.no_cpu:
         cs = synth.set_history(n_adds=args.cpu_sample // 2, n_procs=10, p_fail=0.05, p_info=0.02,
@@ -123,8 +127,10 @@ def main():
                   "data": "synthetic (jepsen_amd/csrc/gen.cpp set, seed 2)",
                   "config": {"workload": "C2 set", "entries": n, "final_read": d.n_aux,
                              "lost": r["lost_count"], "unexpected": r["unexpected_count"],
-                             "valid": r["valid"]},
-                  "roofline": {"bound": "hbm", "kernel": "whole jh_check_set call",
+                             "valid": r["valid"], "n_runs": r["n_runs"], "bitmap_words": r["n_words"],
+                             "output": "jh_check_set_bitmaps (4 result bitmaps)",
+                             "ms_per_call_runs_output": sec_runs * 1e3},
+                  "roofline": {"bound": "hbm", "kernel": "whole jh_check_set_bitmaps call",
                                "achieved": alg / sec / 1e9, "peak": PEAK_HBM_GBS,
                                "unit": "GB/s", "frac": alg / sec / 1e9 / PEAK_HBM_GBS,
                                "traffic": None},

@@ -384,24 +384,34 @@ struct EdnParser {
         while (i < t.size() && t[i] >= '0' && t[i] <= '9') i++;
         if (i == d0) return false;
         std::string_view ip = t.substr(0, i), rest = t.substr(i);
-        if (rest.empty() || rest == "N") {
-            const bool neg = ip[0] == '-';
+        // a decimal integer (optional sign, digits) checked against the int64 range
+        auto checked = [&](std::string_view digits, bool neg, int64_t &v) -> bool {
             uint64_t u = 0;
-            for (size_t j = d0; j < ip.size(); j++) {
-                const uint64_t d = (uint64_t)(ip[j] - '0');
-                if (u > (UINT64_MAX - d) / 10) return fail("integer out of the int64 range");
+            for (char c : digits) {
+                const uint64_t d = (uint64_t)(c - '0');
+                if (u > (UINT64_MAX - d) / 10) return false;
                 u = u * 10 + d;
             }
-            if (u > (neg ? (uint64_t)INT64_MAX + 1 : (uint64_t)INT64_MAX)) return fail("integer out of the int64 range");
-            out = A.leaf(V_INT, neg ? (int64_t)(0 - u) : (int64_t)u);
+            if (u > (neg ? (uint64_t)INT64_MAX + 1 : (uint64_t)INT64_MAX)) return false;
+            v = neg ? (int64_t)(0 - u) : (int64_t)u;
+            return true;
+        };
+        if (rest.empty() || rest == "N") {
+            int64_t v = 0;
+            if (!checked(ip.substr(d0), ip[0] == '-', v)) return fail("integer out of the int64 range");
+            out = A.leaf(V_INT, v);
             return true;
         }
         if (rest[0] == '/') {
             if (!all_digits(rest.substr(1))) return false;
-            long long a = strtoll(std::string(ip).c_str(), nullptr, 10);
-            long long b = strtoll(std::string(rest.substr(1)).c_str(), nullptr, 10);
+            // both parts through the integer path's checked accumulator (ADVICE
+            // r2: strtoll saturated silently, and gcd of -LLONG_MIN is undefined)
+            int64_t a = 0, b = 0;
+            if (!checked(ip.substr(d0), ip[0] == '-', a) || !checked(rest.substr(1), false, b) ||
+                a == INT64_MIN)
+                return fail("ratio part out of the int64 range");
             if (b == 0) return fail("ratio with zero denominator");
-            long long g = std::gcd(a < 0 ? -a : a, b);
+            const int64_t g = std::gcd(a < 0 ? -a : a, b);
             if (g > 1) { a /= g; b /= g; }
             std::string r = std::to_string(a) + "/" + std::to_string(b);
             out = A.text(V_RATIO, r.data(), r.size());

@@ -244,3 +244,19 @@ def test_errors(built):
         ingest.load_columns("/nonexistent/history.edn")
     got = ingest.parse_columns("", fmt="edn")
     assert got.n == 0
+
+
+def test_ratio_out_of_range(built):
+    """a ratio whose numerator or denominator is outside the int64
+    range is an error, as an out-of-range integer is (no silent saturation);
+    in range it is interned reduced, as Clojure reads it."""
+    big = "9" * 25
+    with pytest.raises(JhError, match="int64 range"):
+        ingest.parse_columns('{:type :invoke, :f :write, :value %s/3, :process 0}\n' % big, fmt="edn")
+    with pytest.raises(JhError, match="int64 range"):
+        ingest.parse_columns('{:type :invoke, :f :write, :value 3/%s, :process 0}\n' % big, fmt="edn")
+    with pytest.raises(JhError, match="int64 range"):
+        ingest.parse_columns('{:type :invoke, :f :write, :value -9223372036854775808/2, :process 0}\n', fmt="edn")
+    a = ingest.parse_columns('{:type :invoke, :f :write, :value 4/6, :process 0}\n'
+                             '{:type :invoke, :f :write, :value 2/3, :process 1}\n', fmt="edn")
+    assert a.value[0] == a.value[1]

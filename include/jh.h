@@ -156,7 +156,8 @@ typedef struct jh_key_verdict {
     int64_t explored;          /* memo inserts (WGL cache size) for this key, the same
                                   on every run; -1 for a key in no tuple */
     /* invalid keys, from the search frontier (knossos' :previous-ok / :last-op;
-     * knossos is not vendored, so these definitions are this library's):
+     * knossos is not vendored, so these definitions are this library's and
+     * PARITY-UNPINNED against knossos: oracle and device agree with each other):
      * last_op     = history row of the :ok completion of the last op the
      *               furthest configuration got past (RET[tmax-1]), -1 if none;
      * previous_ok = history row of the last client :ok in the key's
@@ -164,7 +165,15 @@ typedef struct jh_key_verdict {
      * Both -1 for keys that are not invalid. */
     int64_t previous_ok;
     int64_t last_op;
+    /* ABI 4: the analysis that decided the key (knossos' :analyzer):
+     * JH_ANALYZER_WGL (explored = WGL's cache size) or JH_ANALYZER_LINEAR
+     * (explored = configurations the JIT-linearization analysis visited) */
+    int32_t analyzer;
+    int32_t reserved;
 } jh_key_verdict;
+
+#define JH_ANALYZER_WGL    0
+#define JH_ANALYZER_LINEAR 1
 
 typedef struct jh_summary {
     int64_t valid;             /* merge-valid over keys (checker.clj:33-47) */

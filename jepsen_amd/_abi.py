@@ -68,13 +68,16 @@ class JhLinOpts(C.Structure):
 
 
 # every field of jh_key_verdict: the parity tests compare all of them
-VERDICT_FIELDS = ("valid", "cause", "fail_entry", "explored", "previous_ok", "last_op")
+VERDICT_FIELDS = ("valid", "cause", "fail_entry", "explored", "previous_ok", "last_op", "analyzer")
+ANALYZER_WGL, ANALYZER_LINEAR = 0, 1
+ANALYZERS = {ANALYZER_WGL: "wgl", ANALYZER_LINEAR: "linear"}
 
 
 class JhKeyVerdict(C.Structure):
     _fields_ = [("valid", C.c_int32), ("cause", C.c_int32),
                 ("fail_entry", C.c_int64), ("explored", C.c_int64),
-                ("previous_ok", C.c_int64), ("last_op", C.c_int64)]
+                ("previous_ok", C.c_int64), ("last_op", C.c_int64),
+                ("analyzer", C.c_int32), ("reserved", C.c_int32)]
 
 
 class JhSummary(C.Structure):
@@ -138,7 +141,8 @@ try:
     import numpy as _np
     VERDICT_DTYPE = _np.dtype([("valid", _np.int32), ("cause", _np.int32),
                                ("fail_entry", _np.int64), ("explored", _np.int64),
-                               ("previous_ok", _np.int64), ("last_op", _np.int64)])
+                               ("previous_ok", _np.int64), ("last_op", _np.int64),
+                               ("analyzer", _np.int32), ("reserved", _np.int32)])
 except Exception:  # pragma: no cover
     VERDICT_DTYPE = None
 

@@ -4112,11 +4112,23 @@ __global__ void __launch_bounds__(256) k_fail_rows(KeySrc S, jh_key_verdict *out
 // The search frontier of every invalid key (include/jh.h): the failing row is
 // the ok completion of RET[t]; last_op = that of RET[t-1], previous_ok = the
 // last client :ok row before it in the key's segment. -1 for other keys.
-__global__ void __launch_bounds__(256) k_frontier(KeySrc S, jh_key_verdict *out, int64_t K) {
+// The analysis that decided a key (knossos' :analyzer, include/jh.h): in
+// :linear mode the engines mark the cause word while searching (CAUSE_BY_LINEAR
+// for the reachable-set analysis, CAUSE_BY_WGL for a WGL search standing in
+// for it); an unmarked key took no search and gets the mode's own analyzer.
+constexpr int32_t CAUSE_BY_LINEAR = 0x100, CAUSE_BY_WGL = 0x200;
+__global__ void __launch_bounds__(256) k_frontier(KeySrc S, jh_key_verdict *out, int64_t K, int linear_mode) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * 4;
     for (int64_t key = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); key < K; key += nw) {
         const jh_key_verdict v = out[key];
+        if (lane == 0) {
+            out[key].analyzer = (v.cause & CAUSE_BY_LINEAR) ? JH_ANALYZER_LINEAR
+                                : (v.cause & CAUSE_BY_WGL) ? JH_ANALYZER_WGL
+                                : linear_mode ? JH_ANALYZER_LINEAR : JH_ANALYZER_WGL;
+            out[key].cause = v.cause & 0xFF;
+            out[key].reserved = 0;
+        }
         long long prev = -1, last = -1;
         if (v.valid == JH_INVALID && v.fail_entry >= 0) {
             const uint32_t s0 = S.off[key], s1 = S.off[key + 1];
@@ -4341,6 +4353,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const int64_t budget = opts && opts->budget > 0 ? opts->budget : JH_DEFAULT_BUDGET;
     const int64_t init = opts ? opts->init_value : JH_NIL;
     const int32_t lflags = opts ? opts->flags : 0;
+    const bool linear_mode = opts && opts->algorithm == JH_ALGO_LINEAR;
     HIP_TRY(hipEventRecord(ctx->ev[0], st));
 
     // ranges
@@ -5035,7 +5048,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     k_fail_rows<<<(unsigned)std::min<int64_t>((K + 3) / 4, 4096), 256, 0, st>>>(
         KeySrc{rec, pair, off, rB, viol, rank, q + 2}, out_dev, K);
     k_frontier<<<(unsigned)std::min<int64_t>((K + 3) / 4, 4096), 256, 0, st>>>(
-        KeySrc{rec, pair, off, rB, viol, rank, q + 2}, out_dev, K);
+        KeySrc{rec, pair, off, rB, viol, rank, q + 2}, out_dev, K, linear_mode ? 1 : 0);
     long long *sd = ctx->ws<long long>(WS_SUMMARY, 8);
     long long s_init[8] = {0, 0, 0, LLONG_MAX, 0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(sd, s_init, sizeof s_init, hipMemcpyHostToDevice, st));

@@ -346,6 +346,69 @@ done:
 }
 
 /* ------------------------------------------------------------------------ */
+/* knossos.linear/analysis [K] (Lowe's JIT linearization, selected by
+ * :algorithm :linear at jepsen/src/jepsen/checker.clj:141-145): the set of
+ * configurations is carried forward through the history; at each :ok
+ * completion every configuration must linearize the completing op (after
+ * any pending ops, in every order), and the history is linearizable iff the
+ * set survives the last completion. In canonical coordinates that is the
+ * reachable configuration set enumerated layer by layer (layer t = the
+ * configurations whose earliest un-linearized :ok return is the t-th; a
+ * same-layer edge lifts a pending op, a cross-layer edge lifts RET[t]). Its
+ * size -- every configuration it visits except the initial one and the
+ * terminal ones -- is what this analysis explores (WGL's count is a subset).
+ * Returns JH_VALID / JH_INVALID, or JH_UNKNOWN when more than `budget`
+ * configurations are reachable (the analysis would not finish: the caller
+ * falls back to WGL). *tmax = the deepest layer reached (the failing op of
+ * an invalid key is RET[tmax], as for WGL). Configurations of layer tmax are
+ * collected into `front` (sorted later) when it is not NULL. */
+typedef struct { cfg *e; int64_t n, cap; } cvec;
+static void cvec_push(cvec *v, const cfg *c) {
+    if (v->n == v->cap) { v->cap = v->cap ? 2 * v->cap : 256; v->e = (cfg *)realloc(v->e, sizeof(cfg) * v->cap); }
+    v->e[v->n++] = *c;
+}
+static int orc_linear(const orc_key *k, int64_t init, int64_t budget, int64_t *explored, uint32_t *tmax_out,
+               cvec *front) {
+    *explored = 0; *tmax_out = 0;
+    if (k->status) return JH_UNKNOWN;
+    if (k->n_ok == 0) return JH_VALID;
+    cset seen; cset_init(&seen);
+    cvec q = {0, 0, 0};
+    cfg root; memset(&root, 0, sizeof root); root.t = 0; root.s = init;
+    cset_add(&seen, &root); cvec_push(&q, &root);
+    int term = 0;
+    uint32_t tmax = 0;
+    int verdict = JH_INVALID;
+    for (int64_t h = 0; h < q.n; h++) {
+        const cfg c = q.e[h];
+        if (c.t > tmax) tmax = c.t;
+        const int32_t *W = k->w_ops + k->w_off[c.t];
+        const int w = k->w_off[c.t + 1] - k->w_off[c.t];
+        for (int i = 0; i < w; i++) {
+            if (bit_get(c.m, i)) continue;
+            const orc_op *o = &k->ops[W[i]];
+            int64_t s2;
+            if (!cas_step(o->f, o->v1, o->v2, c.s, &s2)) continue;
+            cfg d; d.s = s2;
+            cfg_lift(k, c.t, c.m, i, &d.t, d.m);
+            if (d.t == (uint32_t)k->n_ok) { term = 1; continue; }
+            if (cset_has(&seen, &d)) continue;
+            if (seen.n - 1 >= budget) { verdict = JH_UNKNOWN; goto done; }
+            cset_add(&seen, &d);
+            cvec_push(&q, &d);
+        }
+    }
+    verdict = term ? JH_VALID : JH_INVALID;
+    if (verdict == JH_INVALID && front)
+        for (int64_t h = 0; h < q.n; h++) if (q.e[h].t == tmax) cvec_push(front, &q.e[h]);
+done:
+    *explored = seen.n - 1;
+    *tmax_out = tmax;
+    cset_free(&seen); free(q.e);
+    return verdict;
+}
+
+/* ------------------------------------------------------------------------ */
 /* knossos-style WGL: doubly linked list of call/return entries in history
  * order, lift/unlift, BitSet of linearized op ids, HashSet<(BitSet, model)>.
  * Crashed ops have a call entry and no return entry, so they may be lifted
@@ -508,13 +571,36 @@ int orc_lin_bruteforce(const orc_key *k, int64_t init) {
 }
 
 /* ------------------------------------------------------------------------ */
+/* :algorithm :linear on libjh.so's terms: the JIT-linearization analysis
+ * decides a key when its windows fit the reachable-set engine (at most 32
+ * members, fewer than 4096 interned states) and its reachable set fits the
+ * budget; any other key is decided by WGL and reported with :analyzer :wgl
+ * (the choice knossos.competition makes when :linear cannot finish).
+ * states_ok is the history-wide condition the device computes once. */
+int orc_linear_states_ok = 1;
+static int linear_domain(const orc_key *k) {
+    return k->max_window <= 32 && orc_linear_states_ok && k->n_ok < (1 << 20) - 2;
+}
+
 static void check_one(const jh_history *h, const int64_t *sel, int64_t m,
                       int64_t init, int64_t budget, int list_algo, jh_key_verdict *out) {
     orc_key k;
     orc_key_prepare(h, sel, m, &k);
     out->fail_entry = -1; out->explored = 0;
+    out->analyzer = list_algo == 2 ? JH_ANALYZER_LINEAR : JH_ANALYZER_WGL;
+    out->reserved = 0;
     if (k.status) {
         out->valid = JH_UNKNOWN; out->cause = k.status;
+    } else if (list_algo == 2 && linear_domain(&k) &&
+               (out->valid = orc_linear(&k, init, budget, &out->explored, (uint32_t *)&out->reserved, NULL)) != JH_UNKNOWN) {
+        out->cause = JH_CAUSE_NONE;
+        if (out->valid == JH_INVALID) out->fail_entry = k.ops[k.ret_op[out->reserved]].ret;
+        out->reserved = 0;
+    } else if (list_algo == 2) {
+        out->reserved = 0;
+        out->analyzer = JH_ANALYZER_WGL;
+        out->valid = orc_wgl_canonical(&k, init, budget, &out->explored, &out->fail_entry);
+        out->cause = out->valid == JH_UNKNOWN ? JH_CAUSE_BUDGET : JH_CAUSE_NONE;
     } else if (list_algo) {
         out->valid = orc_wgl_list(&k, init, budget, &out->explored);
         out->cause = out->valid == JH_UNKNOWN ? JH_CAUSE_BUDGET : JH_CAUSE_NONE;
@@ -542,6 +628,7 @@ static void check_one(const jh_history *h, const int64_t *sel, int64_t m,
 
 int orc_check_cas(const jh_history *h, int64_t init, int64_t budget, jh_key_verdict *out) {
     if (budget <= 0) budget = JH_DEFAULT_BUDGET;
+    out->analyzer = JH_ANALYZER_WGL; out->reserved = 0;
     int64_t *sel = (int64_t *)malloc(sizeof(int64_t) * (h->n ? h->n : 1));
     for (int64_t i = 0; i < h->n; i++) sel[i] = i;
     check_one(h, sel, h->n, init, budget, 0, out);
@@ -589,9 +676,10 @@ static void *indep_worker(void *arg) {
         if (!present) {
             o->valid = JH_VALID; o->cause = 0; o->fail_entry = -1; o->explored = -1;
             o->previous_ok = -1; o->last_op = -1;
+            o->analyzer = (J->mode & 4) ? JH_ANALYZER_LINEAR : JH_ANALYZER_WGL; o->reserved = 0;
             continue;
         }
-        check_one(h, sel, m, J->init, J->budget, (J->mode >> 1) & 1, o);
+        check_one(h, sel, m, J->init, J->budget, (J->mode & 4) ? 2 : (J->mode >> 1) & 1, o);
     }
     free(sel);
     return NULL;

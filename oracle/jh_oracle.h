@@ -62,11 +62,20 @@ int  orc_wgl_list(const orc_key *k, int64_t init, int64_t budget,
 /* Brute-force linearization search, no memo, for tiny keys (<= 12 ops). */
 int  orc_lin_bruteforce(const orc_key *k, int64_t init);
 
+/* knossos.linear (JIT linearization) in canonical coordinates: the reachable
+ * configuration set, layer by layer (jh_oracle.c). */
+struct cvec;
+/* history-wide: every interned state id < 4096 (set by the caller, as the
+ * device computes it; the reachable-set engine packs states in 12 bits) */
+extern int orc_linear_states_ok;
+
 /* Whole-history linearizable check (non-independent). */
 int  orc_check_cas(const jh_history *h, int64_t init, int64_t budget,
                    jh_key_verdict *out);
-/* Independent checker. mode 0: O(N) bucketed split; mode 1: the reference's
- * O(K*N) per-key subhistory scan (independent.clj:234-245). threads >= 1. */
+/* Independent checker. mode bit 0: the reference's O(K*N) per-key subhistory
+ * scan (independent.clj:234-245), else one O(N) bucketed split; bit 1: the
+ * knossos-style list WGL instead of the canonical one; bit 2: :algorithm
+ * :linear (JIT linearization where it applies, see jh_oracle.c). */
 int  orc_check_cas_independent(const jh_history *h, int64_t init, int64_t budget,
                                int mode, int threads, jh_key_verdict *out,
                                jh_summary *sum);

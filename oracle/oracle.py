@@ -62,8 +62,38 @@ def check_cas_full(cols, init=A.NIL, budget=A.DEFAULT_BUDGET):
     return {f: getattr(v, f) for f, _ in A.JhKeyVerdict._fields_}
 
 
-def check_cas_independent(cols, init=A.NIL, budget=A.DEFAULT_BUDGET, mode=0, threads=1):
-    """Returns (verdicts structured array [n_keys], summary)."""
+def linear_states_ok(cols, init=A.NIL):
+    """The device's history-wide condition for the reachable-set engine (every
+    interned state id < 4096): the value range of client read / write / cas
+    ops (and the initial value) when it is interned as one range, else the
+    largest number of distinct values of one key (per-key interning)."""
+    cl = (cols.process >= 0) & (cols.f <= A.F_CAS)
+    v = cols.value[cl]
+    v2 = cols.value2[cl & (cols.f == A.F_CAS)] if cols.n else cols.value2[:0]
+    vals = np.concatenate([v[v != A.NIL], v2[v2 != A.NIL]] + ([np.array([init])] if init != A.NIL else []))
+    if len(vals) == 0:
+        return True
+    if int(vals.max()) - int(vals.min()) < 0xFFFE - 3:
+        return int(vals.max()) - int(vals.min()) + 2 < 4096
+    keys = cols.key[cl] if cols.key is not None else np.zeros(int(cl.sum()), np.int64)
+    worst = 0
+    for k in np.unique(keys):
+        sel = cl.copy()
+        sel[cl] = keys == k
+        a = cols.value[sel]
+        b = cols.value2[sel & (cols.f == A.F_CAS)]
+        d = len(np.unique(np.concatenate([a[a != A.NIL], b[b != A.NIL]] + ([np.array([init])] if init != A.NIL else []))))
+        worst = max(worst, d)
+    return worst + 1 < 4096
+
+
+def check_cas_independent(cols, init=A.NIL, budget=A.DEFAULT_BUDGET, mode=0, threads=1, algorithm=None):
+    """Returns (verdicts structured array [n_keys], summary). algorithm
+    "linear": JIT linearization where the device's reachable-set engine
+    applies (mode bit 2), WGL elsewhere, with each key's :analyzer."""
+    if algorithm == "linear":
+        mode |= 4
+        C.c_int.in_dll(lib(), "orc_linear_states_ok").value = 1 if linear_states_ok(cols, init) else 0
     h = cols.as_jh()
     out = np.zeros(max(cols.n_keys, 1), dtype=A.VERDICT_DTYPE)
     s = A.JhSummary()

@@ -157,17 +157,19 @@ CAUSE_ERRORS = {
 }
 
 
-def lin_result(valid, cause, fail_entry, explored, cols=None, previous_ok=-1, last_op=-1):
+def lin_result(valid, cause, fail_entry, explored, cols=None, previous_ok=-1, last_op=-1, analyzer=A.ANALYZER_WGL):
     """Per-history result map of checker/linearizable (checker.clj:139-158).
-    An invalid result carries :op (the ok completion no configuration gets
-    past) and, from the search frontier, :previous-ok and :last-op
-    (include/jh.h; knossos is not vendored, so their exact knossos
-    definitions are parity unpinned)."""
+    :analyzer is the analysis that decided the key (jh_key_verdict.analyzer:
+    :wgl, or :linear under {:algorithm :linear}). An invalid result carries
+    :op (the ok completion no configuration gets past) and, from the search
+    frontier, :previous-ok and :last-op (include/jh.h; knossos is not
+    vendored, so their exact knossos definitions are parity unpinned)."""
     c = A.CAUSES.get(int(cause))
+    an = A.ANALYZERS.get(int(analyzer), "wgl")
     if valid == A.VALID:
-        return {"valid?": True, "analyzer": "wgl", "explored": int(explored)}
+        return {"valid?": True, "analyzer": an, "explored": int(explored)}
     if valid == A.INVALID:
-        r = {"valid?": False, "analyzer": "wgl", "explored": int(explored),
+        r = {"valid?": False, "analyzer": an, "explored": int(explored),
              "fail-entry": int(fail_entry)}
         if cols is not None and 0 <= fail_entry < cols.n:
             r["op"] = H.decode_op(cols, int(fail_entry))
@@ -176,13 +178,16 @@ def lin_result(valid, cause, fail_entry, explored, cols=None, previous_ok=-1, la
             r["last-op"] = H.decode_op(cols, int(last_op)) if 0 <= last_op < cols.n else None
         return r
     if c == "budget":
-        return {"valid?": UNKNOWN, "analyzer": "wgl", "cause": "budget", "explored": int(explored)}
+        return {"valid?": UNKNOWN, "analyzer": an, "cause": "budget", "explored": int(explored)}
     return {"valid?": UNKNOWN, "error": CAUSE_ERRORS.get(c, c), "cause": c}
 
 
 class Linearizable(Checker):
-    """checker.clj:127-158 with {:model (cas-register v)}; every :algorithm
-    (:linear, :wgl, competition) decides the same :valid?."""
+    """checker.clj:127-158 with {:model (cas-register v)}. :algorithm :wgl and
+    the default (competition) report the WGL analysis; :linear runs the
+    JIT-linearization analysis (the reachable configuration set) on every
+    key it can hold and WGL on the rest -- each key's :analyzer says which.
+    Both are complete decision procedures: :valid? is the same."""
 
     def __init__(self, opts):
         model = opts.get("model")
@@ -201,9 +206,17 @@ class Linearizable(Checker):
         if not isinstance(history, H.Columns):
             history = to_device_ops(self.model, list(history))
         cols = _cols(history, keyed=False)
-        r = _ctx().check_cas_full(cols, init=_init_state(self.model, cols), budget=self.budget)
+        r = _ctx().check_cas_full(cols, init=_init_state(self.model, cols), budget=self.budget,
+                                  algorithm=_algorithm(self.algorithm))
         return lin_result(r["valid"], r["cause"], r["fail_entry"], r["explored"], cols,
-                          r["previous_ok"], r["last_op"])
+                          r["previous_ok"], r["last_op"], r["analyzer"])
+
+
+def _algorithm(a):
+    """checker.clj:141-145: (case (:algorithm opts) :linear ... :wgl ... competition)."""
+    a = (a or "competition")
+    a = a.lstrip(":") if isinstance(a, str) else a
+    return A.ALGORITHMS.get(a, A.ALGO_COMPETITION)
 
 
 def linearizable(opts):

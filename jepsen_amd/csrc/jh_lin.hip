@@ -327,8 +327,11 @@ struct DfsArgs {
     // run only when the list length (read on the device) is in [n_min, n_max]
     // (n_max 0: no upper bound): phase 3 picks one of two launched kernels
     int32_t n_min, n_max;
+    int32_t cause_or;           // :linear mode: CAUSE_BY_WGL on the verdicts (k_frontier)
 };
 constexpr unsigned long long SEQ_HANDED = ~0ULL;
+// verdict cause bits naming the engine in :linear mode (k_frontier turns them into jh_key_verdict.analyzer)
+constexpr int32_t CAUSE_BY_LINEAR = 0x100, CAUSE_BY_WGL = 0x200;
 
 constexpr int JH_CANCELLED = 3; // internal: the other search settled the key first
 
@@ -1721,7 +1724,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         }
         jh_key_verdict v;
         v.valid = verdict;
-        v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
+        v.cause = (verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0) | A.cause_or;
         v.explored = inserts;
         v.fail_entry = -1;
         // an invalid key's failing row is resolved by k_fail_rows from tmax
@@ -1812,6 +1815,18 @@ __global__ void __launch_bounds__(1024) k_sort_defer(SortLists L) {
 __global__ void k_unpack_keys(const uint64_t *__restrict__ in, int n, int32_t *__restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = (int32_t)(uint32_t)in[i];
+}
+
+// :linear mode has no WGL phase: every key that needs a search goes to the
+// reachable-set analysis, as if phase 1 had handed it on (q[1] all, q[29]
+// LEAN, q[30] WIDE, as phase 1's deferral counters)
+__global__ void __launch_bounds__(1024) k_linear_lists(const int32_t *__restrict__ list, const int32_t *n_list,
+                                                      const int32_t *__restrict__ list_w, const int32_t *n_list_w,
+                                                      int32_t *defer, int32_t *defer_l, int32_t *defer_w, int32_t *q) {
+    const int nl = *n_list, nw = *n_list_w;
+    for (int i = threadIdx.x; i < nl; i += blockDim.x) { defer[i] = list[i]; defer_l[i] = list[i]; }
+    for (int i = threadIdx.x; i < nw; i += blockDim.x) { defer[nl + i] = list_w[i]; defer_w[i] = list_w[i]; }
+    if (threadIdx.x == 0) { q[1] = nl + nw; q[29] = nl; q[30] = nw; }
 }
 
 // ---------------------------------------------------------------------------
@@ -2909,6 +2924,12 @@ struct BfsArgs {
     uint32_t *vis;          // ncap / 32 + 1
     uint32_t *tmp;          // ncap
     uint64_t *tmpk;         // ncap: the liveness pass's node keys, beside their slots in tmp
+    // :linear mode (knossos.linear, checker.clj:141-145): this search is the
+    // analysis -- a key is valid iff a terminal configuration is reachable,
+    // explored = the reachable configurations (initial and terminal ones
+    // excluded), no WGL count; keys past reach_cap (= budget + 1) go to the
+    // unresolved list, which WGL then decides
+    int32_t linear;
 };
 
 struct BfsShared {
@@ -3678,6 +3699,16 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
     }
     if (sh.status) {
         if (tid == 0 && !(sh.status & 4)) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
+    } else if (A.linear) {
+        // JIT linearization's verdict: the configuration set survives the last return or not
+        if (wid == 0) {
+            jh_key_verdict v;
+            v.valid = sh.term ? JH_VALID : JH_INVALID;
+            v.cause = CAUSE_BY_LINEAR;
+            v.explored = (int64_t)sh.count - 1;
+            v.fail_entry = sh.term ? -1 : ret_row(A.src, K, sh.tmax, lane);
+            if (lane == 0) emit_verdict(A.out, A.claim, key, v);
+        }
     } else if (sh.term) {
         // valid, or :unknown if WGL's count passes the budget: WGL's exact count
         if (tid == 0) { if (n_ok < A.lcap) A.lstart[n_ok] = sh.nnodes; sh.ok = 0; }
@@ -3792,6 +3823,7 @@ struct XwArgs {
     uint32_t gen_base;
     int32_t *flags;
     unsigned long long *probes;
+    int32_t cause_or;           // :linear mode: CAUSE_BY_WGL on the verdicts (k_frontier)
 };
 
 struct XwTbl {
@@ -4087,7 +4119,7 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
             if (pt != t) { t = pt; load_layer(); }
         }
         v.valid = verdict;
-        v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
+        v.cause = (verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0) | A.cause_or;
         v.explored = ins;
         v.fail_entry = verdict == JH_INVALID ? -(int64_t)tmax - 2 : -1;
         if (lane == 0) A.out[key] = v;
@@ -4116,7 +4148,6 @@ __global__ void __launch_bounds__(256) k_fail_rows(KeySrc S, jh_key_verdict *out
 // :linear mode the engines mark the cause word while searching (CAUSE_BY_LINEAR
 // for the reachable-set analysis, CAUSE_BY_WGL for a WGL search standing in
 // for it); an unmarked key took no search and gets the mode's own analyzer.
-constexpr int32_t CAUSE_BY_LINEAR = 0x100, CAUSE_BY_WGL = 0x200;
 __global__ void __launch_bounds__(256) k_frontier(KeySrc S, jh_key_verdict *out, int64_t K, int linear_mode) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * 4;
@@ -4536,13 +4567,15 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipMemsetAsync(a.defer_time, 0xFF, sizeof(unsigned long long), st));
     }
     HIP_TRY(hipEventRecord(ctx->ev[1], st));
-    k_lin_dfs<true><<<waves1, 64, MemoQ::LDS, st>>>(a);
-    HIP_TRY(hipGetLastError());
-    {
+    if (!linear_mode) {
+        k_lin_dfs<true><<<waves1, 64, MemoQ::LDS, st>>>(a);
+        HIP_TRY(hipGetLastError());
         DfsArgs aw = a;
         aw.list = list_w; aw.n_list_dev = q + 13; aw.queue = q + 14;
         aw.defer_kind = d64 + 2 * (K + 1); aw.defer_kind_count = q + Q_DEFER_W;
         k_lin_dfs<false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
+    } else {
+        k_linear_lists<<<1, 1024, 0, st>>>(list, q + 12, list_w, q + 13, defer, defer_l, defer_w, q);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[4], st));
@@ -4552,7 +4585,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const int n_defer = qh[1], n_def_l = qh[Q_DEFER_L], n_def_w = qh[Q_DEFER_W];
     const int n_x = qh[19];
     if (n_def_l + n_def_w != n_defer) throw_jh(JH_EDEVICE, "deferred-key lists disagree");
-    if (n_defer > 0) {
+    if (n_defer > 0 && !linear_mode) {
         // heavy keys, least advanced first (the likely longest searches start
         // first), sorted on the device: no host round trip between the phases
         SortLists sl{};
@@ -4612,6 +4645,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         x.budget = budget; x.init_state = init_state;
         x.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;   // its own table: any gen range works
         x.flags = q + 2; x.probes = (unsigned long long *)(q + 22);
+        x.cause_or = linear_mode ? CAUSE_BY_WGL : 0;
         HIP_TRY(hipEventRecord(ctx->ev[8], st));
         HIP_TRY(hipStreamWaitEvent(ctx->aux2, ctx->ev[8], 0));
         k_lin_xw<<<waves_x, 64, 0, ctx->aux2>>>(x);
@@ -4771,6 +4805,80 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
         HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
         launch_wide();
+    } else if (n_defer > 0 && linear_mode) {
+        // :algorithm :linear (checker.clj:141-145): the reachable-set search
+        // (k_lin_bfs in linear mode) is the analysis for every key it can hold
+        // -- JIT linearization's configuration sets, layer by layer -- on every
+        // CU; the keys it cannot (windows over 32 members, >= 4096 states, more
+        // than budget + 1 configurations) are decided by WGL afterwards on the
+        // same stream, and k_frontier reports each key's analyzer.
+        claim = ctx->ws<int32_t>(WS_CLAIM, K);
+        HIP_TRY(hipMemsetAsync(claim, 0, (size_t)K * sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(q + 3, 0, sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(q + 6, 0, 2 * sizeof(int32_t), st));
+        const uint32_t ncap = 1u << 16;                  // no WGL count: nothing to store
+        const int64_t reach_cap = budget + 1;
+        uint32_t set_cap = 1u << 12;
+        while ((int64_t)set_cap < 2 * reach_cap && set_cap < (1u << 30)) set_cap <<= 1;
+        const uint32_t q_cap = (uint32_t)std::min<int64_t>(reach_cap + 64, (int64_t)1 << 30);
+        const uint32_t lcap = (uint32_t)smax + 2;
+        const uint64_t per_bfs = (uint64_t)set_cap * 8 + 4ULL * q_cap * 8 + scr_bytes_bfs + (uint64_t)ncap * 8 +
+                                 (uint64_t)lcap * 4;
+        wg2 = fit_units(ctx, std::min(n_defer, ctx->n_cu), per_bfs, {WS_BFS_SET, WS_BFS_Q, WS_BFS_NODES});
+        BfsArgs c{};
+        c.src = KeySrc{rec, pair, off, rB, viol, rank, q + 2};
+        c.list = defer; c.n_list = n_defer; c.queue = q; c.out = out_dev;
+        c.unres_list = ctx->ws<int32_t>(WS_BFS_META, n_defer + 1); c.unres_count = q + 3;
+        c.gset = ctx->ws<uint64_t>(WS_BFS_SET, (size_t)wg2 * set_cap); c.gset_cap = set_cap;
+        uint64_t *bq = ctx->ws<uint64_t>(WS_BFS_Q, (size_t)wg2 * 4 * q_cap);
+        c.pend = bq; c.front = bq + (size_t)wg2 * 2 * q_cap; c.q_cap = q_cap;
+        c.scratch = ctx->ws<char>(WS_SCRATCH_BFS, (size_t)wg2 * scr_bytes_bfs); c.scratch_bytes = scr_bytes_bfs;
+        c.budget = budget; c.init_state = init_state; c.states_ok = n_states < 4096 ? 1 : 0;
+        c.claim = claim; c.reach_cap = reach_cap; c.linear = 1;
+        c.ncap = ncap; c.hcap = 1u << 17; c.lcap = lcap;
+        c.nodes = ctx->ws<uint64_t>(WS_BFS_NODES, (size_t)wg2 * ncap);
+        c.lstart = ctx->ws<uint32_t>(WS_BFS_LSTART, (size_t)wg2 * lcap);
+        if (!ctx->lds_attr) {
+            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_bfs, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        BFS_LDS_BYTES));
+            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        MemoH::LDS));
+            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        MemoH::LDS));
+            ctx->lds_attr = true;
+        }
+        // WGL for what the analysis cannot hold: LEAN and WIDE kernels over the
+        // unresolved list (each takes its own kind), after the BFS
+        const int want_f = std::min(n_defer, 4 * ctx->n_cu);
+        const uint64_t per_f = (uint64_t)cap2 * 16 + (uint64_t)stack_cap * sizeof(Frame) + scr_bytes_h;
+        waves2 = fit_units(ctx, want_f, per_f, {WS_MEMO_DEEP, WS_STACK_DEEP, WS_SCRATCH_DEEP});
+        const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;
+        uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
+        if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
+        DfsArgs f = a;
+        f.list = c.unres_list; f.n_list = 0; f.n_list_dev = q + 3; f.queue = q + 6; f.defer = 0;
+        f.defer_list = nullptr; f.defer_count = nullptr;
+        f.defer64 = nullptr; f.defer_kind = nullptr; f.defer_kind_count = nullptr;
+        f.memo = memo2; f.memo_cap = cap2;
+        f.stack = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap);
+        f.scratch = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes_h); f.scratch_bytes = scr_bytes_h;
+        f.budget = budget; f.budget_full = 0; f.claim = nullptr;
+        f.gen_base = ctx->gen_base + (uint32_t)K + 1;
+        f.probes = (unsigned long long *)(q + 8); f.dbg = nullptr; f.defer_time = nullptr;
+        f.seq_start = nullptr; f.exit_count = nullptr; f.cause_or = CAUSE_BY_WGL;
+        HIP_TRY(hipEventRecord(ctx->ev[6], st));
+        k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->ev[5], st));
+        k_lin_seq3<true><<<waves2, 64, MemoM::LDS, st>>>(f);
+        HIP_TRY(hipGetLastError());
+        DfsArgs fw = f;
+        fw.queue = q + 7;
+        k_lin_seqw<<<waves2, 64, MemoX::LDS, st>>>(fw);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->ev[10], st));
+        HIP_TRY(hipEventRecord(ctx->ev[7], st));
     } else if (n_defer > 0) {
         // Heavy keys: two exact searches race per key and the first to settle
         // it writes its verdict (emit_verdict), the other abandons it.

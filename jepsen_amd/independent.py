@@ -7,7 +7,7 @@ the GPU); any other composed checkers still run per key on their own.
 """
 from . import _abi as A
 from . import history as H
-from .checker import (Checker, Compose, Linearizable, check_safe, lin_result, merge_valid,
+from .checker import (Checker, Compose, Linearizable, _algorithm, check_safe, lin_result, merge_valid,
                       _init_state, _ctx)
 from .model import to_device_ops
 
@@ -122,7 +122,8 @@ class IndependentChecker(Checker):
             unkeyed_client = any(int(p) >= 0 and int(k) < 0 for p, k in zip(cols.process, cols.key))
             if cols.n_keys and not unkeyed_client:
                 verdicts, _ = _ctx().check_cas_independent(
-                    cols, init=_init_state(lin.model, cols), budget=lin.budget)
+                    cols, init=_init_state(lin.model, cols), budget=lin.budget,
+                    algorithm=_algorithm(lin.algorithm))
                 lin_res = {}
                 for kid, key in enumerate(cols.keys):
                     v = verdicts[kid]
@@ -130,7 +131,7 @@ class IndependentChecker(Checker):
                         continue
                     lin_res[key] = lin_result(int(v["valid"]), int(v["cause"]), int(v["fail_entry"]),
                                               int(v["explored"]), cols, int(v["previous_ok"]),
-                                              int(v["last_op"]))
+                                              int(v["last_op"]), int(v["analyzer"]))
                 if name is None:
                     return self._results_map(lin_res)
                 results = {}

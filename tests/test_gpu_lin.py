@@ -345,3 +345,42 @@ def test_memo_generation_wrap():
     g2, _ = ctx.check_cas_independent(cols, flags=A.LIN_GEN_JUMP)
     _same(g2, c)
     ctx.close()
+
+
+@pytest.mark.parametrize("seed,kw", [
+    (41, dict(n_keys=300, ops_per_key=200, p_invalid=0.2, p_info=0.05)),
+    (42, dict(n_keys=200, ops_per_key=300, threads_per_key=12, readers=6, p_invalid=0.1, p_info=0.02)),
+    (43, dict(n_keys=40, ops_per_key=260, threads_per_key=60, readers=20, groups=60, process_limit=10 ** 6,
+              p_info=0.08, p_invalid=0.2)),
+])
+def test_linear_algorithm(ctx, seed, kw):
+    """{:algorithm :linear} (checker.clj:141-145): JIT linearization -- the
+    reachable configuration set, layer by layer -- decides every key the
+    device's reachable-set engine holds (:analyzer :linear, explored = the
+    configurations it visited); WGL decides the rest (wide windows, sets
+    past the budget: :analyzer :wgl). Every field equals the oracle's
+    restatement, and :valid? equals the WGL analysis' on every key."""
+    cols, _ = synth.cas_register(seed=seed, **kw)
+    budget = 30000
+    g, gs = ctx.check_cas_independent(cols, budget=budget, algorithm="linear")
+    c, _ = oracle.check_cas_independent(cols, budget=budget, threads=16, algorithm="linear")
+    _same(g, c)
+    w, _ = ctx.check_cas_independent(cols, budget=budget)
+    decided = (g["valid"] != A.UNKNOWN) & (w["valid"] != A.UNKNOWN)
+    assert (g["valid"][decided] == w["valid"][decided]).all()
+    assert (w["analyzer"] == A.ANALYZER_WGL).all()
+    assert (g["analyzer"] == A.ANALYZER_LINEAR).sum() > 0
+    if seed == 43:
+        assert (g["analyzer"] == A.ANALYZER_WGL).sum() > 0
+
+
+def test_linear_algorithm_host_mirror(ctx):
+    """checker.Linearizable({:algorithm "linear"}) reports :analyzer :linear on
+    the reference's perf_test history (valid, perf_test.clj:13-137) and keeps
+    :valid? true; competition reports :wgl."""
+    from jepsen_amd import checker, model
+    d = json.load(open(os.path.join(GOLD, "perf_test.json")))
+    r = checker.Linearizable({"model": model.CASRegister(0), "algorithm": "linear"}).check(None, d["history"], {})
+    assert r["valid?"] is True and r["analyzer"] == "linear"
+    r = checker.Linearizable({"model": model.CASRegister(0)}).check(None, d["history"], {})
+    assert r["valid?"] is True and r["analyzer"] == "wgl"

@@ -254,6 +254,34 @@ int jh_check_cas_independent(jh_ctx *ctx, const jh_history *h,
 int jh_key_index(jh_ctx *ctx, const jh_history *h, int64_t *key_off, int64_t *rows,
                  char *err, size_t errlen);
 
+/* The frontier of invalid keys: knossos' :configs (checker.clj:146-158
+ * passes the analysis through and keeps (take 10 ...) of them). For each
+ * requested key that is invalid, up to per_key (<= 16) configurations of the
+ * last layer its search reaches -- the ways of linearizing the ops before the
+ * failing :ok op from which that op cannot be linearized -- in a canonical
+ * order: register value (nil first, then ascending), then the linearized
+ * members of the window as a bit mask in call order. n_out[i] = the count for
+ * keys[i], or -1 (not invalid, or outside the reachable-set engine: windows
+ * over 32 members, >= 4096 states, more than budget + 1 configurations).
+ * out[i * per_key + j] describes configuration j of keys[i]; its rows are
+ * rows_out[rows_off .. rows_off + n_linearized + n_pending): the invocation
+ * rows of the linearized ops, then of the pending ones (knossos' :pending),
+ * each in call order; rows_cap >= n_keys_q * per_key * 64. knossos is not
+ * vendored: this order, the cut and the layer are this library's
+ * definitions (parity unpinned; the oracle restates them). */
+typedef struct jh_lin_config {
+    int64_t key;
+    int64_t model_value;       /* the register's value in this configuration (JH_NIL: nil) */
+    int32_t n_linearized;
+    int32_t n_pending;
+    int64_t rows_off;
+} jh_lin_config;
+
+int jh_lin_configs(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts,
+                   const int64_t *keys, int64_t n_keys_q, int32_t per_key,
+                   jh_lin_config *out, int32_t *n_out, int64_t *rows_out, int64_t rows_cap,
+                   char *err, size_t errlen);
+
 /* (checker/linearizable {:model (model/cas-register init)}) on a history
  * whose values are not tuples (key column ignored). */
 int jh_check_cas(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts,

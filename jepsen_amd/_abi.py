@@ -95,6 +95,14 @@ class JhSummary(C.Structure):
                 ("wide_entries", C.c_int64), ("xw_entries", C.c_int64), ("waves", C.c_int64 * 4)]
 
 
+class JhLinConfig(C.Structure):
+    _fields_ = [("key", C.c_int64), ("model_value", C.c_int64), ("n_linearized", C.c_int32),
+                ("n_pending", C.c_int32), ("rows_off", C.c_int64)]
+
+
+CONFIGS_PER_KEY = 10          # checker.clj:146-158: (take 10 ...) of :configs and :final-paths
+
+
 class JhSetResult(C.Structure):
     _fields_ = [("valid", C.c_int32), ("cause", C.c_int32),
                 ("attempt_count", C.c_int64), ("acknowledged_count", C.c_int64),

@@ -45,6 +45,9 @@ def lib():
                                                    C.POINTER(A.JhKeyVerdict), C.POINTER(A.JhSummary),
                                                    C.c_char_p, C.c_size_t]
             L.jh_check_cas_independent_device.argtypes = L.jh_check_cas_independent.argtypes
+            L.jh_lin_configs.argtypes = [C.c_void_p, H, C.POINTER(A.JhLinOpts), C.POINTER(C.c_int64), C.c_int64,
+                                         C.c_int32, C.POINTER(A.JhLinConfig), C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_int64), C.c_int64, C.c_char_p, C.c_size_t]
             L.jh_check_cas.argtypes = [C.c_void_p, H, C.POINTER(A.JhLinOpts),
                                        C.POINTER(A.JhKeyVerdict), C.c_char_p, C.c_size_t]
             p64 = C.POINTER(C.c_int64)
@@ -86,7 +89,7 @@ def lib():
 
 EXPORTED_SYMBOLS = ["jh_version", "jh_open", "jh_open_multi", "jh_open_devices", "jh_n_devices", "jh_key_costs", "jh_key_index",
                     "jh_close", "jh_check_cas_independent",
-                    "jh_check_cas", "jh_check_cas_independent_device", "jh_check_counter",
+                    "jh_check_cas", "jh_check_cas_independent_device", "jh_lin_configs", "jh_check_counter",
                     "jh_check_set", "jh_check_set_bitmaps", "jh_check_set_full", "jh_check_total_queue", "jh_check_queue",
                     # include/jh_io.h
                     "jh_ingest_file", "jh_ingest_buffer", "jh_ingest_history", "jh_ingest_time",
@@ -217,6 +220,34 @@ class Context:
                                 err, len(err))
         _raise(rc, err)
         return {f: getattr(v, f) for f, _ in A.JhKeyVerdict._fields_}
+
+    def lin_configs(self, cols, keys, per_key=A.CONFIGS_PER_KEY, init=None, budget=None, **tune):
+        """jh_lin_configs: {key: None | [(model_value, linearized rows, pending rows)]}
+        -- the frontier configurations of each invalid key (include/jh.h)."""
+        h = A.make_history(cols)
+        keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
+        nq = len(keys)
+        out = (A.JhLinConfig * max(nq * per_key, 1))()
+        n_out = np.zeros(max(nq, 1), np.int32)
+        rows = np.zeros(max(nq * per_key * 64, 1), np.int64)
+        err = C.create_string_buffer(1024)
+        rc = lib().jh_lin_configs(self._h, C.byref(h), C.byref(_opts(init, budget, **tune)),
+                                  keys.ctypes.data_as(C.POINTER(C.c_int64)), nq, per_key, out,
+                                  n_out.ctypes.data_as(C.POINTER(C.c_int32)), A.ptr64(rows), len(rows),
+                                  err, len(err))
+        _raise(rc, err)
+        res = {}
+        for i, k in enumerate(keys.tolist()):
+            if n_out[i] < 0:
+                res[k] = None
+                continue
+            cs = []
+            for j in range(n_out[i]):
+                c = out[i * per_key + j]
+                r = rows[c.rows_off:c.rows_off + c.n_linearized + c.n_pending]
+                cs.append((int(c.model_value), r[:c.n_linearized].tolist(), r[c.n_linearized:].tolist()))
+            res[k] = cs
+        return res
 
     # -- counter / set -----------------------------------------------------
     def check_counter(self, cols, reads_cap=None, on_device=False):

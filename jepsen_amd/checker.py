@@ -206,10 +206,31 @@ class Linearizable(Checker):
         if not isinstance(history, H.Columns):
             history = to_device_ops(self.model, list(history))
         cols = _cols(history, keyed=False)
-        r = _ctx().check_cas_full(cols, init=_init_state(self.model, cols), budget=self.budget,
-                                  algorithm=_algorithm(self.algorithm))
-        return lin_result(r["valid"], r["cause"], r["fail_entry"], r["explored"], cols,
-                          r["previous_ok"], r["last_op"], r["analyzer"])
+        init = _init_state(self.model, cols)
+        r = _ctx().check_cas_full(cols, init=init, budget=self.budget, algorithm=_algorithm(self.algorithm))
+        out = lin_result(r["valid"], r["cause"], r["fail_entry"], r["explored"], cols,
+                         r["previous_ok"], r["last_op"], r["analyzer"])
+        if r["valid"] == A.INVALID:
+            cf = _ctx().lin_configs(cols, [0], init=init, budget=self.budget)
+            add_configs(out, cf[0], cols)
+        return out
+
+
+def add_configs(result, configs, cols):
+    """:configs and :final-paths of an invalid result (checker.clj:146-158
+    keeps (take 10 ...) of each), from jh_lin_configs: every configuration of
+    the frontier as {:model, :linearized ops, :pending ops}, and as its final
+    path the step that fails -- the result's :op applied to that model. (The
+    knossos maps these restate are not vendored: parity unpinned.)"""
+    if configs is None:
+        return result
+    def model(v):
+        return {"value": None if v == A.NIL else int(v)}
+    cf = [{"model": model(v), "linearized": [H.decode_op(cols, x) for x in lin],
+           "pending": [H.decode_op(cols, x) for x in pend]} for v, lin, pend in configs]
+    result["configs"] = cf[:A.CONFIGS_PER_KEY]
+    result["final-paths"] = [[{"op": result.get("op"), "model": c["model"]}] for c in cf][:A.CONFIGS_PER_KEY]
+    return result
 
 
 def _algorithm(a):

@@ -168,6 +168,64 @@ int jh_check_cas_independent_device(jh_ctx *ctx, const jh_history *h, const jh_l
     });
 }
 
+__global__ void k_cfg_slots(const int64_t *__restrict__ keys, int n, int64_t K, int32_t *slot) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && keys[i] >= 0 && keys[i] < K) slot[keys[i]] = i;
+}
+
+int jh_lin_configs(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts, const int64_t *keys,
+                   int64_t n_keys_q, int32_t per_key, jh_lin_config *out, int32_t *n_out, int64_t *rows_out,
+                   int64_t rows_cap, char *err, size_t errlen) {
+    if (!ctx || !keys || !out || !n_out || !rows_out) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    if (per_key < 1 || per_key > 16) { set_err(err, errlen, "per_key must be in 1..16"); return JH_EINVAL; }
+    if (n_keys_q < 0 || n_keys_q > (1 << 20)) { set_err(err, errlen, "bad number of keys"); return JH_EINVAL; }
+    if (rows_cap < n_keys_q * per_key * 64) { set_err(err, errlen, "rows_cap < n_keys_q * per_key * 64"); return JH_EINVAL; }
+    ctx = primary(ctx);
+    std::lock_guard<std::mutex> g(ctx->mu);
+    return guarded(err, errlen, [&] {
+        check_hist(h);
+        HIP_TRY(hipSetDevice(ctx->device));
+        hipStream_t st = ctx->stream;
+        const bool keyed = h->key != nullptr && h->n_keys > 0;
+        jh_history d = stage_history(ctx, h, keyed, false);
+        if (!keyed) { d.key = nullptr; d.n_keys = 1; }
+        const int64_t K = d.n_keys;
+        for (int64_t i = 0; i < n_keys_q; i++) n_out[i] = -1;
+        if (n_keys_q == 0 || K == 0) return;
+        const int nq = (int)n_keys_q;
+        int32_t *slot = ctx->ws<int32_t>(WS_CFG_SLOT, K);
+        int64_t *kd = ctx->ws<int64_t>(WS_CFG_KEYS, nq);
+        jh_lin_config *co = ctx->ws<jh_lin_config>(WS_CFG_OUT, (size_t)nq * per_key);
+        int32_t *cn = ctx->ws<int32_t>(WS_CFG_N, nq);
+        int64_t *cr = ctx->ws<int64_t>(WS_CFG_ROWS, (size_t)nq * per_key * 64);
+        HIP_TRY(hipMemsetAsync(slot, 0xFF, sizeof(int32_t) * K, st));
+        HIP_TRY(hipMemsetAsync(cn, 0xFF, sizeof(int32_t) * nq, st));
+        HIP_TRY(hipMemcpyAsync(kd, keys, sizeof(int64_t) * nq, hipMemcpyHostToDevice, st));
+        k_cfg_slots<<<(nq + 255) / 256, 256, 0, st>>>(kd, nq, K, slot);
+        jh_key_verdict *dv = ctx->ws<jh_key_verdict>(WS_VERDICT, std::max<int64_t>(K, 1));
+        LinCfgReq req{kd, nq, per_key, slot, co, cn, cr};
+        lin_check_independent(ctx, &d, opts, keyed, dv, nullptr, st, &req);
+        std::vector<jh_lin_config> hc((size_t)nq * per_key);
+        std::vector<int64_t> hr((size_t)nq * per_key * 64);
+        HIP_TRY(hipMemcpyAsync(n_out, cn, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(hc.data(), co, sizeof(jh_lin_config) * hc.size(), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(hr.data(), cr, sizeof(int64_t) * hr.size(), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        // compact: configuration j of key i keeps slot i * per_key + j; its rows move up
+        int64_t w = 0;
+        for (int i = 0; i < nq; i++)
+            for (int j = 0; j < per_key; j++) {
+                jh_lin_config &c = out[(size_t)i * per_key + j];
+                if (j >= n_out[i]) { memset(&c, 0, sizeof c); c.key = keys[i]; c.rows_off = w; continue; }
+                c = hc[(size_t)i * per_key + j];
+                const int64_t nr = (int64_t)c.n_linearized + c.n_pending;
+                memcpy(rows_out + w, hr.data() + c.rows_off, sizeof(int64_t) * nr);
+                c.rows_off = w;
+                w += nr;
+            }
+    });
+}
+
 int jh_key_index(jh_ctx *ctx, const jh_history *h, int64_t *key_off, int64_t *rows, char *err,
                  size_t errlen) {
     if (!ctx || !key_off || (!rows && h && h->n > 0)) { set_err(err, errlen, "null argument"); return JH_EINVAL; }

@@ -107,6 +107,7 @@ enum WsSlot {
     WS_WG_MEMO, WS_WG_STACK, WS_WG_SCR, WS_S_BYTES, WS_IV_U, WS_IV_IDX, WS_IV_KEY, WS_IV_RINIT, WS_IV_MAX, WS_IV_TMP,
     WS_HELP_START, WS_HELP_TAKEN, WS_DEFER_TIME, WS_BFS_TMPK,
     WS_DEFER64, WS_DEFER64_T, WS_MEMO_WIDE, WS_STACK_WIDE, WS_SCRATCH_WIDE,
+    WS_CFG_SLOT, WS_CFG_OUT, WS_CFG_N, WS_CFG_ROWS, WS_CFG_KEYS,
     WS_COUNT
 };
 
@@ -144,10 +145,19 @@ inline int grid_for(int64_t n, int block, int cap = 65536) {
 // pointers through). Returns a device-pointer view.
 jh_history stage_history(jh_ctx *ctx, const jh_history *h, bool need_key, bool need_aux);
 
-// linearizability (jh_lin.hip)
+// linearizability (jh_lin.hip). cfg: a jh_lin_configs request (the frontier
+// configurations of the listed keys, device buffers; null for a check)
+struct LinCfgReq {
+    const int64_t *keys_dev;      // n_q requested keys
+    int32_t n_q, per_key;
+    const int32_t *slot_dev;      // per key: its index in keys_dev, or -1
+    jh_lin_config *out_dev;       // n_q * per_key
+    int32_t *n_dev;               // n_q, -1 on entry
+    int64_t *rows_dev;            // n_q * per_key * 64
+};
 void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts *opts,
                            bool keyed, jh_key_verdict *out_dev, jh_summary *sum,
-                           hipStream_t stream);
+                           hipStream_t stream, const LinCfgReq *cfg = nullptr);
 // per-key row CSR of an independent history (jh_lin.hip)
 void key_index(jh_ctx *ctx, const jh_history *dh, int64_t *key_off, int64_t *rows, hipStream_t stream);
 // counter (jh_counter.hip)

@@ -2930,6 +2930,17 @@ struct BfsArgs {
     // excluded), no WGL count; keys past reach_cap (= budget + 1) go to the
     // unresolved list, which WGL then decides
     int32_t linear;
+    // frontier configurations of invalid keys (jh_lin_configs, knossos'
+    // :configs): per key its output slot (-1: none); per slot up to cfg_per
+    // configurations of the last layer reached and their window rows
+    const int32_t *cfg_slot;
+    jh_lin_config *cfg_out;
+    int32_t *cfg_n;
+    int64_t *cfg_rows;
+    int32_t cfg_per;
+    const int64_t *col_val, *col_val2;   // the raw value columns (model values)
+    int64_t vmin, init_value;
+    int32_t per_key_values;
 };
 
 struct BfsShared {
@@ -2941,6 +2952,7 @@ struct BfsShared {
     unsigned long long count, ccount, plen;
     uint32_t win_vv[64];    // the current layer's window: v1 | v2 << 16
     uint32_t win_f[64];     // f, or 3 for no member
+    unsigned long long cfg_min;
 };
 
 static_assert(sizeof(BfsShared) <= BFS_HDR, "BFS header");
@@ -3394,6 +3406,97 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
 // layer (fail_entry) equal the sequential search's. A key where a terminal
 // configuration is reachable (valid) or the set outgrows the budget is left
 // to the sequential search, which alone defines :unknown for those.
+// The frontier of an invalid key (knossos' :configs, of which
+// checker.clj:146-158 keeps (take 10 ...)): the configurations of the last
+// layer reached, tmax -- every way of linearizing the ops before RET[tmax]
+// from which RET[tmax] itself cannot be -- in a canonical order (model
+// state, then the linearized members of W(tmax) as a bit mask in call
+// order; nil first, then values ascending), the first cfg_per of them, each
+// as its register value, the window's linearized ops and its pending ops
+// (invocation rows, call order). Selection by cfg_per rounds of a workgroup
+// minimum over the layer (the configurations are distinct); knossos itself
+// is not vendored, so this order and cut are this library's (oracle:
+// orc_lin_configs).
+constexpr int CFG_MAX = 16;
+__device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int key, const int32_t *woff,
+                                 const uint16_t *W, uint32_t n_ok) {
+    const int slot = A.cfg_slot[key];
+    const int lane = tid & 63, wid = tid >> 6;
+    const uint32_t tm = sh.tmax;
+    const uint32_t a = A.lstart[tm], b = tm + 1 < n_ok ? A.lstart[tm + 1] : sh.nnodes;
+    __shared__ unsigned long long sel[CFG_MAX];
+    __shared__ long long wrow[64];
+    __shared__ int nsel;
+    const int per = min(A.cfg_per, CFG_MAX);
+    unsigned long long prev = 0;
+    if (tid == 0) nsel = 0;
+    for (int i = 0; i < per; i++) {
+        if (tid == 0) sh.cfg_min = ~0ULL;
+        __syncthreads();
+        unsigned long long m = ~0ULL;
+        for (uint32_t j = a + tid; j < b; j += BFS_THREADS) {
+            const unsigned long long kk = A.nodes[j] & ((1ULL << 44) - 1);   // s:12 | mask:32
+            if ((i == 0 || kk > prev) && kk < m) m = kk;
+        }
+        for (int o = 32; o > 0; o >>= 1) m = min(m, (unsigned long long)__shfl_xor(m, o));
+        if (lane == 0 && m != ~0ULL) atomicMin(&sh.cfg_min, m);
+        __syncthreads();
+        prev = sh.cfg_min;
+        if (prev == ~0ULL) break;
+        if (tid == 0) { sel[i] = prev; nsel = i + 1; }
+        __syncthreads();
+    }
+    __syncthreads();
+    if (wid != 0) return;
+    // the invocation row of every member of W(tmax)
+    const int wo = woff[tm], w = woff[tm + 1] - wo;
+    for (uint32_t base = sh.K.s0; base < sh.K.s1; base += 64) {
+        const uint32_t p = base + lane;
+        const int rk = p < sh.K.s1 ? A.src.rank[p] : -1;
+        if (rk >= 0)
+            for (int j = 0; j < w; j++)
+                if ((int)W[wo + j] == rk) wrow[j] = (long long)A.src.rows[p];
+    }
+    wave_sync();
+    for (int i = 0; i < nsel; i++) {
+        const uint32_t st = (uint32_t)(sel[i] >> 32) & 0xFFF, mask = (uint32_t)sel[i];
+        long long val = JH_NIL;
+        if (st != 0) {
+            if (!A.per_key_values) val = A.vmin + (long long)st - 1;
+            else if (st == 1 && A.init_value != JH_NIL) val = A.init_value;
+            else {
+                // per-key ids: the raw value of a record of this key carrying the id
+                long long got = JH_NIL;
+                for (uint32_t base = sh.K.s0; base < sh.K.s1; base += 64) {
+                    const uint32_t p = base + lane;
+                    long long v = JH_NIL;
+                    if (p < sh.K.s1) {
+                        const Rec x = A.src.rec[p];
+                        const long long row = (long long)A.src.rows[p];
+                        if (x.proc >= 0 && x.v1 == (int32_t)st) v = A.col_val[row];
+                        else if (x.proc >= 0 && x.f == F_CAS && x.v2 == (int32_t)st) v = A.col_val2[row];
+                    }
+                    const uint64_t hit = ballot(v != JH_NIL);
+                    if (hit) { got = readlane64((uint64_t)v, __builtin_ctzll(hit)); break; }
+                }
+                val = got;
+            }
+        }
+        const int64_t o = ((int64_t)slot * A.cfg_per + i) * 64;
+        const bool in = lane < w, lin = in && ((mask >> lane) & 1);
+        const uint64_t bl = ballot(lin), bp = ballot(in && !lin);
+        const int nl = __popcll(bl);
+        if (lin) A.cfg_rows[o + mbcnt(bl)] = wrow[lane];
+        if (in && !lin) A.cfg_rows[o + nl + mbcnt(bp)] = wrow[lane];
+        if (lane == 0) {
+            jh_lin_config c;
+            c.key = key; c.model_value = val; c.n_linearized = nl; c.n_pending = __popcll(bp); c.rows_off = o;
+            A.cfg_out[(int64_t)slot * A.cfg_per + i] = c;
+        }
+    }
+    if (lane == 0) A.cfg_n[slot] = nsel;
+}
+
 template <bool L>
 __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, uint64_t *gset,
                         uint64_t *pend, uint64_t *front) {
@@ -3701,6 +3804,9 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         if (tid == 0 && !(sh.status & 4)) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
     } else if (A.linear) {
         // JIT linearization's verdict: the configuration set survives the last return or not
+        if (!sh.term && A.cfg_slot && A.cfg_slot[key] >= 0 && !sh.nostore)
+            bfs_dump_configs(A, sh, tid, key, woff, W, n_ok);
+        __syncthreads();
         if (wid == 0) {
             jh_key_verdict v;
             v.valid = sh.term ? JH_VALID : JH_INVALID;
@@ -4374,9 +4480,21 @@ static inline int64_t q64(const int32_t *qh, int i) {
     return (int64_t)(((uint64_t)(uint32_t)qh[i + 1] << 32) | (uint32_t)qh[i]);
 }
 
+// jh_lin_configs: the requested keys are the whole heavy list, all LEAN
+__global__ void k_req_lists(const int64_t *__restrict__ keys, int n, int64_t K, int32_t *defer, int32_t *defer_l,
+                            int32_t *q) {
+    int m = 0;
+    for (int i = 0; i < n; i++) {           // one thread: a handful of keys
+        const int64_t k = keys[i];
+        if (k < 0 || k >= K) continue;
+        defer[m] = (int32_t)k; defer_l[m] = (int32_t)k; m++;
+    }
+    q[1] = m; q[29] = m; q[30] = 0;
+}
+
 void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts *opts,
                            bool keyed, jh_key_verdict *out_dev, jh_summary *sum,
-                           hipStream_t st) {
+                           hipStream_t st, const LinCfgReq *cfgreq) {
     const int64_t n = dh->n;
     const int64_t K = keyed ? dh->n_keys : 1;
     if (K >= (1LL << 23)) throw_jh(JH_EUNSUPPORTED, "more than 2^23 keys in one call");
@@ -4384,7 +4502,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const int64_t budget = opts && opts->budget > 0 ? opts->budget : JH_DEFAULT_BUDGET;
     const int64_t init = opts ? opts->init_value : JH_NIL;
     const int32_t lflags = opts ? opts->flags : 0;
-    const bool linear_mode = opts && opts->algorithm == JH_ALGO_LINEAR;
+    const bool linear_mode = (opts && opts->algorithm == JH_ALGO_LINEAR) || cfgreq;
     HIP_TRY(hipEventRecord(ctx->ev[0], st));
 
     // ranges
@@ -4574,6 +4692,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         aw.list = list_w; aw.n_list_dev = q + 13; aw.queue = q + 14;
         aw.defer_kind = d64 + 2 * (K + 1); aw.defer_kind_count = q + Q_DEFER_W;
         k_lin_dfs<false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
+    } else if (cfgreq) {
+        k_req_lists<<<1, 1, 0, st>>>(cfgreq->keys_dev, cfgreq->n_q, K, defer, defer_l, q);
     } else {
         k_linear_lists<<<1, 1024, 0, st>>>(list, q + 12, list_w, q + 13, defer, defer_l, defer_w, q);
     }
@@ -4583,7 +4703,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const int n_defer = qh[1], n_def_l = qh[Q_DEFER_L], n_def_w = qh[Q_DEFER_W];
-    const int n_x = qh[19];
+    const int n_x = cfgreq ? 0 : qh[19];
     if (n_def_l + n_def_w != n_defer) throw_jh(JH_EDEVICE, "deferred-key lists disagree");
     if (n_defer > 0 && !linear_mode) {
         // heavy keys, least advanced first (the likely longest searches start
@@ -4817,8 +4937,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
         HIP_TRY(hipMemsetAsync(q + 3, 0, sizeof(int32_t), st));
         HIP_TRY(hipMemsetAsync(q + 6, 0, 2 * sizeof(int32_t), st));
-        const uint32_t ncap = 1u << 16;                  // no WGL count: nothing to store
         const int64_t reach_cap = budget + 1;
+        // no WGL count, nothing to store -- except for a configurations request,
+        // which needs the last layer reached: every node
+        const uint32_t ncap = cfgreq ? (uint32_t)std::min<int64_t>(reach_cap + 64, (int64_t)1 << 30) : 1u << 16;
         uint32_t set_cap = 1u << 12;
         while ((int64_t)set_cap < 2 * reach_cap && set_cap < (1u << 30)) set_cap <<= 1;
         const uint32_t q_cap = (uint32_t)std::min<int64_t>(reach_cap + 64, (int64_t)1 << 30);
@@ -4837,6 +4959,12 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         c.budget = budget; c.init_state = init_state; c.states_ok = n_states < 4096 ? 1 : 0;
         c.claim = claim; c.reach_cap = reach_cap; c.linear = 1;
         c.ncap = ncap; c.hcap = 1u << 17; c.lcap = lcap;
+        if (cfgreq) {
+            c.cfg_slot = cfgreq->slot_dev; c.cfg_out = cfgreq->out_dev; c.cfg_n = cfgreq->n_dev;
+            c.cfg_rows = cfgreq->rows_dev; c.cfg_per = cfgreq->per_key;
+            c.col_val = dh->value; c.col_val2 = dh->value2;
+            c.vmin = vmin; c.init_value = init; c.per_key_values = per_key_values ? 1 : 0;
+        }
         c.nodes = ctx->ws<uint64_t>(WS_BFS_NODES, (size_t)wg2 * ncap);
         c.lstart = ctx->ws<uint32_t>(WS_BFS_LSTART, (size_t)wg2 * lcap);
         if (!ctx->lds_attr) {
@@ -4871,12 +4999,14 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        k_lin_seq3<true><<<waves2, 64, MemoM::LDS, st>>>(f);
-        HIP_TRY(hipGetLastError());
-        DfsArgs fw = f;
-        fw.queue = q + 7;
-        k_lin_seqw<<<waves2, 64, MemoX::LDS, st>>>(fw);
-        HIP_TRY(hipGetLastError());
+        if (!cfgreq) {
+            k_lin_seq3<true><<<waves2, 64, MemoM::LDS, st>>>(f);
+            HIP_TRY(hipGetLastError());
+            DfsArgs fw = f;
+            fw.queue = q + 7;
+            k_lin_seqw<<<waves2, 64, MemoX::LDS, st>>>(fw);
+            HIP_TRY(hipGetLastError());
+        }
         HIP_TRY(hipEventRecord(ctx->ev[10], st));
         HIP_TRY(hipEventRecord(ctx->ev[7], st));
     } else if (n_defer > 0) {

@@ -408,6 +408,88 @@ done:
     return verdict;
 }
 
+/* The frontier of an invalid key (libjh's jh_lin_configs, knossos' :configs
+ * kept to (take 10 ...) by checker.clj:146-158): the configurations of the
+ * last layer the analysis reaches, ordered by register value (nil first;
+ * then, with per-key value numbering, the initial value; then ascending) and
+ * then by the linearized-members mask, the first per_key of them; each as
+ * its value and the invocation rows of its linearized, then pending, window
+ * members in call order. Returns the count, or -1 when the key is not
+ * invalid or outside the analysis' domain. */
+/* :algorithm :linear on libjh.so's terms: the JIT-linearization analysis
+ * decides a key when its windows fit the reachable-set engine (at most 32
+ * members, fewer than 4096 interned states) and its reachable set fits the
+ * budget; any other key is decided by WGL and reported with :analyzer :wgl
+ * (the choice knossos.competition makes when :linear cannot finish).
+ * states_ok is the history-wide condition the device computes once. */
+int orc_linear_states_ok = 1;
+static int linear_domain(const orc_key *k) {
+    return k->max_window <= 32 && orc_linear_states_ok && k->n_ok < (1 << 20) - 2;
+}
+
+typedef struct { int64_t bucket, v; uint64_t m; } cfg_ord;
+static int cmp_cfg_ord(const void *a, const void *b) {
+    const cfg_ord *x = (const cfg_ord *)a, *y = (const cfg_ord *)b;
+    if (x->bucket != y->bucket) return x->bucket < y->bucket ? -1 : 1;
+    if (x->v != y->v) return x->v < y->v ? -1 : 1;
+    return x->m < y->m ? -1 : x->m > y->m;
+}
+static int configs_one(const jh_history *h, const int64_t *sel, int64_t m, int64_t init, int64_t budget,
+                       int per_key, int per_key_values, jh_lin_config *out, int64_t *rows) {
+    orc_key k;
+    orc_key_prepare(h, sel, m, &k);
+    int n = -1;
+    if (!k.status && linear_domain(&k)) {
+        cvec front = {0, 0, 0};
+        int64_t explored; uint32_t tmax;
+        if (orc_linear(&k, init, budget, &explored, &tmax, &front) == JH_INVALID) {
+            cfg_ord *o = (cfg_ord *)malloc(sizeof(cfg_ord) * (front.n ? front.n : 1));
+            for (int64_t i = 0; i < front.n; i++) {
+                const int64_t v = front.e[i].s;
+                o[i].bucket = v == JH_NIL ? 0 : (per_key_values && init != JH_NIL && v == init) ? 1 : 2;
+                o[i].v = v; o[i].m = front.e[i].m[0];
+            }
+            qsort(o, front.n, sizeof(cfg_ord), cmp_cfg_ord);
+            n = (int)(front.n < per_key ? front.n : per_key);
+            const int32_t *W = k.w_ops + k.w_off[tmax];
+            const int w = k.w_off[tmax + 1] - k.w_off[tmax];
+            for (int i = 0; i < n; i++) {
+                jh_lin_config *c = &out[i];
+                c->key = 0; c->model_value = o[i].v; c->n_linearized = 0; c->n_pending = 0;
+                c->rows_off = (int64_t)i * 64;
+                int64_t *r = rows + (int64_t)i * 64;
+                for (int j = 0; j < w; j++) if ((o[i].m >> j) & 1) r[c->n_linearized++] = k.ops[W[j]].call;
+                for (int j = 0; j < w; j++) if (!((o[i].m >> j) & 1)) r[c->n_linearized + c->n_pending++] = k.ops[W[j]].call;
+            }
+            free(o);
+        }
+        free(front.e);
+    }
+    orc_key_free(&k);
+    return n;
+}
+
+int orc_lin_configs(const jh_history *h, int64_t init, int64_t budget, const int64_t *keys, int64_t nq,
+                    int32_t per_key, int32_t per_key_values, jh_lin_config *out, int32_t *n_out, int64_t *rows) {
+    if (budget <= 0) budget = JH_DEFAULT_BUDGET;
+    int64_t *sel = (int64_t *)malloc(sizeof(int64_t) * (h->n ? h->n : 1));
+    for (int64_t q = 0; q < nq; q++) {
+        int64_t m = 0;
+        for (int64_t r = 0; r < h->n; r++) {
+            const int64_t kk = h->key ? h->key[r] : 0;
+            if (kk == keys[q] || kk < 0) sel[m++] = r;
+        }
+        n_out[q] = configs_one(h, sel, m, init, budget, per_key, per_key_values, out + q * per_key,
+                               rows + q * per_key * 64);
+        for (int i = 0; i < per_key; i++) {
+            out[q * per_key + i].key = keys[q];
+            out[q * per_key + i].rows_off += q * per_key * 64;
+        }
+    }
+    free(sel);
+    return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* knossos-style WGL: doubly linked list of call/return entries in history
  * order, lift/unlift, BitSet of linearized op ids, HashSet<(BitSet, model)>.
@@ -571,17 +653,6 @@ int orc_lin_bruteforce(const orc_key *k, int64_t init) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* :algorithm :linear on libjh.so's terms: the JIT-linearization analysis
- * decides a key when its windows fit the reachable-set engine (at most 32
- * members, fewer than 4096 interned states) and its reachable set fits the
- * budget; any other key is decided by WGL and reported with :analyzer :wgl
- * (the choice knossos.competition makes when :linear cannot finish).
- * states_ok is the history-wide condition the device computes once. */
-int orc_linear_states_ok = 1;
-static int linear_domain(const orc_key *k) {
-    return k->max_window <= 32 && orc_linear_states_ok && k->n_ok < (1 << 20) - 2;
-}
-
 static void check_one(const jh_history *h, const int64_t *sel, int64_t m,
                       int64_t init, int64_t budget, int list_algo, jh_key_verdict *out) {
     orc_key k;

@@ -69,6 +69,11 @@ struct cvec;
  * device computes it; the reachable-set engine packs states in 12 bits) */
 extern int orc_linear_states_ok;
 
+/* The frontier configurations of invalid keys (restates jh_lin_configs;
+ * rows of configuration j of keys[q] at rows[(q * per_key + j) * 64 ...]). */
+int orc_lin_configs(const jh_history *h, int64_t init, int64_t budget, const int64_t *keys, int64_t nq,
+                    int32_t per_key, int32_t per_key_values, jh_lin_config *out, int32_t *n_out, int64_t *rows);
+
 /* Whole-history linearizable check (non-independent). */
 int  orc_check_cas(const jh_history *h, int64_t init, int64_t budget,
                    jh_key_verdict *out);

@@ -44,6 +44,8 @@ def lib():
         L.orc_interval_str.argtypes = [p64, C.c_int64, C.c_char_p, C.c_int64]
         L.orc_interval_str.restype = C.c_int64
         L.orc_lin_selftest_key.argtypes = [H, C.c_int64, C.c_int64, p64]
+        L.orc_lin_configs.argtypes = [H, C.c_int64, C.c_int64, p64, C.c_int64, C.c_int32, C.c_int32,
+                                      C.POINTER(A.JhLinConfig), C.POINTER(C.c_int32), p64]
         _lib = L
     return _lib
 
@@ -100,6 +102,43 @@ def check_cas_independent(cols, init=A.NIL, budget=A.DEFAULT_BUDGET, mode=0, thr
     lib().orc_check_cas_independent(C.byref(h), init, budget, mode, threads,
                                     out.ctypes.data_as(C.POINTER(A.JhKeyVerdict)), C.byref(s))
     return out[:cols.n_keys], s
+
+
+def per_key_values(cols, init=A.NIL):
+    """Whether the device numbers register values per key (their range spans
+    more than one 16-bit state range)."""
+    cl = (cols.process >= 0) & (cols.f <= A.F_CAS)
+    v = cols.value[cl]
+    v2 = cols.value2[cl & (cols.f == A.F_CAS)]
+    vals = np.concatenate([v[v != A.NIL], v2[v2 != A.NIL]] + ([np.array([init])] if init != A.NIL else []))
+    return len(vals) > 0 and int(vals.max()) - int(vals.min()) >= 0xFFFE - 3
+
+
+def lin_configs(cols, keys, per_key=A.CONFIGS_PER_KEY, init=A.NIL, budget=A.DEFAULT_BUDGET):
+    """orc_lin_configs, the restatement of jh_lin_configs (same return shape
+    as _native.Context.lin_configs)."""
+    C.c_int.in_dll(lib(), "orc_linear_states_ok").value = 1 if linear_states_ok(cols, init) else 0
+    h = cols.as_jh()
+    keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
+    nq = len(keys)
+    out = (A.JhLinConfig * max(nq * per_key, 1))()
+    n_out = np.zeros(max(nq, 1), np.int32)
+    rows = np.zeros(max(nq * per_key * 64, 1), np.int64)
+    lib().orc_lin_configs(C.byref(h), init, budget, A.ptr64(keys), nq, per_key,
+                          1 if per_key_values(cols, init) else 0, out,
+                          n_out.ctypes.data_as(C.POINTER(C.c_int32)), A.ptr64(rows))
+    res = {}
+    for i, k in enumerate(keys.tolist()):
+        if n_out[i] < 0:
+            res[k] = None
+            continue
+        cs = []
+        for j in range(n_out[i]):
+            c = out[i * per_key + j]
+            r = rows[c.rows_off:c.rows_off + c.n_linearized + c.n_pending]
+            cs.append((int(c.model_value), r[:c.n_linearized].tolist(), r[c.n_linearized:].tolist()))
+        res[k] = cs
+    return res
 
 
 def check_cas_independent_range(cols, k0, k1, init=A.NIL, budget=A.DEFAULT_BUDGET, mode=0,

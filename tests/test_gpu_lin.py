@@ -384,3 +384,40 @@ def test_linear_algorithm_host_mirror(ctx):
     assert r["valid?"] is True and r["analyzer"] == "linear"
     r = checker.Linearizable({"model": model.CASRegister(0)}).check(None, d["history"], {})
     assert r["valid?"] is True and r["analyzer"] == "wgl"
+
+
+@pytest.mark.parametrize("seed,init,kw", [
+    (51, None, dict(n_keys=200, ops_per_key=200, p_invalid=0.3, p_info=0.05)),
+    (52, 0, dict(n_keys=120, ops_per_key=300, threads_per_key=12, readers=6, p_invalid=0.3, p_info=0.02)),
+])
+def test_frontier_configs(ctx, seed, init, kw):
+    """knossos' :configs of an invalid key (checker.clj:146-158, row f1):
+    jh_lin_configs returns the configurations of the last layer the analysis
+    reaches, in the canonical order, the first 10 -- register value,
+    linearized and pending window ops -- equal to the oracle's restatement
+    key by key; valid keys have none."""
+    cols, _ = synth.cas_register(seed=seed, init_nil=init is None, **kw)
+    iv = A.NIL if init is None else init
+    c, _ = oracle.check_cas_independent(cols, init=iv, threads=16)
+    bad = np.nonzero(c["valid"] == A.INVALID)[0]
+    good = np.nonzero(c["valid"] == A.VALID)[0][:5]
+    assert len(bad) >= 3
+    keys = np.concatenate([bad, good])
+    g = ctx.lin_configs(cols, keys, init=init)
+    o = oracle.lin_configs(cols, keys, init=iv)
+    assert g == o
+    assert sum(1 for k in bad if g[int(k)]) >= 3
+    assert all(g[int(k)] is None for k in good)
+
+
+def test_frontier_configs_host_map(ctx):
+    """checker.Linearizable on the reference's perf_test history with a nil
+    initial value (invalid: the first read of 0 cannot be linearized) carries
+    :configs and :final-paths, at most 10 of each, every pending op a map of
+    the history."""
+    from jepsen_amd import checker, model
+    d = json.load(open(os.path.join(GOLD, "perf_test.json")))
+    r = checker.Linearizable({"model": model.CASRegister(None)}).check(None, d["history"], {})
+    assert r["valid?"] is False and 0 < len(r["configs"]) <= 10 and len(r["final-paths"]) == len(r["configs"])
+    for cfg in r["configs"]:
+        assert all(op["type"] == "invoke" for op in cfg["pending"] + cfg["linearized"])

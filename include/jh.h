@@ -94,6 +94,7 @@ extern "C" {
 #define JH_CAUSE_NIL_VALUE    6  /* nil where the checker does arithmetic     */
 #define JH_CAUSE_OVERFLOW     7  /* long overflow (Clojure + throws)          */
 #define JH_CAUSE_STATES       8  /* more than 65532 distinct values in one key */
+#define JH_CAUSE_DEFERRED     9  /* JH_LIN_PHASE1_ONLY: past the quick budget, not searched further */
 
 #define JH_MAX_WINDOW 256
 
@@ -126,6 +127,12 @@ typedef struct jh_history {
 #define JH_LIN_INTERN_PER_KEY  4    /* intern values per key even when one global range fits */
 #define JH_LIN_NO_HELPERS      8    /* no late helper workgroups in phase 2 */
 #define JH_LIN_HELPERS_NOW    16    /* late helpers take a key at once (helper_late_us = 0) */
+/* Two-stage checking for rebalancing heavy keys across devices (jh_multi,
+ * jepsen_amd/shard.py): stage 1 settles every key it can under the quick
+ * budget and returns the others as JH_UNKNOWN / JH_CAUSE_DEFERRED; stage 2
+ * sends every key that needs a search straight to the heavy-key engines. */
+#define JH_LIN_PHASE1_ONLY    32
+#define JH_LIN_SKIP_PHASE1    64
 
 typedef struct jh_lin_opts {
     int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */

@@ -27,6 +27,7 @@ CAUSES = {
     6: "nil-value",
     7: "overflow",
     8: "states",
+    9: "deferred",
 }
 
 MAX_WINDOW = 256
@@ -56,6 +57,8 @@ ALGO_COMPETITION, ALGO_WGL, ALGO_LINEAR = 0, 1, 2
 ALGORITHMS = {"competition": ALGO_COMPETITION, "wgl": ALGO_WGL, "linear": ALGO_LINEAR}
 # jh_lin_opts.flags (test hooks)
 LIN_BFS_ONLY, LIN_GEN_JUMP, LIN_INTERN_PER_KEY, LIN_NO_HELPERS, LIN_HELPERS_NOW = 1, 2, 4, 8, 16
+LIN_PHASE1_ONLY, LIN_SKIP_PHASE1 = 32, 64
+CAUSE_DEFERRED = 9
 
 
 class JhLinOpts(C.Structure):

@@ -4480,6 +4480,16 @@ static inline int64_t q64(const int32_t *qh, int i) {
     return (int64_t)(((uint64_t)(uint32_t)qh[i + 1] << 32) | (uint32_t)qh[i]);
 }
 
+__global__ void k_mark_deferred(const int32_t *__restrict__ defer, int n, jh_key_verdict *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        jh_key_verdict v;
+        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_DEFERRED; v.fail_entry = -1; v.explored = 0;
+        v.previous_ok = -1; v.last_op = -1; v.analyzer = JH_ANALYZER_WGL; v.reserved = 0;
+        out[defer[i]] = v;
+    }
+}
+
 // jh_lin_configs: the requested keys are the whole heavy list, all LEAN
 __global__ void k_req_lists(const int64_t *__restrict__ keys, int n, int64_t K, int32_t *defer, int32_t *defer_l,
                             int32_t *q) {
@@ -4684,8 +4694,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipMemsetAsync(a.defer_time, 0, sizeof(unsigned long long) * (K + 2), st));
         HIP_TRY(hipMemsetAsync(a.defer_time, 0xFF, sizeof(unsigned long long), st));
     }
+    const bool skip_p1 = (lflags & JH_LIN_SKIP_PHASE1) != 0 && !linear_mode;
+    const bool p1_only = (lflags & JH_LIN_PHASE1_ONLY) != 0 && !linear_mode && !skip_p1;
     HIP_TRY(hipEventRecord(ctx->ev[1], st));
-    if (!linear_mode) {
+    if (!linear_mode && !skip_p1) {
         k_lin_dfs<true><<<waves1, 64, MemoQ::LDS, st>>>(a);
         HIP_TRY(hipGetLastError());
         DfsArgs aw = a;
@@ -4695,6 +4707,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     } else if (cfgreq) {
         k_req_lists<<<1, 1, 0, st>>>(cfgreq->keys_dev, cfgreq->n_q, K, defer, defer_l, q);
     } else {
+        // :linear, or stage 2 of a two-stage check: every key that needs a
+        // search is a heavy key
         k_linear_lists<<<1, 1024, 0, st>>>(list, q + 12, list_w, q + 13, defer, defer_l, defer_w, q);
     }
     HIP_TRY(hipGetLastError());
@@ -4705,7 +4719,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const int n_defer = qh[1], n_def_l = qh[Q_DEFER_L], n_def_w = qh[Q_DEFER_W];
     const int n_x = cfgreq ? 0 : qh[19];
     if (n_def_l + n_def_w != n_defer) throw_jh(JH_EDEVICE, "deferred-key lists disagree");
-    if (n_defer > 0 && !linear_mode) {
+    if (n_defer > 0 && !linear_mode && !skip_p1 && !p1_only) {
         // heavy keys, least advanced first (the likely longest searches start
         // first), sorted on the device: no host round trip between the phases
         SortLists sl{};
@@ -4907,7 +4921,14 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     // JH_WG=2: the workgroup engine races the BFS in place of the sequential search
     const bool wg_race = wg_env && atoi(wg_env) == 2;
     int wg2 = 0, n_help = 0;
-    if (n_defer > 0 && use_wg) {
+    if (n_defer > 0 && p1_only) {
+        // stage 1 of a two-stage check: the deferred keys come back unsearched
+        k_mark_deferred<<<grid_for(n_defer, 256), 256, 0, st>>>(defer, n_defer, out_dev);
+        HIP_TRY(hipEventRecord(ctx->ev[6], st));
+        HIP_TRY(hipEventRecord(ctx->ev[5], st));
+        HIP_TRY(hipEventRecord(ctx->ev[10], st));
+        HIP_TRY(hipEventRecord(ctx->ev[7], st));
+    } else if (n_defer > 0 && use_wg) {
         // Deferred LEAN keys on k_lin_wg (one workgroup per key, stream st),
         // WIDE keys on their own pipeline (aux4)
         HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));

@@ -12,6 +12,7 @@
 #include "jh_internal.h"
 #include <algorithm>
 #include <queue>
+#include <mutex>
 #include <thread>
 
 namespace {
@@ -218,6 +219,36 @@ int jh_n_devices(const jh_ctx *ctx) {
 
 }  // extern "C"
 
+// Two stages (round 3; VERDICT r2: the window-sum cost model cannot see which
+// keys are heavy, Spearman 0.04 against WGL's insert count):
+//  1. the keys are split by that model (LPT) and every device runs phase 1 on
+//     its part (JH_LIN_PHASE1_ONLY): most keys settle under the quick budget,
+//     the rest come back deferred;
+//  2. the deferred keys of every device are pooled, heaviest estimate first,
+//     and the member threads pull batches from the pool (guided
+//     self-scheduling: a batch is the pool's remainder over twice the device
+//     count, at least one key) and check each batch's sub-history with every
+//     key going straight to the heavy-key engines (JH_LIN_SKIP_PHASE1). A
+//     device that drew light keys comes back for more, as bounded-pmap's
+//     workers do (independent.clj:266-288).
+// The verdicts are the single-device ones key by key (the engines are exact);
+// the summary is recomputed from them.
+namespace {
+struct MultiStats {
+    std::vector<double> ms;            // per device: device time, stage 1 + stage 2
+    std::vector<int64_t> keys2;        // per device: deferred keys checked in stage 2
+};
+
+jh_history sub_view(const SubHist &S) {
+    jh_history sh{};
+    sh.n = (int64_t)S.row.size();
+    sh.process = S.process.data(); sh.type = S.type.data(); sh.f = S.f.data();
+    sh.key = S.key.data(); sh.value = S.value.data(); sh.value2 = S.value2.data();
+    sh.n_keys = (int64_t)S.keys.size();
+    return sh;
+}
+}  // namespace
+
 int multi_check_cas_independent(jh_ctx *g, const jh_history *h, const jh_lin_opts *opts,
                                 jh_key_verdict *out, jh_summary *sum, char *err, size_t errlen) {
     const int n = (int)g->members.size();
@@ -225,7 +256,7 @@ int multi_check_cas_independent(jh_ctx *g, const jh_history *h, const jh_lin_opt
         snprintf(err, errlen, "a multi-device context takes host columns (on_device=0)");
         return JH_EUNSUPPORTED;
     }
-    const int64_t K = h->n_keys;
+    const int64_t K = h->n_keys, N = h->n;
     std::vector<int64_t> cost(K);
     std::vector<SubHist> sub(n);
     try {
@@ -237,52 +268,137 @@ int multi_check_cas_independent(jh_ctx *g, const jh_history *h, const jh_lin_opt
     }
     jh_lin_opts o = opts ? *opts : jh_lin_opts{JH_NIL, 0, 0};
     o.stream = 0;                                   // each device runs on its own ctx stream
+    const bool two_stage = o.algorithm != JH_ALGO_LINEAR && !(o.flags & (JH_LIN_PHASE1_ONLY | JH_LIN_SKIP_PHASE1));
+    jh_lin_opts o1 = o;
+    if (two_stage) o1.flags |= JH_LIN_PHASE1_ONLY;
     std::vector<std::vector<jh_key_verdict>> v(n);
     std::vector<jh_summary> s(n);
     std::vector<int> rc(n, JH_OK);
     std::vector<std::string> msg(n);
-    std::vector<std::thread> th;
-    for (int d = 0; d < n; ++d)
-        th.emplace_back([&, d] {
-            SubHist &S = sub[d];
-            jh_history sh{};
-            sh.n = (int64_t)S.row.size();
-            sh.process = S.process.data(); sh.type = S.type.data(); sh.f = S.f.data();
-            sh.key = S.key.data(); sh.value = S.value.data(); sh.value2 = S.value2.data();
-            sh.n_keys = (int64_t)S.keys.size();
-            v[d].resize(std::max<int64_t>(1, sh.n_keys));
-            char e[512];
-            rc[d] = jh_check_cas_independent(g->members[d], &sh, &o, v[d].data(), &s[d], e, sizeof e);
-            msg[d] = e;
-        });
-    for (auto &x : th) x.join();
+    MultiStats st{std::vector<double>(n, 0.0), std::vector<int64_t>(n, 0)};
+    {
+        std::vector<std::thread> th;
+        for (int d = 0; d < n; ++d)
+            th.emplace_back([&, d] {
+                jh_history sh = sub_view(sub[d]);
+                v[d].resize(std::max<int64_t>(1, sh.n_keys));
+                char e[512];
+                rc[d] = jh_check_cas_independent(g->members[d], &sh, &o1, v[d].data(), &s[d], e, sizeof e);
+                msg[d] = e;
+                st.ms[d] += s[d].device_ms;
+            });
+        for (auto &x : th) x.join();
+    }
     for (int d = 0; d < n; ++d)
         if (rc[d] != JH_OK) {
             snprintf(err, errlen, "device %d: %s", d, msg[d].c_str());
             return rc[d];
         }
-    jh_summary m{};
-    m.first_fail_entry = -1;
-    for (int d = 0; d < n; ++d) {
-        const SubHist &S = sub[d];
+    auto place = [&](const SubHist &S, const std::vector<jh_key_verdict> &vv) {
         for (size_t j = 0; j < S.keys.size(); ++j) {
-            jh_key_verdict x = v[d][j];
+            jh_key_verdict x = vv[j];
             if (x.fail_entry >= 0) x.fail_entry = S.row[x.fail_entry];
             if (x.previous_ok >= 0) x.previous_ok = S.row[x.previous_ok];
             if (x.last_op >= 0) x.last_op = S.row[x.last_op];
             out[S.keys[j]] = x;
         }
-        const jh_summary &a = s[d];
-        m.valid = std::max(m.valid, a.valid);
-        m.n_invalid += a.n_invalid; m.n_unknown += a.n_unknown; m.n_keys += a.n_keys;
-        m.explored += a.explored; m.memo_probes += a.memo_probes;
-        m.n_deferred += a.n_deferred; m.deferred_entries += a.deferred_entries; m.seq_probes += a.seq_probes;
-        if (a.first_fail_entry >= 0) {
-            const int64_t r = S.row[a.first_fail_entry];
-            if (m.first_fail_entry < 0 || r < m.first_fail_entry) m.first_fail_entry = r;
+    };
+    for (int d = 0; d < n; ++d) place(sub[d], v[d]);
+
+    // ---- stage 2: the pooled deferred keys ----
+    std::vector<int64_t> pool;
+    if (two_stage)
+        for (int64_t k = 0; k < K; ++k)
+            if (out[k].valid == JH_UNKNOWN && out[k].cause == JH_CAUSE_DEFERRED) pool.push_back(k);
+    if (!pool.empty()) {
+        std::stable_sort(pool.begin(), pool.end(), [&](int64_t a, int64_t b) { return cost[a] > cost[b]; });
+        // rows of the pooled keys (and the un-keyed rows every key's subhistory keeps)
+        std::vector<int32_t> slot(K, -1);
+        for (size_t i = 0; i < pool.size(); ++i) slot[pool[i]] = (int32_t)i;
+        std::vector<std::vector<int64_t>> rows(pool.size());
+        std::vector<int64_t> unkeyed;
+        for (int64_t i = 0; i < N; ++i) {
+            const int64_t k = h->key ? h->key[i] : -1;
+            if (k < 0 || k >= K) unkeyed.push_back(i);
+            else if (slot[k] >= 0) rows[slot[k]].push_back(i);
         }
-        // devices run concurrently: the call's device times are the slowest device's
-        m.device_ms = std::max(m.device_ms, a.device_ms);
+        std::mutex mu;
+        size_t next = 0;
+        std::vector<std::thread> th;
+        for (int d = 0; d < n; ++d)
+            th.emplace_back([&, d] {
+                jh_lin_opts o2 = o;
+                o2.flags |= JH_LIN_SKIP_PHASE1;
+                for (;;) {
+                    size_t a, b;
+                    {
+                        std::lock_guard<std::mutex> lk(mu);
+                        if (next >= pool.size() || rc[d] != JH_OK) return;
+                        const size_t rest = pool.size() - next;
+                        const size_t take = std::max<size_t>(1, rest / (2 * (size_t)n));
+                        a = next; b = next + take; next = b;
+                    }
+                    SubHist S;
+                    std::vector<int64_t> rr(unkeyed);
+                    std::vector<int64_t> local_of_row;
+                    for (size_t i = a; i < b; ++i) {
+                        S.keys.push_back(pool[i]);
+                        rr.insert(rr.end(), rows[i].begin(), rows[i].end());
+                    }
+                    std::sort(rr.begin(), rr.end());
+                    for (int64_t r : rr) {
+                        const int64_t k = h->key ? h->key[r] : -1;
+                        int64_t lk = -1;
+                        if (k >= 0 && k < K && slot[k] >= 0) lk = (int64_t)slot[k] - (int64_t)a;
+                        S.process.push_back(h->process[r]); S.type.push_back(h->type[r]); S.f.push_back(h->f[r]);
+                        S.key.push_back(lk); S.value.push_back(h->value[r]); S.value2.push_back(h->value2[r]);
+                        S.row.push_back(r);
+                    }
+                    jh_history sh = sub_view(S);
+                    std::vector<jh_key_verdict> vv(std::max<int64_t>(1, sh.n_keys));
+                    jh_summary ss;
+                    char e[512];
+                    const int r = jh_check_cas_independent(g->members[d], &sh, &o2, vv.data(), &ss, e, sizeof e);
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (r != JH_OK) { rc[d] = r; msg[d] = e; return; }
+                    place(S, vv);
+                    st.ms[d] += ss.device_ms;
+                    st.keys2[d] += (int64_t)(b - a);
+                    s[d].seq_probes += ss.seq_probes; s[d].p3_probes += ss.p3_probes;
+                    s[d].wide_probes += ss.wide_probes; s[d].helper_probes += ss.helper_probes;
+                    s[d].seq_ms += ss.seq_ms; s[d].bfs_ms += ss.bfs_ms; s[d].wide_ms += ss.wide_ms;
+                    s[d].p3_ms += ss.p3_ms; s[d].n_phase3 += ss.n_phase3; s[d].n_phase3_wide += ss.n_phase3_wide;
+                }
+            });
+        for (auto &x : th) x.join();
+        for (int d = 0; d < n; ++d)
+            if (rc[d] != JH_OK) {
+                snprintf(err, errlen, "device %d (stage 2): %s", d, msg[d].c_str());
+                return rc[d];
+            }
+    }
+    // the summary from the merged verdicts (merge-valid, counts, first failing row)
+    jh_summary m{};
+    m.first_fail_entry = -1;
+    for (int64_t k = 0; k < K; ++k) {
+        const jh_key_verdict &x = out[k];
+        if (x.explored < 0) continue;                 // a key in no tuple
+        m.n_keys++;
+        m.explored += x.explored;
+        m.valid = std::max<int64_t>(m.valid, x.valid);
+        if (x.valid == JH_INVALID) {
+            m.n_invalid++;
+            if (x.fail_entry >= 0 && (m.first_fail_entry < 0 || x.fail_entry < m.first_fail_entry))
+                m.first_fail_entry = x.fail_entry;
+        }
+        if (x.valid == JH_UNKNOWN) m.n_unknown++;
+    }
+    for (int d = 0; d < n; ++d) {
+        const jh_summary &a = s[d];
+        m.memo_probes += a.memo_probes;
+        m.n_deferred += a.n_deferred; m.deferred_entries += a.deferred_entries; m.seq_probes += a.seq_probes;
+        // devices run concurrently: the call's device time is the slowest device's
+        m.device_ms = std::max(m.device_ms, st.ms[d]);
         m.dfs_ms = std::max(m.dfs_ms, a.dfs_ms);
         m.seq_ms = std::max(m.seq_ms, a.seq_ms);
         m.bfs_ms = std::max(m.bfs_ms, a.bfs_ms);

@@ -82,13 +82,15 @@ int main(int argc, char **argv) {
         jh_key_verdict *vd = (jh_key_verdict *)calloc((size_t)(h.n_keys > 0 ? h.n_keys : 1), sizeof *vd);
         jh_summary s;
         jh_lin_opts o = {JH_NIL, 0, 0};
+        if (argc > 5) o.quick_budget = atoll(argv[5]);       /* a small one: many keys reach stage 2 */
         rc = jh_check_cas_independent(ctx, &v, &o, vd, &s, err, sizeof err);
         if (rc) { fprintf(stderr, "check: %d %s\n", rc, err); jh_close(ctx); return rc; }
         fwrite(vd, sizeof *vd, (size_t)h.n_keys, out);
         fclose(out);
-        printf("valid=%lld n_invalid=%lld n_unknown=%lld first_fail_entry=%lld n_keys=%lld explored=%lld\n",
+        printf("valid=%lld n_invalid=%lld n_unknown=%lld first_fail_entry=%lld n_keys=%lld explored=%lld n_deferred=%lld\n",
                (long long)s.valid, (long long)s.n_invalid, (long long)s.n_unknown,
-               (long long)s.first_fail_entry, (long long)s.n_keys, (long long)s.explored);
+               (long long)s.first_fail_entry, (long long)s.n_keys, (long long)s.explored,
+               (long long)s.n_deferred);
         jh_close(ctx);
         return 0;
     }

@@ -98,11 +98,13 @@ def test_key_costs_edges(built, tmp_path):
     assert (np.fromfile(tmp_path / "c.bin", np.int64) == 0).all()
 
 
-def _check_vs_oracle(tmp_path, cols, devs=None):
+def _check_vs_oracle(tmp_path, cols, devs=None, quick=None):
     from jepsen_amd import _abi as A
     from oracle import oracle
     _write(cols, tmp_path / "h.bin")
     args = ["check", str(tmp_path / "h.bin"), str(tmp_path / "v.bin")] + ([devs] if devs else [])
+    if quick:
+        args.append(str(quick))
     out = _run(*args)
     got = np.fromfile(tmp_path / "v.bin", dtype=A.VERDICT_DTYPE)
     ov, os_ = oracle.check_cas_independent(cols, threads=8)
@@ -127,3 +129,17 @@ def test_check_single_device(built, tmp_path):
 def test_check_multi_context(built, tmp_path, devs):
     out = _check_vs_oracle(tmp_path, _hist(300, 12), devs)
     assert out.startswith(f"devices={len(devs.split(','))}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devs", ["0,0", "0,0,0,0"])
+def test_multi_context_pooled_heavy_keys(built, tmp_path, devs):
+    """jh_open_devices checks in two stages -- phase 1 on
+    each device's cost-model share, then the deferred keys of every device
+    pooled and pulled by the member threads in batches (guided
+    self-scheduling). With a small quick budget most keys take the second
+    stage; every verdict field still equals the oracle's."""
+    cols = _hist(400, 17)
+    out = _check_vs_oracle(tmp_path, cols, devs, quick=40)
+    summ = dict(kv.split("=") for kv in out.split("\n")[1].split())
+    assert int(summ["n_deferred"]) > 50

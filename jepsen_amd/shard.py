@@ -95,3 +95,82 @@ def check_cas_independent_sharded(cols, rank, world, check_fn, device=None, init
         v[f][hit] = rows[v[f][hit]]
     mx, sm = summary_vector(s, rows)
     return mine, v, all_reduce_summary(mx, sm, device)
+
+
+_POOL_CALLS = [0]
+
+
+def check_cas_independent_two_stage(cols, rank, world, check_fn, device=None, init=None, budget=None):
+    """The key split of check_cas_independent_sharded, then the heavy keys
+    rebalanced at run time (the window-sum model cannot
+    tell which keys are heavy):
+
+      1. this rank checks its cost-model share with check_fn(sub, init,
+         budget, stage=1) -- libjh's JH_LIN_PHASE1_ONLY: keys past the quick
+         budget come back :unknown with cause "deferred";
+      2. every rank's deferred keys are gathered (all_gather_object) into one
+         pool, heaviest estimate first, and the ranks pull batches from it
+         through an atomic counter in the rendezvous store (guided
+         self-scheduling: a batch is the remainder over twice the world size),
+         checking each batch's keys from the global history with
+         check_fn(sub, init, budget, stage=2) -- JH_LIN_SKIP_PHASE1.
+
+    Every rank holds the global history (the C4 workload generates it on
+    every rank), so moving a key is free. Returns (global key ids this rank
+    decided, their verdicts, the all-reduced summary dict, stats)."""
+    import torch.distributed as dist
+    costs = key_costs(cols)
+    owner = assign_keys(costs, world)
+    sub, mine, rows = shard_history(cols, owner, rank)
+    v1, _ = check_fn(sub, init, budget, stage=1)
+    v1 = v1.copy()
+    for f in ("fail_entry", "previous_ok", "last_op"):
+        hit = v1[f] >= 0
+        v1[f][hit] = rows[v1[f][hit]]
+    from . import _abi as A
+    deferred = (v1["valid"] == A.UNKNOWN) & (v1["cause"] == A.CAUSE_DEFERRED)
+    lists = [None] * world
+    if dist.is_initialized() and world > 1:
+        dist.all_gather_object(lists, mine[deferred].tolist())
+    else:
+        lists = [mine[deferred].tolist()]
+    pool = np.array(sorted((k for lst in lists for k in lst), key=lambda k: (-int(costs[k]), k)), np.int64)
+    keys_out = [mine[~deferred]]
+    verd_out = [v1[~deferred]]
+    pulled = 0
+    if len(pool):
+        _POOL_CALLS[0] += 1
+        name = f"jh_pool_{_POOL_CALLS[0]}"
+        store = dist.distributed_c10d._get_default_store() if dist.is_initialized() and world > 1 else None
+        local_next = 0
+        while True:
+            rest = len(pool) - (int(store.add(name, 0)) if store else local_next)
+            take = max(1, rest // (2 * world))
+            end = int(store.add(name, take)) if store else local_next + take
+            local_next = end
+            a = end - take
+            if a >= len(pool):
+                break
+            batch = pool[a:min(end, len(pool))]
+            own = np.full(cols.n_keys, -1, np.int64)
+            own[batch] = 0
+            bsub, bkeys, brows = shard_history(cols, np.where(own == 0, 0, 1), 0)
+            vb, _ = check_fn(bsub, init, budget, stage=2)
+            vb = vb.copy()
+            for f in ("fail_entry", "previous_ok", "last_op"):
+                hit = vb[f] >= 0
+                vb[f][hit] = brows[vb[f][hit]]
+            keys_out.append(bkeys)
+            verd_out.append(vb)
+            pulled += len(batch)
+    keys = np.concatenate(keys_out)
+    verd = np.concatenate(verd_out)
+    # the summary of the keys this rank decided; the union over ranks is every key once
+    real = verd["explored"] >= 0
+    inv = real & (verd["valid"] == A.INVALID)
+    ff = int(verd["fail_entry"][inv].min()) if inv.any() else _FAR
+    mx = [int(verd["valid"][real].max()) if real.any() else 0, -ff]
+    sm = [int(inv.sum()), int((real & (verd["valid"] == A.UNKNOWN)).sum()), int(real.sum()),
+          int(verd["explored"][real].sum())]
+    stats = {"deferred_here": int(deferred.sum()), "pool": int(len(pool)), "pulled": pulled}
+    return keys, verd, all_reduce_summary(mx, sm, device), stats

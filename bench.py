@@ -27,20 +27,56 @@ PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: 8 TB/s HBM3E (spec)
 BYTES_PER_ENTRY = 56           # 7 x int64 columns read once
 BYTES_PER_PROBE = 16           # one memo entry {mask, t|state|gen}
 # HBM bytes per launch of a kernel from the rocprofv3 FETCH_SIZE and
-# WRITE_SIZE passes of the same workload (tools/pmc_traffic.py), one file per
-# (workload, kernel) under profiles/: PMC counters cannot be read inside a
-# timed run, and a file of another workload is never used
-TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r02")
+# WRITE_SIZE passes over the SAME history (tools/gpu_pmc.sh + pmc_traffic.py),
+# one file per (workload, seed, kernel) under profiles/r03/: PMC counters
+# cannot be read inside a timed run, and a file of another history (another
+# workload, seed or rank) is never used. The file also holds the algorithmic
+# bytes of the profiled run itself, so traffic / algorithmic is a same-run ratio.
+TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r03")
 
 
-def pmc_traffic(workload, kernel):
-    path = os.path.join(TRAFFIC_DIR, f"traffic_{workload}_{kernel}.json")
+def traffic_name(workload, seed, kernel):
+    k = "".join(c if c.isalnum() else "_" for c in kernel).strip("_")
+    return f"traffic_{workload}_s{seed}_{k}.json"
+
+
+def pmc_traffic(workload, seed, kernel):
+    path = os.path.join(TRAFFIC_DIR, traffic_name(workload, seed, kernel))
     try:
         with open(path) as fh:
             d = json.load(fh)
-        return float(d["traffic_bytes"]), os.path.relpath(path, ROOT)
+        return d, os.path.relpath(path, ROOT)
     except (OSError, ValueError, KeyError):
         return None, None
+
+
+# the search phases a bench line reports a roofline for: (summary field of
+# the time, of the memo probes, of the entries of the keys searched, kernel)
+PHASES = {
+    "phase1": ("dfs_ms", "memo_probes", None, "k_lin_dfs<true>"),
+    "phase2_lean": ("seq_ms", "seq_probes", "lean_entries", "k_lin_seq3<true>"),
+    "phase3_lean": ("p3_ms", "p3_probes", "lean_entries", "k_lin_seq3<true>"),
+    "wide": ("wide_ms", "wide_probes", "wide_entries", "k_lin_seqw"),
+    "xw": ("xw_ms", "xw_probes", "xw_entries", "k_lin_xw"),
+}
+
+
+def phase_rooflines(sums, n_entries):
+    """Per search phase, from jh_summary's per-phase HIP events and probe
+    counters: algorithmic bytes (56 B per entry of the keys the phase
+    searches + 16 B per HBM memo probe) over the phase's time."""
+    out = {}
+    for name, (tf, pf, ef, kern) in PHASES.items():
+        ms = float(np.mean([x[tf] for x in sums]))
+        if ms <= 0:
+            continue
+        probes = float(np.mean([x[pf] for x in sums]))
+        ent = float(n_entries if ef is None else sums[-1][ef])
+        alg = BYTES_PER_ENTRY * ent + BYTES_PER_PROBE * probes
+        ach = alg / (ms / 1e3) / 1e9
+        out[name] = {"kernel": kern, "ms": ms, "alg_bytes": alg, "probes": probes, "entries": ent,
+                     "achieved": ach, "frac": ach / PEAK_HBM_GBS}
+    return out
 
 
 # SURVEY.md 8(d) configurations. Each rank checks its own shard (weak scaling).
@@ -206,21 +242,16 @@ def main():
         total_entries = n_entries
     value = total_entries * args.steps / elapsed
 
-    # ---- rooflines from live HIP events (jh_summary), per kernel ----------
-    # phase 1 (k_lin_dfs): every key's search under the quick budget; it reads
-    # the whole history (56 B/entry) and probes the HBM memo
+    # ---- rooflines from live HIP events (jh_summary), per search phase -----
+    # each phase's kernel has its own events and probe counter (ABI 4); the
+    # line's roofline is the dominant (longest) phase's
     dfs_avg = float(np.mean(dfs_ms)) / 1e3
-    alg1 = BYTES_PER_ENTRY * n_entries + BYTES_PER_PROBE * float(np.mean(probes))
-    ach1 = alg1 / dfs_avg / 1e9 if dfs_avg > 0 else 0.0
-    # phase 2 (the step's dominant kernel): the sequential search of the keys
-    # phase 1 handed on; its algorithmic bytes are those keys' entries plus its
-    # HBM memo probes. The search is latency-bound (one wave walks one key's DFS)
     seq_avg = float(np.mean(seq_ms)) / 1e3
-    alg2 = BYTES_PER_ENTRY * float(s.deferred_entries) + BYTES_PER_PROBE * float(np.mean(seq_probes))
-    ach2 = alg2 / seq_avg / 1e9 if seq_avg > 0 else 0.0
-    dominant = seq_avg > dfs_avg
-    tr_kernel = "k_lin_seq3" if dominant else "k_lin_dfs"
-    traffic, traffic_src = pmc_traffic(args.workload, tr_kernel) if args.keys is None else (None, None)
+    phases = phase_rooflines(sums, n_entries)
+    dom = max(phases, key=lambda k: phases[k]["ms"]) if phases else None
+    seed_used = wl["seed"] + 7919 * (rank if args.seed_rank is None else args.seed_rank)
+    tr, traffic_src = (pmc_traffic(args.workload, seed_used, phases[dom]["kernel"])
+                       if dom and args.keys is None else (None, None))
 
     # host buffers to host verdicts (H2D copy + check + verdicts D2H), over K
     # calls: the boundary's host-buffer entry point, beside the HBM-resident value
@@ -274,19 +305,18 @@ def main():
             "value_kind": "history resident in HBM, verdicts left in HBM (kernel pipeline only); "
                           "host-to-host rate in e2e_host_buffers",
             "e2e_host_buffers": e2e,
-            "roofline": {"bound": "hbm",
-                         "kernel": ("k_lin_seq3<true> (phase 2: the deferred keys' sequential WGL search, four waves per CU)" if dominant
-                                    else "k_lin_dfs (phase 1: every key, quick budget)"),
-                         "achieved": ach2 if dominant else ach1, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": (ach2 if dominant else ach1) / PEAK_HBM_GBS,
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel_ms": (seq_avg if dominant else dfs_avg) * 1e3,
-                         "alg_bytes": alg2 if dominant else alg1,
-                         "note": "latency-bound tree search: one wave per key, LDS memo; bytes are 56 B per entry "
-                                 "of the keys searched + 16 B per HBM memo probe (SURVEY 8(d))"},
-            "roofline_phase1": {"bound": "hbm", "kernel": "k_lin_dfs", "achieved": ach1, "peak": PEAK_HBM_GBS,
-                                "unit": "GB/s", "frac": ach1 / PEAK_HBM_GBS, "kernel_ms": dfs_avg * 1e3,
-                                "alg_bytes": alg1},
+            "roofline": ({"bound": "hbm", "phase": dom, "kernel": phases[dom]["kernel"],
+                          "achieved": phases[dom]["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                          "frac": phases[dom]["frac"],
+                          # FETCH_SIZE + WRITE_SIZE per launch over this same history (tools/gpu_pmc.sh)
+                          "traffic": tr["traffic_bytes"] if tr else None,
+                          "traffic_over_alg_same_run": tr.get("traffic_over_alg") if tr else None,
+                          "traffic_source": traffic_src,
+                          "kernel_ms": phases[dom]["ms"], "alg_bytes": phases[dom]["alg_bytes"],
+                          "note": "latency-bound tree search: one wave per key, LDS memo; bytes are 56 B per "
+                                  "entry of the keys the phase searches + 16 B per HBM memo probe (SURVEY 8(d))"}
+                         if dom else None),
+            "roofline_phases": phases,
             "cpu_baseline": cpu,
             "cpu_baseline_faithful": cpu_faithful,
             "parity_vs_oracle": parity,

@@ -1,21 +1,29 @@
 """HBM traffic per launch of a kernel from rocprofv3 FETCH_SIZE / WRITE_SIZE
-passes (one counter per pass, MI355X_MICROARCH.md "HBM"), written as the JSON
-that bench.py puts into its roofline object as `traffic`.
+passes (one counter per pass, MI355X_MICROARCH.md "HBM") over one history,
+written as the JSON bench.py puts into its roofline object (`traffic`,
+`traffic_over_alg_same_run`).
 
-    python tools/pmc_traffic.py <pmc-dir> profiles/r02/traffic_<workload>_<kernel>.json <kernel-substring> <workload>
+    python tools/pmc_traffic.py <pmc-dir> <kernel-substring> <workload> <seed>
 
+-> profiles/r03/traffic_<workload>_s<seed>_<kernel>.json (bench.traffic_name).
 Both counters are in KiB. The guide's gfx950 calibration: FETCH_SIZE reports
 1/2 of the bytes of wide (16 B/lane) coalesced streaming reads, WRITE_SIZE is
 exact for 16 B/lane streaming stores; other access widths are uncalibrated.
-The search kernel's reads are 8-16 B scattered loads (tables, memo probes,
-stack refills) and its writes 8 B scattered stores (evictions, stack spills),
-so the raw sum is reported (no x2), with the raw counters beside it.
+The search kernels' reads are 8-16 B scattered loads (tables, memo probes,
+stack refills) and their writes 8-16 B scattered stores (evictions, stack
+spills), so the raw sum is reported (no x2), with the raw counters beside it.
+The algorithmic bytes are the profiled run's own (tools/run_once.py prints its
+jh_summary), so the ratio compares traffic and work of the same run.
 """
 import csv
 import glob
 import json
 import os
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import BYTES_PER_ENTRY, BYTES_PER_PROBE, PHASES, TRAFFIC_DIR, traffic_name  # noqa: E402
 
 
 def per_launch(d, counter, kernel):
@@ -24,38 +32,43 @@ def per_launch(d, counter, kernel):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
                 vals.append(float(r["Counter_Value"]) * 1024.0)
-    return sum(vals) / len(vals) if vals else None, len(vals)
+    return vals
 
 
 def main():
-    src, dst = sys.argv[1], sys.argv[2]
-    kernel = sys.argv[3] if len(sys.argv) > 3 else "k_lin_seq<true>"
-    workload = sys.argv[4] if len(sys.argv) > 4 else "c3"
-    fetch, nf = per_launch(src, "FETCH_SIZE", kernel)
-    write, nw = per_launch(src, "WRITE_SIZE", kernel)
-    if fetch is None or write is None:
+    src, kernel, workload, seed = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    fetch, write = per_launch(src, "FETCH_SIZE", kernel), per_launch(src, "WRITE_SIZE", kernel)
+    if not fetch or not write:
         sys.exit(f"no FETCH_SIZE/WRITE_SIZE rows for {kernel} under {src}")
-    # the profiled run's own work (tools/run_once.py's last line): under --pmc
-    # rocprofv3 serializes dispatches, so the phase-2 race runs differently
-    # from the bench and the traffic is compared with the same run's
-    # algorithmic bytes, not the bench's
     run = {}
-    try:
-        last = [ln for ln in open(os.path.join(src, "fetch.log")) if ln.startswith("keys=")][-1]
-        run = {k: float(v) for k, v in (f.split("=") for f in last.split()) if k}
-    except (OSError, IndexError, ValueError):
-        pass
-    alg = None
-    if "seq_probes" in run and "k_lin_seq" in kernel:
-        alg = 56.0 * run["deferred_entries"] + 16.0 * run["seq_probes"]  # per call (the last of the reps)
-    out = {"kernel": kernel, "fetch_bytes": fetch, "write_bytes": write,
-           "profiled_run": run, "alg_bytes_same_run": alg,
-           "traffic_bytes": fetch + write, "launches": [nf, nw],
-           "correction": "none: scattered 8-16 B accesses are uncalibrated on gfx950 (MI355X_MICROARCH.md HBM)",
-           "workload": f"tools/run_once.py {workload} 2 (the bench.py {workload} rank-0 history)"}
+    for log in ("fetch.log", "write.log"):
+        try:
+            lines = [ln for ln in open(os.path.join(src, log)) if ln.startswith("SUMMARY ")]
+            run[log] = json.loads(lines[-1][8:])
+        except (OSError, IndexError, ValueError):
+            pass
+    # the phase whose kernel this is (bench.PHASES): its entries and probes in each pass's run
+    alg = {}
+    for log, d in run.items():
+        for name, (tf, pf, ef, kern) in PHASES.items():
+            if kern.split("<")[0] in kernel and (("<" not in kernel) or kern in kernel) and d.get(tf, 0) > 0:
+                ent = d["entries"] if ef is None else d[ef]
+                alg[log] = BYTES_PER_ENTRY * ent + BYTES_PER_PROBE * d[pf]
+                break
+    # every launch of the kernel in a pass (reps calls) counts; per launch = mean
+    f1, w1 = sum(fetch) / len(fetch), sum(write) / len(write)
+    a = [alg[k] for k in ("fetch.log", "write.log") if k in alg]
+    alg_run = sum(a) / len(a) if a else None
+    out = {"kernel": kernel, "workload": workload, "seed": seed,
+           "fetch_bytes": f1, "write_bytes": w1, "traffic_bytes": f1 + w1,
+           "launches": [len(fetch), len(write)], "alg_bytes_same_run": alg_run,
+           "traffic_over_alg": (f1 + w1) / alg_run if alg_run else None,
+           "profiled_runs": run,
+           "correction": "none: scattered 8-16 B accesses are uncalibrated on gfx950 (MI355X_MICROARCH.md HBM)"}
+    dst = os.path.join(TRAFFIC_DIR, traffic_name(workload, seed, kernel))
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
-    print(json.dumps(out))
+    print(json.dumps({k: v for k, v in out.items() if k != "profiled_runs"}))
 
 
 if __name__ == "__main__":

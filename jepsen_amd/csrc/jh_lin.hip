@@ -73,11 +73,6 @@ using MemoQ = MemoCfg<JH_MEMOQ_LG, JH_MEMOQ_BLOOM>;
 using MemoH = MemoCfg<12, JH_MEMOH_BLOOM>;   // heavy keys: 128 KB memo + 16 KB Bloom = 152 KB -> 1 wave/CU
                                               // (16 KB Bloom vs 8 KB: -4..7% on the heaviest C3 keys)
 using MemoM = MemoCfg<10, 15>;   // very heavy keys: 32 KB memo + 4 KB Bloom = 37 KB -> 4 waves/CU
-// WIDE deferred keys (dfs_search<.., LEAN=false>): the search keeps every
-// configuration in the wave's HBM table and uses the LDS only for the Bloom
-// filter in front of it, so the memo part is a token 16 slots: 16.5 KB per
-// wave, up to 9 waves per CU
-using MemoX = MemoCfg<2, 17>;
 constexpr int STATE_BITS = 20, T_BITS = 20, GEN_BITS = 24;
 constexpr uint32_t STATE_MASK = (1u << STATE_BITS) - 1, T_MASK = (1u << T_BITS) - 1;
 
@@ -1593,6 +1588,368 @@ done:
     return verdict;
 }
 
+// ---------------------------------------------------------------------------
+// WIDE keys (windows of 41-64 members, or >= 256 states) with an LDS memo:
+// dfs_lean's search with 16-byte LDS entries {mask:64, 1|t:15|state:16}.
+// Round 2 searched these keys with every configuration in the HBM table
+// behind a Bloom filter (dfs_search), one HBM round trip per step once the
+// filter saturates (C5's deep searches); the layered LDS memo keeps the
+// layers near the current one on chip exactly as for LEAN keys (theta: below
+// it, entries may sit in HBM; at or above it, the LDS is exact), so most
+// steps of a deep search probe LDS only.
+__device__ __forceinline__ uint32_t w_t(uint64_t y) { return (uint32_t)(y >> 16) & 0x7FFF; }
+__device__ __forceinline__ uint32_t w_s(uint64_t y) { return (uint32_t)y & 0xFFFF; }
+__device__ __forceinline__ void w_hash(uint64_t m, uint32_t y, uint32_t &h1, uint32_t &h2) {
+    const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+    h1 = (lo ^ __builtin_rotateleft32(hi, 16) ^ __builtin_rotateleft32(y, 8)) * 0x9E3779B1u;
+    h2 = (lo + __builtin_rotateleft32(hi, 5) + __builtin_rotateleft32(y, 11)) * 0x85EBCA77u;
+}
+
+// dfs_lean's eviction for 16-byte entries (stage: SLOTS x 16 B of global scratch)
+template <class M>
+__device__ __noinline__ uint64_t memo_evict_w(ulonglong2 *lmemo, uint32_t *bcnt, uint32_t *bloom, uint64_t *memo,
+                                              ulonglong2 *stage, uint32_t cap_mask, uint32_t gen, uint32_t t_cur,
+                                              uint32_t theta_old, int lane) {
+    int bins = 0;
+#pragma unroll 1
+    for (int r = 0; r < M::SLOTS / 64; r++) {
+        const ulonglong2 x = lmemo[lane + 64 * r];
+        stage[lane + 64 * r] = x;
+        const uint32_t xt = w_t(x.y);
+        const int d = x.y == 0 ? 99 : (xt >= t_cur ? 0 : (int)min(t_cur - xt, 15u));
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            const int cnt = __popcll(ballot(d == b));
+            if (lane == b) bins += cnt;
+        }
+    }
+    int acc = 0, dstar = -1;
+#pragma unroll 1
+    for (int b = 0; b < 16; b++) {
+        acc += readlane(bins, b);
+        if (acc > M::EVICT / 2) break;
+        dstar = b;
+    }
+    uint32_t th2;
+    if (dstar < 0) th2 = t_cur + 1;
+    else {
+        th2 = t_cur > (uint32_t)dstar ? t_cur - (uint32_t)dstar : 0u;
+        if (dstar == 15) th2 = t_cur - min(t_cur, 15u);
+    }
+    th2 = max(th2, theta_old);
+    wave_sync();
+#pragma unroll 1
+    for (int r = 0; r < M::SLOTS / 64; r++) lmemo[lane + 64 * r] = make_ulonglong2(0, 0);
+    for (int i = lane; i < M::BKT / 4; i += 64) bcnt[i] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    wave_sync();
+    int kept = 0;
+    uint32_t th_min = 0;
+#pragma unroll 1
+    for (int r = 0; r < M::SLOTS / 64; r++) {
+        const ulonglong2 x = stage[lane + 64 * r];
+        if (x.y == 0) continue;
+        const uint32_t xt = w_t(x.y);
+        bool to_hbm = xt < th2;
+        uint32_t h1, h2;
+        w_hash(x.x, (uint32_t)x.y, h1, h2);
+        if (!to_hbm) {
+            const uint32_t b1 = h1 >> (32 - M::LG), b2 = h2 >> (32 - M::LG);
+            bool placed = false;
+            for (int j = 0; j < 2 && !placed; j++) {
+                const uint32_t b = j ? b2 : b1;
+                const uint32_t sh = 8 * (b & 3);
+                const uint32_t old = (atomicAdd(&bcnt[b >> 2], 1u << sh) >> sh) & 0xFF;
+                if (old < 4) { lmemo[4 * b + old] = x; placed = true; }
+                else atomicSub(&bcnt[b >> 2], 1u << sh);
+            }
+            if (placed) kept++;
+            else { to_hbm = true; th_min = max(th_min, xt + 1); }
+        }
+        if (to_hbm) {
+            hbm_insert(memo, cap_mask, gen, xt, w_s(x.y), x.x);
+            bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        kept += __shfl_xor(kept, o);
+        th_min = max(th_min, (uint32_t)__shfl_xor((int)th_min, o));
+    }
+    th2 = max(th2, th_min);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    wave_sync();
+    return ((uint64_t)th2 << 32) | (uint32_t)kept;
+}
+
+// dfs_lean for WIDE keys: the same state machine (expand / insert / pop), the
+// same search order and memo contents (explored counts equal WGL's), 16-byte
+// LDS keys. M::SLOTS 16-byte slots; M::LDS counts them as 8 bytes, so the
+// kernels pass MemoW16<M>::LDS.
+template <class M>
+__device__ __forceinline__ int dfs_lean_w(const DfsArgs &A, const KeyInfo &K, const char *tb, int key, int lane,
+                                          uint64_t *memo, Frame *stack, uint64_t *stage64,
+                                          long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes) {
+    const OpC *ops = (const OpC *)tb;
+    const Lay *lay = (const Lay *)(tb + tblc_ops_bytes(K));
+    const uint32_t n_ok = (uint32_t)K.n_ok;
+    const int n_ops = K.n_ops;
+    const uint32_t cap_mask = A.memo_cap - 1;
+    const uint32_t gen = (A.gen_base + (uint32_t)key + 1) & ((1u << GEN_BITS) - 1);
+    constexpr int OFF_BLOOM = LDS_TBL + M::SLOTS * 16, OFF_CNT = OFF_BLOOM + M::BLOOM / 8;
+    ulonglong2 *lmemo = (ulonglong2 *)(jh_lds + LDS_TBL);
+    uint32_t *bloom = (uint32_t *)(jh_lds + OFF_BLOOM);
+    uint32_t *bcnt = (uint32_t *)(jh_lds + OFF_CNT);
+    uint8_t *bcnt8 = (uint8_t *)bcnt;
+    ulonglong2 *stage = (ulonglong2 *)stage64;
+    for (int i = lane; i < M::SLOTS; i += 64) lmemo[i] = make_ulonglong2(0, 0);
+    for (int i = lane; i < M::BKT / 4; i += 64) bcnt[i] = 0;
+    for (int i = lane; i < M::BLOOM / 32; i += 64) bloom[i] = 0;
+    uint32_t theta = 0;
+    int lcount = 0;
+
+    uint32_t tb0 = 0, drq = 0, dhi = 0;
+    auto load_lay = [&](uint32_t base) {
+        tb0 = base;
+        const uint32_t u = base + (uint32_t)lane;
+        if (u < n_ok) { const Lay e = lay[u]; drq = e.rq; dhi = e.hi; }
+    };
+    auto lay_hi = [&](uint32_t u) -> uint32_t {
+        if (u - tb0 >= 64u) load_lay(u >= 32 ? u - 32 : 0);
+        return (uint32_t)readlane((int)dhi, (int)(u - tb0));
+    };
+    int pb = 0;
+    uint32_t urq = RQ_EMPTY;
+    auto load_up = [&](int base) {
+        pb = base;
+        const int j = base + lane;
+        urq = j < n_ops ? ops[j].rq : RQ_EMPTY;
+    };
+    uint32_t fm_lo = 0, fm_hi = 0, f_ti = 0, f_s = 0, fr_lo = 0, fr_hi = 0;
+
+    load_lay(0);
+    uint32_t t = 0, tmax = 0, depth = 0, ring_lo = 0;
+    uint64_t mask = 0;
+    uint32_t s = (uint32_t)A.init_state;
+    int verdict = -1;
+    uint32_t ins = 0;
+    uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
+    uint32_t chk = min(budget, 1023u);
+    int w = (int)(lay_hi(0) >> 6), P = w;
+    uint32_t r = lay_hi(0) & 63;
+    uint32_t rn = n_ok > 1 ? (lay_hi(1) & 63) : 0;
+    uint32_t wrq = lane < w ? ops[lane].rq : RQ_EMPTY;
+    load_up(P);
+    wave_sync();
+    uint64_t absent = 0, nm_r = 0, km = 0;
+    uint32_t u_r = 0, ky = 0, b1 = 0, b2 = 0, n1 = 0, n2 = 0, h1 = 0, h2 = 0, nvl = 0;
+    auto child_keys = [&]() {
+        u_r = t; nm_r = 0;
+        if ((absent >> r) & 1) {
+            uint64_t nm = drop_bit(mask, r);
+            uint32_t u = t + 1;
+            if (u >= n_ok) nm = 0;
+            else if ((nm >> rn) & 1) {
+                uint32_t ru = rn;
+                for (;;) {
+                    nm = drop_bit(nm, ru);
+                    u++;
+                    if (u >= n_ok) { nm = 0; break; }
+                    ru = lay_hi(u) & 63;
+                    if (!((nm >> ru) & 1)) break;
+                }
+            }
+            u_r = u; nm_r = nm;
+        }
+        nvl = wrq >> 16;
+        const bool is_r = lane == (int)r;
+        km = is_r ? nm_r : (mask | (1ULL << lane));
+        ky = 0x80000000u | ((is_r ? u_r : t) << 16) | nvl;
+        w_hash(km, ky, h1, h2);
+        b1 = h1 >> (32 - M::LG);
+        b2 = h2 >> (32 - M::LG);
+    };
+
+expand:
+    {
+        const uint32_t req = wrq & 0xFFFF;
+        absent = (ballot(req == s) | ballot(req == RQ_ANY)) & ~mask;
+    }
+    if (!absent) goto pop;
+    child_keys();
+    {
+        const bool cl = (absent >> lane) & 1;
+        const uint32_t a1 = cl ? b1 : 0u, a2 = cl ? b2 : 0u;
+        n1 = bcnt8[a1]; n2 = bcnt8[a2];
+        __builtin_amdgcn_sched_barrier(0);
+        const ulonglong2 x0 = lmemo[4 * a1], x1 = lmemo[4 * a1 + 1], x2 = lmemo[4 * a1 + 2], x3 = lmemo[4 * a1 + 3];
+        const ulonglong2 y0 = lmemo[4 * a2], y1 = lmemo[4 * a2 + 1], y2 = lmemo[4 * a2 + 2], y3 = lmemo[4 * a2 + 3];
+        const uint64_t kyy = ky;
+        const bool hit = (x0.x == km && x0.y == kyy) | (x1.x == km && x1.y == kyy) | (x2.x == km && x2.y == kyy) |
+                         (x3.x == km && x3.y == kyy) | (y0.x == km && y0.y == kyy) | (y1.x == km && y1.y == kyy) |
+                         (y2.x == km && y2.y == kyy) | (y3.x == km && y3.y == kyy);
+        absent &= ~ballot(hit);
+        if (t < theta && absent) {
+            uint64_t low = absent;
+            if (u_r >= theta) low &= ~(1ULL << r);
+            const bool maybe = ((low >> lane) & 1) && bloom_test2<M>(bloom, lk_bl(h1), lk_bl(h2));
+            bool found = false;
+            if (maybe) found = (hbm_probe(memo, cap_mask, gen, w_t(ky), w_s(ky), km, my_probes) >> 32) == 0;
+            absent &= ~ballot(found);
+        }
+    }
+    if (!absent) goto pop;
+
+insert:
+    {
+        if (ins >= chk) {
+            if (ins >= budget && !extend_budget(A, budget)) { verdict = JH_UNKNOWN; goto done; }
+            if (A.claim) {
+                int c = 0;
+                if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (readlane(c, 0)) { verdict = JH_CANCELLED; goto done; }
+            }
+            chk = min(budget, ins + 1024);
+        }
+        const int i = __builtin_ctzll(absent);
+        ins++;
+        const uint32_t ns = (uint32_t)readlane((int)nvl, i);
+        const bool to_r = (uint32_t)i == r;
+        const uint32_t nt = to_r ? u_r : t;
+        {
+            const bool pick1 = n1 <= n2;
+            const uint32_t bs = pick1 ? b1 : b2, nsl = pick1 ? n1 : n2;
+            const uint64_t full_m = ballot(nsl >= 4);
+            if (!((full_m >> i) & 1)) {
+                if (lane == i) {
+                    lmemo[4 * bs + nsl] = make_ulonglong2(km, (uint64_t)ky);
+                    bcnt8[bs] = (uint8_t)(nsl + 1);
+                }
+                if (++lcount >= M::EVICT) {
+                    const uint64_t er = memo_evict_w<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
+                    lcount = rfl((int)(uint32_t)er);
+                    theta = rflu((uint32_t)(er >> 32));
+                }
+            } else {
+                const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
+                if (lane == i) {
+                    hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
+                    bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
+                }
+                theta = max(theta, nt + 1);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
+        }
+        if (depth - ring_lo == 64) {
+            const uint32_t kk = ((uint32_t)lane - ring_lo) & 63;
+            if (kk < 32) {
+                Frame fr;
+                fr.mask = ((uint64_t)fm_hi << 32) | fm_lo; fr.t_i = f_ti; fr.s = (int32_t)f_s;
+                fr.rest = ((uint64_t)fr_hi << 32) | fr_lo; fr.pad[0] = fr.pad[1] = 0;
+                stack[ring_lo + kk] = fr;
+            }
+            ring_lo += 32;
+        }
+        {
+            const uint64_t nrest = absent & (absent - 1);
+            const bool me = lane == (int)(depth & 63);
+            fm_lo = me ? (uint32_t)mask : fm_lo;
+            fm_hi = me ? (uint32_t)(mask >> 32) : fm_hi;
+            f_ti = me ? ((t << 6) | (uint32_t)i) : f_ti;
+            f_s = me ? s : f_s;
+            fr_lo = me ? (uint32_t)nrest : fr_lo;
+            fr_hi = me ? (uint32_t)(nrest >> 32) : fr_hi;
+        }
+        depth++;
+        s = ns;
+        if (!to_r) {
+            mask |= 1ULL << i;
+            goto expand;
+        }
+        mask = nm_r;
+        if (nt >= n_ok) { t = nt; tmax = max(tmax, t); verdict = JH_VALID; goto done; }
+        for (uint32_t u = t; u < nt; u++) {
+            const uint32_t ru = u == t ? r : (lay_hi(u) & 63);
+            const uint32_t sh = (uint32_t)wave_shl1((int)wrq);
+            if (lane >= (int)ru) wrq = sh;
+            w--;
+            if (lane == w) wrq = RQ_EMPTY;
+            const int c = (int)(lay_hi(u + 1) >> 6);
+            if (c > 0) {
+                if (P < pb || P + c > pb + 64) load_up(c <= 32 && P >= 32 ? P - 32 : P);
+                for (int kk = 0; kk < c; kk++) {
+                    const uint32_t x = (uint32_t)readlane((int)urq, P - pb + kk);
+                    if (lane == w + kk) wrq = x;
+                }
+                w += c; P += c;
+            }
+        }
+        t = nt;
+        tmax = max(tmax, t);
+        r = lay_hi(t) & 63;
+        rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
+        goto expand;
+    }
+
+pop:
+    if (depth == ring_lo) {
+        if (depth == 0) { verdict = JH_INVALID; goto done; }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t lo = depth >= 32 ? depth - 32 : 0;
+        const uint32_t kk = ((uint32_t)lane - lo) & 63;
+        if (kk < depth - lo) {
+            const Frame fr = stack[lo + kk];
+            fm_lo = (uint32_t)fr.mask; fm_hi = (uint32_t)(fr.mask >> 32); f_ti = fr.t_i; f_s = (uint32_t)fr.s;
+            fr_lo = (uint32_t)fr.rest; fr_hi = (uint32_t)(fr.rest >> 32);
+        }
+        ring_lo = lo;
+    }
+    depth--;
+    {
+        const int ln = (int)(depth & 63);
+        absent = ((uint64_t)(uint32_t)readlane((int)fr_hi, ln) << 32) | (uint32_t)readlane((int)fr_lo, ln);
+        const uint32_t pt = (uint32_t)readlane((int)f_ti, ln) >> 6;
+        mask = ((uint64_t)(uint32_t)readlane((int)fm_hi, ln) << 32) | (uint32_t)readlane((int)fm_lo, ln);
+        s = (uint32_t)readlane((int)f_s, ln);
+        if (pt != t) {
+            for (uint32_t u = t; u > pt; u--) {
+                const int c = (int)(lay_hi(u) >> 6);
+                w -= c; P -= c;
+                if (lane >= w) wrq = RQ_EMPTY;
+                const uint32_t h = lay_hi(u - 1);
+                const int ru = (int)(h & 63);
+                const uint32_t sh = (uint32_t)wave_shr1((int)wrq);
+                if (lane > ru) wrq = sh;
+                const uint32_t x = (uint32_t)readlane((int)drq, (int)(u - 1 - tb0));
+                if (lane == ru) wrq = x;
+                w++;
+            }
+            t = pt;
+            r = lay_hi(t) & 63;
+            rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
+        }
+    }
+    if (!absent) goto pop;
+    child_keys();
+    {
+        const bool cl = (absent >> lane) & 1;
+        const uint32_t a1 = cl ? b1 : 0u, a2 = cl ? b2 : 0u;
+        n1 = bcnt8[a1]; n2 = bcnt8[a2];
+    }
+    goto insert;
+
+done:
+    inserts = ins;
+    tmax_out = tmax;
+    return verdict;
+}
+// LDS bytes of a dfs_lean_w wave: 16-byte slots + Bloom + fill counts
+template <class M>
+constexpr int lds_w() { return LDS_TBL + M::SLOTS * 16 + M::BLOOM / 8 + M::BKT; }
+
 // Per-key search tables, built once per call for every key by one wave per
 // key (pass 1, then pass 2 + layer sweep into a bump-allocated slot of the
 // tables arena). The search kernels then only search: their hot loop does not
@@ -1668,7 +2025,9 @@ __global__ void __launch_bounds__(256) k_key_tables(TblArgs A) {
     }
 }
 
-template <class M, bool LEAN>
+// LEAN: dfs_lean (8-byte LDS keys); else WL: dfs_lean_w (16-byte LDS keys),
+// else dfs_search (every configuration in the HBM table)
+template <class M, bool LEAN, bool WL = false>
 __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     const int lane = threadIdx.x;
     uint64_t *memo = A.memo + (size_t)blockIdx.x * A.memo_cap * 2;
@@ -1702,6 +2061,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
                                __HIP_MEMORY_SCOPE_AGENT);
         int verdict;
         if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
+        else if constexpr (WL) verdict = dfs_lean_w<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         if (A.dbg && lane == 0) { A.dbg[16 * (size_t)blockIdx.x + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * (size_t)blockIdx.x + 3] += 1; }
         if (verdict == JH_CANCELLED) continue;
@@ -1776,8 +2136,12 @@ template <bool LEAN>
 __global__ void __launch_bounds__(64) k_lin_seq3(DfsArgs A) { lin_dfs_waves<MemoM, LEAN>(A); }
 // the deferred WIDE keys (phases 2 and 3): their own list, stream and waves,
 // as many as there are keys (up to 4 per CU, bounded by free HBM), beside the
-// LEAN pipeline instead of behind it
-__global__ void __launch_bounds__(64) k_lin_seqw(DfsArgs A) { lin_dfs_waves<MemoX, false>(A); }
+// LEAN pipeline instead of behind it; 2 048 16-byte LDS memo slots + 4 KB
+// Bloom per wave (37 KB: four waves per CU)
+using MemoWL = MemoCfg<9, 15>;
+constexpr int SEQW_LDS = lds_w<MemoWL>();
+constexpr uint64_t SEQW_SCR = MemoWL::SLOTS * 16;   // per wave: the eviction stage
+__global__ void __launch_bounds__(64) k_lin_seqw(DfsArgs A) { lin_dfs_waves<MemoWL, false, true>(A); }
 
 // Deferred keys, least advanced first (phase 1's progress, ties by key: the
 // likely longest searches start first), then the key ids alone: one workgroup
@@ -4811,7 +5175,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     DfsArgs bw{};
     auto prep_wide = [&]() {
         if (n_def_w == 0) return;
-        const uint64_t per_w = (uint64_t)cap2 * 16 + (uint64_t)stack_cap * sizeof(Frame) + MemoX::SLOTS * 8;
+        const uint64_t per_w = (uint64_t)cap2 * 16 + (uint64_t)stack_cap * sizeof(Frame) + SEQW_SCR;
         int want_w = std::min(n_def_w, 4 * ctx->n_cu);
         if (opts && opts->wide_waves > 0) want_w = std::min(want_w, opts->wide_waves);
         waves_w = fit_units(ctx, want_w, per_w, {WS_MEMO_WIDE, WS_STACK_WIDE, WS_SCRATCH_WIDE});
@@ -4826,8 +5190,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         bw.budget = split3w ? p2 : budget; bw.budget_full = split3w ? budget : 0;
         bw.memo = memow; bw.memo_cap = cap2;
         bw.stack = ctx->ws<Frame>(WS_STACK_WIDE, (size_t)waves_w * stack_cap);
-        bw.scratch = ctx->ws<char>(WS_SCRATCH_WIDE, (size_t)waves_w * MemoX::SLOTS * 8);
-        bw.scratch_bytes = MemoX::SLOTS * 8;
+        bw.scratch = ctx->ws<char>(WS_SCRATCH_WIDE, (size_t)waves_w * SEQW_SCR);
+        bw.scratch_bytes = SEQW_SCR;
         bw.gen_base = ctx->gen_base + (uint32_t)K + 1;
         bw.claim = claim;                    // the BFS may settle a WIDE key with a narrow window
         bw.probes = (unsigned long long *)(q + Q_PROBES_WIDE);
@@ -4837,7 +5201,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         if (waves_w == 0) return;
         HIP_TRY(hipStreamWaitEvent(ctx->aux4, ctx->ev[6], 0));
         HIP_TRY(hipEventRecord(ctx->ev[14], ctx->aux4));
-        k_lin_seqw<<<waves_w, 64, MemoX::LDS, ctx->aux4>>>(bw);
+        k_lin_seqw<<<waves_w, 64, SEQW_LDS, ctx->aux4>>>(bw);
         HIP_TRY(hipGetLastError());
         if (split3w) {
             DfsArgs c3 = bw;
@@ -4845,7 +5209,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             c3.defer_list = nullptr; c3.defer_count = nullptr;
             c3.budget = budget; c3.budget_full = 0;
             c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
-            k_lin_seqw<<<waves_w, 64, MemoX::LDS, ctx->aux4>>>(c3);
+            k_lin_seqw<<<waves_w, 64, SEQW_LDS, ctx->aux4>>>(c3);
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipEventRecord(ctx->ev[15], ctx->aux4));
@@ -5025,7 +5389,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             HIP_TRY(hipGetLastError());
             DfsArgs fw = f;
             fw.queue = q + 7;
-            k_lin_seqw<<<waves2, 64, MemoX::LDS, st>>>(fw);
+            k_lin_seqw<<<waves2, 64, SEQW_LDS, st>>>(fw);
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipEventRecord(ctx->ev[10], st));

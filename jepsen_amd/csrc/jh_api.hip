@@ -86,7 +86,6 @@ int jh_open(int device, jh_ctx **out) {
         HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&c->aux3, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&c->aux4, hipStreamNonBlocking));
         for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -116,7 +115,6 @@ void jh_close(jh_ctx *ctx) {
         if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
         if (ctx->aux2) (void)hipStreamDestroy(ctx->aux2);
         if (ctx->aux3) (void)hipStreamDestroy(ctx->aux3);
-        if (ctx->aux4) (void)hipStreamDestroy(ctx->aux4);
     }
     delete ctx;
 }

@@ -54,7 +54,6 @@ struct jh_ctx {
     hipStream_t aux = nullptr;     // second stream for racing searches (jh_lin.hip)
     hipStream_t aux2 = nullptr;    // third stream: windows wider than 64 (jh_lin.hip)
     hipStream_t aux3 = nullptr;    // fourth stream: phase-2 late helpers (jh_lin.hip)
-    hipStream_t aux4 = nullptr;    // fifth stream: the deferred WIDE keys (jh_lin.hip)
     std::mutex mu;
     std::vector<Buf> bufs;
     hipEvent_t ev[24] = {};

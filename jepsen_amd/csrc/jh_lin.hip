@@ -323,6 +323,12 @@ struct DfsArgs {
     // (n_max 0: no upper bound): phase 3 picks one of two launched kernels
     int32_t n_min, n_max;
     int32_t cause_or;           // :linear mode: CAUSE_BY_WGL on the verdicts (k_frontier)
+    // k_lin_seq_lw runs two roles in one grid: this role's waves are blocks
+    // wave_off.. (their per-wave tables are indexed from 0)
+    int32_t wave_off;
+    // [0] first wave start, [1] last wave end (s_memrealtime, 100 MHz): the
+    // role's time when it shares a launch with another role (or null)
+    unsigned long long *t_span;
 };
 constexpr unsigned long long SEQ_HANDED = ~0ULL;
 // verdict cause bits naming the engine in :linear mode (k_frontier turns them into jh_key_verdict.analyzer)
@@ -2030,13 +2036,15 @@ __global__ void __launch_bounds__(256) k_key_tables(TblArgs A) {
 template <class M, bool LEAN, bool WL = false>
 __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     const int lane = threadIdx.x;
-    uint64_t *memo = A.memo + (size_t)blockIdx.x * A.memo_cap * 2;
-    Frame *stack = A.stack + (size_t)blockIdx.x * A.stack_cap;
-    uint64_t *stage = (uint64_t *)(A.scratch + (size_t)blockIdx.x * A.scratch_bytes);
+    const size_t wv = (size_t)(blockIdx.x - A.wave_off);
+    uint64_t *memo = A.memo + wv * A.memo_cap * 2;
+    Frame *stack = A.stack + wv * A.stack_cap;
+    uint64_t *stage = (uint64_t *)(A.scratch + wv * A.scratch_bytes);
     unsigned long long my_probes = 0;
     const int n_list = A.n_list_dev ? *A.n_list_dev : A.n_list;
     if (n_list < A.n_min || (A.n_max > 0 && n_list > A.n_max)) return;
     const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
+    if (A.t_span && lane == 0) atomicMin(&A.t_span[0], __builtin_amdgcn_s_memrealtime());
     if (A.defer_time && lane == 0) atomicMin(&A.defer_time[0], __builtin_amdgcn_s_memrealtime());
     for (;;) {
         int idx = 0;
@@ -2063,7 +2071,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else if constexpr (WL) verdict = dfs_lean_w<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
-        if (A.dbg && lane == 0) { A.dbg[16 * (size_t)blockIdx.x + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * (size_t)blockIdx.x + 3] += 1; }
+        if (A.dbg && lane == 0) { A.dbg[16 * wv + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * wv + 3] += 1; }
         if (verdict == JH_CANCELLED) continue;
         if (verdict == JH_UNKNOWN && A.defer && inserts >= A.budget &&
             (A.budget_full == 0 || inserts < A.budget_full)) {
@@ -2091,9 +2099,10 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         if (verdict == JH_INVALID) v.fail_entry = -(int64_t)tmax - 2;
         if (lane == 0) emit_verdict(A.out, A.claim, key, v);
     }
-    if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 9] = __builtin_amdgcn_s_memtime() - t_begin;
+    if (A.dbg && lane == 0) A.dbg[16 * wv + 9] = __builtin_amdgcn_s_memtime() - t_begin;
+    if (A.t_span && lane == 0) atomicMax(&A.t_span[1], __builtin_amdgcn_s_memrealtime());
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
-    if (A.dbg && lane == 0) A.dbg[16 * (size_t)blockIdx.x + 15] = my_probes;
+    if (A.dbg && lane == 0) A.dbg[16 * wv + 15] = my_probes;
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
     if (lane == 0 && A.exit_count) atomicAdd(A.exit_count, 1);
     if (A.defer_time && lane == 0) atomicMax(&A.defer_time[1], __builtin_amdgcn_s_memrealtime());
@@ -2142,6 +2151,15 @@ using MemoWL = MemoCfg<9, 15>;
 constexpr int SEQW_LDS = lds_w<MemoWL>();
 constexpr uint64_t SEQW_SCR = MemoWL::SLOTS * 16;   // per wave: the eviction stage
 __global__ void __launch_bounds__(64) k_lin_seqw(DfsArgs A) { lin_dfs_waves<MemoWL, false, true>(A); }
+// phase 2 of LEAN and WIDE keys in one grid (blocks 0..n_l-1 LEAN, the rest
+// WIDE; both 37 KB of LDS): one stream for both, so the heavy-key pass needs
+// no more streams than the hardware has queues
+struct DfsPair { DfsArgs l, w; int32_t n_l; };
+constexpr int SEQLW_LDS = MemoM::LDS > SEQW_LDS ? MemoM::LDS : SEQW_LDS;
+__global__ void __launch_bounds__(64) k_lin_seq_lw(DfsPair P) {
+    if ((int)blockIdx.x < P.n_l) lin_dfs_waves<MemoM, true>(P.l);
+    else lin_dfs_waves<MemoWL, false, true>(P.w);
+}
 
 // Deferred keys, least advanced first (phase 1's progress, ties by key: the
 // likely longest searches start first), then the key ids alone: one workgroup
@@ -4840,6 +4858,7 @@ constexpr int Q_WORDS = 64;
 constexpr int Q_ENT_ALL = 24, Q_DEFER_L = 29, Q_DEFER_W = 30, Q_DEFER3W = 31;
 constexpr int Q_PROBES_HELP = 32, Q_PROBES_P3 = 34, Q_PROBES_WIDE = 36;
 constexpr int Q_ENT_LEAN = 40, Q_ENT_WIDE = 42, Q_ENT_XW = 44;
+constexpr int Q_T_WIDE = 46;        // [46..47] first WIDE wave start, [48..49] last end (s_memrealtime)
 static inline int64_t q64(const int32_t *qh, int i) {
     return (int64_t)(((uint64_t)(uint32_t)qh[i + 1] << 32) | (uint32_t)qh[i]);
 }
@@ -5008,6 +5027,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     uint64_t *d64 = ctx->ws<uint64_t>(WS_DEFER64, 3 * (size_t)(K + 1));
     unsigned long long *probes = (unsigned long long *)(q + 4);
     HIP_TRY(hipMemsetAsync(q, 0, Q_WORDS * sizeof(int32_t), st));
+    HIP_TRY(hipMemsetAsync(q + Q_T_WIDE, 0xFF, 2 * sizeof(int32_t), st));
 
     // per-key search tables for every key (<= 8 B per entry + 32 B per key)
     KeyMeta *meta = ctx->ws<KeyMeta>(WS_META, K);
@@ -5196,23 +5216,22 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         bw.claim = claim;                    // the BFS may settle a WIDE key with a narrow window
         bw.probes = (unsigned long long *)(q + Q_PROBES_WIDE);
         bw.seq_start = nullptr; bw.exit_count = nullptr; bw.dbg = nullptr; bw.defer_time = nullptr;
+        bw.t_span = (unsigned long long *)(q + Q_T_WIDE);
     };
-    auto launch_wide = [&]() {
+    // phase 2 of the WIDE keys alone (paths without the two-role grid), then phase 3
+    auto launch_wide = [&](hipStream_t sw, bool p2) {
         if (waves_w == 0) return;
-        HIP_TRY(hipStreamWaitEvent(ctx->aux4, ctx->ev[6], 0));
-        HIP_TRY(hipEventRecord(ctx->ev[14], ctx->aux4));
-        k_lin_seqw<<<waves_w, 64, SEQW_LDS, ctx->aux4>>>(bw);
+        if (p2) k_lin_seqw<<<waves_w, 64, SEQW_LDS, sw>>>(bw);
         HIP_TRY(hipGetLastError());
         if (split3w) {
             DfsArgs c3 = bw;
             c3.list = defer3w; c3.n_list = 0; c3.n_list_dev = q + Q_DEFER3W; c3.queue = q + 20; c3.defer = 0;
             c3.defer_list = nullptr; c3.defer_count = nullptr;
-            c3.budget = budget; c3.budget_full = 0;
+            c3.budget = budget; c3.budget_full = 0; c3.wave_off = 0;
             c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
-            k_lin_seqw<<<waves_w, 64, SEQW_LDS, ctx->aux4>>>(c3);
+            k_lin_seqw<<<waves_w, 64, SEQW_LDS, sw>>>(c3);
             HIP_TRY(hipGetLastError());
         }
-        HIP_TRY(hipEventRecord(ctx->ev[15], ctx->aux4));
     };
 
     unsigned long long *acc_stats = nullptr;
@@ -5294,7 +5313,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipEventRecord(ctx->ev[7], st));
     } else if (n_defer > 0 && use_wg) {
         // Deferred LEAN keys on k_lin_wg (one workgroup per key, stream st),
-        // WIDE keys on their own pipeline (aux4)
+        // WIDE keys on the aux stream
         HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
         WgArgs wa{};
         if (n_def_l > 0) wa = build_wg(ctx->n_cu, nullptr, q);
@@ -5308,8 +5327,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
         HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
         HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
+        launch_wide(ctx->aux, true);
         HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
-        launch_wide();
     } else if (n_defer > 0 && linear_mode) {
         // :algorithm :linear (checker.clj:141-145): the reachable-set search
         // (k_lin_bfs in linear mode) is the analysis for every key it can hold
@@ -5401,7 +5420,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         //    terminal configuration (invalid) within the budget, and valid
         //    keys whose reachable set it can store (WGL's exact count);
         //  - the sequential search with the full budget (aux stream: LEAN
-        //    keys; aux4: WIDE keys) settles every key.
+        //    and WIDE keys in one grid) settles every key.
         claim = ctx->ws<int32_t>(WS_CLAIM, K);
         HIP_TRY(hipMemsetAsync(claim, 0, (size_t)K * sizeof(int32_t), st));
         // q[0] (phase 1's queue) becomes the BFS's; q[3] its give-up count; q[6] phase 2's queue
@@ -5535,18 +5554,25 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // (an allocation after the fork would synchronise the device)
         prep_wide();
         HIP_TRY(hipEventRecord(ctx->ev[6], st));
-        // fork: the BFS on st, the LEAN sequential search on aux, WIDE on aux4, helpers on aux3
+        // fork: the BFS on st, the LEAN and WIDE sequential searches on aux
+        // (one grid), helpers on aux3
         HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
         k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        if (bfs_only || waves2 == 0) {}
-        else if (wg_race) k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux>>>(wr);
-        else if (p2_m) k_lin_seq3<true><<<waves2, 64, MemoM::LDS, ctx->aux>>>(b);
-        else k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
+        bool wide_done = bfs_only;
+        if (bfs_only || (waves2 == 0 && waves_w == 0)) {}
+        else if (wg_race) { if (waves2) k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux>>>(wr); }
+        else if (p2_m) {
+            DfsPair pr;
+            pr.l = b; pr.w = bw; pr.n_l = waves2;
+            pr.w.wave_off = waves2;
+            k_lin_seq_lw<<<waves2 + waves_w, 64, SEQLW_LDS, ctx->aux>>>(pr);
+            wide_done = true;
+        } else if (waves2) k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
-        if (!bfs_only) launch_wide();
+        if (!bfs_only) launch_wide(ctx->aux, !wide_done);
         if (n_help > 0) {
             // every helper leaves once the sequential search has left its
             // queue (or after HELPER_MAX_TICKS): joined before the verdicts are read
@@ -5631,7 +5657,6 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipEventRecord(ctx->ev[7], st));
     }
     if (n_x > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[9], 0));
-    if (waves_w > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[15], 0));
     HIP_TRY(hipEventRecord(ctx->ev[2], st));
     if (defer_times && n_defer > 0) {
         // timeline: when each deferred key was handed on (us after phase 1's
@@ -5729,7 +5754,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             sum->seq_ms = a2;
             if (!use_wg) { HIP_TRY(hipEventElapsedTime(&b2, ctx->ev[6], ctx->ev[5])); sum->bfs_ms = b2; }
             if (split3) { float c2 = 0; HIP_TRY(hipEventElapsedTime(&c2, ctx->ev[10], ctx->ev[7])); sum->p3_ms = c2; }
-            if (waves_w > 0) { float d2 = 0; HIP_TRY(hipEventElapsedTime(&d2, ctx->ev[14], ctx->ev[15])); sum->wide_ms = d2; }
+            // the WIDE waves' own span (they share a grid with the LEAN ones)
+            if (waves_w > 0 && q64(qh, Q_T_WIDE + 2) > q64(qh, Q_T_WIDE)) sum->wide_ms = (q64(qh, Q_T_WIDE + 2) - q64(qh, Q_T_WIDE)) / 1e5;
         }
         if (n_x > 0) { float e2 = 0; HIP_TRY(hipEventElapsedTime(&e2, ctx->ev[8], ctx->ev[9])); sum->xw_ms = e2; }
         sum->p3_probes = q64(qh, Q_PROBES_P3);

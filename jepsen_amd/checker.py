@@ -12,7 +12,7 @@ import numpy as np
 
 from . import _abi as A
 from . import history as H
-from .model import CASRegister, Mutex, Register, UnorderedQueue, to_device_ops
+from .model import CASRegister, Mutex, Register, UnorderedQueue, is_inconsistent, to_device_ops
 
 UNKNOWN = "unknown"
 
@@ -212,25 +212,57 @@ class Linearizable(Checker):
                          r["previous_ok"], r["last_op"], r["analyzer"])
         if r["valid"] == A.INVALID:
             cf = _ctx().lin_configs(cols, [0], init=init, budget=self.budget)
-            add_configs(out, cf[0], cols)
+            add_configs(out, cf[0], cols, self.model)
+            from .report import maybe_render
+            maybe_render(test, opts, cols, out)
         return out
 
 
-def add_configs(result, configs, cols):
+def add_configs(result, configs, cols, model=None):
     """:configs and :final-paths of an invalid result (checker.clj:146-158
     keeps (take 10 ...) of each), from jh_lin_configs: every configuration of
-    the frontier as {:model, :linearized ops, :pending ops}, and as its final
-    path the step that fails -- the result's :op applied to that model. (The
-    knossos maps these restate are not vendored: parity unpinned.)"""
+    the frontier as {:model, :linearized ops, :pending ops}. Its final path is
+    the step no configuration gets past: from the configuration's model, the
+    result's :op, whose step is inconsistent from every frontier model (a
+    model it could step from would have a successor past :op's completion).
+    The knossos maps these restate are not vendored: parity unpinned."""
     if configs is None:
         return result
-    def model(v):
+    def model_map(v):
         return {"value": None if v == A.NIL else int(v)}
-    cf = [{"model": model(v), "linearized": [H.decode_op(cols, x) for x in lin],
+    cf = [{"model": model_map(v), "linearized": [H.decode_op(cols, x) for x in lin],
            "pending": [H.decode_op(cols, x) for x in pend]} for v, lin, pend in configs]
     result["configs"] = cf[:A.CONFIGS_PER_KEY]
-    result["final-paths"] = [[{"op": result.get("op"), "model": c["model"]}] for c in cf][:A.CONFIGS_PER_KEY]
+    op = result.get("op")
+    result["final-paths"] = [[{"op": None, "model": c["model"]},
+                              {"op": op, "model": _final_step(model, c["model"]["value"], op)}]
+                             for c in cf][:A.CONFIGS_PER_KEY]
     return result
+
+
+def _final_step(model, value, op):
+    """knossos.model/step of a frontier model on the failing op, as the
+    {:inconsistent msg} map the path ends in (model.py's messages)."""
+    if op is None:
+        return None
+    v = op.get("value")
+    if hasattr(v, "key") and hasattr(v, "value"):       # an independent tuple
+        op = dict(op, value=v.value)
+    if isinstance(model, Mutex):
+        m = Mutex(bool(value))
+        cas = op.get("value")
+        op = dict(op, f="acquire" if list(cas or []) == [0, 1] else "release")
+    elif isinstance(model, Register):
+        m = Register(value)
+    else:
+        m = CASRegister(value)
+    try:
+        r = m.step(op)
+    except (ValueError, TypeError) as e:
+        return {"error": str(e)}
+    if is_inconsistent(r):
+        return {"inconsistent": r.msg}
+    return {"value": getattr(r, "value", None)}
 
 
 def _algorithm(a):

@@ -136,8 +136,10 @@ class IndependentChecker(Checker):
                 if bad:
                     # the frontier of every invalid key, one device call (jh_lin_configs)
                     cf = _ctx().lin_configs(cols, bad, init=_init_state(lin.model, cols), budget=lin.budget)
+                    from .report import maybe_render
                     for kid in bad:
-                        add_configs(lin_res[cols.keys[kid]], cf[kid], cols)
+                        add_configs(lin_res[cols.keys[kid]], cf[kid], cols, lin.model)
+                        maybe_render(test, {"subdirectory": [DIR, cols.keys[kid]]}, cols, lin_res[cols.keys[kid]])
                 if name is None:
                     return self._results_map(lin_res)
                 results = {}

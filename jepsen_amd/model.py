@@ -24,6 +24,18 @@ def is_inconsistent(m):
     return isinstance(m, Inconsistent)
 
 
+def _s(v):
+    """Clojure's str of a value inside a message: nil prints as nothing,
+    vectors as [a b]."""
+    if v is None:
+        return ""
+    if isinstance(v, (list, tuple)):
+        return "[" + " ".join("nil" if x is None else _s(x) for x in v) + "]"
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    return str(v)
+
+
 @dataclass(frozen=True)
 class CASRegister:
     """knossos.model/->CASRegister (perf_test.clj:134 uses (->CASRegister 0))."""
@@ -37,11 +49,11 @@ class CASRegister:
             cur, new = v
             if cur == self.value:
                 return CASRegister(new)
-            return inconsistent(f"can't CAS {self.value} from {cur} to {new}")
+            return inconsistent(f"can't CAS {_s(self.value)} from {_s(cur)} to {_s(new)}")
         if f == "read":
             if v is None or v == self.value:
                 return self
-            return inconsistent(f"can't read {v} from register {self.value}")
+            return inconsistent(f"can't read {_s(v)} from register {_s(self.value)}")
         raise ValueError(f"No matching clause: {f}")
 
 

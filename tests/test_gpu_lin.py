@@ -421,3 +421,5 @@ def test_frontier_configs_host_map(ctx):
     assert r["valid?"] is False and 0 < len(r["configs"]) <= 10 and len(r["final-paths"]) == len(r["configs"])
     for cfg in r["configs"]:
         assert all(op["type"] == "invoke" for op in cfg["pending"] + cfg["linearized"])
+    for p in r["final-paths"]:
+        assert p[-1]["op"] == r["op"] and p[-1]["model"] == {"inconsistent": "can't read 0 from register "}

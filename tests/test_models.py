@@ -142,3 +142,47 @@ def test_register_and_unknown_ops():
     assert H.is_tuple(t[0]["value"]) and t[0]["value"].key == "k" and t[0]["value"].val == [0, 1]
     assert M.Register(3).step({"f": "read", "value": 3}) == M.Register(3)
     assert M.is_inconsistent(M.Mutex(True).step({"f": "acquire"}))
+
+
+def test_final_paths_end_inconsistent(built):
+    """:final-paths (checker.clj:146-158) built from the frontier's
+    configurations: each path starts at a configuration's model and ends in
+    the failing :op, whose step from that model is inconsistent, with the
+    knossos message text (nil prints as nothing: Clojure's str)."""
+    import json
+    import os
+    from jepsen_amd import checker
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "perf_test.json")))
+    cols = H.encode(d["history"])
+    r = oracle.check_cas_full(cols, init=A.NIL)
+    assert r["valid"] == A.INVALID
+    out = checker.lin_result(r["valid"], r["cause"], r["fail_entry"], r["explored"], cols,
+                             r["previous_ok"], r["last_op"], r["analyzer"])
+    checker.add_configs(out, oracle.lin_configs(cols, [0], init=A.NIL)[0], cols, M.CASRegister(None))
+    assert 0 < len(out["final-paths"]) == len(out["configs"]) <= 10
+    for p in out["final-paths"]:
+        assert p[0]["op"] is None and p[-1]["op"] == out["op"]
+        assert p[-1]["model"] == {"inconsistent": "can't read 0 from register "}
+    assert M.CASRegister(1).step({"f": "cas", "value": [2, None]}).msg == "can't CAS 1 from 2 to "
+
+
+def test_linear_svg_render(built, tmp_path):
+    """checker.clj:146-153: an invalid result is rendered to linear.svg under
+    the store path and (:subdirectory opts); no store dir, no file; a
+    rendering error is logged, not raised."""
+    import json
+    import os
+    from jepsen_amd import checker, report
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "perf_test.json")))
+    cols = H.encode(d["history"])
+    r = oracle.check_cas_full(cols, init=A.NIL)
+    out = checker.lin_result(r["valid"], r["cause"], r["fail_entry"], r["explored"], cols,
+                             r["previous_ok"], r["last_op"], r["analyzer"])
+    checker.add_configs(out, oracle.lin_configs(cols, [0], init=A.NIL)[0], cols, M.CASRegister(None))
+    p = report.maybe_render({"store-dir": str(tmp_path)}, {"subdirectory": ["independent", 7]}, cols, out)
+    assert p == os.path.join(str(tmp_path), "independent", "7", "linear.svg")
+    svg = open(p).read()
+    assert svg.startswith("<svg") and svg.rstrip().endswith("</svg>")
+    assert "can&apos;t read 0 from register" in svg or "can't read 0 from register" in svg
+    assert report.maybe_render({}, {}, cols, out) is None
+    assert report.maybe_render({"store-dir": str(tmp_path)}, {}, cols, {"valid?": False}) is None

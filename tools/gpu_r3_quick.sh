@@ -13,4 +13,5 @@ timeout -k 10 200 python -u bench.py --steps 3 --warmup 1 --no-cpu --e2e 0 --see
 timeout -k 10 200 python -u bench.py --steps 3 --warmup 1 --no-cpu --e2e 0 --seed-rank 6 > $O/bench_c3_rank6.log 2>&1 || exit 1
 JH_LIB=$R/jepsen_amd/variants/libjh_tune.so JH_DEBUG=2 timeout -k 10 200 python -u bench.py --steps 1 --warmup 1 --no-cpu --e2e 0 --no-parity --seed-rank 3 > $O/dbg_rank3.log 2>&1 || exit 1
 JH_LIB=$R/jepsen_amd/variants/libjh_tune.so JH_DEBUG=1 JH_DEFER_TIMES=1 timeout -k 10 200 python -u bench.py --steps 1 --warmup 1 --no-cpu --e2e 0 --no-parity > $O/dbg_rank0.log 2>&1 || exit 1
+JH_LIB=$R/jepsen_amd/variants/libjh_stats.so JH_DEBUG=2 timeout -k 10 200 python -u bench.py --steps 1 --warmup 1 --no-cpu --e2e 0 --no-parity > $O/stats_rank0.log 2>&1 || exit 1
 exit 0

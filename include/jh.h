@@ -133,6 +133,9 @@ typedef struct jh_history {
  * sends every key that needs a search straight to the heavy-key engines. */
 #define JH_LIN_PHASE1_ONLY    32
 #define JH_LIN_SKIP_PHASE1    64
+/* Phase 1 keeps every key it started until the quick budget (no hand-over of
+ * long searches to the heavy-key pass once its queue is empty). */
+#define JH_LIN_NO_HANDOVER   128
 
 typedef struct jh_lin_opts {
     int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */
@@ -150,7 +153,9 @@ typedef struct jh_lin_opts {
     int32_t p2_waves_per_cu;   /* 1: phase 2 at one wave per CU with the 128 KB LDS memo; else 4 */
     int32_t lean_waves;        /* at most this many phase-2 waves for LEAN keys; <=0: no cap */
     int32_t wide_waves;        /* at most this many waves for WIDE keys; <=0: no cap */
-    int64_t reserved;          /* zero */
+    int32_t handover_min;      /* phase 1: once its queue is empty, searches past this many
+                                  inserts go to the heavy-key pass; 0: default (2048), <0: never */
+    int32_t reserved;          /* zero */
 } jh_lin_opts;
 
 #define JH_DEFAULT_BUDGET (1 << 20)

@@ -58,6 +58,7 @@ ALGORITHMS = {"competition": ALGO_COMPETITION, "wgl": ALGO_WGL, "linear": ALGO_L
 # jh_lin_opts.flags (test hooks)
 LIN_BFS_ONLY, LIN_GEN_JUMP, LIN_INTERN_PER_KEY, LIN_NO_HELPERS, LIN_HELPERS_NOW = 1, 2, 4, 8, 16
 LIN_PHASE1_ONLY, LIN_SKIP_PHASE1 = 32, 64
+LIN_NO_HANDOVER = 128
 CAUSE_DEFERRED = 9
 
 
@@ -67,7 +68,8 @@ class JhLinOpts(C.Structure):
                 ("quick_budget", C.c_int64), ("phase2_budget", C.c_int64),
                 ("helpers", C.c_int32), ("helper_late_us", C.c_int32),
                 ("xw_waves", C.c_int32), ("p2_waves_per_cu", C.c_int32),
-                ("lean_waves", C.c_int32), ("wide_waves", C.c_int32), ("reserved", C.c_int64)]
+                ("lean_waves", C.c_int32), ("wide_waves", C.c_int32),
+                ("handover_min", C.c_int32), ("reserved", C.c_int32)]
 
 
 # every field of jh_key_verdict: the parity tests compare all of them

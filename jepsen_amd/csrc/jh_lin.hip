@@ -329,6 +329,11 @@ struct DfsArgs {
     // [0] first wave start, [1] last wave end (s_memrealtime, 100 MHz): the
     // role's time when it shares a launch with another role (or null)
     unsigned long long *t_span;
+    // phase 1: once its queue is empty, a search past handover_min inserts
+    // stops and goes to the heavy-key pass (which restarts it with its own
+    // budget, so verdicts and counts do not change) instead of holding the
+    // phase open while every other wave idles; 0: never
+    int32_t handover_min;
 };
 constexpr unsigned long long SEQ_HANDED = ~0ULL;
 // verdict cause bits naming the engine in :linear mode (k_frontier turns them into jh_key_verdict.analyzer)
@@ -358,8 +363,17 @@ __device__ __forceinline__ bool extend_budget(const DfsArgs &A, uint32_t &budget
     budget = (uint32_t)min<int64_t>(A.budget_full, 0x7FFFFFFF);
     return true;
 }
+// phase 1's hand-over check (every 1 024 inserts): the queue has run dry
+__device__ __forceinline__ bool handover(const DfsArgs &A, uint32_t ins) {
+    if (A.handover_min <= 0 || ins < (uint32_t)A.handover_min) return false;
+    int q = 0;
+    if ((threadIdx.x & 63) == 0) q = __hip_atomic_load(A.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    q = __builtin_amdgcn_readlane(q, 0);
+    return q >= (A.n_list_dev ? *A.n_list_dev : A.n_list);
+}
 constexpr int64_t P2_BUDGET = 1 << 16;  // phase-2 inserts before a key moves to phase 3
 constexpr int64_t QUICK_BUDGET = 8192;  // phase-1 inserts before a key is deferred
+constexpr int32_t HANDOVER_MIN = 2048;  // phase-1 inserts after which a search may be handed over
 // phase-2 late helpers (workgroups, one per CU) and how long a key must have run
 // in the sequential search before one takes it: 32 and 250 us measured against
 // 16 and 2 000 us (C3 rank 0 43.2 -> 40.9 ms, ranks 3 / 6 unchanged; the sweep
@@ -1110,6 +1124,7 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
         PROF_MARK(q2); PROF_ADD(pc_probe, q0, q2);
         if (absent) {
             if (ins >= budget && !extend_budget(A, budget)) { verdict = JH_UNKNOWN; break; }
+            if ((ins & 1023) == 1023 && handover(A, ins)) { ins = budget; verdict = JH_UNKNOWN; break; }
             if (A.claim && (ins & 1023) == 1023) {
                 // racing k_lin_bfs: stop if it settled this key first
                 int c = 0;
@@ -1433,6 +1448,7 @@ insert:
     {
         if (ins >= chk) {
             if (ins >= budget && !extend_budget(A, budget)) { verdict = JH_UNKNOWN; goto done; }
+            if (handover(A, ins)) { ins = budget; verdict = JH_UNKNOWN; goto done; }
             if (A.claim) {
                 // racing k_lin_bfs: stop if it settled this key first
                 int c = 0;
@@ -1811,6 +1827,7 @@ insert:
     {
         if (ins >= chk) {
             if (ins >= budget && !extend_budget(A, budget)) { verdict = JH_UNKNOWN; goto done; }
+            if (handover(A, ins)) { ins = budget; verdict = JH_UNKNOWN; goto done; }
             if (A.claim) {
                 int c = 0;
                 if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -5064,6 +5081,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     a.scratch = scr; a.scratch_bytes = scr_bytes; a.budget = quick; a.defer = quick < budget ? 1 : 0;
     a.init_state = init_state; a.gen_base = ctx->gen_base; a.flags = q + 2; a.probes = probes;
     a.states8 = n_states <= 256 ? 1 : 0;
+    a.handover_min = a.defer && !(lflags & JH_LIN_NO_HANDOVER) ? HANDOVER_MIN : 0;
+    if (a.handover_min && opts && opts->handover_min) a.handover_min = std::max(0, opts->handover_min);
+    if (const char *e = tune_env("JH_HANDOVER_MIN")) a.handover_min = a.defer ? std::max(0, atoi(e)) : 0;
     const char *dbgenv = tune_env("JH_DEBUG");
     const bool dbg2 = dbgenv && atoi(dbgenv) >= 2;
     unsigned long long *dbg = nullptr;
@@ -5203,6 +5223,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         uint64_t *memow = ctx->ws<uint64_t>(WS_MEMO_WIDE, (size_t)waves_w * cap2 * 2, /*zero=*/true);
         if (clear_memo && !freshw) HIP_TRY(hipMemsetAsync(memow, 0, ctx->bufs[WS_MEMO_WIDE].bytes, st));
         bw = a;
+        bw.handover_min = 0;
         bw.list = defer_w; bw.n_list = n_def_w; bw.n_list_dev = nullptr; bw.queue = q + 7;
         bw.defer64 = nullptr; bw.defer_kind = nullptr; bw.defer_kind_count = nullptr;
         split3w = waves_w < n_def_w && budget > p2;
@@ -5264,6 +5285,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         uint64_t *work = ctx->ws<uint64_t>(WS_WG_WORK, (size_t)n_wg * work_cap, /*zero=*/true);
         WgArgs wa{};
         wa.d = a;
+        wa.d.handover_min = 0;
         wa.d.list = defer_l; wa.d.n_list = n_def_l; wa.d.n_list_dev = nullptr; wa.d.queue = wg_queue; wa.d.defer = 0;
         wa.d.defer_list = nullptr; wa.d.defer_count = nullptr;
         wa.d.defer64 = nullptr; wa.d.defer_kind = nullptr; wa.d.defer_kind_count = nullptr;
@@ -5389,6 +5411,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
         if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
         DfsArgs f = a;
+        f.handover_min = 0;
         f.list = c.unres_list; f.n_list = 0; f.n_list_dev = q + 3; f.queue = q + 6; f.defer = 0;
         f.defer_list = nullptr; f.defer_count = nullptr;
         f.defer64 = nullptr; f.defer_kind = nullptr; f.defer_kind_count = nullptr;
@@ -5536,6 +5559,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // phase 2 stops at p2 inserts and phase 3 restarts those keys
         split3 = waves2 < n_def_l && budget > p2;
         DfsArgs b = a;
+        b.handover_min = 0;
         b.list = defer_l; b.n_list = n_def_l; b.n_list_dev = nullptr; b.queue = q + 6; b.defer = split3 ? 1 : 0;
         b.defer_list = defer3; b.defer_count = q + 16;
         b.defer64 = nullptr; b.defer_kind = nullptr; b.defer_kind_count = nullptr;

@@ -123,6 +123,22 @@ def test_phase3_handover(ctx, p2, waves):
     assert s.n_phase3 > 0
 
 
+@pytest.mark.parametrize("handover", [64, 1024, -1])
+def test_phase1_handover(ctx, handover):
+    """Phase 1 hands a search past handover_min inserts to the heavy-key pass
+    once its queue is empty (the pass restarts it with the full budget): the
+    hand-over only moves keys between phases, so verdicts, causes, failing
+    rows and WGL counts equal the oracle's at two budgets, and a lower
+    threshold defers at least as many keys as none (-1)."""
+    cols, _ = synth.cas_register(n_keys=600, ops_per_key=300, p_invalid=0.1, p_info=0.05, seed=97)
+    for budget in (None, 5000):
+        g, s = ctx.check_cas_independent(cols, budget=budget, quick_budget=4000, handover_min=handover)
+        c, _ = oracle.check_cas_independent(cols, budget=budget or A.DEFAULT_BUDGET, threads=8)
+        _same(g, c)
+        _, s0 = ctx.check_cas_independent(cols, budget=budget, quick_budget=4000, flags=A.LIN_NO_HANDOVER)
+        assert s.n_deferred >= s0.n_deferred
+
+
 @pytest.mark.parametrize("waves", [None, 1])
 def test_windows_wider_than_64(ctx, waves):
     """Windows of 65..256 members (k_lin_xw, 4-word masks) and wider than

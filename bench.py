@@ -119,7 +119,12 @@ def parse():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--seed-rank", type=int, default=None,
                     help="generate the history rank R of a multi-GPU run would check (rehearsal on one GPU)")
-    return ap.parse_args()
+    ap.add_argument("--opt", action="append", default=[], metavar="FIELD=INT",
+                    help="a jh_lin_opts tuning field for A/B runs (e.g. handover_min=2048); "
+                         "recorded in config.opts")
+    a = ap.parse_args()
+    a.tune = {k: int(v) for k, v in (o.split("=", 1) for o in a.opt)}
+    return a
 
 
 def main():
@@ -198,7 +203,7 @@ def main():
     red_sum = torch.zeros(4, dtype=torch.int64, device=dev)
 
     def step():
-        s = ctx.check_cas_independent_device(DCols, verd.data_ptr(), budget=budget)
+        s = ctx.check_cas_independent_device(DCols, verd.data_ptr(), budget=budget, **args.tune)
         if dist is not None:
             # RCCL verdict summary all-reduce over xGMI: merge-valid (MAX),
             # failures/unknown/keys counts (SUM), first failing row (MIN as -MAX)
@@ -300,7 +305,7 @@ def main():
                        "deferred_keys": int(s.n_deferred), "deferred_entries": int(s.deferred_entries),
                        "phase1_ms": dfs_avg * 1e3, "phase2_seq_ms": seq_avg * 1e3,
                        "phase2_bfs_ms": float(np.mean(bfs_ms)),
-                       "phases": phase_table(sums)},
+                       "phases": phase_table(sums), "opts": args.tune or None},
             "shard": shard_info,
             "value_kind": "history resident in HBM, verdicts left in HBM (kernel pipeline only); "
                           "host-to-host rate in e2e_host_buffers",

@@ -154,7 +154,7 @@ typedef struct jh_lin_opts {
     int32_t lean_waves;        /* at most this many phase-2 waves for LEAN keys; <=0: no cap */
     int32_t wide_waves;        /* at most this many waves for WIDE keys; <=0: no cap */
     int32_t handover_min;      /* phase 1: once its queue is empty, searches past this many
-                                  inserts go to the heavy-key pass; 0: default (2048), <0: never */
+                                  inserts go to the heavy-key pass; 0: default (off), <0: never */
     int32_t reserved;          /* zero */
 } jh_lin_opts;
 

@@ -373,7 +373,11 @@ __device__ __forceinline__ bool handover(const DfsArgs &A, uint32_t ins) {
 }
 constexpr int64_t P2_BUDGET = 1 << 16;  // phase-2 inserts before a key moves to phase 3
 constexpr int64_t QUICK_BUDGET = 8192;  // phase-1 inserts before a key is deferred
-constexpr int32_t HANDOVER_MIN = 2048;  // phase-1 inserts after which a search may be handed over
+// phase-1 inserts after which a search may be handed over once the queue is
+// empty; 0 = off by default. Round 1 measured it at 1 024 (phase 1 12.4 -> 8.0
+// ms but 3x the keys restart in phase 2: C3 59.5 -> 69.9 ms); re-measured
+// against the round-3 heavy-key pass through jh_lin_opts.handover_min
+constexpr int32_t HANDOVER_MIN = 0;
 // phase-2 late helpers (workgroups, one per CU) and how long a key must have run
 // in the sequential search before one takes it: 32 and 250 us measured against
 // 16 and 2 000 us (C3 rank 0 43.2 -> 40.9 ms, ranks 3 / 6 unchanged; the sweep
@@ -5082,7 +5086,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     a.init_state = init_state; a.gen_base = ctx->gen_base; a.flags = q + 2; a.probes = probes;
     a.states8 = n_states <= 256 ? 1 : 0;
     a.handover_min = a.defer && !(lflags & JH_LIN_NO_HANDOVER) ? HANDOVER_MIN : 0;
-    if (a.handover_min && opts && opts->handover_min) a.handover_min = std::max(0, opts->handover_min);
+    if (a.defer && !(lflags & JH_LIN_NO_HANDOVER) && opts && opts->handover_min)
+        a.handover_min = std::max(0, opts->handover_min);
     if (const char *e = tune_env("JH_HANDOVER_MIN")) a.handover_min = a.defer ? std::max(0, atoi(e)) : 0;
     const char *dbgenv = tune_env("JH_DEBUG");
     const bool dbg2 = dbgenv && atoi(dbgenv) >= 2;

@@ -3990,50 +3990,51 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             if (tid == 0) { sh.mode = 1; sh.ovf = 0; }
             __syncthreads();
         };
-        // a configuration new to the set: count it, store it for the WGL count
-        auto added = [&](uint32_t cs, uint32_t cm) -> bool {
-            const unsigned long long n = atomicAdd(&sh.count, 1ULL);
-            if ((long long)n >= A.reach_cap) atomicOr(&sh.status, 2);
-            const unsigned id = atomicAdd(&sh.nnodes, 1u);
-            if (id < A.ncap) A.nodes[id] = bfs_pack(t, cs, cm); else sh.nostore = 1;
-            return true;
-        };
-        // insert (s, mask) of layer t into the set; true if new (not counted yet)
-        auto insert_raw = [&](uint32_t cs, uint32_t cm) -> bool {
-            if (sh.status & 2) return false;
-            if (sh.mode == 0) {
-                // keep the LDS set under 3/4 load (+ at most one insert per thread in flight)
-                if (sh.lcount >= LSET * 3 / 4) { sh.ovf = 1; return false; }
-                const uint64_t k = (((uint64_t)cs << 32) | cm) + 1;
-                uint32_t h = lset_hash(k);
-                for (;;) {
-                    const unsigned long long prev = atomicCAS((unsigned long long *)&lset[h], 0ULL, k);
-                    if (prev == 0) break;
-                    if (prev == k) return false;
-                    h = (h + 1) & (LSET - 1);
-                }
-                atomicAdd(&sh.lcount, 1u);
-            } else {
-                const uint64_t k = bfs_pack(t, cs, cm);
-                uint32_t h = (uint32_t)jh_mix64(k) & gmask;
-                for (uint32_t probe = 0;; probe++) {
-                    if (probe > gmask) { atomicOr(&sh.status, 2); return false; }
-                    const unsigned long long prev = atomicCAS((unsigned long long *)&gset[h], BFS_EMPTY, k);
-                    if (prev == BFS_EMPTY) break;
-                    if (prev == k) return false;
-                    h = (h + 1) & gmask;
-                }
-            }
-            return true;
-        };
-        auto insert = [&](uint32_t cs, uint32_t cm) -> bool { return insert_raw(cs, cm) && added(cs, cm); };
         // the global set's inserts of up to 8 children, their first probes all
         // in flight together (a lone CAS per child was one HBM round trip each,
         // serial per thread: the forward pass's bound once a layer is global)
         auto insert8 = [&](const uint64_t (&ck)[8], bool (&nw)[8]) {
             if (sh.mode == 0) {
+                // the LDS set: room for the wave's candidates reserved with one
+                // LDS atomic (a per-insert count on one address serialises lane
+                // by lane), the eight CAS issued together, collisions resolved
+                // after, the duplicates' reservation given back
 #pragma unroll
-                for (int q = 0; q < 8; q++) nw[q] = ck[q] ? insert_raw((uint32_t)(ck[q] >> 32), (uint32_t)ck[q]) : false;
+                for (int q = 0; q < 8; q++) nw[q] = false;
+                if (sh.status & 2) return;
+                uint32_t cand = 0;
+#pragma unroll
+                for (int q = 0; q < 8; q++) cand += (uint32_t)__popcll(ballot(ck[q] != 0));
+                if (cand == 0) return;
+                int room = 1;
+                if (lane == 0) {
+                    const uint32_t old = atomicAdd(&sh.lcount, cand);
+                    if (old + cand > (uint32_t)(LSET * 3 / 4)) { atomicSub(&sh.lcount, cand); sh.ovf = 1; room = 0; }
+                }
+                if (!readlane(room, 0)) return;
+                uint64_t k[8];
+                uint32_t h[8];
+                unsigned long long pv[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    k[q] = ck[q] ? ck[q] + 1 : 0;
+                    h[q] = lset_hash(k[q]);
+                    pv[q] = k[q] ? atomicCAS((unsigned long long *)&lset[h[q]], 0ULL, k[q]) : 0ULL;
+                }
+                uint32_t dups = 0;
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    if (!k[q]) continue;
+                    if (pv[q] == 0) { nw[q] = true; continue; }
+                    if (pv[q] == k[q]) { dups++; continue; }
+                    for (uint32_t hh = (h[q] + 1) & (LSET - 1);; hh = (hh + 1) & (LSET - 1)) {
+                        const unsigned long long x = atomicCAS((unsigned long long *)&lset[hh], 0ULL, k[q]);
+                        if (x == 0) { nw[q] = true; break; }
+                        if (x == k[q]) { dups++; break; }
+                    }
+                }
+                for (int o = 32; o > 0; o >>= 1) dups += (uint32_t)__shfl_xor((int)dups, o);
+                if (lane == 0 && dups) atomicSub(&sh.lcount, dups);
                 return;
             }
             uint64_t g[8];
@@ -4104,18 +4105,69 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         for (;;) {
         if (tid == 0) sh.npend2 = 0;
         __syncthreads();
-        for (unsigned i = tid; i < np; i += BFS_THREADS) {
-            const uint64_t e = pcur[i];
-            const uint32_t u = (uint32_t)(e >> 44);
-            if (u == t) {
-                const uint32_t cs = (uint32_t)(e >> 32) & 0xFFF, cm = (uint32_t)e;
-                if (insert(cs, cm)) {
-                    const unsigned pos = atomicAdd(&sh.nfront, 1u);
-                    if (pos < A.q_cap) fcur[pos] = ((uint64_t)cs << 32) | cm; else atomicOr(&sh.status, 2);
+        // per wave: the later layers' entries carried over and the new
+        // configurations counted with one LDS atomic per counter (same-address
+        // atomics serialise lane by lane); LDS-set room reserved per wave
+        for (unsigned i0 = tid - lane; i0 < np; i0 += BFS_THREADS) {
+            const unsigned i = i0 + lane;
+            const uint64_t e = i < np ? pcur[i] : 0;
+            const bool here = i < np && (uint32_t)(e >> 44) == t;
+            const uint64_t lm = ballot(i < np && !here);
+            unsigned pb = 0;
+            if (lane == 0 && lm) pb = atomicAdd(&sh.npend2, (unsigned)__popcll(lm));
+            pb = readlane(pb, 0);
+            if (i < np && !here) pnxt[pb + mbcnt(lm)] = e;
+            const uint64_t hm = ballot(here);
+            if (!hm || (sh.status & 2)) continue;
+            const uint32_t cs = (uint32_t)(e >> 32) & 0xFFF, cm = (uint32_t)e;
+            bool nw = false;
+            if (sh.mode == 0) {
+                int room = 1;
+                if (lane == 0) {
+                    const uint32_t cand = (uint32_t)__popcll(hm);
+                    const uint32_t old = atomicAdd(&sh.lcount, cand);
+                    if (old + cand > (uint32_t)(LSET * 3 / 4)) { atomicSub(&sh.lcount, cand); sh.ovf = 1; room = 0; }
                 }
-            } else {
-                const unsigned pos = atomicAdd(&sh.npend2, 1u);
-                pnxt[pos] = e;
+                if (!readlane(room, 0)) continue;
+                if (here) {
+                    const uint64_t k = (((uint64_t)cs << 32) | cm) + 1;
+                    for (uint32_t h = lset_hash(k);; h = (h + 1) & (LSET - 1)) {
+                        const unsigned long long x = atomicCAS((unsigned long long *)&lset[h], 0ULL, k);
+                        if (x == 0) { nw = true; break; }
+                        if (x == k) break;
+                    }
+                }
+                const uint32_t dups = (uint32_t)__popcll(hm & ~ballot(nw));
+                if (lane == 0 && dups) atomicSub(&sh.lcount, dups);
+            } else if (here) {
+                const uint64_t g = bfs_pack(t, cs, cm);
+                uint32_t h = (uint32_t)jh_mix64(g) & gmask;
+                for (uint32_t probe = 0;; probe++) {
+                    if (probe > gmask) { atomicOr(&sh.status, 2); break; }
+                    const unsigned long long x = atomicCAS((unsigned long long *)&gset[h], BFS_EMPTY, g);
+                    if (x == BFS_EMPTY) { nw = true; break; }
+                    if (x == g) break;
+                    h = (h + 1) & gmask;
+                }
+            }
+            const uint64_t nm = ballot(nw);
+            if (!nm) continue;
+            const uint32_t tot = (uint32_t)__popcll(nm);
+            unsigned nb0 = 0, fb0 = 0;
+            if (lane == 0) {
+                const unsigned long long c0 = atomicAdd(&sh.count, (unsigned long long)tot);
+                if ((long long)(c0 + tot) > A.reach_cap) atomicOr(&sh.status, 2);
+                nb0 = atomicAdd(&sh.nnodes, tot);
+                fb0 = atomicAdd(&sh.nfront, tot);
+            }
+            nb0 = readlane(nb0, 0);
+            fb0 = readlane(fb0, 0);
+            if (nw) {
+                const unsigned below = mbcnt(nm);
+                if (nb0 + below < A.ncap) A.nodes[nb0 + below] = bfs_pack(t, cs, cm);
+                else sh.nostore = 1;
+                if (fb0 + below < A.q_cap) fcur[fb0 + below] = ((uint64_t)cs << 32) | cm;
+                else atomicOr(&sh.status, 2);
             }
         }
         __syncthreads();
@@ -4142,11 +4194,17 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             __syncthreads();
             if (sh.status & 4) break;
             for (;;) {
-            for (unsigned i0 = tid - lane; i0 < nf; i0 += BFS_THREADS) {
-                const unsigned i = i0 + lane;
-                const uint64_t c = i < nf ? fcur[i] : 0xFFFFFFFFull;    // past the end: every member taken
+            // one item per (frontier configuration, 8 members): a round's work
+            // spread over every wave, not one configuration's members in series
+            const unsigned ng = (unsigned)(w + 7) >> 3;
+            const unsigned items = nf * ng;
+            for (unsigned i0 = tid - lane; i0 < items; i0 += BFS_THREADS) {
+                const unsigned it = i0 + lane;
+                const unsigned i = it < items ? it / ng : 0;
+                const uint64_t c = it < items ? fcur[i] : 0xFFFFFFFFull;    // past the end: every member taken
                 const uint32_t s = (uint32_t)(c >> 32), mask = (uint32_t)c;
-                for (int j0 = 0; j0 < w; j0 += 8) {
+                {
+                    const int j0 = it < items ? (int)(it - i * ng) * 8 : 0;
                     uint64_t ck[8];       // same-layer children of members j0..j0+7: s2 << 32 | mask'
 #pragma unroll
                     for (int q = 0; q < 8; q++) {

@@ -141,3 +141,119 @@ def test_wide_windows_agree(built, seed):
             assert r["canonical_explored"] == r["list_explored"], r
             settled += r["canonical"] != A.UNKNOWN
     assert sum(64 < w <= A.MAX_WINDOW for w in widths) >= 8 and settled >= 2
+
+
+def _jit_frontier(cols, key, init):
+    """The frontier of an invalid key from the definition (knossos.linear's
+    just-in-time linearization over op maps, no canonical coordinates): the
+    set of (linearized ops, register value) reachable by linearizing invoked
+    ops; at each :ok completion keep the configurations that linearized it.
+    At the first completion no configuration can linearize, the whole closure
+    is the frontier. Returns (window rows in call order, [(value, linearized
+    row set)]) or None when the key is valid. :fail ops are dropped (complete
+    marks them :fails?), so are :ok reads of nil (they constrain nothing:
+    DESIGN §2); histories here have no :info."""
+    NIL = A.NIL
+    rows = [i for i in range(cols.n) if int(cols.key[i]) == key]
+    open_by_proc, ops = {}, {}
+    for i in rows:
+        p, ty = int(cols.process[i]), int(cols.type[i])
+        if ty == A.TYPE_INVOKE:
+            open_by_proc[p] = i
+            ops[i] = {"f": int(cols.f[i]), "v": int(cols.value[i]), "v2": int(cols.value2[i]), "ret": None}
+        else:
+            inv = open_by_proc.pop(p)
+            if ty == A.TYPE_FAIL:
+                ops[inv]["fail"] = True
+            elif ty == A.TYPE_OK:
+                ops[inv]["ret"] = i
+                if ops[inv]["f"] == 0:               # read: the completion carries the value
+                    ops[inv]["v"] = int(cols.value[i])
+                    if ops[inv]["v"] == A.NIL:
+                        ops[inv]["fail"] = True
+    def step(s, o):
+        if o["f"] == 1:
+            return o["v"]
+        if o["f"] == 2:
+            return o["v2"] if s == o["v"] else None
+        return s if (o["v"] == NIL or o["v"] == s) else None
+    configs = {(frozenset(), init)}
+    avail, done = set(), set()
+    reach = set(configs)
+    for i in rows:
+        if int(cols.type[i]) == A.TYPE_INVOKE:
+            if not ops[i].get("fail"):
+                avail.add(i)
+            continue
+        if int(cols.type[i]) != A.TYPE_OK:
+            continue
+        inv = next((o for o in avail if ops[o]["ret"] == i), None)
+        if inv is None:                              # a dropped op's completion
+            continue
+        seen, stack = set(configs), list(configs)
+        while stack:
+            L, s = stack.pop()
+            for o in avail - L:
+                s2 = step(s, ops[o])
+                if s2 is None:
+                    continue
+                c = (L | {o}, s2)
+                if c not in seen:
+                    seen.add(c)
+                    stack.append(c)
+        nxt = {c for c in seen if inv in c[0]}
+        reach |= seen
+        if not nxt:
+            window = sorted(avail - done)
+            _jit_frontier.reach = len(reach)
+            return window, sorted(seen, key=lambda c: (
+                0 if c[1] == NIL else 2, c[1], sum(1 << j for j, r in enumerate(window) if r in c[0])))
+        configs = nxt
+        done.add(inv)
+    return None
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_frontier_configs_from_definition(built, seed):
+    """orc_lin_configs (the restatement jh_lin_configs is checked against on
+    the GPU) equals the frontier computed from the definition by a
+    just-in-time linearization over op maps: the first 10 configurations in
+    the canonical order, each value, linearized window rows and pending
+    window rows, for every invalid key; None for every valid key."""
+    cols, _ = synth.cas_register(n_keys=60, ops_per_key=24, threads_per_key=3, readers=1, n_values=3,
+                                 process_limit=10 ** 6, p_info=0.0, p_invalid=0.5, nemesis_every=10 ** 9,
+                                 seed=seed)
+    got = oracle.lin_configs(cols, list(range(cols.n_keys)), init=A.NIL)
+    n_bad = 0
+    for k in range(cols.n_keys):
+        ref = _jit_frontier(cols, k, A.NIL)
+        if ref is None:
+            assert got[k] is None, k
+            continue
+        n_bad += 1
+        window, front = ref
+        want = [(v, [r for r in window if r in L], [r for r in window if r not in L]) for L, v in front][:10]
+        assert [(int(v), list(map(int, lin)), list(map(int, pend))) for v, lin, pend in got[k]] == want, k
+    assert n_bad >= 5
+
+
+def test_linear_analysis_from_definition(built):
+    """The oracle's :linear analysis (orc_linear) against the same
+    just-in-time linearization from the definition: :valid? equal to WGL's on
+    every key, :analyzer :linear on every key of the reachable-set domain, and
+    its explored count the reachable configurations (initial and terminal
+    ones excluded) -- for invalid keys the closure sizes summed over the
+    layers, which the definition recounts."""
+    cols, _ = synth.cas_register(n_keys=60, ops_per_key=24, threads_per_key=3, readers=1, n_values=3,
+                                 process_limit=10 ** 6, p_info=0.0, p_invalid=0.5, nemesis_every=10 ** 9,
+                                 seed=13)
+    lin, _ = oracle.check_cas_independent(cols, init=A.NIL, algorithm="linear")
+    wgl, _ = oracle.check_cas_independent(cols, init=A.NIL)
+    assert (lin["valid"] == wgl["valid"]).all()
+    assert (lin["analyzer"] == A.ANALYZER_LINEAR).all()
+    for k in range(cols.n_keys):
+        ref = _jit_frontier(cols, k, A.NIL)
+        assert (ref is None) == (int(lin["valid"][k]) == A.VALID), k
+        if ref is not None:
+            assert int(lin["explored"][k]) == _jit_frontier.reach - 1, k
+    assert (lin["valid"] == A.INVALID).sum() >= 5

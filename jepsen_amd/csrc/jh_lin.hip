@@ -3287,6 +3287,15 @@ constexpr int BFS_LDS_BYTES = BFS_HDR + BFS_TBL + LSET * 8;   // 157 KB: one wor
 constexpr int LV_CAP = 4096, LV_H = 8192;
 static_assert(LV_CAP * 8 + LV_CAP * 4 + LV_H * 4 + LV_CAP + LV_CAP * 2 + 512 <= LSET * 8, "liveness LDS");
 __device__ __forceinline__ uint32_t lv_hash(uint64_t k) { return (uint32_t)jh_mix64(k) & (LV_H - 1); }
+// the count pass's per-bucket live sets of layers past LV_CAP: two LDS sets
+// of GL_H keys (not a power of two: both fit beside the bucket histogram),
+// at most half full; GL_XLIVE marks a node whose cross-layer child is live
+constexpr uint32_t GL_H = 8064, GL_CAP = GL_H / 2;
+constexpr uint32_t GL_XLIVE = 0x80000000u;
+static_assert(512 + 2 * GL_H * 8 <= LSET * 8, "count-pass live sets");
+__device__ __forceinline__ uint32_t gl_hash(uint64_t k) {
+    return (uint32_t)(((uint64_t)(uint32_t)jh_mix64(k) * GL_H) >> 32);
+}
 constexpr uint64_t BFS_EMPTY = ~0ULL;
 // A valid key is settled by the BFS (instead of waiting for the sequential
 // search) when its whole reachable set is complete and smaller than the
@@ -3356,6 +3365,7 @@ struct BfsShared {
     uint32_t win_vv[64];    // the current layer's window: v1 | v2 << 16
     uint32_t win_f[64];     // f, or 3 for no member
     unsigned long long cfg_min;
+    unsigned gl_cnt[2], gl_ovf[2];   // the count pass's per-bucket LDS live sets (two in turn)
 };
 
 static_assert(sizeof(BfsShared) <= BFS_HDR, "BFS header");
@@ -3687,22 +3697,107 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
             A.tmpk[pos] = x;
         }
         __syncthreads();
-        // one work item per (node, 8 members): the children's lookups of a
-        // bucket all in flight at once, instead of a node's batches in series
-        const uint32_t nb = (uint32_t)(w + 7) / 8;
+        // Bucket by bucket, largest masks first. A node's same-layer children
+        // hold one member more, so they are the previous bucket's nodes: that
+        // bucket's LIVE keys are kept in an LDS set and the children become
+        // LDS lookups. The cross-layer child (member RET[t], a later layer
+        // whose marks are final) is looked up in HBM once per node, the whole
+        // layer's lookups in flight together, before the buckets. A bucket
+        // whose live keys overflow its LDS set sends the next bucket to HBM
+        // lookups of every child (bfs_any_live8).
+        const uint32_t n = b - a;
+        uint64_t *gl_base = (uint64_t *)(jh_lds + BFS_HDR + BFS_TBL + 512);
+        for (uint32_t i0 = tid; i0 < n; i0 += 4 * BFS_THREADS) {
+            uint64_t k4[4];
+            int c4[4];
+            int64_t sl4[4];
+            uint64_t in4[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i = i0 + (uint32_t)u * BFS_THREADS;
+                uint64_t ck = 0;
+                c4[u] = 0;
+                if (i < n) {
+                    const uint64_t x = A.tmpk[i];
+                    c4[u] = bfs_child_w(sh, rpos, n_ok, (uint32_t)t, rt, w, (uint32_t)(x >> 32) & 0xFFF, (uint32_t)x,
+                                        (int)rt, &ck);
+                }
+                k4[u] = c4[u] == 2 ? ck : 0;
+            }
+            bfs_lookup_batch<4>(ent, hmask, k4, sl4, in4);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i = i0 + (uint32_t)u * BFS_THREADS;
+                if (i < n && (c4[u] == 3 || (in4[u] & BFS_LIVE))) A.tmp[i] |= GL_XLIVE;
+            }
+        }
+        int prev_state = 0;          // the previous bucket's live set: 0 empty, 1 in LDS, 2 overflowed
+        int cur = 0, par = 0;
         for (int p = 32; p >= 0; p--) {
-            const uint32_t bs = hist[33 + p], be = p > 0 ? hist[33 + p - 1] : b - a;
-            if (bs == be) continue;
-            const uint32_t items = (be - bs) * nb;
-            for (uint32_t q = tid; q < items; q += BFS_THREADS) {
-                const uint32_t sl = A.tmp[bs + q / nb];
-                const int j0 = (int)(q % nb) * 8;
-                const uint64_t x = A.tmpk[bs + q / nb];
+            const uint32_t bs = hist[33 + p], be = p > 0 ? hist[33 + p - 1] : n;
+            if (bs == be) { prev_state = 0; continue; }
+            uint64_t *cs = gl_base + (cur ? GL_H : 0);
+            const uint64_t *ps = gl_base + (cur ? 0 : GL_H);
+            for (uint32_t i = tid; i < GL_H; i += BFS_THREADS) cs[i] = 0;
+            if (tid == 0) { sh.gl_cnt[par] = 0; sh.gl_ovf[par] = 0; }
+            __syncthreads();
+            for (uint32_t i0 = bs + tid - lane; i0 < be; i0 += BFS_THREADS) {
+                const uint32_t i = i0 + lane;
+                const bool act = i < be;
+                const uint32_t sw = act ? A.tmp[i] : 0;
+                const uint64_t x = act ? A.tmpk[i] : 0;
                 const uint32_t s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
-                if (bfs_any_live8(ent, hmask, sh, rpos, n_ok, (uint32_t)t, rt, w, s0, m0, j0))
-                    atomicOr((unsigned long long *)&ent[sl].y, BFS_LIVE);
+                bool live = (sw & GL_XLIVE) != 0;
+                if (act && !live && prev_state == 1) {
+                    for (int j0 = 0; j0 < w && !live; j0 += 8) {
+                        uint64_t kk[8];
+                        uint32_t h[8];
+                        uint64_t e[8];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            uint64_t ck = 0;
+                            const int j = j0 + u;
+                            kk[u] = ((uint32_t)j != rt &&
+                                     bfs_child_w(sh, rpos, n_ok, (uint32_t)t, rt, w, s0, m0, j, &ck) == 1) ? ck + 1 : 0;
+                            h[u] = gl_hash(kk[u]);
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; u++) e[u] = kk[u] ? ps[h[u]] : 0;
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            if (!kk[u] || !e[u]) continue;
+                            if (e[u] == kk[u]) { live = true; continue; }
+                            for (uint32_t hh = h[u] + 1 == GL_H ? 0 : h[u] + 1;; hh = hh + 1 == GL_H ? 0 : hh + 1) {
+                                const uint64_t y = ps[hh];
+                                if (y == 0) break;
+                                if (y == kk[u]) { live = true; break; }
+                            }
+                        }
+                    }
+                } else if (act && !live && prev_state == 2) {
+                    for (int j0 = 0; j0 < w && !live; j0 += 8)
+                        live = bfs_any_live8(ent, hmask, sh, rpos, n_ok, (uint32_t)t, rt, w, s0, m0, j0);
+                }
+                if (act && live) atomicOr((unsigned long long *)&ent[sw & ~GL_XLIVE].y, BFS_LIVE);
+                // this bucket's live keys into its LDS set: room reserved per wave
+                const uint64_t lm = ballot(act && live);
+                if (!lm) continue;
+                int room = 1;
+                if (lane == 0) {
+                    const uint32_t c = (uint32_t)__popcll(lm);
+                    const uint32_t old = atomicAdd(&sh.gl_cnt[par], c);
+                    if (old + c > GL_CAP) { sh.gl_ovf[par] = 1; room = 0; }
+                }
+                if (readlane(room, 0) && act && live) {
+                    const uint64_t k = x + 1;
+                    for (uint32_t hh = gl_hash(k);; hh = hh + 1 == GL_H ? 0 : hh + 1)
+                        if (atomicCAS((unsigned long long *)&cs[hh], 0ULL, k) == 0ULL) break;
+                }
             }
             __syncthreads();
+            prev_state = sh.gl_ovf[par] ? 2 : 1;
+            cur ^= 1;
+            par ^= 1;
         }
     }
     stamp(6);

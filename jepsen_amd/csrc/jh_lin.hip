@@ -3601,14 +3601,23 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
             if (tid < 2) hist[tid] = tid ? 0u : 32u;               // [0] min popcount, [1] max
             if (tid >= 2 && tid < 2 + 2 * 33) hist[tid] = 0;      // [2+p] count, [35+p] fill
             __syncthreads();
-            for (uint32_t i = tid; i < n; i += BFS_THREADS) {
-                const uint64_t x = A.nodes[a + i];
+            for (uint32_t i0 = tid - lane; i0 < n; i0 += BFS_THREADS) {
+                const uint32_t i = i0 + lane;
+                const uint64_t x = i < n ? A.nodes[a + i] : 0;
+                const uint32_t pc = (uint32_t)__popc((uint32_t)x);
+                {
+                    // popcount range: one LDS atomic per wave
+                    uint32_t pmn = i < n ? pc : 32u, pmx = pc;
+                    for (int o = 32; o > 0; o >>= 1) {
+                        pmn = min(pmn, (uint32_t)__shfl_xor((int)pmn, o));
+                        pmx = max(pmx, (uint32_t)__shfl_xor((int)pmx, o));
+                    }
+                    if (lane == 0) { atomicMin(&hist[0], pmn); atomicMax(&hist[1], pmx); }
+                }
+                if (i >= n) continue;
                 const uint32_t sl = slot_of[a + i];
                 lk[i] = x;
                 ls[i] = sl;
-                const uint32_t pc = (uint32_t)__popc((uint32_t)x);
-                atomicMin(&hist[0], pc);
-                atomicMax(&hist[1], pc);
                 atomicAdd(&hist[2 + pc], 1u);
                 uint32_t h = lv_hash(x);
                 while (atomicCAS(&lh[h], 0u, i + 1) != 0u) h = (h + 1) & (LV_H - 1);
@@ -3855,30 +3864,37 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
         { uint32_t *tp = fa; fa = fb; fb = tp; }
         __syncthreads();
         // one work item per (node, 8 members), as in the liveness pass
+        // (wave-uniform loop: the new nodes are counted with one LDS atomic per
+        // wave and child, not one per node on a single address)
         const uint32_t nbc = (uint32_t)(sh.maxw + 7) / 8;
-        for (uint32_t qq = tid; qq < nf * nbc; qq += BFS_THREADS) {
-            const uint64_t x = bfs_keyat(ent, fa[qq / nbc]);
-            const uint32_t t = (uint32_t)(x >> 44), s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
-            const int w = woff[t + 1] - woff[t];
+        for (uint32_t q0 = tid - lane; q0 < nf * nbc; q0 += BFS_THREADS) {
+            const uint32_t qq = q0 + lane;
+            const bool act = qq < nf * nbc;
+            uint64_t k[8];
+            int64_t sl[8];
+            uint64_t inf[8];
             {
+                const uint64_t x = act ? bfs_keyat(ent, fa[qq / nbc]) : 0;
+                const uint32_t t = (uint32_t)(x >> 44), s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
                 const int j0 = (int)(qq % nbc) * 8;
-                if (j0 >= w) continue;
-                uint64_t k[8];
-                int64_t sl[8];
-                uint64_t inf[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
                     uint64_t ck = 0;
-                    const int c = bfs_child(ops, woff, W, rpos, n_ok, t, s0, m0, j0 + i, &ck);
+                    const int c = act ? bfs_child(ops, woff, W, rpos, n_ok, t, s0, m0, j0 + i, &ck) : 0;
                     k[i] = (c == 1 || c == 2) ? ck : 0;
                 }
-                bfs_lookup_batch<8>(ent, hmask, k, sl, inf);
+            }
+            bfs_lookup_batch<8>(ent, hmask, k, sl, inf);
 #pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    if (sl[i] < 0 || !visit((uint32_t)sl[i], inf[i])) continue;
-                    const uint32_t pos = atomicAdd(&sh.cnext, 1u);
-                    if (pos < A.ncap / 2) fb[pos] = (uint32_t)sl[i];
-                }
+            for (int i = 0; i < 8; i++) {
+                const bool nw = sl[i] >= 0 && visit((uint32_t)sl[i], inf[i]);
+                const uint64_t m = ballot(nw);
+                if (!m) continue;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&sh.cnext, (uint32_t)__popcll(m));
+                base = readlane(base, 0);
+                const uint32_t pos = base + mbcnt(m);
+                if (nw && pos < A.ncap / 2) fb[pos] = (uint32_t)sl[i];
             }
         }
         __syncthreads();

@@ -5199,7 +5199,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     int64_t quick = std::min<int64_t>(budget, QUICK_BUDGET);
     if (opts && opts->quick_budget > 0)
         quick = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(budget, memo_cap1 / 2), opts->quick_budget));
-    const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * (163840 / MemoQ::LDS));
+    int p1_per_cu = 163840 / MemoQ::LDS;
+    if (opts && opts->p1_waves_per_cu > 0) p1_per_cu = std::min(p1_per_cu, (int)opts->p1_waves_per_cu);
+    const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * p1_per_cu);
     uint64_t *memo = ctx->ws<uint64_t>(WS_MEMO, (size_t)waves1 * memo_cap1 * 2, /*zero=*/true);
     if (clear_memo) HIP_TRY(hipMemsetAsync(memo, 0, ctx->bufs[WS_MEMO].bytes, st));
     const uint32_t stack_cap = (uint32_t)smax + 2;

@@ -92,6 +92,7 @@ NOW = A.LIN_HELPERS_NOW
     dict(flags=NOW, quick_budget=40, phase2_budget=300, lean_waves=8),
     dict(flags=NOW, quick_budget=40, p2_waves_per_cu=1),
     dict(flags=A.LIN_NO_HELPERS, quick_budget=40),
+    dict(p1_waves_per_cu=1, quick_budget=500, handover_min=100),
 ])
 def test_late_helpers(ctx, tune):
     """Phase-2 late helpers (the workgroup engine racing the sequential search

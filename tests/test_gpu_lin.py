@@ -386,9 +386,12 @@ def test_linear_algorithm(ctx, seed, kw):
     decided = (g["valid"] != A.UNKNOWN) & (w["valid"] != A.UNKNOWN)
     assert (g["valid"][decided] == w["valid"][decided]).all()
     assert (w["analyzer"] == A.ANALYZER_WGL).all()
-    assert (g["analyzer"] == A.ANALYZER_LINEAR).sum() > 0
     if seed == 43:
-        assert (g["analyzer"] == A.ANALYZER_WGL).sum() > 0
+        # windows of up to 60 members: every key past the reachable-set
+        # engine's 32, so WGL decides each one (knossos' competition fallback)
+        assert (g["analyzer"] == A.ANALYZER_WGL).all()
+    else:
+        assert (g["analyzer"] == A.ANALYZER_LINEAR).sum() > 0
 
 
 def test_linear_algorithm_host_mirror(ctx):

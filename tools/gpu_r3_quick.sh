@@ -3,7 +3,6 @@
 O=${1:-gpurun_out/r3q}
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p $O
-timeout -k 10 60 ./tools/probe/streams > $O/streams_probe.log 2>&1 || true
 timeout -k 10 300 python -u -m pytest tests/test_gpu_counter_set.py -x -v --timeout 200 --timeout-method thread > $O/cs_tests.log 2>&1 || exit 1
 timeout -k 10 700 python -u -m pytest tests/test_gpu_lin.py tests/test_gpu_limits.py -x -v --timeout 300 --timeout-method thread > $O/lin_tests.log 2>&1 || exit 1
 timeout -k 10 200 python -u bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 > $O/bench_c3.log 2>&1 || exit 1

@@ -348,6 +348,14 @@ int jh_check_set_bitmaps(jh_ctx *ctx, const jh_history *h, jh_set_result *res,
                          int64_t words_cap, int64_t *base, int64_t *n_words,
                          char *err, size_t errlen);
 
+/* Page-locked host memory for result buffers a caller keeps across calls
+ * (jh_check_counter's triples, jh_check_set_bitmaps' bitmaps): their D2H then
+ * runs at PCIe speed instead of through the runtime's pageable staging
+ * copies. Not in the reference's interface (a JVM has no such thing): the
+ * JNA shim allocates one per checker instance and reuses it. */
+int jh_host_alloc(size_t bytes, void **out, char *err, size_t errlen);
+int jh_host_free(void *p);
+
 /* (checker/set-full {:linearizable? linearizable}), checker.clj:236-534.
  * Elements are the :value of every :invoke :add by an integer process; a
  * set :read's :value is its CSR range in aux (value = offset, value2 =

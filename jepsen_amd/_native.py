@@ -65,6 +65,8 @@ def lib():
                                                C.c_int64, C.c_char_p, C.c_size_t]
             L.jh_check_queue.argtypes = [C.c_void_p, H, C.POINTER(A.JhQueueResult), p64, C.c_int64,
                                          C.c_char_p, C.c_size_t]
+            L.jh_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p), C.c_char_p, C.c_size_t]
+            L.jh_host_free.argtypes = [C.c_void_p]
             # history ingest (include/jh_io.h), host code in the same library
             pp = C.POINTER(C.c_void_p)
             L.jh_ingest_file.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, pp, C.c_char_p, C.c_size_t]
@@ -91,6 +93,7 @@ EXPORTED_SYMBOLS = ["jh_version", "jh_open", "jh_open_multi", "jh_open_devices",
                     "jh_close", "jh_check_cas_independent",
                     "jh_check_cas", "jh_check_cas_independent_device", "jh_lin_configs", "jh_check_counter",
                     "jh_check_set", "jh_check_set_bitmaps", "jh_check_set_full", "jh_check_total_queue", "jh_check_queue",
+                    "jh_host_alloc", "jh_host_free",
                     # include/jh_io.h
                     "jh_ingest_file", "jh_ingest_buffer", "jh_ingest_history", "jh_ingest_time",
                     "jh_ingest_values_interned", "jh_ingest_table_size", "jh_ingest_table_entry", "jh_ingest_free"]
@@ -128,6 +131,28 @@ def key_costs(cols):
     rc = lib().jh_key_costs(C.byref(h), out.ctypes.data_as(C.POINTER(C.c_int64)), err, len(err))
     _raise(rc, err)
     return out[:cols.n_keys]
+
+
+class HostBuffer:
+    """Page-locked host memory from jh_host_alloc, viewed as a numpy array:
+    result buffers reused across calls (check_counter's reads, the set
+    bitmaps), so their D2H runs at PCIe speed. Freed with the object."""
+
+    def __init__(self, count, dtype):
+        dt = np.dtype(dtype)
+        p = C.c_void_p()
+        err = C.create_string_buffer(256)
+        _raise(lib().jh_host_alloc(max(int(count), 1) * dt.itemsize, C.byref(p), err, len(err)), err)
+        self._p = p
+        buf = (C.c_char * (max(int(count), 1) * dt.itemsize)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=dt, count=max(int(count), 1))
+
+    def __del__(self):
+        p = getattr(self, "_p", None)
+        if p is not None and p.value:
+            self.array = None
+            lib().jh_host_free(p)
+            self._p = None
 
 
 class Context:
@@ -250,11 +275,18 @@ class Context:
         return res
 
     # -- counter / set -----------------------------------------------------
-    def check_counter(self, cols, reads_cap=None, on_device=False):
-        """on_device: cols' columns are device pointers (the history already in HBM)."""
+    def check_counter(self, cols, reads_cap=None, on_device=False, out=None):
+        """on_device: cols' columns are device pointers (the history already in HBM).
+        out: an int64 array of >= 3 * reads_cap to receive the triples (e.g. a
+        HostBuffer's, reused across calls); the returned reads view it."""
         h = A.make_history(cols, on_device=on_device)
         cap = cols.n if reads_cap is None else reads_cap
-        reads = np.zeros(3 * max(cap, 1), np.int64)
+        if out is not None:
+            if out.dtype != np.int64 or len(out) < 3 * max(cap, 1) or not out.flags.c_contiguous:
+                raise ValueError("out: contiguous int64 array of at least 3 * reads_cap")
+            reads = out
+        else:
+            reads = np.zeros(3 * max(cap, 1), np.int64)
         nr, ne, fe = C.c_int64(), C.c_int64(), C.c_int64()
         valid, cause = C.c_int32(), C.c_int32()
         err = C.create_string_buffer(1024)
@@ -281,10 +313,11 @@ class Context:
         out["n_runs"] = list(r.n_runs)
         return out
 
-    def check_set_bitmaps(self, cols, words_cap=None, on_device=False):
+    def check_set_bitmaps(self, cols, words_cap=None, on_device=False, out=None):
         """jh_check_set_bitmaps: the counts plus the four result sets (ok,
         lost, unexpected, recovered) as uint32 bitmaps over [base, base + 32 *
-        n_words); bits_to_runs turns one into sorted [lo hi] runs."""
+        n_words); bits_to_runs turns one into sorted [lo hi] runs. out: four
+        uint32 arrays of words_cap words (e.g. HostBuffers', reused)."""
         h = A.make_history(cols, on_device=on_device)
         r = A.JhSetResult()
         err = C.create_string_buffer(1024)
@@ -296,7 +329,13 @@ class Context:
             # the span is bounded by the history's own values
             cap = 1 << 16
         for _ in range(2):
-            bits = [np.zeros(max(cap, 1), np.uint32) for _ in range(4)]
+            if out is not None:
+                if words_cap is None or len(out) != 4 or any(
+                        b.dtype != np.uint32 or len(b) < max(cap, 1) or not b.flags.c_contiguous for b in out):
+                    raise ValueError("out: four contiguous uint32 arrays of words_cap words")
+                bits = list(out)
+            else:
+                bits = [np.zeros(max(cap, 1), np.uint32) for _ in range(4)]
             rc = lib().jh_check_set_bitmaps(self._h, C.byref(h), C.byref(r), *[b.ctypes.data_as(p32) for b in bits],
                                             cap, C.byref(base), C.byref(nw), err, len(err))
             _raise(rc, err)

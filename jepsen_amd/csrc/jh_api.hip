@@ -310,6 +310,17 @@ int jh_check_set_bitmaps(jh_ctx *ctx, const jh_history *h, jh_set_result *res, u
     });
 }
 
+int jh_host_alloc(size_t bytes, void **out, char *err, size_t errlen) {
+    if (!out) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    *out = nullptr;
+    return guarded(err, errlen, [&] { HIP_TRY(hipHostMalloc(out, bytes ? bytes : 16, hipHostMallocDefault)); });
+}
+
+int jh_host_free(void *p) {
+    if (!p) return JH_OK;
+    return hipHostFree(p) == hipSuccess ? JH_OK : JH_EDEVICE;
+}
+
 int jh_check_set_full(jh_ctx *ctx, const jh_history *h, const int64_t *time, int32_t linearizable,
                       jh_set_full_result *res, int64_t *lost, int64_t *never_read, int64_t *stale,
                       int64_t list_cap, char *err, size_t errlen) {

@@ -106,7 +106,16 @@ __global__ void __launch_bounds__(256) k_cnt_prange(const int64_t *__restrict__ 
 // process beyond the first PAIR_PROCS, go to a spill list (k_cnt_pair_spill)
 // and their words stay CW_PEND until it completes them.
 constexpr int PAIR_PROCS = 32, PAIR_GROUPS = CHUNK / 64;
-__global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ proc,
+constexpr int PER = CHUNK / 256;            // rows per thread per chunk (row k * 256 + tid)
+// One chunk per block; 36 KB of LDS and < 128 VGPRs give four blocks per CU
+// (round 2: 50 KB, three blocks, 1.59 ms per 100 M rows), so more chunks'
+// loads are in flight while others pair in LDS.
+// A spilled invocation is stored as its row when its walk must start right
+// after it (a process beyond the chunk's first PAIR_PROCS), as ~row when the
+// chunk already showed every later row of its process in the chunk to be
+// :info, so the walk starts at the chunk's end (a crashed op's walk then ends
+// at once: its process' last row lies inside the chunk).
+__global__ void __launch_bounds__(256, 4) k_cnt_pack(const int64_t *__restrict__ proc,
                                                   const int64_t *__restrict__ type,
                                                   const int64_t *__restrict__ f,
                                                   const int64_t *__restrict__ val, int64_t n,
@@ -119,151 +128,175 @@ __global__ void __launch_bounds__(256) k_cnt_pack(const int64_t *__restrict__ pr
     __shared__ int8_t hc[HSLOTS];                   // its compact index, -1 beyond PAIR_PROCS
     __shared__ uint8_t sc[CHUNK];                   // the chunk's rows: f2 << 2 | type
     __shared__ int16_t sp[CHUNK];                   // each row's partner in the chunk (-1: none)
-    __shared__ int8_t rc[CHUNK];                    // each row's compact process index (-1: none)
-    __shared__ long long sv[CHUNK];                 // the chunk's values
+    __shared__ int16_t rs[CHUNK];                   // each row's hash slot (-1: none)
     __shared__ unsigned long long M[PAIR_GROUPS][PAIR_PROCS];
     __shared__ int nd, nls, gbase;
     __shared__ int32_t ls[CHUNK];                   // this chunk's spilled invocations
     __shared__ long long sh[4];
-    const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
-    const int nc = (int)min<int64_t>(CHUNK, n - c0);
-    for (int i = threadIdx.x; i < HSLOTS; i += blockDim.x) { hk[i] = 0; hv[i] = -1; hc[i] = -1; }
-    for (int i = threadIdx.x; i < PAIR_GROUPS * PAIR_PROCS; i += blockDim.x) (&M[0][0])[i] = 0;
-    if (threadIdx.x == 0) { nd = 0; nls = 0; }
-    __syncthreads();
+    const int tid = threadIdx.x;
     long long am = 0, na = 0;
-    // all of this thread's rows in flight at once (the loop below waits on LDS)
-    constexpr int PER = CHUNK / 256;
-    long long rp[PER], rt[PER], rf[PER], rv[PER];
+    {
+        const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
+        const int nc = (int)min<int64_t>(CHUNK, n - c0);
+        // every row of the thread in flight at once, then compacted
+        // (process offset, f2 << 2 | type, value)
+        long long rp[PER], rt[PER], rf[PER], cv[PER];
 #pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const int i = k * 256 + threadIdx.x;
-        if (i < nc) { rp[k] = proc[c0 + i]; rt[k] = type[c0 + i]; rf[k] = f[c0 + i]; rv[k] = val[c0 + i]; }
-    }
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const int i = k * 256 + threadIdx.x;
-        if (i >= nc) break;
-        const int64_t r = c0 + i;
-        const long long p = rp[k];
-        const int64_t ty = rt[k] & 3, ff = rf[k];
-        const uint32_t f2 = ff == JH_F_ADD ? F2_ADD : ff == JH_F_READ ? F2_READ : F2_OTHER;
-        const uint32_t pk = (uint32_t)(p - pmin);                                  // span < 2^28
-        sc[i] = (uint8_t)((f2 << 2) | (uint32_t)ty);
-        sv[i] = rv[k];
-        sp[i] = -1;
-        if (f2 == F2_ADD && (ty == T_INVOKE || ty == T_OK)) {
-            const long long v = rv[k];
-            if (v != JH_NIL) am = max(am, v < 0 ? (v == LLONG_MIN ? LLONG_MAX : -v) : v);
-            na++;
+        for (int k = 0; k < PER; k++) {
+            const int64_t r = c0 + k * 256 + tid;
+            if (r < n) { rp[k] = proc[r]; rt[k] = type[r]; rf[k] = f[r]; cv[k] = val[r]; }
+            else { rp[k] = pmin; rt[k] = T_INFO; rf[k] = 0; cv[k] = 0; }
         }
-        uint32_t h = (uint32_t)jh_mix64((uint64_t)p) & (HSLOTS - 1);
-        int slot = -1;
-        for (int probe = 0; probe < 64; probe++) {
-            uint32_t cur = hk[h];
-            if (cur == 0) {
-                cur = atomicCAS(&hk[h], 0u, pk + 1);
-                if (cur == 0) {
-                    const int c = atomicAdd(&nd, 1);
-                    hc[h] = (int8_t)(c < PAIR_PROCS ? c : -1);
-                    cur = pk + 1;
-                }
+        uint32_t cp[PER], cx[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            cp[k] = (uint32_t)(rp[k] - pmin);                                      // span < 2^28
+            const uint32_t f2 = rf[k] == JH_F_ADD ? F2_ADD : rf[k] == JH_F_READ ? F2_READ : F2_OTHER;
+            cx[k] = (f2 << 2) | (uint32_t)(rt[k] & 3);
+        }
+        for (int i = tid; i < HSLOTS; i += 256) { hk[i] = 0; hv[i] = -1; hc[i] = -1; }
+        for (int i = tid; i < PAIR_GROUPS * PAIR_PROCS; i += 256) (&M[0][0])[i] = 0;
+        if (tid == 0) { nd = 0; nls = 0; }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int i = k * 256 + tid;
+            if (i >= nc) break;
+            const int64_t r = c0 + i;
+            const uint32_t pk = cp[k];
+            const uint32_t ty = cx[k] & 3, f2 = cx[k] >> 2;
+            sc[i] = (uint8_t)cx[k];
+            sp[i] = -1;
+            if (f2 == F2_ADD && (ty == T_INVOKE || ty == T_OK)) {
+                const long long v = cv[k];
+                if (v != JH_NIL) am = max(am, v < 0 ? (v == LLONG_MIN ? LLONG_MAX : -v) : v);
+                na++;
             }
-            if (cur == pk + 1) { slot = (int)h; break; }
-            h = (h + 1) & (HSLOTS - 1);
+            uint32_t h = (uint32_t)jh_mix64((uint64_t)pk) & (HSLOTS - 1);
+            int slot = -1;
+            for (int probe = 0; probe < 64; probe++) {
+                uint32_t cur = hk[h];
+                if (cur == 0) {
+                    cur = atomicCAS(&hk[h], 0u, pk + 1);
+                    if (cur == 0) {
+                        const int c = atomicAdd(&nd, 1);
+                        hc[h] = (int8_t)(c < PAIR_PROCS ? c : -1);
+                        cur = pk + 1;
+                    }
+                }
+                if (cur == pk + 1) { slot = (int)h; break; }
+                h = (h + 1) & (HSLOTS - 1);
+            }
+            // the process' last row: the wave's last lane of each slot only
+            // (one LDS atomic per process per wave, not per row)
+            const int nxt = __shfl_down(slot, 1);
+            // (lane + 1 holds row i + 1: past the chunk's end it is inactive)
+            if (slot >= 0) { if ((tid & 63) == 63 || i + 1 >= nc || nxt != slot) atomicMax(&hv[slot], (int)r); }
+            else atomicMax(&last[pk], (int)r);
+            rs[i] = (int16_t)slot;
         }
-        if (slot >= 0) atomicMax(&hv[slot], (int)r);
-        else atomicMax(&last[pk], (int)r);
-        rc[i] = slot >= 0 ? (int8_t)slot : (int8_t)-1;   // provisional: low byte of the hash slot
-        ls[i] = slot;                                     // (the full slot, until the spill list needs ls)
+        __syncthreads();
+        for (int i = tid; i < HSLOTS; i += 256)
+            if (hk[i]) atomicMax(&last[hk[i] - 1], hv[i]);
+        // compact process index of every row (the hash is complete now), and the
+        // group masks of non-:info rows
+        int8_t rc[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int i = k * 256 + tid;
+            rc[k] = -1;
+            if (i >= nc) continue;
+            const int slot = rs[i];
+            const int c = slot >= 0 ? hc[slot] : -1;
+            rc[k] = (int8_t)c;
+            if (c >= 0 && (sc[i] & 3) != T_INFO) atomicOr(&M[i >> 6][c], 1ULL << (i & 63));
+        }
+        __syncthreads();
+        bool walk_from_end[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int i = k * 256 + tid;
+            walk_from_end[k] = false;
+            if (i >= nc) continue;
+            const uint32_t x = sc[i];
+            if ((x & 3) != T_INVOKE) continue;
+            const int c = rc[k];
+            int got = -1;
+            if (c >= 0) {
+                const int g = i >> 6, l = i & 63;
+                const unsigned long long after = l == 63 ? 0ULL : (M[g][c] & (~0ULL << (l + 1)));
+                if (after) got = (g << 6) + __builtin_ctzll(after);
+                else
+                    for (int g2 = g + 1; g2 < PAIR_GROUPS && (g2 << 6) < nc; g2++)
+                        if (M[g2][c]) { got = (g2 << 6) + __builtin_ctzll(M[g2][c]); break; }
+                walk_from_end[k] = got < 0;      // every later row of its process in the chunk is :info
+            }
+            if (got >= 0 && (sc[got] & 3) == T_INVOKE) {
+                atomicMin(&m->viol1, ((unsigned long long)(c0 + got) << 4) | JH_CAUSE_DOUBLE_INVOKE);
+                got = -2;
+            }
+            sp[i] = (int16_t)got;                      // -1: spill (no completion in the chunk)
+            if (got >= 0) sp[got] = (int16_t)i;
+        }
+        __syncthreads();
+        // the contribution words
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int i = k * 256 + tid;
+            if (i >= nc) continue;
+            const uint32_t x = sc[i];
+            const uint32_t ty = x & 3, f2 = x >> 2;
+            const int64_t r = c0 + i;
+            const int c = sp[i];
+            uint32_t w = CW_NONE;
+            if (ty == T_INVOKE) {
+                if (c == -1) {
+                    // spills gather in LDS: one global atomic per chunk
+                    ls[atomicAdd(&nls, 1)] = walk_from_end[k] ? ~(int32_t)r : (int32_t)r;
+                    w = f2 == F2_READ ? CW_INVREAD : f2 == F2_ADD ? CW_PEND : CW_NONE;
+                } else if (f2 == F2_READ) {
+                    w = CW_INVREAD;
+                } else if (f2 == F2_ADD && c >= 0 && (sc[c] & 3) != T_FAIL) {
+                    // (remove :fails?) keeps it: upper += (or inv ok)
+                    long long v = cv[k];
+                    bool own = true;
+                    if (v == JH_NIL) { v = val[c0 + c]; own = false; }
+                    if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
+                    else {
+                        w = cw_make(CW_HI, v);
+                        if ((w & CW_X) && !own) pair[r] = (int32_t)(c0 + c);
+                    }
+                }
+            } else if (ty == T_OK || ty == T_FAIL) {
+                const uint32_t u = c < 0 ? CW_U : 0u;      // no invocation in the chunk (yet)
+                if (ty == T_OK && f2 == F2_ADD) {
+                    const long long v = cv[k];
+                    if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
+                    else w = cw_make(CW_LO, v);
+                } else if (ty == T_OK && f2 == F2_READ) {
+                    // its pending read must come from an [:invoke :read] (checker.clj:713-716)
+                    if (c >= 0 && (sc[c] >> 2) != F2_READ)
+                        atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_ORPHAN);
+                    else {
+                        w = CW_OKREAD;
+                        if (c >= 0) pair[r] = (int32_t)(c0 + c);
+                    }
+                }
+                w |= u;
+            }
+            cw[r] = w;
+        }
+        __syncthreads();
+        if (tid == 0 && nls) gbase = (int)atomicAdd(n_spill, (unsigned int)nls);
+        __syncthreads();
+        for (int k = tid; k < nls; k += 256) spill[gbase + k] = ls[k];
     }
     am = block_reduce256(am, RedMax(), sh);
     na = block_reduce256(na, RedSum(), sh);
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         if (am) atomicMax(&m->amax_abs, am);
         if (na) atomicAdd((unsigned long long *)&m->n_add, (unsigned long long)na);
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < HSLOTS; i += blockDim.x)
-        if (hk[i]) atomicMax(&last[hk[i] - 1], hv[i]);
-    // compact process index of every row (the hash is complete now), and the
-    // group masks of non-:info rows
-    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
-        const int slot = ls[i];
-        const int c = slot >= 0 ? hc[slot] : -1;
-        rc[i] = (int8_t)c;
-        if (c >= 0 && (sc[i] & 3) != T_INFO) atomicOr(&M[i >> 6][c], 1ULL << (i & 63));
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
-        const uint32_t x = sc[i];
-        if ((x & 3) != T_INVOKE) continue;
-        const int c = rc[i];
-        int got = -1;
-        if (c >= 0) {
-            const int g = i >> 6, l = i & 63;
-            const unsigned long long after = l == 63 ? 0ULL : (M[g][c] & (~0ULL << (l + 1)));
-            if (after) got = (g << 6) + __builtin_ctzll(after);
-            else
-                for (int g2 = g + 1; g2 < PAIR_GROUPS && (g2 << 6) < nc; g2++)
-                    if (M[g2][c]) { got = (g2 << 6) + __builtin_ctzll(M[g2][c]); break; }
-        }
-        if (got >= 0 && (sc[got] & 3) == T_INVOKE) {
-            atomicMin(&m->viol1, ((unsigned long long)(c0 + got) << 4) | JH_CAUSE_DOUBLE_INVOKE);
-            got = -2;
-        }
-        sp[i] = (int16_t)got;                      // -1: spill (no completion in the chunk)
-        if (got >= 0) sp[got] = (int16_t)i;
-    }
-    if (threadIdx.x == 0) nls = 0;
-    __syncthreads();
-    // the contribution words
-    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
-        const uint32_t x = sc[i];
-        const uint32_t ty = x & 3, f2 = x >> 2;
-        const int64_t r = c0 + i;
-        const int c = sp[i];
-        uint32_t w = CW_NONE;
-        if (ty == T_INVOKE) {
-            if (c == -1) {
-                ls[atomicAdd(&nls, 1)] = (int32_t)r;   // spills gather in LDS: one global atomic per chunk
-                w = f2 == F2_READ ? CW_INVREAD : f2 == F2_ADD ? CW_PEND : CW_NONE;
-            } else if (f2 == F2_READ) {
-                w = CW_INVREAD;
-            } else if (f2 == F2_ADD && c >= 0 && (sc[c] & 3) != T_FAIL) {
-                // (remove :fails?) keeps it: upper += (or inv ok)
-                long long v = sv[i];
-                bool own = true;
-                if (v == JH_NIL) { v = sv[c]; own = false; }
-                if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
-                else {
-                    w = cw_make(CW_HI, v);
-                    if ((w & CW_X) && !own) pair[r] = (int32_t)(c0 + c);
-                }
-            }
-        } else if (ty == T_OK || ty == T_FAIL) {
-            const uint32_t u = c < 0 ? CW_U : 0u;      // no invocation in the chunk (yet)
-            if (ty == T_OK && f2 == F2_ADD) {
-                const long long v = sv[i];
-                if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
-                else w = cw_make(CW_LO, v);
-            } else if (ty == T_OK && f2 == F2_READ) {
-                // its pending read must come from an [:invoke :read] (checker.clj:713-716)
-                if (c >= 0 && (sc[c] >> 2) != F2_READ)
-                    atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_ORPHAN);
-                else {
-                    w = CW_OKREAD;
-                    if (c >= 0) pair[r] = (int32_t)(c0 + c);
-                }
-            }
-            w |= u;
-        }
-        cw[r] = w;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0 && nls) gbase = (int)atomicAdd(n_spill, (unsigned int)nls);
-    __syncthreads();
-    for (int k = threadIdx.x; k < nls; k += blockDim.x) spill[gbase + k] = ls[k];
 }
 
 // the spilled invocations: one thread each walks its process' rows forward
@@ -281,12 +314,15 @@ __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restric
                                                         CntMeta *m) {
     const unsigned int ns = *n_spill;
     for (unsigned int s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
-        const int64_t r = spill[s];
+        const int32_t se = spill[s];
+        const int64_t r = se >= 0 ? se : ~se;
         const long long p = proc[r];
         const int64_t ff = f[r];
         const int64_t lr = last[p - pmin];
         int64_t got = -1;
-        for (int64_t j = r + 1; j <= lr; j++) {
+        // from the chunk's end when the chunk held only :info rows of p after r
+        const int64_t j0 = se >= 0 ? r + 1 : (r / CHUNK + 1) * CHUNK;
+        for (int64_t j = j0; j <= lr; j++) {
             if (proc[j] != p) continue;
             const int64_t ty = type[j] & 3;
             if (ty == T_INFO) continue;

@@ -26,18 +26,34 @@ struct SetMeta {
     unsigned long long first_lost_row;
 };
 
+// Row pairs: both rows in one 16-byte load when the columns are 16-byte
+// aligned (vec; workspace and torch allocations are), two 8-byte loads
+// otherwise; a trailing odd row is the last pair's first half
+__device__ __forceinline__ longlong2 ld_pair(const int64_t *__restrict__ c, int64_t i, int64_t n, bool vec) {
+    if (2 * i + 1 < n) return vec ? ((const longlong2 *)c)[i] : make_longlong2(c[2 * i], c[2 * i + 1]);
+    return make_longlong2(c[2 * i], 0);
+}
+
 __global__ void __launch_bounds__(256) k_set_scan(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
-                           const int64_t *__restrict__ val, int64_t n, SetMeta *m) {
+                           const int64_t *__restrict__ val, int64_t n, int vec, SetMeta *m) {
     long long lo = LLONG_MAX, hi = LLONG_MIN, fr = -1;
     int na = 0, nd = 0;
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
-         r += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t ty = type[r], ff = f[r];
-        if (ff == JH_F_ADD && (ty == T_INVOKE || ty == T_OK)) {
-            const int64_t v = val[r];
-            if (v == JH_NIL) { if (ty == T_INVOKE) na = 1; else nd = 1; }
-            else { lo = min(lo, (long long)v); hi = max(hi, (long long)v); }
-        } else if (ff == JH_F_READ && ty == T_OK) fr = max(fr, (long long)r);
+    const int64_t np = (n + 1) / 2;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const longlong2 t2 = ld_pair(type, i, n, vec), f2 = ld_pair(f, i, n, vec), v2 = ld_pair(val, i, n, vec);
+        const int64_t tt[2] = {t2.x, t2.y}, ffs[2] = {f2.x, f2.y}, vv[2] = {v2.x, v2.y};
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int64_t r = 2 * i + k;
+            if (r >= n) break;
+            const int64_t ty = tt[k], ff = ffs[k];
+            if (ff == JH_F_ADD && (ty == T_INVOKE || ty == T_OK)) {
+                const int64_t v = vv[k];
+                if (v == JH_NIL) { if (ty == T_INVOKE) na = 1; else nd = 1; }
+                else { lo = min(lo, (long long)v); hi = max(hi, (long long)v); }
+            } else if (ff == JH_F_READ && ty == T_OK) fr = max(fr, (long long)r);
+        }
     }
     __shared__ long long sh[4];
     __shared__ int shi[4];
@@ -55,12 +71,22 @@ __global__ void __launch_bounds__(256) k_set_scan(const int64_t *__restrict__ ty
     }
 }
 
-__global__ void __launch_bounds__(256) k_set_range(const int64_t *__restrict__ aux, int64_t off, int64_t cnt, SetMeta *m) {
+// the final read's element range (its first element need not be 16-byte
+// aligned: the pairs start at the aligned address below it)
+__global__ void __launch_bounds__(256) k_set_range(const int64_t *__restrict__ aux, int64_t off, int64_t cnt, int vec, SetMeta *m) {
     long long lo = LLONG_MAX, hi = LLONG_MIN;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cnt;
+    const int64_t a0 = off & ~1LL, np = (off + cnt - a0 + 1) / 2;
+    const longlong2 *p2 = (const longlong2 *)(aux + a0);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np;
          i += (int64_t)gridDim.x * blockDim.x) {
-        const long long v = aux[off + i];
-        lo = min(lo, v); hi = max(hi, v);
+        const int64_t j = a0 + 2 * i;
+        if (vec && j >= off && j + 1 < off + cnt) {
+            const longlong2 x = p2[i];
+            lo = min(lo, min(x.x, x.y)); hi = max(hi, max(x.x, x.y));
+        } else {
+            for (int k = 0; k < 2; k++)
+                if (j + k >= off && j + k < off + cnt) { const long long v = aux[j + k]; lo = min(lo, v); hi = max(hi, v); }
+        }
     }
     __shared__ long long sh[4];
     lo = block_reduce256(lo, RedMin(), sh);
@@ -163,45 +189,155 @@ __global__ void __launch_bounds__(256) k_set_mark_read(const int64_t *__restrict
     mark_flush(R, tr, br);
 }
 
-// Byte-map marking (element spans up to BYTEMAP_MAX): every element sets
-// its own byte with a plain store -- idempotent, so no atomics and no
-// ordering -- and one streaming pass packs the bytes into the three bitmaps.
-// Final-read elements arrive in any order (hash order on the JVM), which
-// makes bit atomics on a 12 MB bitmap the bottleneck; byte stores are not.
-constexpr unsigned long long BYTEMAP_MAX = 1ULL << 32;
+// Dense spans (up to RB_SPAN_MAX elements): the attempts and acknowledged
+// sets go through byte maps -- plain idempotent byte stores in row order (set
+// elements are added in ascending order in Jepsen's set workloads, so the
+// stores are nearly sequential), then one packing pass -- and the final read,
+// whose elements come in any order (hash order on the JVM), is bucketed by
+// element range before its bits are set in LDS (k_rb_*): round 2 stored one
+// byte per read element straight into a byte map, and each random byte store
+// cost a 32-byte write at the memory side (WRITE_SIZE 1.5 GB for 47 M
+// elements).
+constexpr unsigned long long RB_SPAN_MAX = 1ULL << 31;
+constexpr int RB_CH = 32768;        // read elements per block of the histogram / scatter passes
+constexpr int RB_MAXBINS = 4096;    // element-range buckets
+constexpr int RB_MAXSB = 19;        // 2^19 elements per bucket at most: a 64 KB LDS bitmap
 
-// The final read is marked first (k_set_bytes_read), so the pass over the
-// rows also finds the first lost row: the lowest :ok :add whose element the
-// read lacks (lost = adds - R, checker.clj:214-215)
+// runs of one value in consecutive lanes: each lane's run start lane and the
+// run's length (one LDS atomic per run instead of per lane: sorted input puts
+// a whole wave on one address, random input spreads it)
+__device__ __forceinline__ void lane_runs(long long v, int &start, int &len) {
+    const int lane = threadIdx.x & 63;
+    const long long pv = __shfl_up(v, 1);
+    const uint64_t hm = __ballot(lane == 0 || pv != v);
+    const uint64_t upto = lane == 63 ? ~0ULL : ((2ULL << lane) - 1);
+    start = 63 - __builtin_clzll(hm & upto);
+    const uint64_t after = hm & ~upto;
+    len = (after ? __builtin_ctzll(after) : 64) - start;
+}
+
+__global__ void __launch_bounds__(256) k_rb_hist(const int64_t *__restrict__ e, int64_t cnt, long long vmin, int sb,
+                                                 int nbins, int nblk, uint32_t *__restrict__ hist) {
+    extern __shared__ uint32_t lh[];
+    for (int i = threadIdx.x; i < nbins; i += blockDim.x) lh[i] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t c0 = (int64_t)blockIdx.x * RB_CH, c1 = min(cnt, c0 + RB_CH);
+    for (int64_t base = c0; base < c1; base += 1024) {       // same trip count for every lane
+        long long v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) { const int64_t i = base + k * 256 + threadIdx.x; v[k] = i < c1 ? e[i] : 0; }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int64_t i = base + k * 256 + threadIdx.x;
+            const long long b = i < c1 ? (long long)((uint64_t)(v[k] - vmin) >> sb) : -1;
+            int s0, len;
+            lane_runs(b, s0, len);
+            if (b >= 0 && lane == s0) atomicAdd(&lh[b], (uint32_t)len);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nbins; i += blockDim.x) hist[(size_t)i * nblk + blockIdx.x] = lh[i];
+}
+
+// each element's offset in its bucket, at the bucket's next free position
+// (pos: the exclusive scan of hist, bucket-major)
+__global__ void __launch_bounds__(256) k_rb_scatter(const int64_t *__restrict__ e, int64_t cnt, long long vmin, int sb,
+                                                    int nbins, int nblk, const uint32_t *__restrict__ pos,
+                                                    uint32_t *__restrict__ out) {
+    extern __shared__ uint32_t cur[];
+    for (int i = threadIdx.x; i < nbins; i += blockDim.x) cur[i] = pos[(size_t)i * nblk + blockIdx.x];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint64_t lowm = (1ULL << sb) - 1;
+    const int64_t c0 = (int64_t)blockIdx.x * RB_CH, c1 = min(cnt, c0 + RB_CH);
+    for (int64_t base = c0; base < c1; base += 1024) {
+        long long v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) { const int64_t i = base + k * 256 + threadIdx.x; v[k] = i < c1 ? e[i] : 0; }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int64_t i = base + k * 256 + threadIdx.x;
+            const uint64_t d = (uint64_t)(v[k] - vmin);
+            const long long b = i < c1 ? (long long)(d >> sb) : -1;
+            int s0, len;
+            lane_runs(b, s0, len);
+            uint32_t p0 = 0;
+            if (b >= 0 && lane == s0) p0 = atomicAdd(&cur[b], (uint32_t)len);
+            p0 = (uint32_t)__shfl((int)p0, s0);
+            if (b >= 0) out[p0 + (uint32_t)(lane - s0)] = (uint32_t)(d & lowm);
+        }
+    }
+}
+
+// one block per bucket: its elements' bits in an LDS bitmap, then every word
+// of the bucket's range written out (so R needs no clearing)
+__global__ void __launch_bounds__(256) k_rb_build(const uint32_t *__restrict__ in, const uint32_t *__restrict__ pos,
+                                                  int nblk, int nbins, int64_t cnt, int sb, int64_t nw,
+                                                  uint32_t *__restrict__ R) {
+    extern __shared__ uint32_t bits[];
+    const int words = 1 << (sb - 5);
+    const int lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < words; i += blockDim.x) bits[i] = 0;
+    __syncthreads();
+    const int b = blockIdx.x;
+    const int64_t s0 = pos[(size_t)b * nblk];
+    const int64_t s1 = b + 1 < nbins ? (int64_t)pos[(size_t)(b + 1) * nblk] : cnt;
+    for (int64_t base = s0; base < s1; base += blockDim.x) {
+        const int64_t i = base + threadIdx.x;
+        long long w = -1;
+        uint32_t bit = 0;
+        if (i < s1) { const uint32_t x = in[i]; w = x >> 5; bit = 1u << (x & 31); }
+        // lanes holding one word OR-combined first (a segmented scan), the
+        // last lane of each run writes
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const long long wn = __shfl_up(w, o);
+            const uint32_t bn = (uint32_t)__shfl_up((int)bit, o);
+            if (lane >= o && wn == w) bit |= bn;
+        }
+        const long long wnext = __shfl_down(w, 1);
+        if (w >= 0 && (lane == 63 || wnext != w)) atomicOr(&bits[w], bit);
+    }
+    __syncthreads();
+    const int64_t w0 = (int64_t)b * words;
+    for (int i = threadIdx.x; i < words; i += blockDim.x)
+        if (w0 + i < nw) R[w0 + i] = bits[i];
+}
+
+// one pass over the rows (24 B each, row pairs): :invoke :add elements into the
+// A byte map, :ok :add elements into D, and the first lost row -- the lowest
+// :ok :add whose element the final read R lacks (lost = adds - R,
+// checker.clj:214-215)
 __global__ void __launch_bounds__(256) k_set_bytes_rows(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
                                                         const int64_t *__restrict__ val, int64_t n, long long vmin,
                                                         uint8_t *__restrict__ Ab, uint8_t *__restrict__ Db,
-                                                        const uint8_t *__restrict__ Rb, SetMeta *m) {
+                                                        const uint32_t *__restrict__ R, int vec, SetMeta *m) {
     unsigned long long best = ~0ULL;
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-        if (f[r] != JH_F_ADD) continue;
-        const int64_t ty = type[r];
-        if (ty == T_INVOKE) Ab[val[r] - vmin] = 1;
-        else if (ty == T_OK) {
-            const int64_t b = val[r] - vmin;
-            Db[b] = 1;
-            if (!Rb[b]) best = min(best, (unsigned long long)r);
+    const int64_t np = (n + 1) / 2;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np; i += (int64_t)gridDim.x * blockDim.x) {
+        const longlong2 t2 = ld_pair(type, i, n, vec), f2 = ld_pair(f, i, n, vec), v2 = ld_pair(val, i, n, vec);
+        const int64_t tt[2] = {t2.x, t2.y}, ffs[2] = {f2.x, f2.y}, vv[2] = {v2.x, v2.y};
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int64_t r = 2 * i + k;
+            if (r >= n || ffs[k] != JH_F_ADD) continue;
+            const int64_t b = vv[k] - vmin;
+            if (tt[k] == T_INVOKE) Ab[b] = 1;
+            else if (tt[k] == T_OK) {
+                Db[b] = 1;
+                if (!((R[b >> 5] >> (b & 31)) & 1)) best = min(best, (unsigned long long)r);
+            }
         }
     }
     for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o));
     if ((threadIdx.x & 63) == 0 && best != ~0ULL) atomicMin(&m->first_lost_row, best);
 }
 
-__global__ void __launch_bounds__(256) k_set_bytes_read(const int64_t *__restrict__ aux, int64_t off, int64_t cnt,
-                                                        long long vmin, uint8_t *__restrict__ Rb) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * blockDim.x)
-        Rb[aux[off + i] - vmin] = 1;
-}
-
-// 32 bytes -> one bitmap word, for each of A, D, R
+// 32 bytes -> one bitmap word, for each of A and D
 __global__ void __launch_bounds__(256) k_set_pack_bits(const uint8_t *__restrict__ bytes, int64_t span_pad, int64_t nw,
                                                        uint32_t *__restrict__ bits) {
-    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < 3 * nw; w += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < 2 * nw; w += (int64_t)gridDim.x * blockDim.x) {
         const int64_t s = w / nw, ww = w - s * nw;
         const uint4 *src = (const uint4 *)(bytes + s * span_pad + ww * 32);
         const uint4 a = src[0], b = src[1];
@@ -338,7 +474,8 @@ static bool set_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, S
     memset(&mi, 0, sizeof mi);
     mi.vmin = LLONG_MAX; mi.vmax = LLONG_MIN; mi.final_row = -1; mi.first_lost_row = ~0ULL;
     HIP_TRY(hipMemcpyAsync(m, &mi, sizeof mi, hipMemcpyHostToDevice, st));
-    if (n > 0) k_set_scan<<<grid_for(n, 256, 4096), 256, 0, st>>>(dh->type, dh->f, dh->value, n, m);
+    const int vec = ((uintptr_t)dh->type | (uintptr_t)dh->f | (uintptr_t)dh->value) % 16 == 0;
+    if (n > 0) k_set_scan<<<grid_for((n + 1) / 2, 256, 4096), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vec, m);
     HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     res->final_read_entry = mh.final_row;
@@ -353,7 +490,7 @@ static bool set_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, S
     if (!dh->aux && rd[1] > 0) throw_jh(JH_EINVAL, "set read without an aux element array");
     const int64_t off = rd[0], cnt = rd[1];
     if (cnt > 0)
-        k_set_range<<<grid_for(cnt, 256, 4096), 256, 0, st>>>(dh->aux, off, cnt, m);
+        k_set_range<<<grid_for(cnt / 2 + 1, 256, 4096), 256, 0, st>>>(dh->aux, off, cnt, (uintptr_t)dh->aux % 16 == 0, m);
     HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     vmin = mh.vmin;
@@ -364,20 +501,36 @@ static bool set_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, S
     nw = (int64_t)((span + 31) / 32);
     uint32_t *bits = ctx->ws<uint32_t>(WS_S_BITS, 3 * nw);
     A = bits; D = bits + nw; R = bits + 2 * nw;
-    // byte maps (plain idempotent stores, then one packing pass) when the span
-    // is dense enough for 3 bytes per element of span to be cheap next to the
-    // history; sparse or huge spans mark the bitmaps directly (a
-    // sparse set over a wide range no longer allocates 3 x span bytes)
-    if (span <= BYTEMAP_MAX && span <= 8ULL * (unsigned long long)(n + cnt) + 4096) {
+    // dense spans: A / D byte maps, R bucketed (k_rb_*); sparse or huge spans
+    // mark the bitmaps directly (a sparse set over a wide range does
+    // not allocate a byte per element of span)
+    int sb = 5;
+    while (sb < RB_MAXSB && (span >> sb) > 1024) sb++;
+    const int nbins = (int)((span + (1ULL << sb) - 1) >> sb);
+    if (span <= RB_SPAN_MAX && nbins <= RB_MAXBINS && span <= 8ULL * (unsigned long long)(n + cnt) + 4096) {
+        if (cnt > 0) {
+            const int nblk = (int)((cnt + RB_CH - 1) / RB_CH);
+            const size_t nh = (size_t)nbins * nblk;
+            uint32_t *hist = ctx->ws<uint32_t>(WS_S_RB_HIST, 2 * nh + 1);
+            uint32_t *pos = hist + nh;
+            uint32_t *rin = ctx->ws<uint32_t>(WS_S_RB_OUT, cnt);
+            const int64_t *e = dh->aux + off;
+            k_rb_hist<<<nblk, 256, nbins * 4, st>>>(e, cnt, vmin, sb, nbins, nblk, hist);
+            size_t tb = 0;
+            HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, hist, pos, (int)nh, st));
+            HIP_TRY(hipcub::DeviceScan::ExclusiveSum(ctx->ws<char>(WS_S_TMP, tb), tb, hist, pos, (int)nh, st));
+            k_rb_scatter<<<nblk, 256, nbins * 4, st>>>(e, cnt, vmin, sb, nbins, nblk, pos, rin);
+            k_rb_build<<<nbins, 256, (1 << sb) / 8, st>>>(rin, pos, nblk, nbins, cnt, sb, nw, R);
+        } else {
+            HIP_TRY(hipMemsetAsync(R, 0, sizeof(uint32_t) * nw, st));
+        }
         const int64_t span_pad = nw * 32;
-        uint8_t *bytes = ctx->ws<uint8_t>(WS_S_BYTES, 3 * span_pad);
-        HIP_TRY(hipMemsetAsync(bytes, 0, 3 * span_pad, st));
-        if (cnt > 0)
-            k_set_bytes_read<<<grid_for(cnt, 256, 16384), 256, 0, st>>>(dh->aux, off, cnt, vmin, bytes + 2 * span_pad);
+        uint8_t *bytes = ctx->ws<uint8_t>(WS_S_BYTES, 2 * span_pad);
+        HIP_TRY(hipMemsetAsync(bytes, 0, 2 * span_pad, st));
         if (n > 0)
-            k_set_bytes_rows<<<grid_for(n, 256, 16384), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, bytes,
-                                                                     bytes + span_pad, bytes + 2 * span_pad, m);
-        k_set_pack_bits<<<grid_for(3 * nw, 256, 16384), 256, 0, st>>>(bytes, span_pad, nw, bits);
+            k_set_bytes_rows<<<grid_for((n + 1) / 2, 256, 16384), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, bytes,
+                                                                               bytes + span_pad, R, vec, m);
+        k_set_pack_bits<<<grid_for(2 * nw, 256, 16384), 256, 0, st>>>(bytes, span_pad, nw, bits);
     } else {
         HIP_TRY(hipMemsetAsync(bits, 0, sizeof(uint32_t) * 3 * nw, st));
         if (n > 0) k_set_mark_rows<<<(unsigned)((n + MARK_CH - 1) / MARK_CH), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, A, D);

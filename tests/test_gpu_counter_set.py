@@ -124,3 +124,96 @@ def test_set_edge_cases(ctx):
     c = oracle.check_set(cols)
     _set_same(ctx.check_set(cols), c)
     _bits_same(ctx.check_set_bitmaps(cols), c)
+
+
+def test_counter_many_procs(ctx):
+    """More processes than a chunk's compact pairing index (32): their
+    invocations take the spill walk from the next row; heavy :info makes many
+    walks start at the chunk's end (crashed ops, retired processes)."""
+    cols = synth.counter(n_ops=300000, n_procs=300, read_every=11, p_fail=0.05, p_info=0.1,
+                         n_bad_reads=5, seed=9)
+    g = ctx.check_counter(cols)
+    c = oracle.check_counter(cols)
+    assert (g["valid"], g["cause"], g["n_reads"], g["n_errors"], g["first_err_entry"]) == \
+        (c["valid"], c["cause"], c["n_reads"], c["n_errors"], c["first_err_entry"])
+    assert (g["reads"] == c["reads"]).all()
+
+
+def test_counter_host_buffer(ctx):
+    """Triples into a reused page-locked buffer (jh_host_alloc): same result."""
+    from jepsen_amd._native import HostBuffer
+    cols = synth.counter(n_ops=100000, n_procs=10, read_every=11, p_fail=0.05, p_info=0.02,
+                         n_bad_reads=2, seed=4)
+    hb = HostBuffer(3 * int(cols.n), np.int64)
+    c = oracle.check_counter(cols)
+    for _ in range(2):
+        g = ctx.check_counter(cols, out=hb.array)
+        assert (g["reads"] == c["reads"]).all() and g["n_errors"] == c["n_errors"]
+
+
+class _DevCols:
+    """The columns copied to device memory (hipMalloc through the HIP runtime
+    libjh.so already loaded -- no second runtime from torch in this process),
+    each starting `shift` int64s into its allocation (shift 1: 8-byte aligned
+    only)."""
+
+    def __init__(self, cols, shift):
+        import ctypes as C
+        from jepsen_amd import _native
+        _native.lib()
+        path = next((ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln), "libamdhip64.so")
+        self._hip = hip = C.CDLL(path)
+        hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        hip.hipFree.argtypes = [C.c_void_p]
+        self._bufs = []
+        self.n, self.n_keys = int(cols.n), int(cols.n_keys)
+
+        def put(a):
+            a = np.ascontiguousarray(a, dtype=np.int64)
+            p = C.c_void_p()
+            assert hip.hipMalloc(C.byref(p), 8 * (len(a) + shift + 1)) == 0
+            self._bufs.append(p)
+            dst = p.value + 8 * shift
+            assert hip.hipMemcpy(dst, a.ctypes.data, 8 * len(a), 1) == 0       # hipMemcpyHostToDevice
+            return dst
+        for k in ("process", "type", "f", "key", "value", "value2"):
+            setattr(self, k, put(getattr(cols, k)))
+        self.aux, self.n_aux = put(cols.aux), len(cols.aux)
+
+    def __del__(self):
+        for p in getattr(self, "_bufs", []):
+            self._hip.hipFree(p)
+
+
+@pytest.mark.parametrize("shift", [0, 1])
+def test_set_device_columns_alignment(ctx, shift):
+    """Device-resident columns 16-byte aligned (row pairs in one load) and only
+    8-byte aligned (two loads per pair): same result as the oracle."""
+    cols = synth.set_history(n_adds=200001, n_procs=10, p_fail=0.05, p_info=0.03,
+                             n_lost=5, n_unexpected=2, seed=11)
+    c = oracle.check_set(cols)
+    d = _DevCols(cols, shift)
+    _bits_same(ctx.check_set_bitmaps(d, words_cap=1 << 16, on_device=True), c)
+    _set_same(ctx.check_set(d, runs_cap=int(cols.n) + 8, on_device=True), c)
+
+
+def test_set_sparse_span(ctx):
+    """Elements spread over a span far wider than the history: the direct
+    bitmap path (no byte maps, no buckets)."""
+    inv = lambda p, f, v: {"process": p, "type": "invoke", "f": f, "value": v}
+    ok = lambda p, f, v: {"process": p, "type": "ok", "f": f, "value": v}
+    h, els = [], []
+    for i in range(400):
+        v = i * 100_003 if i % 2 else -i * 77_777
+        h += [inv(i % 5, "add", v), ok(i % 5, "add", v)]
+        if i % 9:
+            els.append(v)
+    els.append(5)                       # never attempted: unexpected
+    rng = np.random.default_rng(3)
+    rng.shuffle(els)
+    h += [inv(7, "read", None), ok(7, "read", [int(x) for x in els])]
+    cols = H.encode(h, keyed=False)
+    c = oracle.check_set(cols)
+    _set_same(ctx.check_set(cols), c)
+    _bits_same(ctx.check_set_bitmaps(cols, words_cap=1 << 22), c)

@@ -76,7 +76,11 @@ def main():
     cols = synth.counter(n_ops=half, n_procs=10, read_every=101, p_fail=0.05, p_info=0.01,
                          n_bad_reads=10, seed=2)
     d = DevCols(cols, dev)
-    r, sec = timed(lambda: ctx.check_counter(d, reads_cap=1 << 24, on_device=True), args.steps, args.warmup)
+    # the triples land in a reused page-locked buffer (jh_host_alloc), as a
+    # JNA shim would keep one per checker
+    reads_buf = _native.HostBuffer(3 << 20, np.int64)
+    r, sec = timed(lambda: ctx.check_counter(d, reads_cap=1 << 20, on_device=True, out=reads_buf.array),
+                   args.steps, args.warmup)
     n = int(cols.n)
     alg = 56.0 * n + 24.0 * r["n_reads"]
     cpu = None
@@ -108,7 +112,9 @@ def main():
     d = DevCols(cols, dev)
     # the product path: the four result sets come back as bitmaps (4 B per 32
     # elements of span); the runs output (16 B per run) is timed beside it
-    r, sec = timed(lambda: ctx.check_set_bitmaps(d, words_cap=1 << 22, on_device=True), args.steps, args.warmup)
+    bit_bufs = [_native.HostBuffer(1 << 22, np.uint32) for _ in range(4)]
+    r, sec = timed(lambda: ctx.check_set_bitmaps(d, words_cap=1 << 22, on_device=True,
+                                                 out=[b.array for b in bit_bufs]), args.steps, args.warmup)
     _, sec_runs = timed(lambda: ctx.check_set(d, runs_cap=1 << 25, on_device=True), 2, 1)
     n = int(cols.n)
     alg = 56.0 * n + 8.0 * d.n_aux + 16.0 * r["n_words"]

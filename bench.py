@@ -54,9 +54,9 @@ def pmc_traffic(workload, seed, kernel):
 # the time, of the memo probes, of the entries of the keys searched, kernel)
 PHASES = {
     "phase1": ("dfs_ms", "memo_probes", None, "k_lin_dfs<true>"),
-    "phase2_lean": ("seq_ms", "seq_probes", "lean_entries", "k_lin_seq3<true>"),
+    "phase2_lean": ("seq_ms", "seq_probes", "lean_entries", "k_lin_seq_lw"),   # LEAN role of the two-role grid
     "phase3_lean": ("p3_ms", "p3_probes", "lean_entries", "k_lin_seq3<true>"),
-    "wide": ("wide_ms", "wide_probes", "wide_entries", "k_lin_seqw"),
+    "wide": ("wide_ms", "wide_probes", "wide_entries", "k_lin_seq_lw"),         # its WIDE role (phase 3: k_lin_seqw)
     "xw": ("xw_ms", "xw_probes", "xw_entries", "k_lin_xw"),
 }
 

@@ -199,7 +199,7 @@ __global__ void __launch_bounds__(256) k_set_mark_read(const int64_t *__restrict
 // cost a 32-byte write at the memory side (WRITE_SIZE 1.5 GB for 47 M
 // elements).
 constexpr unsigned long long RB_SPAN_MAX = 1ULL << 31;
-constexpr int RB_CH = 32768;        // read elements per block of the histogram / scatter passes
+constexpr int RB_CH = 8192;         // read elements per block of the histogram / scatter passes
 constexpr int RB_MAXBINS = 4096;    // element-range buckets
 constexpr int RB_MAXSB = 19;        // 2^19 elements per bucket at most: a 64 KB LDS bitmap
 
@@ -241,23 +241,53 @@ __global__ void __launch_bounds__(256) k_rb_hist(const int64_t *__restrict__ e, 
 }
 
 // each element's offset in its bucket, at the bucket's next free position
-// (pos: the exclusive scan of hist, bucket-major)
+// (pos: the exclusive scan of hist, bucket-major). The block's elements are
+// first sorted by bucket in LDS, then written out as one contiguous run per
+// bucket: a 4-byte store per element to a random bucket cost a 32-byte write
+// at the memory side.
 __global__ void __launch_bounds__(256) k_rb_scatter(const int64_t *__restrict__ e, int64_t cnt, long long vmin, int sb,
-                                                    int nbins, int nblk, const uint32_t *__restrict__ pos,
-                                                    uint32_t *__restrict__ out) {
-    extern __shared__ uint32_t cur[];
-    for (int i = threadIdx.x; i < nbins; i += blockDim.x) cur[i] = pos[(size_t)i * nblk + blockIdx.x];
+                                                    int nbins, int nblk, const uint32_t *__restrict__ hist,
+                                                    const uint32_t *__restrict__ pos, uint32_t *__restrict__ out) {
+    extern __shared__ uint32_t lds_rb[];
+    uint32_t *loff = lds_rb, *gb = loff + nbins, *cur = gb + nbins;
+    uint32_t *st_low = cur + nbins;
+    uint16_t *st_bin = (uint16_t *)(st_low + RB_CH);
+    __shared__ uint32_t part[256];
+    const int tid = threadIdx.x, lane = tid & 63;
+    // the block's bucket counts -> local offsets (a block scan over the buckets)
+    const int per = (nbins + 255) / 256;
+    uint32_t acc = 0;
+    for (int k = 0; k < per; k++) {
+        const int bi = tid * per + k;
+        if (bi < nbins) acc += hist[(size_t)bi * nblk + blockIdx.x];
+    }
+    part[tid] = acc;
     __syncthreads();
-    const int lane = threadIdx.x & 63;
+    for (int o = 1; o < 256; o <<= 1) {
+        const uint32_t v = tid >= o ? part[tid - o] : 0u;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    acc = part[tid] - acc;                          // exclusive prefix of this thread's first bucket
+    for (int k = 0; k < per; k++) {
+        const int bi = tid * per + k;
+        if (bi < nbins) {
+            loff[bi] = acc; cur[bi] = acc;
+            gb[bi] = pos[(size_t)bi * nblk + blockIdx.x];
+            acc += hist[(size_t)bi * nblk + blockIdx.x];
+        }
+    }
+    __syncthreads();
     const uint64_t lowm = (1ULL << sb) - 1;
     const int64_t c0 = (int64_t)blockIdx.x * RB_CH, c1 = min(cnt, c0 + RB_CH);
     for (int64_t base = c0; base < c1; base += 1024) {
         long long v[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) { const int64_t i = base + k * 256 + threadIdx.x; v[k] = i < c1 ? e[i] : 0; }
+        for (int k = 0; k < 4; k++) { const int64_t i = base + k * 256 + tid; v[k] = i < c1 ? e[i] : 0; }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const int64_t i = base + k * 256 + threadIdx.x;
+            const int64_t i = base + k * 256 + tid;
             const uint64_t d = (uint64_t)(v[k] - vmin);
             const long long b = i < c1 ? (long long)(d >> sb) : -1;
             int s0, len;
@@ -265,14 +295,24 @@ __global__ void __launch_bounds__(256) k_rb_scatter(const int64_t *__restrict__ 
             uint32_t p0 = 0;
             if (b >= 0 && lane == s0) p0 = atomicAdd(&cur[b], (uint32_t)len);
             p0 = (uint32_t)__shfl((int)p0, s0);
-            if (b >= 0) out[p0 + (uint32_t)(lane - s0)] = (uint32_t)(d & lowm);
+            if (b >= 0) {
+                const uint32_t lp = p0 + (uint32_t)(lane - s0);
+                st_low[lp] = (uint32_t)(d & lowm);
+                st_bin[lp] = (uint16_t)b;
+            }
         }
+    }
+    __syncthreads();
+    const int nb = (int)(c1 - c0);
+    for (int i = tid; i < nb; i += 256) {
+        const uint32_t bi = st_bin[i];
+        out[gb[bi] + ((uint32_t)i - loff[bi])] = st_low[i];
     }
 }
 
 // one block per bucket: its elements' bits in an LDS bitmap, then every word
 // of the bucket's range written out (so R needs no clearing)
-__global__ void __launch_bounds__(256) k_rb_build(const uint32_t *__restrict__ in, const uint32_t *__restrict__ pos,
+__global__ void __launch_bounds__(1024) k_rb_build(const uint32_t *__restrict__ in, const uint32_t *__restrict__ pos,
                                                   int nblk, int nbins, int64_t cnt, int sb, int64_t nw,
                                                   uint32_t *__restrict__ R) {
     extern __shared__ uint32_t bits[];
@@ -283,21 +323,34 @@ __global__ void __launch_bounds__(256) k_rb_build(const uint32_t *__restrict__ i
     const int b = blockIdx.x;
     const int64_t s0 = pos[(size_t)b * nblk];
     const int64_t s1 = b + 1 < nbins ? (int64_t)pos[(size_t)(b + 1) * nblk] : cnt;
-    for (int64_t base = s0; base < s1; base += blockDim.x) {
-        const int64_t i = base + threadIdx.x;
-        long long w = -1;
-        uint32_t bit = 0;
-        if (i < s1) { const uint32_t x = in[i]; w = x >> 5; bit = 1u << (x & 31); }
-        // lanes holding one word OR-combined first (a segmented scan), the
-        // last lane of each run writes
+    // eight elements per thread in flight; lanes holding one word are
+    // OR-combined first (a segmented scan) only when neighbouring lanes share
+    // words at all (sorted input), else each lane sets its bit directly
+    for (int64_t base = s0; base < s1; base += 8 * (int64_t)blockDim.x) {
+        uint32_t xs[8];
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const long long wn = __shfl_up(w, o);
-            const uint32_t bn = (uint32_t)__shfl_up((int)bit, o);
-            if (lane >= o && wn == w) bit |= bn;
+        for (int k = 0; k < 8; k++) {
+            const int64_t i = base + k * (int64_t)blockDim.x + threadIdx.x;
+            xs[k] = i < s1 ? in[i] : ~0u;
         }
-        const long long wnext = __shfl_down(w, 1);
-        if (w >= 0 && (lane == 63 || wnext != w)) atomicOr(&bits[w], bit);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const long long w = xs[k] != ~0u ? (long long)(xs[k] >> 5) : -1;
+            uint32_t bit = xs[k] != ~0u ? 1u << (xs[k] & 31) : 0u;
+            const long long pw = __shfl_up(w, 1);
+            if (__ballot(lane > 0 && w >= 0 && pw == w)) {
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const long long wn = __shfl_up(w, o);
+                    const uint32_t bn = (uint32_t)__shfl_up((int)bit, o);
+                    if (lane >= o && wn == w) bit |= bn;
+                }
+                const long long wnext = __shfl_down(w, 1);
+                if (w >= 0 && (lane == 63 || wnext != w)) atomicOr(&bits[w], bit);
+            } else if (w >= 0) {
+                atomicOr(&bits[w], bit);
+            }
+        }
     }
     __syncthreads();
     const int64_t w0 = (int64_t)b * words;
@@ -505,7 +558,7 @@ static bool set_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, S
     // mark the bitmaps directly (a sparse set over a wide range does
     // not allocate a byte per element of span)
     int sb = 5;
-    while (sb < RB_MAXSB && (span >> sb) > 1024) sb++;
+    while (sb < RB_MAXSB && (span >> sb) > 256) sb++;
     const int nbins = (int)((span + (1ULL << sb) - 1) >> sb);
     if (span <= RB_SPAN_MAX && nbins <= RB_MAXBINS && span <= 8ULL * (unsigned long long)(n + cnt) + 4096) {
         if (cnt > 0) {
@@ -519,8 +572,10 @@ static bool set_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, S
             size_t tb = 0;
             HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, hist, pos, (int)nh, st));
             HIP_TRY(hipcub::DeviceScan::ExclusiveSum(ctx->ws<char>(WS_S_TMP, tb), tb, hist, pos, (int)nh, st));
-            k_rb_scatter<<<nblk, 256, nbins * 4, st>>>(e, cnt, vmin, sb, nbins, nblk, pos, rin);
-            k_rb_build<<<nbins, 256, (1 << sb) / 8, st>>>(rin, pos, nblk, nbins, cnt, sb, nw, R);
+            const int sc_lds = nbins * 12 + RB_CH * 6;
+            HIP_TRY(hipFuncSetAttribute((const void *)k_rb_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, sc_lds));
+            k_rb_scatter<<<nblk, 256, sc_lds, st>>>(e, cnt, vmin, sb, nbins, nblk, hist, pos, rin);
+            k_rb_build<<<nbins, 1024, (1 << sb) / 8, st>>>(rin, pos, nblk, nbins, cnt, sb, nw, R);
         } else {
             HIP_TRY(hipMemsetAsync(R, 0, sizeof(uint32_t) * nw, st));
         }

@@ -19,17 +19,19 @@
 //                 of every process (LDS-privatised) and the add-value range  32 / 4
 //   k_cnt_pair_spill  the few invocations the chunk could not pair (thread
 //                 per spill, walks its process' rows): completes their words ~0
-//   k_cnt_tile_sums / hipcub scan / k_cnt_tile_scan
+//   hipcub scan / k_cnt_tile_scan
 //                 reduce-then-scan of {lower, upper, reads} over 2048-row
-//                 tiles of contribution words; writes only at read rows (the
-//                 ok read's row and upper, the invoke read's lower)       2 x 4 / ~0
+//                 tiles of contribution words: each tile's sums come from the
+//                 pack (a tile is a chunk) plus atomics of k_cnt_pair_spill,
+//                 so one scan pass reads the words; writes only at read rows
+//                 (the ok read's row and upper, the invoke read's lower)    4 / ~0
 //   k_cnt_triples the triples, in history order, errors, first failing row
 //                 (over the ~1% read rows only)
 // Round 2 packed a 4-byte row code and re-read code, pair and value (16 B per
-// row) in both scan passes; the contribution word carries what they need.
-// (A single-pass decoupled look-back scan over the 49 K tiles was measured
-// at 20.8 ms on MI355X: the tile-to-tile look-back chain is serial latency
-// across XCDs. Reduce-then-scan costs one extra 4 B/row read.)
+// row) in both scan passes; the contribution word carries what they need, and
+// round 3 folds the reduce pass into the pack. (A single-pass decoupled
+// look-back scan over the 49 K tiles was measured at 20.8 ms on MI355X: the
+// tile-to-tile look-back chain is serial latency across XCDs.)
 #include "jh_internal.h"
 #include <hipcub/hipcub.hpp>
 
@@ -105,24 +107,41 @@ __global__ void __launch_bounds__(256) k_cnt_prange(const int64_t *__restrict__ 
 // reads per row. Invocations with no completion in the chunk, or of a
 // process beyond the first PAIR_PROCS, go to a spill list (k_cnt_pair_spill)
 // and their words stay CW_PEND until it completes them.
+// per-row contributions and prefixes of lower / upper / ok reads (an :ok
+// :read still marked U has no invocation: an orphan, never a read row, so
+// pair is only ever read where it was written)
+struct CntAcc {
+    long long lo, hi;
+    int nr, flags;
+};
+
+// Reduce-then-scan over tiles of CNT_TILE rows. A tile is a pack chunk: the
+// pack writes each tile's sums {lower, upper, ok reads} (k_cnt_pair_spill adds
+// what the spilled invocations complete), then one scan pass reads the
+// contribution words (4 B per row).
+constexpr int CNT_TILE = 2048, CNT_PER = CNT_TILE / 256;
+static_assert(CNT_TILE == CHUNK, "a counter tile is a pack chunk");
 constexpr int PAIR_PROCS = 32, PAIR_GROUPS = CHUNK / 64;
-constexpr int PER = CHUNK / 256;            // rows per thread per chunk (row k * 256 + tid)
-// One chunk per block; 36 KB of LDS and < 128 VGPRs give four blocks per CU
-// (round 2: 50 KB, three blocks, 1.59 ms per 100 M rows), so more chunks'
-// loads are in flight while others pair in LDS.
+constexpr int PACK_THREADS = 512;
+constexpr int PER = CHUNK / PACK_THREADS;   // rows per thread per chunk (row k * PACK_THREADS + tid)
+// One chunk per 512-thread block (four rows per thread), 32 KB of LDS (round
+// 2: 256 threads and 50 KB: 1.59 ms per 100 M rows). Measured against it:
+// 256-thread blocks at four and six per CU (1.34 / 1.44 ms) and a chunk per
+// wave with the pairing done by ballots instead of LDS (1.61 ms: ~200 VALU
+// instructions per row).
 // A spilled invocation is stored as its row when its walk must start right
 // after it (a process beyond the chunk's first PAIR_PROCS), as ~row when the
 // chunk already showed every later row of its process in the chunk to be
 // :info, so the walk starts at the chunk's end (a crashed op's walk then ends
 // at once: its process' last row lies inside the chunk).
-__global__ void __launch_bounds__(256, 4) k_cnt_pack(const int64_t *__restrict__ proc,
+__global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__restrict__ proc,
                                                   const int64_t *__restrict__ type,
                                                   const int64_t *__restrict__ f,
                                                   const int64_t *__restrict__ val, int64_t n,
                                                   long long pmin, int32_t *__restrict__ last,
                                                   uint32_t *__restrict__ cw, int32_t *__restrict__ pair,
-                                                  int32_t *__restrict__ spill, unsigned int *__restrict__ n_spill,
-                                                  CntMeta *m) {
+                                                  int32_t *__restrict__ spill, int32_t *__restrict__ spill_n,
+                                                  CntMeta *m, CntAcc *__restrict__ agg) {
     __shared__ uint32_t hk[HSLOTS];                 // process - pmin + 1 (0: empty)
     __shared__ int hv[HSLOTS];                      // its last row
     __shared__ int8_t hc[HSLOTS];                   // its compact index, -1 beyond PAIR_PROCS
@@ -130,11 +149,11 @@ __global__ void __launch_bounds__(256, 4) k_cnt_pack(const int64_t *__restrict__
     __shared__ int16_t sp[CHUNK];                   // each row's partner in the chunk (-1: none)
     __shared__ int16_t rs[CHUNK];                   // each row's hash slot (-1: none)
     __shared__ unsigned long long M[PAIR_GROUPS][PAIR_PROCS];
-    __shared__ int nd, nls, gbase;
-    __shared__ int32_t ls[CHUNK];                   // this chunk's spilled invocations
-    __shared__ long long sh[4];
+    __shared__ int nd, nls;
+    __shared__ long long sh[5][PACK_THREADS / 64];
     const int tid = threadIdx.x;
     long long am = 0, na = 0;
+    long long t_lo = 0, t_hi = 0, t_nr = 0;          // this tile's sums
     {
         const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
         const int nc = (int)min<int64_t>(CHUNK, n - c0);
@@ -143,7 +162,7 @@ __global__ void __launch_bounds__(256, 4) k_cnt_pack(const int64_t *__restrict__
         long long rp[PER], rt[PER], rf[PER], cv[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int64_t r = c0 + k * 256 + tid;
+            const int64_t r = c0 + k * PACK_THREADS + tid;
             if (r < n) { rp[k] = proc[r]; rt[k] = type[r]; rf[k] = f[r]; cv[k] = val[r]; }
             else { rp[k] = pmin; rt[k] = T_INFO; rf[k] = 0; cv[k] = 0; }
         }
@@ -154,13 +173,13 @@ __global__ void __launch_bounds__(256, 4) k_cnt_pack(const int64_t *__restrict__
             const uint32_t f2 = rf[k] == JH_F_ADD ? F2_ADD : rf[k] == JH_F_READ ? F2_READ : F2_OTHER;
             cx[k] = (f2 << 2) | (uint32_t)(rt[k] & 3);
         }
-        for (int i = tid; i < HSLOTS; i += 256) { hk[i] = 0; hv[i] = -1; hc[i] = -1; }
-        for (int i = tid; i < PAIR_GROUPS * PAIR_PROCS; i += 256) (&M[0][0])[i] = 0;
+        for (int i = tid; i < HSLOTS; i += PACK_THREADS) { hk[i] = 0; hv[i] = -1; hc[i] = -1; }
+        for (int i = tid; i < PAIR_GROUPS * PAIR_PROCS; i += PACK_THREADS) (&M[0][0])[i] = 0;
         if (tid == 0) { nd = 0; nls = 0; }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int i = k * 256 + tid;
+            const int i = k * PACK_THREADS + tid;
             if (i >= nc) break;
             const int64_t r = c0 + i;
             const uint32_t pk = cp[k];
@@ -196,14 +215,12 @@ __global__ void __launch_bounds__(256, 4) k_cnt_pack(const int64_t *__restrict__
             rs[i] = (int16_t)slot;
         }
         __syncthreads();
-        for (int i = tid; i < HSLOTS; i += 256)
-            if (hk[i]) atomicMax(&last[hk[i] - 1], hv[i]);
         // compact process index of every row (the hash is complete now), and the
         // group masks of non-:info rows
         int8_t rc[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int i = k * 256 + tid;
+            const int i = k * PACK_THREADS + tid;
             rc[k] = -1;
             if (i >= nc) continue;
             const int slot = rs[i];
@@ -215,7 +232,7 @@ __global__ void __launch_bounds__(256, 4) k_cnt_pack(const int64_t *__restrict__
         bool walk_from_end[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int i = k * 256 + tid;
+            const int i = k * PACK_THREADS + tid;
             walk_from_end[k] = false;
             if (i >= nc) continue;
             const uint32_t x = sc[i];
@@ -242,7 +259,7 @@ __global__ void __launch_bounds__(256, 4) k_cnt_pack(const int64_t *__restrict__
         // the contribution words
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int i = k * 256 + tid;
+            const int i = k * PACK_THREADS + tid;
             if (i >= nc) continue;
             const uint32_t x = sc[i];
             const uint32_t ty = x & 3, f2 = x >> 2;
@@ -252,7 +269,8 @@ __global__ void __launch_bounds__(256, 4) k_cnt_pack(const int64_t *__restrict__
             if (ty == T_INVOKE) {
                 if (c == -1) {
                     // spills gather in LDS: one global atomic per chunk
-                    ls[atomicAdd(&nls, 1)] = walk_from_end[k] ? ~(int32_t)r : (int32_t)r;
+                    // the chunk's own spill region: no global atomic
+                    spill[c0 + atomicAdd(&nls, 1)] = walk_from_end[k] ? ~(int32_t)r : (int32_t)r;
                     w = f2 == F2_READ ? CW_INVREAD : f2 == F2_ADD ? CW_PEND : CW_NONE;
                 } else if (f2 == F2_READ) {
                     w = CW_INVREAD;
@@ -265,6 +283,7 @@ __global__ void __launch_bounds__(256, 4) k_cnt_pack(const int64_t *__restrict__
                     else {
                         w = cw_make(CW_HI, v);
                         if ((w & CW_X) && !own) pair[r] = (int32_t)(c0 + c);
+                        t_hi += v;
                     }
                 }
             } else if (ty == T_OK || ty == T_FAIL) {
@@ -272,31 +291,43 @@ __global__ void __launch_bounds__(256, 4) k_cnt_pack(const int64_t *__restrict__
                 if (ty == T_OK && f2 == F2_ADD) {
                     const long long v = cv[k];
                     if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
-                    else w = cw_make(CW_LO, v);
+                    else { w = cw_make(CW_LO, v); t_lo += v; }
                 } else if (ty == T_OK && f2 == F2_READ) {
                     // its pending read must come from an [:invoke :read] (checker.clj:713-716)
                     if (c >= 0 && (sc[c] >> 2) != F2_READ)
                         atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_ORPHAN);
                     else {
                         w = CW_OKREAD;
-                        if (c >= 0) pair[r] = (int32_t)(c0 + c);
+                        if (c >= 0) { pair[r] = (int32_t)(c0 + c); t_nr++; }   // U-marked: counted when claimed
                     }
                 }
                 w |= u;
             }
             cw[r] = w;
         }
-        __syncthreads();
-        if (tid == 0 && nls) gbase = (int)atomicAdd(n_spill, (unsigned int)nls);
-        __syncthreads();
-        for (int k = tid; k < nls; k += 256) spill[gbase + k] = ls[k];
     }
-    am = block_reduce256(am, RedMax(), sh);
-    na = block_reduce256(na, RedSum(), sh);
+    for (int o = 32; o > 0; o >>= 1) {
+        am = max(am, (long long)__shfl_xor(am, o)); na += (long long)__shfl_xor(na, o);
+        t_lo += (long long)__shfl_xor(t_lo, o); t_hi += (long long)__shfl_xor(t_hi, o); t_nr += (long long)__shfl_xor(t_nr, o);
+    }
+    if ((tid & 63) == 0) {
+        sh[0][tid >> 6] = am; sh[1][tid >> 6] = na; sh[2][tid >> 6] = t_lo; sh[3][tid >> 6] = t_hi; sh[4][tid >> 6] = t_nr;
+    }
+    __syncthreads();                                  // (also orders every nls increment)
     if (tid == 0) {
+        for (int w = 1; w < PACK_THREADS / 64; w++) {
+            am = max(am, sh[0][w]); na += sh[1][w]; t_lo += sh[2][w]; t_hi += sh[3][w]; t_nr += sh[4][w];
+        }
+        agg[blockIdx.x] = CntAcc{t_lo, t_hi, (int)t_nr, 0};
+        spill_n[blockIdx.x] = nls;
         if (am) atomicMax(&m->amax_abs, am);
         if (na) atomicAdd((unsigned long long *)&m->n_add, (unsigned long long)na);
     }
+    // the last row of each of the chunk's processes, after the last barrier
+    // (these few atomics hit the same addresses from every block: no barrier
+    // waits on them)
+    for (int i = tid; i < HSLOTS; i += PACK_THREADS)
+        if (hk[i]) atomicMax(&last[hk[i] - 1], hv[i]);
 }
 
 // the spilled invocations: one thread each walks its process' rows forward
@@ -309,12 +340,15 @@ __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restric
                                                         const int64_t *__restrict__ val, int64_t n,
                                                         long long pmin, const int32_t *__restrict__ last,
                                                         const int32_t *__restrict__ spill,
-                                                        const unsigned int *__restrict__ n_spill,
+                                                        const int32_t *__restrict__ spill_n, int64_t n_chunks,
                                                         uint32_t *__restrict__ cw, int32_t *__restrict__ pair,
-                                                        CntMeta *m) {
-    const unsigned int ns = *n_spill;
-    for (unsigned int s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
-        const int32_t se = spill[s];
+                                                        CntMeta *m, CntAcc *__restrict__ agg) {
+    // 16 lanes per chunk: its spills are spill[chunk * CHUNK ..][0 .. spill_n[chunk])
+    const int sl = threadIdx.x & 15;
+    for (int64_t ch = (int64_t)blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4); ch < n_chunks;
+         ch += (int64_t)gridDim.x * (blockDim.x >> 4))
+    for (int s = sl; s < spill_n[ch]; s += 16) {
+        const int32_t se = spill[ch * CHUNK + s];
         const int64_t r = se >= 0 ? se : ~se;
         const long long p = proc[r];
         const int64_t ff = f[r];
@@ -331,6 +365,10 @@ __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restric
             break;
         }
         if (got >= 0) atomicAnd(&cw[got], ~CW_U);
+        // a claimed :ok :read counts in its tile as a read row (unless the
+        // branch below strips it as an orphan)
+        if (got >= 0 && (ff == JH_F_ADD || ff == JH_F_READ) && (type[got] & 3) == T_OK && f[got] == JH_F_READ)
+            atomicAdd(&agg[got / CNT_TILE].nr, 1);
         if (ff == JH_F_ADD) {
             uint32_t w = CW_NONE;
             const bool failed = got >= 0 && (type[got] & 3) == T_FAIL;
@@ -342,6 +380,7 @@ __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restric
                 else {
                     w = cw_make(CW_HI, v);
                     if ((w & CW_X) && !own) pair[r] = (int32_t)got;
+                    atomicAdd((unsigned long long *)&agg[r / CNT_TILE].hi, (unsigned long long)v);
                 }
             }
             cw[r] = w;
@@ -355,50 +394,6 @@ __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restric
     }
 }
 
-// per-row contributions and prefixes of lower / upper / ok reads (an :ok
-// :read still marked U has no invocation: an orphan, never a read row, so
-// pair is only ever read where it was written)
-struct CntAcc {
-    long long lo, hi;
-    int nr, flags;
-};
-
-// Reduce-then-scan over tiles of CNT_TILE rows (each tile's words are read
-// twice, 4 B each time).
-constexpr int CNT_TILE = 2048, CNT_PER = CNT_TILE / 256;
-
-__global__ void __launch_bounds__(256) k_cnt_tile_sums(const uint32_t *__restrict__ cw,
-                                                       const int32_t *__restrict__ pair,
-                                                       const int64_t *__restrict__ val, int64_t n,
-                                                       CntMeta *m, CntAcc *__restrict__ agg) {
-    __shared__ long long sh[4];
-    const int64_t base = (int64_t)blockIdx.x * CNT_TILE;
-    long long lo = 0, hi = 0, nr = 0;
-    unsigned long long orphan = ~0ULL;
-    // 8 consecutive words per thread, two 16-byte loads
-    const int64_t r0 = base + (int64_t)threadIdx.x * CNT_PER;
-    uint32_t w[CNT_PER];
-    if (r0 + CNT_PER <= n) {
-        const uint4 a = *(const uint4 *)(cw + r0), b = *(const uint4 *)(cw + r0 + 4);
-        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
-    } else {
-#pragma unroll
-        for (int j = 0; j < CNT_PER; j++) w[j] = r0 + j < n ? cw[r0 + j] : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < CNT_PER; j++) {
-        const uint32_t k = w[j] & 7;
-        if (w[j] & CW_U) orphan = min(orphan, (unsigned long long)(r0 + j));
-        if (k == CW_LO) lo += cw_val(w[j], val, pair, r0 + j);
-        else if (k == CW_HI) hi += cw_val(w[j], val, pair, r0 + j);
-        else if (k == CW_OKREAD && !(w[j] & CW_U)) nr++;
-    }
-    if (orphan != ~0ULL) atomicMin(&m->viol1, (orphan << 4) | JH_CAUSE_ORPHAN);
-    lo = block_reduce256(lo, RedSum(), sh);
-    hi = block_reduce256(hi, RedSum(), sh);
-    nr = block_reduce256(nr, RedSum(), sh);
-    if (threadIdx.x == 0) agg[blockIdx.x] = CntAcc{lo, hi, (int)nr, 0};
-}
 
 // thread t takes rows CNT_PER*t .. of the tile in order, from the tile's
 // exclusive prefix; writes only at read rows
@@ -407,7 +402,7 @@ __global__ void __launch_bounds__(256) k_cnt_tile_scan(const uint32_t *__restric
                                                        const int64_t *__restrict__ val, int64_t n,
                                                        const CntAcc *__restrict__ pre,
                                                        int32_t *__restrict__ rd_row, int64_t *__restrict__ rd_hi,
-                                                       int64_t *__restrict__ lo_at, CntAcc *total) {
+                                                       int64_t *__restrict__ lo_at, CntAcc *total, CntMeta *m) {
     __shared__ long long sc[3][4];
     const int tid = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * CNT_TILE;
@@ -421,13 +416,17 @@ __global__ void __launch_bounds__(256) k_cnt_tile_scan(const uint32_t *__restric
         for (int j = 0; j < CNT_PER; j++) w[j] = r0 + j < n ? cw[r0 + j] : 0u;
     }
     long long lo = 0, hi = 0, nr = 0;
+    unsigned long long orphan = ~0ULL;        // a completion no invocation claimed
 #pragma unroll
     for (int j = 0; j < CNT_PER; j++) {
         const uint32_t k = w[j] & 7;
+        if (w[j] & CW_U) orphan = min(orphan, (unsigned long long)(r0 + j));
         if (k == CW_LO) lo += cw_val(w[j], val, pair, r0 + j);
         else if (k == CW_HI) hi += cw_val(w[j], val, pair, r0 + j);
         else if (k == CW_OKREAD && !(w[j] & CW_U)) nr++;
     }
+    for (int o = 32; o > 0; o >>= 1) orphan = min(orphan, (unsigned long long)__shfl_xor(orphan, o));
+    if ((tid & 63) == 0 && orphan != ~0ULL) atomicMin(&m->viol1, (orphan << 4) | JH_CAUSE_ORPHAN);
     // block exclusive scan of the per-thread sums: wave shuffles, then the
     // totals of the waves before
     long long il = lo, ih = hi, in = nr;
@@ -520,27 +519,25 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
     uint32_t *cw = ctx->ws<uint32_t>(WS_C_PT, n + 8);
     HIP_TRY(hipMemsetAsync(last, 0xFF, sizeof(int32_t) * (span + 1), st));
     int32_t *spill = ctx->ws<int32_t>(WS_C_IDX, n);          // reused for the read rows below
-    unsigned int *n_spill = (unsigned int *)ctx->ws<int32_t>(WS_C_FLAG, 4);
-    HIP_TRY(hipMemsetAsync(n_spill, 0, sizeof(unsigned int), st));
-    k_cnt_pack<<<(int)((n + CHUNK - 1) / CHUNK), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
-                                                              mh.pmin, last, cw, pair, spill, n_spill, m);
-    k_cnt_pair_spill<<<grid_for(n / 64 + 1, 256, 4096), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
-                                                                      mh.pmin, last, spill, n_spill, cw, pair, m);
+    const int64_t n_tiles = (n + CNT_TILE - 1) / CNT_TILE;
+    CntAcc *agg = ctx->ws<CntAcc>(WS_C_OUT2, 2 * n_tiles + 1);     // written by every pack block
+    int32_t *spill_n = ctx->ws<int32_t>(WS_C_FLAG, n_tiles);       // likewise
+    CntAcc *pre = agg + n_tiles;
+    CntAcc *total = pre + n_tiles;
+    k_cnt_pack<<<(int)n_tiles, PACK_THREADS, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
+                                                     mh.pmin, last, cw, pair, spill, spill_n, m, agg);
+    k_cnt_pair_spill<<<grid_for(n_tiles * 16, 256, 16384), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
+                                                                      mh.pmin, last, spill, spill_n, n_tiles, cw, pair, m, agg);
 
     // reduce-then-scan over tiles of contribution words
     int32_t *rd_row = ctx->ws<int32_t>(WS_C_IDX, n);
     int64_t *rd_hi = ctx->ws<int64_t>(WS_C_HI, n);
     int64_t *lo_at = ctx->ws<int64_t>(WS_C_LO, n);
-    const int64_t n_tiles = (n + CNT_TILE - 1) / CNT_TILE;
-    CntAcc *agg = ctx->ws<CntAcc>(WS_C_OUT2, 2 * n_tiles + 1);
-    CntAcc *pre = agg + n_tiles;
-    CntAcc *total = pre + n_tiles;
-    k_cnt_tile_sums<<<(unsigned)n_tiles, 256, 0, st>>>(cw, pair, dh->value, n, m, agg);
     size_t tb = 0;
     HIP_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, tb, agg, pre, CntSumOp(), CntAcc{0, 0, 0, 0}, (int)n_tiles, st));
     void *tmp = ctx->ws<char>(WS_S_TMP, tb);
     HIP_TRY(hipcub::DeviceScan::ExclusiveScan(tmp, tb, agg, pre, CntSumOp(), CntAcc{0, 0, 0, 0}, (int)n_tiles, st));
-    k_cnt_tile_scan<<<(unsigned)n_tiles, 256, 0, st>>>(cw, pair, dh->value, n, pre, rd_row, rd_hi, lo_at, total);
+    k_cnt_tile_scan<<<(unsigned)n_tiles, 256, 0, st>>>(cw, pair, dh->value, n, pre, rd_row, rd_hi, lo_at, total, m);
     // the triples of every :ok :read (their count stays on the device: the
     // kernel reads it), then one host round trip for the verdict
     const int64_t cap = std::min(n, reads_cap);

@@ -334,6 +334,11 @@ struct DfsArgs {
     // budget, so verdicts and counts do not change) instead of holding the
     // phase open while every other wave idles; 0: never
     int32_t handover_min;
+    // phase 1: a search raises its wave's issue priority (s_setprio 1..3) at
+    // prio_ins, 2 x and 4 x prio_ins inserts, so the few long searches of a
+    // crowded CU (26 waves) run near a lone wave's speed while the many short
+    // ones fill the gaps; 0: off
+    int32_t prio_ins;
 };
 constexpr unsigned long long SEQ_HANDED = ~0ULL;
 // verdict cause bits naming the engine in :linear mode (k_frontier turns them into jh_key_verdict.analyzer)
@@ -378,6 +383,8 @@ constexpr int64_t QUICK_BUDGET = 8192;  // phase-1 inserts before a key is defer
 // ms but 3x the keys restart in phase 2: C3 59.5 -> 69.9 ms); re-measured
 // against the round-3 heavy-key pass through jh_lin_opts.handover_min
 constexpr int32_t HANDOVER_MIN = 0;
+// phase-1 issue priority by insert count (DfsArgs.prio_ins): 0 = off until measured
+constexpr int32_t P1_PRIO_INS = 0;
 // phase-2 late helpers (workgroups, one per CU) and how long a key must have run
 // in the sequential search before one takes it: 32 and 250 us measured against
 // 16 and 2 000 us (C3 rank 0 43.2 -> 40.9 ms, ranks 3 / 6 unchanged; the sweep
@@ -1459,6 +1466,11 @@ insert:
                 if (lane == 0) c = __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (readlane(c, 0)) { verdict = JH_CANCELLED; goto done; }
             }
+            if (A.prio_ins > 0 && ins >= (uint32_t)A.prio_ins) {
+                if (ins >= 4u * (uint32_t)A.prio_ins) __builtin_amdgcn_s_setprio(3);
+                else if (ins >= 2u * (uint32_t)A.prio_ins) __builtin_amdgcn_s_setprio(2);
+                else __builtin_amdgcn_s_setprio(1);
+            }
             chk = min(budget, ins + 1024);
         }
         const int i = __builtin_ctzll(absent);
@@ -2085,6 +2097,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         // the HBM table only (WIDE). One mode per kernel: the two searches do
         // not share a register allocation.
         if ((A.states8 && mt.maxw <= 40) != LEAN) continue;
+        if (A.prio_ins > 0) __builtin_amdgcn_s_setprio(0);
         if (A.seq_start && lane == 0)
             __hip_atomic_store(&A.seq_start[key], __builtin_amdgcn_s_memrealtime() | 1ULL, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -5260,6 +5273,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     if (a.defer && !(lflags & JH_LIN_NO_HANDOVER) && opts && opts->handover_min)
         a.handover_min = std::max(0, opts->handover_min);
     if (const char *e = tune_env("JH_HANDOVER_MIN")) a.handover_min = a.defer ? std::max(0, atoi(e)) : 0;
+    a.prio_ins = P1_PRIO_INS;
+    if (const char *e = tune_env("JH_P1_PRIO")) a.prio_ins = std::max(0, atoi(e));
     const char *dbgenv = tune_env("JH_DEBUG");
     const bool dbg2 = dbgenv && atoi(dbgenv) >= 2;
     unsigned long long *dbg = nullptr;
@@ -5284,6 +5299,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         aw.list = list_w; aw.n_list_dev = q + 13; aw.queue = q + 14;
         aw.defer_kind = d64 + 2 * (K + 1); aw.defer_kind_count = q + Q_DEFER_W;
         k_lin_dfs<false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
+        a.prio_ins = 0;                       // the heavy-key passes inherit a: no priorities there
     } else if (cfgreq) {
         k_req_lists<<<1, 1, 0, st>>>(cfgreq->keys_dev, cfgreq->n_q, K, defer, defer_l, q);
     } else {
@@ -5291,6 +5307,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // search is a heavy key
         k_linear_lists<<<1, 1024, 0, st>>>(list, q + 12, list_w, q + 13, defer, defer_l, defer_w, q);
     }
+    a.prio_ins = 0;
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[4], st));
     int32_t qh[Q_WORDS];

@@ -3543,23 +3543,24 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
     for (uint32_t i = tid; i < N / 32 + 1; i += BFS_THREADS) A.vis[i] = 0;
     __syncthreads();
     // four nodes per thread per pass, their first CAS in flight together
-    for (uint32_t i0 = tid; i0 < N; i0 += 4 * BFS_THREADS) {
-        uint64_t k[4];
-        uint32_t h[4];
-        unsigned long long pv[4];
+    constexpr int HBN = 4;
+    for (uint32_t i0 = tid; i0 < N; i0 += HBN * BFS_THREADS) {
+        uint64_t k[HBN];
+        uint32_t h[HBN];
+        unsigned long long pv[HBN];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < HBN; u++) {
             const uint32_t i = i0 + (uint32_t)u * BFS_THREADS;
             k[u] = i < N ? A.nodes[i] : 0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < HBN; u++) {
             const uint32_t i = i0 + (uint32_t)u * BFS_THREADS;
             h[u] = (uint32_t)jh_mix64(k[u]) & hmask;
             pv[u] = i < N ? atomicCAS((unsigned long long *)&ent[h[u]].x, BFS_EMPTY, k[u]) : BFS_EMPTY;
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < HBN; u++) {
             const uint32_t i = i0 + (uint32_t)u * BFS_THREADS;
             if (i >= N) continue;
             uint32_t hh = h[u];
@@ -5316,9 +5317,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const int n_defer = qh[1], n_def_l = qh[Q_DEFER_L], n_def_w = qh[Q_DEFER_W];
     const int n_x = cfgreq ? 0 : qh[19];
     if (n_def_l + n_def_w != n_defer) throw_jh(JH_EDEVICE, "deferred-key lists disagree");
-    if (n_defer > 0 && !linear_mode && !skip_p1 && !p1_only) {
+    if (n_defer > 0 && !linear_mode && !skip_p1) {
         // heavy keys, least advanced first (the likely longest searches start
         // first), sorted on the device: no host round trip between the phases
+        // (stage 1 of a two-stage check reads the list too: k_mark_deferred)
         SortLists sl{};
         const int nn[3] = {n_defer, n_def_l, n_def_w};
         int32_t *outs[3] = {defer, defer_l, defer_w};

@@ -3310,6 +3310,17 @@ __device__ __forceinline__ uint32_t gl_hash(uint64_t k) {
     return (uint32_t)(((uint64_t)(uint32_t)jh_mix64(k) * GL_H) >> 32);
 }
 constexpr uint64_t BFS_EMPTY = ~0ULL;
+// JH_DEBUG=2: where a BFS closure round's time goes (tid 0's s_memtime, summed
+// over workgroups): [0] claim + first barrier, [1] tid 0's items, [2] the
+// barrier after the items, [3] swap + counters + last barrier, [4] rounds,
+// [5] layer formation (clear, window, pending scan), [6] layers
+#ifdef JH_BFS_PROF
+#define BFS_PROF(x) x
+#else
+#define BFS_PROF(x)
+#endif
+__device__ unsigned long long g_bfs_prof[8];
+__device__ unsigned long long g_bfs_prof_x[4];   // [0] insert8, [1] record8, [2] tid 0's items ([7] above: load + children)
 // A valid key is settled by the BFS (instead of waiting for the sequential
 // search) when its whole reachable set is complete and smaller than the
 // budget; only for sets this large, which the DFS takes milliseconds over.
@@ -4077,6 +4088,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
     uint64_t *pcur = pend, *pnxt = pend + A.q_cap;
     uint64_t *fcur = front, *fnxt = front + A.q_cap;
     for (uint32_t t = 0; t < n_ok; t++) {
+        BFS_PROF(const unsigned long long lf0 = __builtin_amdgcn_s_memtime();)
         // ---- form layer t: dedupe its entries from the pending list ---------
         for (int i = tid; i < LSET; i += BFS_THREADS) lset[i] = 0;
         const int wo = woff[t], w = woff[t + 1] - wo;
@@ -4305,6 +4317,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         // ---- close layer t under same-layer lifts ---------------------------
         if (sh.status) break;
         const uint32_t r = sh.r;
+        BFS_PROF(if (A.dbg && tid == 0) { atomicAdd(&g_bfs_prof[5], __builtin_amdgcn_s_memtime() - lf0); atomicAdd(&g_bfs_prof[6], 1ULL); })
         while (sh.nfront > 0 && !sh.status) {
             rounds++;
             const unsigned nf = sh.nfront;
@@ -4317,6 +4330,8 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                     sh.status |= 4;
             }
             __syncthreads();
+            BFS_PROF(unsigned long long pt = 0;
+            if (A.dbg && tid == 0) { pt = __builtin_amdgcn_s_memtime(); atomicAdd(&g_bfs_prof[0], pt - rt0); atomicAdd(&g_bfs_prof[4], 1ULL); })
             if (sh.status & 4) break;
             for (;;) {
             // one item per (frontier configuration, 8 members): a round's work
@@ -4325,6 +4340,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             const unsigned items = nf * ng;
             for (unsigned i0 = tid - lane; i0 < items; i0 += BFS_THREADS) {
                 const unsigned it = i0 + lane;
+                BFS_PROF(unsigned long long pq0 = A.dbg && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;)
                 const unsigned i = it < items ? it / ng : 0;
                 const uint64_t c = it < items ? fcur[i] : 0xFFFFFFFFull;    // past the end: every member taken
                 const uint32_t s = (uint32_t)(c >> 32), mask = (uint32_t)c;
@@ -4359,12 +4375,17 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                             ck[q] = ((uint64_t)(uint32_t)s2 << 32) | (mask | (1u << j));
                         }
                     }
+                    BFS_PROF(if (A.dbg && tid == 0) { const unsigned long long q = __builtin_amdgcn_s_memtime(); atomicAdd(&g_bfs_prof[7], q - pq0); pq0 = q; })
                     bool nw[8];
                     insert8(ck, nw);
+                    BFS_PROF(if (A.dbg && tid == 0) { const unsigned long long q = __builtin_amdgcn_s_memtime(); atomicAdd(&g_bfs_prof_x[0], q - pq0); pq0 = q; })
                     record8(ck, nw);
+                    BFS_PROF(if (A.dbg && tid == 0) { const unsigned long long q = __builtin_amdgcn_s_memtime(); atomicAdd(&g_bfs_prof_x[1], q - pq0); atomicAdd(&g_bfs_prof_x[2], 1ULL); })
                 }
             }
+            BFS_PROF(if (A.dbg && tid == 0) { const unsigned long long q = __builtin_amdgcn_s_memtime(); atomicAdd(&g_bfs_prof[1], q - pt); pt = q; })
             __syncthreads();
+            BFS_PROF(if (A.dbg && tid == 0) { const unsigned long long q = __builtin_amdgcn_s_memtime(); atomicAdd(&g_bfs_prof[2], q - pt); pt = q; })
             if (sh.ovf) { migrate(); continue; }
             break;
             }
@@ -4378,6 +4399,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                 else { d[12] += __builtin_amdgcn_s_memtime() - rt0; d[13] += nf; }
             }
             __syncthreads();
+            BFS_PROF(if (A.dbg && tid == 0) atomicAdd(&g_bfs_prof[3], __builtin_amdgcn_s_memtime() - pt);)
         }
         if (sh.status) break;
     }
@@ -5860,6 +5882,23 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                             (double)h[16 * w] / std::max(1ULL, h[16 * w + 1]), h[16 * w + 5], h[16 * w + 6],
                             h[16 * w + 7], h[16 * w + 8], h[16 * w + 10], h[16 * w + 9], h[16 * w + 11],
                             h[16 * w + 12], h[16 * w + 13], h[16 * w + 14] & 0xFFFFFFFF, h[16 * w + 14] >> 32, h[16 * w + 15], h[16 * w + 2]);
+#ifdef JH_BFS_PROF
+            {
+                unsigned long long bp[8];
+                HIP_TRY(hipMemcpyFromSymbol(bp, HIP_SYMBOL(g_bfs_prof), sizeof bp));
+                const double nr = (double)std::max(1ULL, bp[4]), nl = (double)std::max(1ULL, bp[6]);
+                unsigned long long bx[4];
+                HIP_TRY(hipMemcpyFromSymbol(bx, HIP_SYMBOL(g_bfs_prof_x), sizeof bx));
+                const double ni = (double)std::max(1ULL, bx[2]);
+                fprintf(stderr, "[jh-bfs-prof] rounds=%llu cyc/round: claim+barrier %.0f items %.0f barrier %.0f tail %.0f | "
+                        "layers=%llu formation cyc/layer %.0f | tid0 items=%llu cyc/item: load+children %.0f insert8 %.0f record8 %.0f\n",
+                        bp[4], bp[0] / nr, bp[1] / nr, bp[2] / nr, bp[3] / nr, bp[6], bp[5] / nl, bx[2], bp[7] / ni, bx[0] / ni, bx[1] / ni);
+                memset(bx, 0, sizeof bx);
+                HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bfs_prof_x), bx, sizeof bx));
+                memset(bp, 0, sizeof bp);
+                HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bfs_prof), bp, sizeof bp));
+            }
+#endif
             std::vector<unsigned long long> g((size_t)waves2 * 16);
             HIP_TRY(hipMemcpy(g.data(), dbg + 16 * 256, g.size() * 8, hipMemcpyDeviceToHost));
             for (int w = 0; w < waves2; w++)

@@ -1997,7 +1997,8 @@ constexpr int lds_w() { return LDS_TBL + M::SLOTS * 16 + M::BLOOM / 8 + M::BKT; 
 // bytes of a k_lin_xw key's tables (ops, windows per layer)
 __device__ __forceinline__ uint64_t a16(uint64_t x) { return (x + 15) & ~15ULL; }
 __device__ __forceinline__ uint64_t xw_bytes(int n_ops, int n_ok, long long sumW) {
-    return 3 * a16((uint64_t)n_ops * 4) + a16((uint64_t)(n_ok + 1) * 4) + a16((uint64_t)sumW * 4 + 1024);
+    return 3 * a16((uint64_t)n_ops * 4) + a16((uint64_t)(n_ok + 1) * 4) + a16((uint64_t)sumW * 4 + 1024) +
+           a16((uint64_t)sumW * 8 + 2048);
 }
 
 struct KeyMeta {
@@ -4513,11 +4514,24 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A0) {
 // with many crashed ops) and almost all of them are deep searches, so this
 // path is kept simple: tables in global scratch (ops, windows W(t) listed
 // per layer), every configuration in the wave's HBM table (48-byte entries
-// {mask[4], gen|t|state}, buckets of 4), the stack in HBM. A step is one
-// HBM round trip per probed slice (plus one per pop).
+// {mask[4], gen|t|state}, buckets of 4), the stack in HBM with its top
+// XW_RING frames mirrored in LDS. A step is one HBM round trip per probed
+// slice, plus one to load the next layer's members when t moves (a pop reads
+// its frame from LDS; the frame carries the layer's window offset and width).
 constexpr int XW_SL = JH_MAX_WINDOW / 64;        // mask words / member slices
 constexpr uint32_t XW_HB = 4;                    // entries per bucket
 constexpr int XW_EW = 6;                         // words per entry
+constexpr int XW_FW = 8;                         // words per stack frame
+// LDS ring of the top stack frames: 1.5 KB, under what k_lin_bfs's 157 KB
+// leaves of a CU (the two share CUs in C5)
+constexpr int XW_RING = 24;
+// JH_XW_PROF builds: where a step's time goes (s_memtime, summed over waves)
+#ifdef JH_XW_PROF
+#define XW_PROF(x) x
+#else
+#define XW_PROF(x)
+#endif
+__device__ unsigned long long g_xw_prof[12];
 
 struct XwArgs {
     KeySrc src;
@@ -4530,7 +4544,7 @@ struct XwArgs {
     uint64_t scratch_bytes;
     uint64_t *memo;             // per wave: memo_cap entries x XW_EW words
     uint32_t memo_cap;          // power of two
-    uint64_t *stack;            // per wave: stack_cap frames x XW_EW words
+    uint64_t *stack;            // per wave: stack_cap frames x XW_FW words
     uint32_t stack_cap;
     int64_t budget;
     int32_t init_state;
@@ -4546,15 +4560,17 @@ struct XwTbl {
     int32_t *a;       // ok returns before the invocation (the op joins W(a))
     int32_t *woff;    // W(t) = W[woff[t] .. woff[t+1])
     uint32_t *W;      // op ids: 32-bit, long keys come here
+    uint2 *P;         // {rq, rr} of W's ops, in W's order: a layer is one load
 };
-__device__ __forceinline__ XwTbl xw_tbl(char *tb, int n_ops, int n_ok) {
+__device__ __forceinline__ XwTbl xw_tbl(char *tb, int n_ops, int n_ok, long long sumW) {
     XwTbl T;
     uint64_t o = 0;
     T.rq = (uint32_t *)(tb + o); o += a16((uint64_t)n_ops * 4);
     T.rr = (int32_t *)(tb + o); o += a16((uint64_t)n_ops * 4);
     T.a = (int32_t *)(tb + o); o += a16((uint64_t)n_ops * 4);
     T.woff = (int32_t *)(tb + o); o += a16((uint64_t)(n_ok + 1) * 4);
-    T.W = (uint32_t *)(tb + o);
+    T.W = (uint32_t *)(tb + o); o += a16((uint64_t)sumW * 4 + 1024);
+    T.P = (uint2 *)(tb + o);
     return T;
 }
 
@@ -4604,7 +4620,10 @@ __device__ int xw_fill(const KeySrc &S, uint32_t s0, uint32_t s1, int n_ops, int
                 bool keep = false;
                 if (idx < w) { prev = T.W[offp + idx]; keep = T.rr[prev] != t - 1; }
                 const uint64_t bk = ballot(keep);
-                if (keep) T.W[offt + nk + mbcnt(bk)] = (uint32_t)prev;
+                if (keep) {
+                    T.W[offt + nk + mbcnt(bk)] = (uint32_t)prev;
+                    T.P[offt + nk + mbcnt(bk)] = make_uint2(T.rq[prev], (uint32_t)T.rr[prev]);
+                }
                 nk += __popcll(bk);
             }
         }
@@ -4614,7 +4633,10 @@ __device__ int xw_fill(const KeySrc &S, uint32_t s0, uint32_t s1, int n_ops, int
             const bool in = j < n_ops && T.a[j] <= t;
             const uint64_t ba = ballot(in);
             const int c = __popcll(ba);             // a is non-decreasing: a prefix
-            if (in && nk + added + lane < JH_MAX_WINDOW) T.W[offt + nk + added + lane] = (uint32_t)j;
+            if (in && nk + added + lane < JH_MAX_WINDOW) {
+                T.W[offt + nk + added + lane] = (uint32_t)j;
+                T.P[offt + nk + added + lane] = make_uint2(T.rq[j], (uint32_t)T.rr[j]);
+            }
             added += c; nxt += c;
             if (c < 64) break;
         }
@@ -4631,18 +4653,28 @@ __device__ int xw_fill(const KeySrc &S, uint32_t s0, uint32_t s1, int n_ops, int
     return maxw;
 }
 
-__device__ __forceinline__ uint64_t xw_hash(uint32_t t, uint32_t s, const uint64_t *m) {
-    uint64_t h = jh_mix64(((uint64_t)t << 32) | s);
+// a configuration's hash: the XOR of one Zobrist word per linearized member
+// (a child's is its parent's ^ its member's word; the RET child's, whose
+// mask is re-indexed onto the next window, is a wave reduction), mixed once
+// with (t, state) -- one 64-bit mix per probe instead of one per mask word
+__device__ __forceinline__ uint64_t xw_zw(int b) { return jh_mix64(0x9E3779B97F4A7C15ULL * (uint64_t)(b + 1)); }
+__device__ __forceinline__ uint64_t xw_hash(uint32_t t, uint32_t s, uint64_t hm) {
+    return jh_mix64(hm ^ (((uint64_t)t << 32) | s));
+}
+__device__ __forceinline__ uint64_t xw_zsum(const uint64_t *m, const uint64_t *zk, int lane) {
+    uint64_t x = 0;
 #pragma unroll
-    for (int w = 0; w < XW_SL; w++) h = jh_mix64(h ^ (m[w] + (uint64_t)w * 0x9E3779B97F4A7C15ULL));
-    return h;
+    for (int q = 0; q < XW_SL; q++) x ^= ((m[q] >> lane) & 1) ? zk[q] : 0ULL;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
+    return rfl64(x);
 }
 
 // probe: slot | absent << 32 (absent: the slot an insert of this key takes)
 __device__ uint64_t xw_probe(const uint64_t *memo, uint32_t cap_mask, uint32_t gen, uint32_t t,
-                             uint32_t s, const uint64_t *m, unsigned long long &probes) {
+                             uint32_t s, const uint64_t *m, uint64_t hm, unsigned long long &probes) {
     const uint64_t want = ((uint64_t)gen << 40) | ((uint64_t)t << 20) | s;
-    uint32_t b = (uint32_t)xw_hash(t, s, m) & cap_mask & ~(XW_HB - 1);
+    uint32_t b = (uint32_t)xw_hash(t, s, hm) & cap_mask & ~(XW_HB - 1);
     for (;;) {
         const ulonglong2 *B = (const ulonglong2 *)(memo + (size_t)b * XW_EW);
         ulonglong2 e[XW_HB * 3];
@@ -4675,10 +4707,15 @@ __device__ __forceinline__ void xw_store(uint64_t *memo, uint32_t slot, uint32_t
 __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
     const int lane = threadIdx.x;
     __shared__ unsigned long long nm_sh[XW_SL];
+    __shared__ uint64_t ring[XW_RING * XW_FW];
+    XW_PROF(unsigned long long pf[12] = {0};)
     char *tb = A.scratch + (size_t)blockIdx.x * A.scratch_bytes;
     uint64_t *memo = A.memo + (size_t)blockIdx.x * A.memo_cap * XW_EW;
-    uint64_t *stk = A.stack + (size_t)blockIdx.x * A.stack_cap * XW_EW;
+    uint64_t *stk = A.stack + (size_t)blockIdx.x * A.stack_cap * XW_FW;
     const uint32_t cap_mask = A.memo_cap - 1;
+    uint64_t zk[XW_SL];          // this lane's members' Zobrist words
+#pragma unroll
+    for (int k = 0; k < XW_SL; k++) zk[k] = xw_zw(64 * k + lane);
     unsigned long long my_probes = 0;
     for (;;) {
         int idx = 0;
@@ -4695,7 +4732,7 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
             if (lane == 0) { atomicOr(A.flags, 2); A.out[key] = v; }
             continue;
         }
-        const XwTbl T = xw_tbl(tb, n_ops, n_ok);
+        const XwTbl T = xw_tbl(tb, n_ops, n_ok, sumW);
         const int maxw = xw_fill(A.src, A.src.off[key], A.src.off[key + 1], n_ops, n_ok, sumW, lane, T);
         if (maxw > JH_MAX_WINDOW) {
             if (lane == 0) A.out[key] = v;
@@ -4709,29 +4746,37 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
         uint64_t mask[XW_SL] = {0, 0, 0, 0};
         uint32_t mrq[XW_SL];
         int32_t mrr[XW_SL];
-        int w = 0, r = 0, start = 0;
-        auto load_layer = [&]() {
-            const int o = T.woff[t];
-            w = T.woff[t + 1] - o;
+        int w = 0, r = 0, start = 0, lo = 0;
+        // layer t's members: W(t) = P[o .. o + w)
+        auto load_layer = [&](int o, int wt) {
+            XW_PROF(const unsigned long long l0 = __builtin_amdgcn_s_memtime();)
+            lo = o; w = wt;
             r = 0;
 #pragma unroll
             for (int k = 0; k < XW_SL; k++) {
                 const int j = 64 * k + lane;
                 mrq[k] = RQ_EMPTY; mrr[k] = -2;
-                if (j < w) { const int id = T.W[o + j]; mrq[k] = T.rq[id]; mrr[k] = T.rr[id]; }
+                if (j < w) { const uint2 pr = T.P[o + j]; mrq[k] = pr.x; mrr[k] = (int32_t)pr.y; }
                 const uint64_t b = ballot(j < w && mrr[k] == (int32_t)t);
                 if (b) r = 64 * k + __builtin_ctzll(b);
             }
+            XW_PROF(pf[2] += __builtin_amdgcn_s_memtime() - l0; pf[7]++;)
         };
-        load_layer();
+        load_layer(T.woff[0], T.woff[1] - T.woff[0]);
+        uint32_t rlo = 0;      // the LDS ring holds frames [rlo, depth)
+        uint64_t hm = 0;       // Zobrist sum of the configuration's mask
+        XW_PROF(const unsigned long long k0 = __builtin_amdgcn_s_memtime();)
         int verdict = -1;
         for (;;) {
             // expand: candidates from `start` on, in call order, slice by slice
             bool took = false;
             uint32_t u_r = t;
-            uint64_t nm_r[XW_SL] = {0, 0, 0, 0};
+            uint64_t nm_r[XW_SL] = {0, 0, 0, 0}, hr = 0;
             bool lifted = false;
-#pragma unroll 1
+            int wo0 = 0, wo1 = 0;          // woff[u_r], woff[u_r + 1]: loaded beside the probes
+            // unrolled: static slice indices (no register-array selects, no
+            // SGPR spills: 4.02 -> 3.37 s of C5's k_lin_xw)
+#pragma unroll
             for (int k = 0; k < XW_SL && !took; k++) {
                 if (64 * k >= w) break;
                 const int j = 64 * k + lane;
@@ -4742,6 +4787,7 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
                 if (!lifted && (r >> 6) == k && ((cand >> (r & 63)) & 1)) {
                     // the RET child: lift RET[t], keep lifting while the next
                     // layer's RET op is already linearized, compact onto W(u)
+                    XW_PROF(const unsigned long long f0 = __builtin_amdgcn_s_memtime();)
                     lifted = true;
                     uint64_t lin[XW_SL];
 #pragma unroll
@@ -4757,6 +4803,7 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
                     }
                     u_r = u;
                     if (u < (uint32_t)n_ok) {
+                        wo0 = T.woff[u]; wo1 = T.woff[u + 1];
                         if (lane < XW_SL) nm_sh[lane] = 0;
                         wave_sync();
                         int base = 0;
@@ -4772,7 +4819,9 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
 #pragma unroll
                         for (int q = 0; q < XW_SL; q++) nm_r[q] = rfl64(nm_sh[q]);
                         wave_sync();
+                        hr = xw_zsum(nm_r, zk, lane);
                     }
+                    XW_PROF(pf[9] += __builtin_amdgcn_s_memtime() - f0;)
                 }
                 // every candidate lane probes its child
                 const bool is_r = j == r;
@@ -4780,30 +4829,40 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
 #pragma unroll
                 for (int q = 0; q < XW_SL; q++) cm[q] = is_r ? nm_r[q] : (mask[q] | (q == k ? (1ULL << lane) : 0ULL));
                 const uint32_t ct = is_r ? u_r : t, cs = mrq[k] >> 16;
+                const uint64_t chm = is_r ? hr : (hm ^ zk[k]);
                 bool found = false;
                 uint32_t slot = 0;
+                XW_PROF(const unsigned long long q0 = __builtin_amdgcn_s_memtime();)
                 if (cl) {
-                    const uint64_t pr = xw_probe(memo, cap_mask, gen, ct, cs, cm, my_probes);
+                    const uint64_t pr = xw_probe(memo, cap_mask, gen, ct, cs, cm, chm, my_probes);
                     found = (pr >> 32) == 0;
                     slot = (uint32_t)pr;
                 }
                 const uint64_t absent = cand & ~ballot(found);
+                XW_PROF(pf[1] += __builtin_amdgcn_s_memtime() - q0; pf[6]++;)
                 if (!absent) continue;
                 const int i = __builtin_ctzll(absent);
                 if (ins >= budget) { verdict = JH_UNKNOWN; break; }
                 ins++;
+                XW_PROF(const unsigned long long h0 = __builtin_amdgcn_s_memtime();)
                 if (lane == i) xw_store(memo, slot, gen, ct, cs, cm);
-                // push the parent (t, s, member, mask)
+                // push the parent (t, its window, member, s, mask): HBM, and
+                // the LDS ring slot a pop reads while the frame stays in it
                 if (lane == 0) {
-                    uint64_t *f = stk + (size_t)depth * XW_EW;
-                    f[0] = mask[0]; f[1] = mask[1]; f[2] = mask[2]; f[3] = mask[3];
-                    f[4] = ((uint64_t)t << 32) | (uint32_t)(64 * k + i);
-                    f[5] = s;
+                    uint64_t *f = stk + (size_t)depth * XW_FW;
+                    uint64_t *g = ring + (depth % XW_RING) * XW_FW;
+                    const uint64_t f4 = ((uint64_t)t << 32) | ((uint32_t)w << 16) | (uint32_t)(64 * k + i);
+                    const uint64_t f5 = ((uint64_t)(uint32_t)lo << 32) | s;
+                    f[0] = mask[0]; f[1] = mask[1]; f[2] = mask[2]; f[3] = mask[3]; f[4] = f4; f[5] = f5; f[6] = hm;
+                    g[0] = mask[0]; g[1] = mask[1]; g[2] = mask[2]; g[3] = mask[3]; g[4] = f4; g[5] = f5; g[6] = hm;
                 }
                 depth++;
+                if (depth - rlo > (uint32_t)XW_RING) rlo = depth - XW_RING;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                XW_PROF(pf[4] += __builtin_amdgcn_s_memtime() - h0; pf[5]++;)
                 s = (uint32_t)readlane((int)cs, i);
+                hm = readlane64(chm, i);
                 const uint32_t nt = (uint32_t)readlane((int)ct, i);
 #pragma unroll
                 for (int q = 0; q < XW_SL; q++) mask[q] = readlane64(cm[q], i);
@@ -4813,25 +4872,38 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
                     t = nt;
                     tmax = max(tmax, t);
                     if (t >= (uint32_t)n_ok) { verdict = JH_VALID; break; }
-                    load_layer();
+                    load_layer(wo0, wo1 - wo0);     // nt != t only for the RET child: t == u_r
                 }
             }
             if (verdict >= 0) break;
             if (took) continue;
             // pop
             if (depth == 0) { verdict = JH_INVALID; break; }
+            XW_PROF(const unsigned long long o0 = __builtin_amdgcn_s_memtime();)
             depth--;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            const uint64_t *f = stk + (size_t)depth * XW_EW;
+            uint64_t ti, f5;
+            if (depth >= rlo) {
+                const uint64_t *g = ring + (depth % XW_RING) * XW_FW;
 #pragma unroll
-            for (int q = 0; q < XW_SL; q++) mask[q] = rfl64(f[q]);
-            const uint64_t ti = rfl64(f[4]);
-            s = (uint32_t)rfl64(f[5]);
-            start = (int)(uint32_t)ti + 1;
+                for (int q = 0; q < XW_SL; q++) mask[q] = rfl64(g[q]);
+                ti = rfl64(g[4]); f5 = rfl64(g[5]); hm = rfl64(g[6]);
+            } else {
+                const uint64_t *f = stk + (size_t)depth * XW_FW;
+#pragma unroll
+                for (int q = 0; q < XW_SL; q++) mask[q] = rfl64(f[q]);
+                ti = rfl64(f[4]); f5 = rfl64(f[5]); hm = rfl64(f[6]);
+                rlo = depth;
+                XW_PROF(pf[10]++;)
+            }
+            s = (uint32_t)f5;
+            start = (int)(ti & 0xFFFF) + 1;
             const uint32_t pt = (uint32_t)(ti >> 32);
-            if (pt != t) { t = pt; load_layer(); }
+            XW_PROF(pf[3] += __builtin_amdgcn_s_memtime() - o0; pf[8]++;)
+            if (pt != t) { t = pt; load_layer((int)(f5 >> 32), (int)((ti >> 16) & 0xFFFF)); }
         }
+        XW_PROF(pf[0] += __builtin_amdgcn_s_memtime() - k0; pf[11]++;)
         v.valid = verdict;
         v.cause = (verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0) | A.cause_or;
         v.explored = ins;
@@ -4840,6 +4912,7 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
     }
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
+    XW_PROF(if (lane == 0) for (int k = 0; k < 12; k++) atomicAdd(&g_xw_prof[k], pf[k]);)
 }
 
 __global__ void __launch_bounds__(256) k_fail_rows(KeySrc S, jh_key_verdict *out, int64_t K) {
@@ -5386,7 +5459,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // one wave per key, up to four per CU (round 2 capped this at 128 waves)
         int want_x = std::min(n_x, 4 * ctx->n_cu);
         if (opts && opts->xw_waves > 0) want_x = std::min(n_x, opts->xw_waves);
-        const uint64_t per_x = (uint64_t)capx * XW_EW * 8 + (uint64_t)stack_cap * XW_EW * 8 + scr_x;
+        const uint64_t per_x = (uint64_t)capx * XW_EW * 8 + (uint64_t)stack_cap * XW_FW * 8 + scr_x;
         waves_x = fit_units(ctx, want_x, per_x, {WS_MEMO_X, WS_STACK_X, WS_SCRATCH_X});
         const bool freshx = ctx->ws_fresh(WS_MEMO_X) || ctx->bufs[WS_MEMO_X].bytes < (size_t)waves_x * capx * XW_EW * 8;
         uint64_t *memox = ctx->ws<uint64_t>(WS_MEMO_X, (size_t)waves_x * capx * XW_EW, /*zero=*/true);
@@ -5396,7 +5469,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         x.list = list_x; x.n_list = n_x; x.queue = q + 21; x.meta = meta; x.out = out_dev;
         x.scratch = ctx->ws<char>(WS_SCRATCH_X, (size_t)waves_x * scr_x); x.scratch_bytes = scr_x;
         x.memo = memox; x.memo_cap = capx;
-        x.stack = ctx->ws<uint64_t>(WS_STACK_X, (size_t)waves_x * stack_cap * XW_EW); x.stack_cap = stack_cap;
+        x.stack = ctx->ws<uint64_t>(WS_STACK_X, (size_t)waves_x * stack_cap * XW_FW); x.stack_cap = stack_cap;
         x.budget = budget; x.init_state = init_state;
         x.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;   // its own table: any gen range works
         x.flags = q + 2; x.probes = (unsigned long long *)(q + 22);
@@ -6016,6 +6089,19 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             if (waves_w > 0 && q64(qh, Q_T_WIDE + 2) > q64(qh, Q_T_WIDE)) sum->wide_ms = (q64(qh, Q_T_WIDE + 2) - q64(qh, Q_T_WIDE)) / 1e5;
         }
         if (n_x > 0) { float e2 = 0; HIP_TRY(hipEventElapsedTime(&e2, ctx->ev[8], ctx->ev[9])); sum->xw_ms = e2; }
+#ifdef JH_XW_PROF
+        if (n_x > 0) {
+            unsigned long long x[12];
+            HIP_TRY(hipMemcpyFromSymbol(x, HIP_SYMBOL(g_xw_prof), sizeof x));
+            const double ni = (double)std::max(1ULL, x[5]);
+            fprintf(stderr, "[jh-xw-prof] keys=%llu inserts=%llu cyc/insert: search %.0f | probe %.0f (%.2f slice probes) "
+                    "push %.0f lift %.0f | layer loads %.2f x %.0f cyc | pops %.2f x %.0f cyc (HBM frames %llu)\n",
+                    x[11], x[5], x[0] / ni, x[1] / ni, x[6] / ni, x[4] / ni, x[9] / ni, x[7] / ni,
+                    x[2] / (double)std::max(1ULL, x[7]), x[8] / ni, x[3] / (double)std::max(1ULL, x[8]), x[10]);
+            memset(x, 0, sizeof x);
+            HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_xw_prof), x, sizeof x));
+        }
+#endif
         sum->p3_probes = q64(qh, Q_PROBES_P3);
         sum->wide_probes = q64(qh, Q_PROBES_WIDE);
         sum->xw_probes = q64(qh, 22);

@@ -4747,6 +4747,12 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
         uint32_t mrq[XW_SL];
         int32_t mrr[XW_SL];
         int w = 0, r = 0, start = 0, lo = 0;
+        // after a pop: the popped member's slice and which of its children
+        // were absent when the parent took that member. The table never
+        // drops an entry, so the others are still present: only these are
+        // probed again (none left: no round trip for the slice)
+        int k_known = -1;
+        uint64_t abs_known = 0;
         // layer t's members: W(t) = P[o .. o + w)
         auto load_layer = [&](int o, int wt) {
             XW_PROF(const unsigned long long l0 = __builtin_amdgcn_s_memtime();)
@@ -4781,7 +4787,8 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
                 if (64 * k >= w) break;
                 const int j = 64 * k + lane;
                 const uint32_t req = mrq[k] & 0xFFFF;
-                const bool cl = j < w && j >= start && !((mask[k] >> lane) & 1) && (req == s || req == RQ_ANY);
+                const bool cl = j < w && j >= start && !((mask[k] >> lane) & 1) && (req == s || req == RQ_ANY) &&
+                                (k != k_known || ((abs_known >> lane) & 1));
                 const uint64_t cand = ballot(cl);
                 if (!cand) continue;
                 if (!lifted && (r >> 6) == k && ((cand >> (r & 63)) & 1)) {
@@ -4854,7 +4861,9 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
                     const uint64_t f4 = ((uint64_t)t << 32) | ((uint32_t)w << 16) | (uint32_t)(64 * k + i);
                     const uint64_t f5 = ((uint64_t)(uint32_t)lo << 32) | s;
                     f[0] = mask[0]; f[1] = mask[1]; f[2] = mask[2]; f[3] = mask[3]; f[4] = f4; f[5] = f5; f[6] = hm;
+                    f[7] = absent;
                     g[0] = mask[0]; g[1] = mask[1]; g[2] = mask[2]; g[3] = mask[3]; g[4] = f4; g[5] = f5; g[6] = hm;
+                    g[7] = absent;
                 }
                 depth++;
                 if (depth - rlo > (uint32_t)XW_RING) rlo = depth - XW_RING;
@@ -4868,6 +4877,7 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
                 for (int q = 0; q < XW_SL; q++) mask[q] = readlane64(cm[q], i);
                 took = true;
                 start = 0;
+                k_known = -1;
                 if (nt != t) {
                     t = nt;
                     tmax = max(tmax, t);
@@ -4888,17 +4898,18 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
                 const uint64_t *g = ring + (depth % XW_RING) * XW_FW;
 #pragma unroll
                 for (int q = 0; q < XW_SL; q++) mask[q] = rfl64(g[q]);
-                ti = rfl64(g[4]); f5 = rfl64(g[5]); hm = rfl64(g[6]);
+                ti = rfl64(g[4]); f5 = rfl64(g[5]); hm = rfl64(g[6]); abs_known = rfl64(g[7]);
             } else {
                 const uint64_t *f = stk + (size_t)depth * XW_FW;
 #pragma unroll
                 for (int q = 0; q < XW_SL; q++) mask[q] = rfl64(f[q]);
-                ti = rfl64(f[4]); f5 = rfl64(f[5]); hm = rfl64(f[6]);
+                ti = rfl64(f[4]); f5 = rfl64(f[5]); hm = rfl64(f[6]); abs_known = rfl64(f[7]);
                 rlo = depth;
                 XW_PROF(pf[10]++;)
             }
             s = (uint32_t)f5;
             start = (int)(ti & 0xFFFF) + 1;
+            k_known = (int)(ti & 0xFFFF) >> 6;
             const uint32_t pt = (uint32_t)(ti >> 32);
             XW_PROF(pf[3] += __builtin_amdgcn_s_memtime() - o0; pf[8]++;)
             if (pt != t) { t = pt; load_layer((int)(f5 >> 32), (int)((ti >> 16) & 0xFFFF)); }

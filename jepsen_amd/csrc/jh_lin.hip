@@ -3387,7 +3387,7 @@ struct BfsShared {
     unsigned npend, npend2, nfront, nnext, tmax, lcount, r;
     unsigned nnodes, nostore, dlen, clen, cnext, ok;
     unsigned long long count, ccount, plen;
-    uint32_t win_vv[64];    // the current layer's window: v1 | v2 << 16
+    alignas(16) uint32_t win_vv[64];    // the current layer's window: v1 | v2 << 16
     uint32_t win_f[64];     // f, or 3 for no member
     unsigned long long cfg_min;
     unsigned gl_cnt[2], gl_ovf[2];   // the count pass's per-bucket LDS live sets (two in turn)
@@ -3483,13 +3483,23 @@ __device__ __forceinline__ void bfs_lookup_batch(const ulonglong2 *ent, uint32_t
     }
 }
 
-// bfs_child for layer t with its window in LDS (sh.win_vv / sh.win_f, r = RET's position)
-__device__ __forceinline__ int bfs_child_w(const BfsShared &sh, const uint8_t *rpos, uint32_t n_ok, uint32_t t,
-                                           uint32_t r, int w, uint32_t s, uint32_t mask, int j, uint64_t *ck) {
+// the window's operations of members j0 .. j0+7 (j0 a multiple of 8 below
+// 64): four 16-byte LDS reads issued together, instead of one dependent LDS
+// round trip per member inside the children's branches
+struct Win8 { uint32_t f[8], vv[8]; };
+__device__ __forceinline__ void win8(const BfsShared &sh, int j0, Win8 &x) {
+    const uint4 *pf = (const uint4 *)&sh.win_f[j0 & 56], *pv = (const uint4 *)&sh.win_vv[j0 & 56];
+    const uint4 a = pf[0], b = pf[1], c = pv[0], d = pv[1];
+    x.f[0] = a.x; x.f[1] = a.y; x.f[2] = a.z; x.f[3] = a.w; x.f[4] = b.x; x.f[5] = b.y; x.f[6] = b.z; x.f[7] = b.w;
+    x.vv[0] = c.x; x.vv[1] = c.y; x.vv[2] = c.z; x.vv[3] = c.w; x.vv[4] = d.x; x.vv[5] = d.y; x.vv[6] = d.z; x.vv[7] = d.w;
+}
+
+// bfs_child for layer t with member j's operation given (f, vv = v1 | v2 << 16; r = RET's position)
+__device__ __forceinline__ int bfs_child_fv(uint32_t f, uint32_t vv, const uint8_t *rpos, uint32_t n_ok, uint32_t t,
+                                            uint32_t r, int w, uint32_t s, uint32_t mask, int j, uint64_t *ck) {
     if (j >= w || ((mask >> j) & 1)) return 0;
-    const uint32_t vv = sh.win_vv[j];
     int s2;
-    if (!cas_step((int)sh.win_f[j], (int)(vv & 0xFFFF), (int)(vv >> 16), (int)s, &s2)) return 0;
+    if (!cas_step((int)f, (int)(vv & 0xFFFF), (int)(vv >> 16), (int)s, &s2)) return 0;
     if ((uint32_t)j != r) { *ck = bfs_pack(t, (uint32_t)s2, mask | (1u << j)); return 1; }
     uint64_t nm = mask | (1u << j);
     uint32_t u = t, ru = r;
@@ -3504,6 +3514,13 @@ __device__ __forceinline__ int bfs_child_w(const BfsShared &sh, const uint8_t *r
     return 2;
 }
 
+// bfs_child for layer t with its window in LDS (sh.win_vv / sh.win_f, r = RET's position)
+__device__ __forceinline__ int bfs_child_w(const BfsShared &sh, const uint8_t *rpos, uint32_t n_ok, uint32_t t,
+                                           uint32_t r, int w, uint32_t s, uint32_t mask, int j, uint64_t *ck) {
+    if (j >= w || ((mask >> j) & 1)) return 0;
+    return bfs_child_fv(sh.win_f[j], sh.win_vv[j], rpos, n_ok, t, r, w, s, mask, j, ck);
+}
+
 // live if any child among members j0 .. j0+7 is terminal or live
 __device__ __forceinline__ bool bfs_any_live8(const ulonglong2 *ent, uint32_t hmask, const BfsShared &sh,
                                               const uint8_t *rpos, uint32_t n_ok, uint32_t t, uint32_t r, int w,
@@ -3512,10 +3529,12 @@ __device__ __forceinline__ bool bfs_any_live8(const ulonglong2 *ent, uint32_t hm
     int64_t sl[8];
     uint64_t inf[8];
     bool term = false;
+    Win8 wn;
+    win8(sh, j0, wn);
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         uint64_t ck = 0;
-        const int c = bfs_child_w(sh, rpos, n_ok, t, r, w, s0, m0, j0 + i, &ck);
+        const int c = bfs_child_fv(wn.f[i], wn.vv[i], rpos, n_ok, t, r, w, s0, m0, j0 + i, &ck);
         term |= c == 3;
         k[i] = (c == 1 || c == 2) ? ck : 0;
     }
@@ -3680,11 +3699,14 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
                     const uint32_t s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
                     uint64_t ck[8];
                     uint32_t h[8], e[8];
+                    Win8 wn;
+                    win8(sh, j0, wn);
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
                         ck[u] = 0;
                         const int j = j0 + u;
-                        if ((uint32_t)j != rt && bfs_child_w(sh, rpos, n_ok, (uint32_t)t, rt, w, s0, m0, j, &ck[u]) != 1)
+                        if ((uint32_t)j != rt &&
+                            bfs_child_fv(wn.f[u], wn.vv[u], rpos, n_ok, (uint32_t)t, rt, w, s0, m0, j, &ck[u]) != 1)
                             ck[u] = 0;
                         if ((uint32_t)j == rt) ck[u] = 0;
                         h[u] = lv_hash(ck[u]);
@@ -3788,12 +3810,15 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
                         uint64_t kk[8];
                         uint32_t h[8];
                         uint64_t e[8];
+                        Win8 wn;
+                        win8(sh, j0, wn);
 #pragma unroll
                         for (int u = 0; u < 8; u++) {
                             uint64_t ck = 0;
                             const int j = j0 + u;
                             kk[u] = ((uint32_t)j != rt &&
-                                     bfs_child_w(sh, rpos, n_ok, (uint32_t)t, rt, w, s0, m0, j, &ck) == 1) ? ck + 1 : 0;
+                                     bfs_child_fv(wn.f[u], wn.vv[u], rpos, n_ok, (uint32_t)t, rt, w, s0, m0, j, &ck) == 1)
+                                    ? ck + 1 : 0;
                             h[u] = gl_hash(kk[u]);
                         }
 #pragma unroll
@@ -4348,12 +4373,14 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                 {
                     const int j0 = it < items ? (int)(it - i * ng) * 8 : 0;
                     uint64_t ck[8];       // same-layer children of members j0..j0+7: s2 << 32 | mask'
+                    Win8 wn;
+                    win8(sh, j0, wn);
 #pragma unroll
                     for (int q = 0; q < 8; q++) {
                         ck[q] = 0;
                         const int j = j0 + q;
                         if (j >= w || ((mask >> j) & 1)) continue;
-                        const uint32_t f = sh.win_f[j], vv = sh.win_vv[j];
+                        const uint32_t f = wn.f[q], vv = wn.vv[q];
                         const int v1 = (int)(vv & 0xFFFF), v2 = (int)(vv >> 16);
                         int s2;
                         if (!cas_step((int)f, v1, v2, (int)s, &s2)) continue;

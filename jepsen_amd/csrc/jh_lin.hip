@@ -813,14 +813,17 @@ __device__ __forceinline__ void hbm_insert(uint64_t *memo, uint32_t cap_mask, ui
         ulonglong2 e[HB];
 #pragma unroll
         for (uint32_t j = 0; j < HB; j++) e[j] = B[j];
+        // the first slot of another generation and its tag word, selected
+        // with static indices (e[j0] put the bucket through scratch memory:
+        // a store and a reload per insert)
         int j0 = -1;
+        unsigned long long exp = 0;
 #pragma unroll
         for (int j = HB - 1; j >= 0; j--)
-            if ((e[j].y >> 40) != gen) j0 = j;
+            if ((e[j].y >> 40) != gen) { j0 = j; exp = e[j].y; }
         if (j0 < 0) { b = (b + HB) & cap_mask; continue; }
         // lanes of one wave may race for a slot (evictions insert from all
         // lanes at once): claim it with a CAS on the tag word
-        unsigned long long exp = e[j0].y;
         if (__hip_atomic_compare_exchange_strong((unsigned long long *)&memo[2 * (size_t)(b + j0) + 1],
                                                  &exp, (unsigned long long)w1,
                                                  __ATOMIC_RELAXED, __ATOMIC_RELAXED,

@@ -325,9 +325,11 @@ class Context:
         base, nw = C.c_int64(), C.c_int64()
         cap = 0 if words_cap is None else int(words_cap)
         if words_cap is None:
-            # size from a first call's n_words would cost a second device pass:
-            # the span is bounded by the history's own values
-            cap = 1 << 16
+            # the element span is bounded by the history's own values (the :add
+            # rows' and the reads' elements): size the output from them on the
+            # host so the device pass runs once; a device-resident history has
+            # no host copy to bound, so it starts small and grows once
+            cap = _set_span_words(cols) if not on_device else 1 << 16
         for _ in range(2):
             if out is not None:
                 if words_cap is None or len(out) != 4 or any(
@@ -399,6 +401,22 @@ class Context:
         rc = lib().jh_check_queue(self._h, C.byref(h), C.byref(r), A.ptr64(pairs[0]), cap, err, len(err))
         _raise(rc, err)
         return self._queue_out(r, pairs, ["final_queue"])
+
+
+def _set_span_words(cols):
+    """Bitmap words covering every element jh_check_set_bitmaps can see: the
+    non-nil values of the :add invocations / completions and every read
+    element in aux (a superset of the final read's), as jh_set.hip's
+    k_set_scan / k_set_range bound [vmin, vmax]."""
+    v = np.asarray(cols.value)
+    t = np.asarray(cols.type)
+    sel = (np.asarray(cols.f) == A.F_ADD) & ((t == A.TYPE_INVOKE) | (t == A.TYPE_OK)) & (v != A.NIL)
+    vals = v[sel]
+    aux = np.asarray(cols.aux) if cols.aux is not None else np.zeros(0, np.int64)
+    lo = min([int(x.min()) for x in (vals, aux) if len(x)], default=0)
+    hi = max([int(x.max()) for x in (vals, aux) if len(x)], default=0)
+    # (a span over 2^34 elements is refused by the library before any copy)
+    return max(1, min(((hi - lo) >> 5) + 2, (1 << 29) + 1))
 
 
 def bits_to_runs(words, base):

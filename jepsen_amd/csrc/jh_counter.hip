@@ -365,10 +365,19 @@ __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restric
             break;
         }
         if (got >= 0) atomicAnd(&cw[got], ~CW_U);
-        // a claimed :ok :read counts in its tile as a read row (unless the
-        // branch below strips it as an orphan)
-        if (got >= 0 && (ff == JH_F_ADD || ff == JH_F_READ) && (type[got] & 3) == T_OK && f[got] == JH_F_READ)
-            atomicAdd(&agg[got / CNT_TILE].nr, 1);
+        const bool got_okread = got >= 0 && (type[got] & 3) == T_OK && f[got] == JH_F_READ;
+        if (got_okread) {
+            // an :ok :read counts in its tile as a read row only when it
+            // completes an [:invoke :read] (checker.clj:713-716); completing
+            // anything else it has no pending read: an orphan, stripped of its
+            // kind as the in-chunk pairing does (k_cnt_pack), so no later pass
+            // reads its pair[] (never written for it)
+            if (ff == JH_F_READ) atomicAdd(&agg[got / CNT_TILE].nr, 1);
+            else {
+                atomicMin(&m->viol2, ((unsigned long long)got << 4) | JH_CAUSE_ORPHAN);
+                atomicAnd(&cw[got], ~7u);
+            }
+        }
         if (ff == JH_F_ADD) {
             uint32_t w = CW_NONE;
             const bool failed = got >= 0 && (type[got] & 3) == T_FAIL;
@@ -384,12 +393,8 @@ __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restric
                 }
             }
             cw[r] = w;
-        } else if (ff == JH_F_READ && got >= 0 && (type[got] & 3) == T_OK) {
+        } else if (ff == JH_F_READ && got_okread) {
             pair[got] = (int32_t)r;
-        } else if (got >= 0 && (type[got] & 3) == T_OK && f[got] == JH_F_READ) {
-            // an :ok :read completing an invocation that is not a read
-            atomicMin(&m->viol2, ((unsigned long long)got << 4) | JH_CAUSE_ORPHAN);
-            atomicAnd(&cw[got], ~7u);
         }
     }
 }

@@ -1342,7 +1342,7 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
     const uint32_t lb_lo = lane < 32 ? 1u << lane : 0u, lb_hi = lane >= 32 ? 1u << (lane - 32) : 0u;
     uint32_t theta = 0;
     int lcount = 0;
-    uint32_t n_steps = 0, n_lay = 0, n_up = 0, n_spill = 0, n_refill = 0, n_slow = 0, n_evict = 0;
+    uint32_t n_steps = 0, n_lay = 0, n_up = 0, n_spill = 0, n_refill = 0, n_slow = 0, n_evict = 0, n_hbm = 0;
     const unsigned long long probes0 = my_probes;
 
     // layer-table window: lane j holds lay[tb0 + j]
@@ -1494,6 +1494,7 @@ insert:
                 if (++lcount >= M::EVICT) {
                     DFS_STAT(n_evict++);
                     const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
+                    DFS_STAT(n_hbm += (uint32_t)lcount - (uint32_t)er);
                     lcount = rfl((int)(uint32_t)er);
                     theta = rflu((uint32_t)(er >> 32));
                 }
@@ -1505,6 +1506,7 @@ insert:
                     bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
                 }
                 theta = max(theta, nt + 1);
+                DFS_STAT(n_hbm++);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             }
@@ -1623,7 +1625,7 @@ done:
     if (A.dbg && lane == 0) {
         unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
         d[4] += n_steps; d[5] += ins; d[6] += n_evict; d[7] += n_lay; d[10] += n_up;
-        d[11] += n_spill; d[12] += n_refill; d[13] += n_slow; d[14] += my_probes - probes0;
+        d[11] += n_spill; d[12] += n_refill; d[13] += n_slow; d[14] += my_probes - probes0; d[8] += n_hbm;
     }
 #endif
     return verdict;
@@ -5486,9 +5488,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         HIP_TRY(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
         unsigned long long tot[16] = {0}, mx9 = 0;
         for (int w = 0; w < waves1; w++) { for (int k = 0; k < 16; k++) tot[k] += h[16 * w + k]; mx9 = std::max(mx9, h[16 * w + 9]); }
-        fprintf(stderr, "[jh-dfs] waves=%d keys=%llu search=%.0f cyc/key | steps=%llu inserts=%llu evict=%llu lay-loads=%llu op-loads=%llu spills=%llu refills=%llu slow=%llu hbm-probes=%llu | cyc/step=%.0f | wave-busy avg=%.0f max=%llu cyc\n",
+        fprintf(stderr, "[jh-dfs] waves=%d keys=%llu search=%.0f cyc/key | steps=%llu inserts=%llu evict=%llu lay-loads=%llu op-loads=%llu spills=%llu refills=%llu slow=%llu hbm-probes=%llu hbm-inserts=%llu | cyc/step=%.0f | wave-busy avg=%.0f max=%llu cyc\n",
                 waves1, tot[3], (double)tot[2] / std::max(1ULL, tot[3]), tot[4], tot[5], tot[6], tot[7], tot[10],
-                tot[11], tot[12], tot[13], tot[14], (double)tot[2] / std::max(1ULL, tot[4]), (double)tot[9] / waves1, mx9);
+                tot[11], tot[12], tot[13], tot[14], tot[8], (double)tot[2] / std::max(1ULL, tot[4]), (double)tot[9] / waves1, mx9);
         HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 512) * 16, st));
     }
     int waves_x = 0;

@@ -65,6 +65,52 @@ def test_counter_errors(ctx):
         assert (g["valid"], g["cause"]) == (c["valid"], c["cause"]) and g["valid"] == A.UNKNOWN
 
 
+def _counter_same(g, c):
+    assert (g["valid"], g["cause"]) == (c["valid"], c["cause"])
+    assert g["n_reads"] == c["n_reads"] and g["n_errors"] == c["n_errors"]
+    assert g["first_err_entry"] == c["first_err_entry"]
+    if c["n_reads"]:
+        assert (g["reads"] == c["reads"]).all()
+
+
+@pytest.mark.parametrize("n_procs", [4, 40])
+@pytest.mark.parametrize("at", [2040, 2047, 4095])
+def test_counter_mismatched_completion_across_chunks(ctx, n_procs, at):
+    """an [:invoke :add] whose completion is an [:ok :read]
+    in a later 2048-row chunk (the pack spills it), or of a process past the
+    chunk's 32 tracked ones, is an orphan read exactly as inside one chunk --
+    the verdict may not depend on where the chunk boundaries fall."""
+    inv = lambda p, f, v: {"process": p, "type": "invoke", "f": f, "value": v}
+    ok = lambda p, f, v: {"process": p, "type": "ok", "f": f, "value": v}
+    h, total, p = [], 0, 0
+    while len(h) < at:
+        q = 1 + (p % (n_procs - 1))        # processes 1..n_procs-1 as filler
+        h += [inv(q, "add", 1), ok(q, "add", 1)]
+        total += 1
+        p += 1
+        if p % 50 == 0:
+            h += [inv(q, "read", None), ok(q, "read", total)]
+    h = h[:at]
+    if len(h) % 2:
+        h.pop()
+    h.append(inv(0, "add", 1))                      # process 0's invocation ...
+    for k in range(12):                             # ... past the chunk boundary
+        q = 1 + (k % (n_procs - 1))
+        h += [inv(q, "add", 1), ok(q, "add", 1)]
+    h.append(ok(0, "read", 5))                      # ... completed by a read
+    h += [inv(1, "read", None), ok(1, "read", 7)]
+    cols = H.encode(h, keyed=False)
+    _counter_same(ctx.check_counter(cols), oracle.check_counter(cols))
+
+
+def test_counter_many_processes_random(ctx):
+    """More than the pack's 32 tracked processes per chunk, with :info and
+    :fail completions, against the oracle."""
+    cols = synth.counter(n_ops=300000, n_procs=90, read_every=7, p_fail=0.05, p_info=0.02,
+                         n_bad_reads=5, seed=11)
+    _counter_same(ctx.check_counter(cols), oracle.check_counter(cols))
+
+
 def _set_same(g, c):
     for k in ("valid", "cause", "attempt_count", "acknowledged_count", "ok_count", "lost_count",
               "recovered_count", "unexpected_count", "first_fail_entry", "final_read_entry"):

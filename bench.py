@@ -51,31 +51,42 @@ def pmc_traffic(workload, seed, kernel):
 
 
 # the search phases a bench line reports a roofline for: (summary field of
-# the time, of the memo probes, of the entries of the keys searched, kernel)
+# the time, of the memo probes, of the entries of the keys searched, of the
+# number of keys searched, kernel). Streamed (ABI 5), the phase-2 LEAN role,
+# the WIDE role and xw each have their own span (first key to last wave end).
 PHASES = {
-    "phase1": ("dfs_ms", "memo_probes", None, "k_lin_dfs<true>"),
-    "phase2_lean": ("seq_ms", "seq_probes", "lean_entries", "k_lin_seq_lw"),   # LEAN role of the two-role grid
-    "phase3_lean": ("p3_ms", "p3_probes", "lean_entries", "k_lin_seq3<true>"),
-    "wide": ("wide_ms", "wide_probes", "wide_entries", "k_lin_seq_lw"),         # its WIDE role (phase 3: k_lin_seqw)
-    "xw": ("xw_ms", "xw_probes", "xw_entries", "k_lin_xw"),
+    "phase1": ("dfs_ms", "memo_probes", None, None, "k_lin_dfs<true>"),
+    "phase2_lean": ("seq_ms", "seq_probes", "lean_entries", "n_lean_deferred", "k_lin_seq_lw"),
+    "phase3_lean": ("p3_ms", "p3_probes", "p3_entries", "n_phase3", "k_lin_seq3<true>"),
+    "wide": ("wide_ms", "wide_probes", "wide_entries", "n_deferred_wide", "k_lin_seq_lwx"),
+    "xw": ("xw_ms", "xw_probes", "xw_entries", "n_xw", "k_lin_seq_lwx"),
 }
 
 
+def _field(x, f):
+    if f == "n_lean_deferred":
+        return x["n_deferred"] - x["n_deferred_wide"]
+    return x[f]
+
+
 def phase_rooflines(sums, n_entries):
-    """Per search phase, from jh_summary's per-phase HIP events and probe
+    """Per search phase, from jh_summary's per-phase times and probe
     counters: algorithmic bytes (56 B per entry of the keys the phase
-    searches + 16 B per HBM memo probe) over the phase's time."""
+    searches + 16 B per HBM memo probe) over the phase's time.
+    A phase that searched no key is not a phase of this line (its launch may
+    still have run empty): skipped."""
     out = {}
-    for name, (tf, pf, ef, kern) in PHASES.items():
+    for name, (tf, pf, ef, kf, kern) in PHASES.items():
         ms = float(np.mean([x[tf] for x in sums]))
-        if ms <= 0:
+        keys = float(np.mean([_field(x, kf) for x in sums])) if kf else 1.0
+        if ms <= 0 or keys <= 0:
             continue
         probes = float(np.mean([x[pf] for x in sums]))
-        ent = float(n_entries if ef is None else sums[-1][ef])
+        ent = float(n_entries if ef is None else np.mean([x[ef] for x in sums]))
         alg = BYTES_PER_ENTRY * ent + BYTES_PER_PROBE * probes
         ach = alg / (ms / 1e3) / 1e9
         out[name] = {"kernel": kern, "ms": ms, "alg_bytes": alg, "probes": probes, "entries": ent,
-                     "achieved": ach, "frac": ach / PEAK_HBM_GBS}
+                     "keys": keys, "achieved": ach, "frac": ach / PEAK_HBM_GBS}
     return out
 
 
@@ -305,6 +316,9 @@ def main():
                        "deferred_keys": int(s.n_deferred), "deferred_entries": int(s.deferred_entries),
                        "phase1_ms": dfs_avg * 1e3, "phase2_seq_ms": seq_avg * 1e3,
                        "phase2_bfs_ms": float(np.mean(bfs_ms)),
+                       # ABI 5: heavy keys started while phase 1 ran (the streaming pass), when
+                       "streamed": bool(s.streamed), "phase2_start_ms": float(np.mean([x["p2_start_ms"] for x in sums])),
+                       "phase1_span_ms": float(np.mean([x["p1_span_ms"] for x in sums])),
                        "phases": phase_table(sums), "opts": args.tune or None},
             "shard": shard_info,
             "value_kind": "history resident in HBM, verdicts left in HBM (kernel pipeline only); "
@@ -345,7 +359,8 @@ def phase_table(sums):
     return {"phase1": {"ms": mean("dfs_ms"), "probes": mean("memo_probes")},
             "phase2_lean": {"ms": mean("seq_ms"), "probes": mean("seq_probes"), "keys": last["n_deferred"] - last["n_deferred_wide"],
                             "entries": last["lean_entries"], "waves": last["waves"][0], "helper_probes": mean("helper_probes")},
-            "phase3_lean": {"ms": mean("p3_ms"), "probes": mean("p3_probes"), "keys": last["n_phase3"], "waves": last["waves"][2]},
+            "phase3_lean": {"ms": mean("p3_ms"), "probes": mean("p3_probes"), "keys": last["n_phase3"],
+                            "entries": last["p3_entries"], "waves": last["waves"][2]},
             "bfs": {"ms": mean("bfs_ms")},
             "wide": {"ms": mean("wide_ms"), "probes": mean("wide_probes"), "keys": last["n_deferred_wide"],
                      "entries": last["wide_entries"], "waves": last["waves"][1], "phase3_keys": last["n_phase3_wide"]},

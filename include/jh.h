@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define JH_ABI_VERSION 4
+#define JH_ABI_VERSION 5
 
 /* Return codes. Anything non-zero also writes a NUL-terminated message into
  * the caller's err buffer; the JNA shim throws ex-info and check-safe turns
@@ -94,7 +94,8 @@ extern "C" {
 #define JH_CAUSE_NIL_VALUE    6  /* nil where the checker does arithmetic     */
 #define JH_CAUSE_OVERFLOW     7  /* long overflow (Clojure + throws)          */
 #define JH_CAUSE_STATES       8  /* more than 65532 distinct values in one key */
-#define JH_CAUSE_DEFERRED     9  /* JH_LIN_PHASE1_ONLY: past the quick budget, not searched further */
+#define JH_CAUSE_DEFERRED     9  /* JH_LIN_PHASE1_ONLY: past the quick budget, not searched further;
+                                    explored = the quick search's progress (deepest layer / layers x 10^6) */
 
 #define JH_MAX_WINDOW 256
 
@@ -136,6 +137,9 @@ typedef struct jh_history {
 /* Phase 1 keeps every key it started until the quick budget (no hand-over of
  * long searches to the heavy-key pass once its queue is empty). */
 #define JH_LIN_NO_HANDOVER   128
+/* The heavy-key pass starts after phase 1 has ended (the round-3 schedule)
+ * instead of consuming phase 1's deferrals as they are made. Same verdicts. */
+#define JH_LIN_NO_STREAM     256
 
 typedef struct jh_lin_opts {
     int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */
@@ -221,6 +225,13 @@ typedef struct jh_summary {
     int64_t wide_entries;      /* entries of the deferred WIDE keys */
     int64_t xw_entries;        /* entries of the k_lin_xw keys */
     int64_t waves[4];          /* launched waves: phase-2 LEAN, WIDE, phase-3 LEAN, xw */
+    /* ABI 5 (round 4): the streaming heavy-key pass (JH_LIN_NO_STREAM turns it
+     * off). When streamed, seq_ms / bfs_ms / xw_ms are the engines' own spans
+     * (first key taken to last wave end), p3_ms runs from the end of phase 2. */
+    int64_t streamed;          /* 1: heavy keys started while phase 1 still ran */
+    int64_t p3_entries;        /* entries of the LEAN keys restarted in phase 3 */
+    double  p2_start_ms;       /* first heavy key taken, ms after phase 1's first wave (-1: none) */
+    double  p1_span_ms;        /* phase 1's first wave to its last wave's end (streamed) */
 } jh_summary;
 
 typedef struct jh_ctx jh_ctx;

@@ -6,7 +6,7 @@ every struct layout.
 """
 import ctypes as C
 
-JH_ABI_VERSION = 4
+JH_ABI_VERSION = 5
 
 JH_OK, JH_EINVAL, JH_EUNSUPPORTED, JH_EDEVICE, JH_ENOMEM = 0, 1, 2, 3, 4
 TYPE_INVOKE, TYPE_OK, TYPE_FAIL, TYPE_INFO = 0, 1, 2, 3
@@ -59,6 +59,7 @@ ALGORITHMS = {"competition": ALGO_COMPETITION, "wgl": ALGO_WGL, "linear": ALGO_L
 LIN_BFS_ONLY, LIN_GEN_JUMP, LIN_INTERN_PER_KEY, LIN_NO_HELPERS, LIN_HELPERS_NOW = 1, 2, 4, 8, 16
 LIN_PHASE1_ONLY, LIN_SKIP_PHASE1 = 32, 64
 LIN_NO_HANDOVER = 128
+LIN_NO_STREAM = 256
 CAUSE_DEFERRED = 9
 
 
@@ -97,7 +98,10 @@ class JhSummary(C.Structure):
                 ("p3_probes", C.c_int64), ("wide_probes", C.c_int64), ("xw_probes", C.c_int64),
                 ("helper_probes", C.c_int64), ("n_deferred_wide", C.c_int64), ("n_phase3", C.c_int64),
                 ("n_phase3_wide", C.c_int64), ("n_xw", C.c_int64), ("lean_entries", C.c_int64),
-                ("wide_entries", C.c_int64), ("xw_entries", C.c_int64), ("waves", C.c_int64 * 4)]
+                ("wide_entries", C.c_int64), ("xw_entries", C.c_int64), ("waves", C.c_int64 * 4),
+                # ABI 5: the streaming heavy-key pass
+                ("streamed", C.c_int64), ("p3_entries", C.c_int64), ("p2_start_ms", C.c_double),
+                ("p1_span_ms", C.c_double)]
 
 
 class JhLinConfig(C.Structure):

@@ -110,6 +110,7 @@ void jh_close(jh_ctx *ctx) {
         (void)hipSetDevice(ctx->device);
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         for (auto &b : ctx->bufs) if (b.p) (void)hipFree(b.p);
+        if (ctx->hflag) (void)hipHostFree(ctx->hflag);
         for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         if (ctx->aux) (void)hipStreamDestroy(ctx->aux);

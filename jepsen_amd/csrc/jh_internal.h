@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 #include <string>
 #include "../../include/jh.h"
@@ -61,6 +62,8 @@ struct jh_ctx {
     bool lds_attr = false;        // >64 KB dynamic-LDS attributes set for this device's kernels
     bool lds_attr_wg = false;
     int n_cu = 256;
+    int32_t *hflag = nullptr;     // host-mapped flag: phase 1's queue drained (jh_lin.hip)
+    int32_t *hflag_dev = nullptr;
     void *pinned = nullptr;       // small pinned staging for scalars
     size_t pinned_bytes = 0;
     std::vector<jh_ctx *> members;  // jh_open_multi: one context per device (jh_multi.hip); empty otherwise

@@ -339,8 +339,55 @@ struct DfsArgs {
     // crowded CU (26 waves) run near a lone wave's speed while the many short
     // ones fill the gaps; 0: off
     int32_t prio_ins;
+    // The streaming heavy-key pass (round 4: the heavy keys start when phase 1
+    // defers them, not when phase 1 ends). Phase 1 also appends each deferred
+    // key (int32) to s_all and to its kind's s_kind (lists filled with -1
+    // first; their lengths are defer_count / defer_kind_count), counts every
+    // key it finishes in p1_count, and the wave that first finds the last
+    // phase-1 kernel's queue empty raises *drained (host-mapped memory) so the
+    // host launches the consumers then, into CUs that phase 1 is leaving.
+    // Consumers: `list` is live, *live_n long, and complete once *p1_done ==
+    // p1_tot[0] + p1_tot[1] (phase 1's LEAN and WIDE list lengths).
+    int32_t *s_all, *s_kind;
+    int32_t *p1_count;          // phase 1 (producer): incremented per finished key
+    const int32_t *p1_done;     // consumers: the same counter, read
+    const int32_t *p1_tot;
+    int32_t *drained;
+    const int32_t *live_n;
 };
 constexpr unsigned long long SEQ_HANDED = ~0ULL;
+
+__device__ __forceinline__ int ld_agent(const int32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every key of phase 1 finished: no more deferrals (p1_done is raised after
+// the key's list entries are written, with release order)
+__device__ __forceinline__ bool p1_finished(const int32_t *done, const int32_t *tot) {
+    return ld_agent(done) >= ld_agent(tot) + ld_agent(tot + 1);
+}
+// One lane: the key at index idx of a live list, waiting until phase 1 has
+// appended it; -1 once phase 1 has finished without reaching idx. A wait
+// past STREAM_WATCHDOG (a bug, not a slow search: phase 1's longest search
+// is bounded by its quick budget) sets flag 512 and gives up, so the grid
+// always drains.
+constexpr unsigned long long STREAM_WATCHDOG = 3000000000ULL;   // 30 s of s_memrealtime (100 MHz)
+__device__ int stream_key(const int32_t *list, const int32_t *live_n, const int32_t *done, const int32_t *tot,
+                          int idx, int32_t *flags) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (idx < ld_agent(live_n)) {
+            for (;;) {
+                const int k = ld_agent(&list[idx]);
+                if (k >= 0) return k;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > STREAM_WATCHDOG) { atomicOr(flags, 512); return -1; }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        if (p1_finished(done, tot) && idx >= ld_agent(live_n)) return -1;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > STREAM_WATCHDOG) { atomicOr(flags, 512); return -1; }
+        __builtin_amdgcn_s_sleep(20);
+    }
+}
 // verdict cause bits naming the engine in :linear mode (k_frontier turns them into jh_key_verdict.analyzer)
 constexpr int32_t CAUSE_BY_LINEAR = 0x100, CAUSE_BY_WGL = 0x200;
 
@@ -354,14 +401,17 @@ constexpr int JH_CANCELLED = 3; // internal: the other search settled the key fi
 // instead of starting over.
 __device__ __forceinline__ bool extend_budget(const DfsArgs &A, uint32_t &budget) {
     if (A.budget_full <= (int64_t)budget) return false;
-    int q = 0, d = 0;
+    int q = 0, d = 0, n = 0;
     if ((threadIdx.x & 63) == 0) {
         q = __hip_atomic_load(A.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         d = __hip_atomic_load(A.defer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // a live list is only known to be exhausted once phase 1 has finished
+        if (A.live_n) n = p1_finished(A.p1_done, A.p1_tot) ? ld_agent(A.live_n) : 0x7FFFFFFF;
+        else n = A.n_list_dev ? *A.n_list_dev : A.n_list;
     }
     q = __builtin_amdgcn_readlane(q, 0);
     d = __builtin_amdgcn_readlane(d, 0);
-    const int n = A.n_list_dev ? *A.n_list_dev : A.n_list;
+    n = __builtin_amdgcn_readlane(n, 0);
     // with keys already handed to phase 3 it runs anyway (4 waves per CU for
     // many deep searches): join it rather than delay its start
     if (q < n || d > 0) return false;
@@ -975,6 +1025,224 @@ __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint32_t *bcnt, uin
     return ((uint64_t)th2 << 32) | (uint32_t)kept;
 }
 
+// ---------------------------------------------------------------------------
+// Phase 1's HBM memo in blocks (round 4). The hash table above costs every
+// evicted entry a random 128-byte line: its bucket read, then the CAS and the
+// store write the line back -- phase 1 moved 2.0 GB in and 3.2 GB out for
+// 0.6 GB of algorithmic bytes (profiles/r03/traffic_c3_s3_k_lin_dfs_true.json)
+// though its searches probe HBM rarely (~1 Bloom-positive lane per 300 steps).
+// Here a key's evicted entries (8-byte LEAN keys, no generation tag: the
+// blocks are the key's own) fill 8 KB blocks of 1 024 slots to at most half,
+// one block after the other, so an eviction writes whole lines of a few
+// blocks. Lane b of the wave holds block b's layer range [tlo, thi]; a probe
+// of a Bloom-positive child reads one 64-byte group of every block whose range
+// holds the child's layer, all lanes at once: one round trip, as before.
+// The entries are staged in registers (no global stage either).
+constexpr int BLK_SLOTS = 1024;          // 8-byte slots per block (8 KB)
+constexpr int BLK_FILL = 512;            // entries per block at most (load 1/2)
+constexpr int BLK_MAX = 64;              // blocks per key (lane b: block b); 32 K entries
+constexpr int BLK_GROUPS = BLK_SLOTS / 8;
+constexpr int32_t FLAG_BLK_FULL = 2048;  // flags: a key needed more than BLK_MAX blocks
+struct BlkState {
+    uint32_t nblk, fill;      // blocks used; entries in the last one (wave-uniform)
+    uint32_t tlo, thi;        // lane b: block b's layer range
+    uint32_t ovf;             // a block beyond BLK_MAX was needed: the key's memo is incomplete
+};
+__device__ __forceinline__ uint32_t blk_group(uint64_t k) {
+    return (uint32_t)(jh_mix64(k) >> 40) & (BLK_GROUPS - 1);
+}
+// one lane: k (unique in the key's memo) into block blk, from its hash group
+// on; the group is read first so the CAS goes to its first empty slot
+__device__ __forceinline__ void blk_put(uint64_t *blk, uint64_t k) {
+    uint32_t g = blk_group(k);
+    for (int it = 0; it < BLK_GROUPS; it++) {
+        unsigned long long *p = (unsigned long long *)(blk + 8 * g);
+        int j0 = 8;
+#pragma unroll
+        for (int j = 7; j >= 0; j--)
+            if (__hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) j0 = j;
+        for (int j = j0; j < 8; j++) {
+            unsigned long long exp = 0;
+            if (__hip_atomic_compare_exchange_strong(p + j, &exp, (unsigned long long)k, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                return;
+        }
+        g = (g + 1) & (BLK_GROUPS - 1);
+    }
+}
+// one lane: is k in block blk (a group with an empty slot ends the probe)
+__device__ __forceinline__ bool blk_has(const uint64_t *blk, uint64_t k) {
+    uint32_t g = blk_group(k);
+    for (int it = 0; it < BLK_GROUPS; it++) {
+        const unsigned long long *p = (const unsigned long long *)(blk + 8 * g);
+        unsigned long long e[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) e[j] = __hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool hit = false, room = false;
+#pragma unroll
+        for (int j = 0; j < 8; j++) { hit |= e[j] == k; room |= e[j] == 0; }
+        if (hit) return true;
+        if (room) return false;
+        g = (g + 1) & (BLK_GROUPS - 1);
+    }
+    return false;
+}
+// wave min / max of a per-lane value over the lanes in m (m != 0)
+__device__ __forceinline__ uint32_t wave_min_in(uint64_t m, int lane, uint32_t v) {
+    uint32_t x = ((m >> lane) & 1) ? v : 0xFFFFFFFFu;
+    for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_max_in(uint64_t m, int lane, uint32_t v) {
+    uint32_t x = ((m >> lane) & 1) ? v : 0u;
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+    return x;
+}
+// the lanes' entries x (where v) into the key's blocks: the last block up to
+// BLK_FILL, then a fresh one (zeroed first); their layer ranges widen
+__device__ __forceinline__ void blk_add(uint64_t *region, BlkState &s, uint64_t x, bool v, int lane) {
+    const uint64_t m = ballot(v);
+    if (!m) return;
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    const uint32_t rank = (uint32_t)mbcnt(m);
+    const uint32_t room = s.nblk ? BLK_FILL - s.fill : 0;
+    const uint32_t cur = s.nblk - 1, nb = s.nblk;
+    if (cnt > room) {
+        if (nb >= BLK_MAX) { s.ovf = 1; return; }
+        uint4 *z = (uint4 *)(region + (size_t)nb * BLK_SLOTS);
+#pragma unroll
+        for (int r = 0; r < BLK_SLOTS * 8 / 16 / 64; r++) z[lane + 64 * r] = make_uint4(0, 0, 0, 0);
+        // the zeros in L2 before the CAS inserts (L2 atomics) of other lanes
+        __builtin_amdgcn_s_waitcnt(0);
+        wave_sync();
+    }
+    const bool in_cur = rank < room;
+    if (v) blk_put(region + (size_t)(in_cur ? cur : nb) * BLK_SLOTS, x);
+    const uint32_t xt = lk_t(x);
+    const uint64_t mc = ballot(v && in_cur), mn = m & ~mc;
+    if (mc) {
+        const uint32_t lo = wave_min_in(mc, lane, xt), hi = wave_max_in(mc, lane, xt);
+        if (lane == (int)cur) { s.tlo = min(s.tlo, lo); s.thi = max(s.thi, hi); }
+    }
+    if (mn) {
+        const uint32_t lo = wave_min_in(mn, lane, xt), hi = wave_max_in(mn, lane, xt);
+        if (lane == (int)nb) { s.tlo = lo; s.thi = hi; }
+        s.nblk = nb + 1;
+        s.fill = cnt - room;
+    } else {
+        s.fill += cnt;
+    }
+}
+// memo_evict for the block memo: the same theta rule; the LDS table is not
+// rebuilt but compacted bucket by bucket in place (a lane owns whole buckets:
+// the entries at or above theta keep their slots' order, the others go to the
+// blocks), so nothing is staged and no entry can fail to find a place.
+// Returns the blocks, the new theta and the entries kept.
+struct EvictBlk { BlkState s; uint32_t theta; int kept; };
+template <class M>
+__device__ __forceinline__ EvictBlk memo_evict_blk(uint64_t *lmemo, uint32_t *bcnt, uint32_t *bloom, uint64_t *region,
+                                                BlkState s, uint32_t t_cur, uint32_t theta_old, int lane) {
+    int bins = 0;                                  // lane b < 16 holds bin b
+#pragma unroll 1
+    for (int r = 0; r < M::SLOTS / 64; r++) {
+        const uint64_t x = lmemo[lane + 64 * r];
+        const uint32_t xt = lk_t(x);
+        const int d = x == 0 ? 99 : (xt >= t_cur ? 0 : (int)min(t_cur - xt, 15u));
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            const int cnt = __popcll(ballot(d == b));
+            if (lane == b) bins += cnt;
+        }
+    }
+    int acc = 0, dstar = -1;
+#pragma unroll 1
+    for (int b = 0; b < 16; b++) {
+        acc += readlane(bins, b);
+        if (acc > M::EVICT / 2) break;
+        dstar = b;
+    }
+    uint32_t th2;
+    if (dstar < 0) th2 = t_cur + 1;
+    else {
+        th2 = t_cur > (uint32_t)dstar ? t_cur - (uint32_t)dstar : 0u;
+        if (dstar == 15) th2 = t_cur - min(t_cur, 15u);
+    }
+    th2 = max(th2, theta_old);
+    uint8_t *bcnt8 = (uint8_t *)bcnt;
+    int kept = 0;
+#pragma unroll 1
+    for (int bb = 0; bb < M::BKT / 64; bb++) {
+        const uint32_t b = (uint32_t)lane + 64u * (uint32_t)bb;
+        const uint32_t n = bcnt8[b];
+        uint64_t e[4];
+        bool ev[4];
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            e[j] = (uint32_t)j < n ? lmemo[4 * b + j] : 0;
+            const bool keep = (uint32_t)j < n && lk_t(e[j]) >= th2;
+            ev[j] = (uint32_t)j < n && !keep;
+            if (keep) { lmemo[4 * b + w] = e[j]; w++; }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) if ((uint32_t)j >= w) lmemo[4 * b + j] = 0;
+        bcnt8[b] = (uint8_t)w;
+        kept += (int)w;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            blk_add(region, s, e[j], ev[j], lane);
+            if (ev[j]) {
+                uint32_t h1, h2;
+                lk_hash((uint32_t)e[j], (uint32_t)(e[j] >> 32), h1, h2);
+                bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o);
+    // the LDS rewrite and the block writes (stores, L2 atomics) done before
+    // the search goes on
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    wave_sync();
+    EvictBlk r;
+    r.s = s; r.theta = th2; r.kept = kept;
+    return r;
+}
+// one child into the blocks (both its LDS buckets full). Inlined like
+// memo_evict_blk: as calls they kept 122 VGPRs live in phase 1's loop (4
+// waves per SIMD instead of 5); inline 90, no scratch
+template <class M>
+__device__ __forceinline__ BlkState blk_add_one(uint64_t *region, BlkState s, uint64_t x, bool v, uint32_t *bloom,
+                                             uint32_t bl1, uint32_t bl2, int lane) {
+    blk_add(region, s, x, v, lane);
+    if (v) bloom_set2<M>(bloom, bl1, bl2);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    wave_sync();
+    return s;
+}
+// the Bloom-positive lanes (maybe) of a step: which children are in the
+// blocks. One round trip per such lane: every block whose layer range holds
+// the child's layer is probed at once (lane b: block b).
+struct BlkFind { uint64_t found; uint32_t probes; };
+__device__ __forceinline__ BlkFind blk_find(const uint64_t *region, BlkState s, uint64_t maybe, uint64_t k, uint32_t kt,
+                                         int lane) {
+    BlkFind f{0, 0};
+    while (maybe) {
+        const int i = __builtin_ctzll(maybe);
+        maybe &= maybe - 1;
+        const uint64_t ki = readlane64(k, i);
+        const uint32_t ti = (uint32_t)readlane((int)kt, i);
+        const bool mine = (uint32_t)lane < s.nblk && s.tlo <= ti && ti <= s.thi;
+        f.probes += (uint32_t)__popcll(ballot(mine));
+        const bool hit = mine && blk_has(region + (size_t)lane * BLK_SLOTS, ki);
+        if (ballot(hit)) f.found |= 1ULL << i;
+    }
+    return f;
+}
+
 __device__ __forceinline__ uint64_t drop_bit(uint64_t m, uint32_t r) {
     const uint64_t lo = (1ULL << r) - 1;
     return (m & lo) | ((m >> 1) & ~lo);
@@ -1322,7 +1590,7 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
 // Search order and memo contents are exactly WGL's (orc_wgl_canonical,
 // oracle/jh_oracle.c, which does probe after a backtrack and never finds the
 // child present): explored counts stay identical.
-template <class M>
+template <class M, bool BLK = false>
 __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, const char *tb, int key, int lane,
                         uint64_t *memo, Frame *stack, uint64_t *stage,
                         long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes) {
@@ -1344,6 +1612,8 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
     int lcount = 0;
     uint32_t n_steps = 0, n_lay = 0, n_up = 0, n_spill = 0, n_refill = 0, n_slow = 0, n_evict = 0, n_hbm = 0;
     const unsigned long long probes0 = my_probes;
+    // BLK (phase 1): the HBM part of the memo is this key's blocks in `memo`
+    BlkState blks{0u, 0u, 0xFFFFFFFFu, 0u, 0u};
 
     // layer-table window: lane j holds lay[tb0 + j]
     uint32_t tb0 = 0, drq = 0, dhi = 0;
@@ -1451,9 +1721,18 @@ expand:
             const uint32_t kt = khi >> 16 & 0x7FFF, ks = (khi >> 8) & 0xFF;
             const uint64_t km = k & ((1ULL << 40) - 1);
             const bool maybe = ((low >> lane) & 1) && bloom_test2<M>(bloom, lk_bl(h1), lk_bl(h2));
-            bool found = false;
-            if (maybe) found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
-            absent &= ~ballot(found);
+            if constexpr (BLK) {
+                const uint64_t mm = ballot(maybe);
+                if (mm) {
+                    const BlkFind fr = blk_find(memo, blks, mm, k, kt, lane);
+                    absent &= ~fr.found;
+                    my_probes += fr.probes;
+                }
+            } else {
+                bool found = false;
+                if (maybe) found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
+                absent &= ~ballot(found);
+            }
         }
     }
     if (!absent) goto pop;
@@ -1493,22 +1772,45 @@ insert:
                 }
                 if (++lcount >= M::EVICT) {
                     DFS_STAT(n_evict++);
-                    const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
-                    DFS_STAT(n_hbm += (uint32_t)lcount - (uint32_t)er);
-                    lcount = rfl((int)(uint32_t)er);
-                    theta = rflu((uint32_t)(er >> 32));
+                    if constexpr (BLK) {
+                        const EvictBlk e = memo_evict_blk<M>(lmemo, bcnt, bloom, memo, blks, nt, theta, lane);
+                        blks = e.s;
+                        DFS_STAT(n_hbm += (uint32_t)lcount - (uint32_t)e.kept);
+                        lcount = rfl(e.kept);
+                        theta = rflu(e.theta);
+                    } else {
+                        const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
+                        DFS_STAT(n_hbm += (uint32_t)lcount - (uint32_t)er);
+                        lcount = rfl((int)(uint32_t)er);
+                        theta = rflu((uint32_t)(er >> 32));
+                    }
                 }
             } else {
                 // both buckets full: HBM, and theta rises above the layer
-                const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
-                if (lane == i) {
-                    hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
-                    bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
+                if constexpr (BLK) {
+                    blks = blk_add_one<M>(memo, blks, ((uint64_t)khi << 32) | klo, lane == i, bloom, lk_bl(h1), lk_bl(h2), lane);
+                } else {
+                    const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
+                    if (lane == i) {
+                        hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
+                        bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
                 theta = max(theta, nt + 1);
                 DFS_STAT(n_hbm++);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
+            if constexpr (BLK) {
+                if (blks.ovf) {
+                    // more blocks than BLK_MAX (only with a quick budget over 32 K
+                    // inserts): the memo is incomplete, so the key goes to the
+                    // heavy-key pass, which restarts it
+                    if (!A.defer && lane == 0) atomicOr(A.flags, FLAG_BLK_FULL);
+                    ins = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
+                    verdict = JH_UNKNOWN;
+                    goto done;
+                }
             }
         }
         // push the parent; a full ring spills its oldest half to HBM
@@ -2072,7 +2374,7 @@ __global__ void __launch_bounds__(256) k_key_tables(TblArgs A) {
 
 // LEAN: dfs_lean (8-byte LDS keys); else WL: dfs_lean_w (16-byte LDS keys),
 // else dfs_search (every configuration in the HBM table)
-template <class M, bool LEAN, bool WL = false>
+template <class M, bool LEAN, bool WL = false, bool BLK = false>
 __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     const int lane = threadIdx.x;
     const size_t wv = (size_t)(blockIdx.x - A.wave_off);
@@ -2083,14 +2385,34 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     const int n_list = A.n_list_dev ? *A.n_list_dev : A.n_list;
     if (n_list < A.n_min || (A.n_max > 0 && n_list > A.n_max)) return;
     const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
-    if (A.t_span && lane == 0) atomicMin(&A.t_span[0], __builtin_amdgcn_s_memrealtime());
+    bool spanned = false;       // t_span[0]: the first key any wave of the role took
     if (A.defer_time && lane == 0) atomicMin(&A.defer_time[0], __builtin_amdgcn_s_memrealtime());
+    // phase 1 (streaming): this key is finished -- after its list entries
+    auto p1_key_done = [&]() {
+        if (A.p1_count && lane == 0) __hip_atomic_fetch_add(A.p1_count, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    };
     for (;;) {
         int idx = 0;
         if (lane == 0) idx = atomicAdd(A.queue, 1);
         idx = readlane(idx, 0);
-        if (idx >= n_list) break;
-        const int key = A.list[idx];
+        int key;
+        if (A.live_n) {
+            int k = -1;
+            if (lane == 0) k = stream_key(A.list, A.live_n, A.p1_done, A.p1_tot, idx, A.flags);
+            key = readlane(k, 0);
+            if (key < 0) break;
+        } else {
+            if (idx >= n_list) {
+                // the first wave to find the queue empty: the host may launch
+                // the streaming consumers now (system scope: host-mapped)
+                if (A.drained && idx == n_list && lane == 0)
+                    __hip_atomic_store(A.drained, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            key = A.list[idx];
+        }
+        if (A.t_span && !spanned && lane == 0) atomicMin(&A.t_span[0], __builtin_amdgcn_s_memrealtime());
+        spanned = true;
         const KeyMeta mt = A.meta[key];
         KeyInfo K;
         K.n_ops = mt.n_ops; K.n_ok = mt.n_ok; K.sumW = 0;
@@ -2102,17 +2424,17 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         // the LDS memo packs states in 8 bits and masks in 40 (LEAN); else
         // the HBM table only (WIDE). One mode per kernel: the two searches do
         // not share a register allocation.
-        if ((A.states8 && mt.maxw <= 40) != LEAN) continue;
+        if ((A.states8 && mt.maxw <= 40) != LEAN) { p1_key_done(); continue; }
         if (A.prio_ins > 0) __builtin_amdgcn_s_setprio(0);
         if (A.seq_start && lane == 0)
             __hip_atomic_store(&A.seq_start[key], __builtin_amdgcn_s_memrealtime() | 1ULL, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         int verdict;
-        if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
+        if constexpr (LEAN) verdict = dfs_lean<M, BLK>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else if constexpr (WL) verdict = dfs_lean_w<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         if (A.dbg && lane == 0) { A.dbg[16 * wv + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * wv + 3] += 1; }
-        if (verdict == JH_CANCELLED) continue;
+        if (verdict == JH_CANCELLED) { p1_key_done(); continue; }
         if (verdict == JH_UNKNOWN && A.defer && inserts >= A.budget &&
             (A.budget_full == 0 || inserts < A.budget_full)) {
             if (lane == 0) {
@@ -2123,11 +2445,17 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
                 const uint64_t pk = ((uint64_t)((uint64_t)tmax * 1000000u / (uint64_t)max(1, K.n_ok)) << 32) |
                                     (uint32_t)key;
                 if (A.defer64) A.defer64[d] = pk;
-                if (A.defer_kind) A.defer_kind[atomicAdd(A.defer_kind_count, 1)] = pk;
+                if (A.defer_kind) {
+                    const int dk = atomicAdd(A.defer_kind_count, 1);
+                    A.defer_kind[dk] = pk;
+                    if (A.s_kind) __hip_atomic_store(&A.s_kind[dk], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (A.s_all) __hip_atomic_store(&A.s_all[d], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (A.defer_time) A.defer_time[2 + key] = __builtin_amdgcn_s_memrealtime();
                 if (A.seq_start)
                     __hip_atomic_store(&A.seq_start[key], SEQ_HANDED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            p1_key_done();
             continue;
         }
         jh_key_verdict v;
@@ -2138,6 +2466,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         // an invalid key's failing row is resolved by k_fail_rows from tmax
         if (verdict == JH_INVALID) v.fail_entry = -(int64_t)tmax - 2;
         if (lane == 0) emit_verdict(A.out, A.claim, key, v);
+        p1_key_done();
     }
     if (A.dbg && lane == 0) A.dbg[16 * wv + 9] = __builtin_amdgcn_s_memtime() - t_begin;
     if (A.t_span && lane == 0) atomicMax(&A.t_span[1], __builtin_amdgcn_s_memrealtime());
@@ -2171,8 +2500,12 @@ __global__ void __launch_bounds__(256) k_list_cost(const int32_t *__restrict__ l
 }
 
 // phase 1: every key under the quick budget
+// (five waves per SIMD: phase 1's 20 resident waves per CU; the block memo's
+// out-of-line calls would otherwise take the register allocation past it)
 template <bool LEAN>
-__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) { lin_dfs_waves<MemoQ, LEAN>(A); }
+__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
+    lin_dfs_waves<MemoQ, LEAN, false, LEAN>(A);
+}
 // heavy keys: the full-budget sequential search racing k_lin_bfs, one wave
 // per CU with a 128 KB LDS memo
 template <bool LEAN>
@@ -2308,6 +2641,7 @@ struct WgShared {
     uint32_t w_cur, r_cur;    // the current layer's window size and RET position
     uint32_t nchild;          // children of the staged chunk
     unsigned long long pick;  // helper mode: (longest running, lowest list index) candidate
+    int n_live;               // helper mode: the list's length at this scan (live in streaming)
     uint32_t win[64];         // the current layer's window: need | becomes << 16 per member
     const uint32_t *woff;     // the key's window table (wtab_build)
     const uint32_t *wrq;
@@ -2344,6 +2678,9 @@ struct WgArgs {
     int32_t seq_waves;
     int32_t *taken;
     uint64_t late_ticks;
+    // streaming heavy-key pass: the sequential search's wave count on the
+    // device (its early and late grids); d.live_n etc. make d.list live
+    const int32_t *seq_waves_dev;
 };
 
 __device__ __forceinline__ uint64_t lk_make(uint32_t t, uint32_t s, uint64_t m) {
@@ -3170,15 +3507,22 @@ __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned 
         if (tid == 0) {
             sh.pick = ~0ULL;
             sh.cmd = 0;
-            const bool over = __hip_atomic_load(W.seq_exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= W.seq_waves ||
+            const int waves = W.seq_waves_dev ? ld_agent(W.seq_waves_dev) : W.seq_waves;
+            // streaming: the sequential search's waves may all be idle
+            // (left the queue) before phase 1 has finished deferring
+            const bool more = A.live_n && !p1_finished(A.p1_done, A.p1_tot);
+            const bool over = (!more && __hip_atomic_load(W.seq_exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= waves) ||
                               __builtin_amdgcn_s_memrealtime() - t_enter > HELPER_MAX_TICKS;
             sh.key = over ? -1 : -2;
+            sh.n_live = A.live_n ? ld_agent(A.live_n) : A.n_list;
         }
         __syncthreads();
         if (sh.key == -1) return;
         const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-        for (int i = tid; i < A.n_list; i += WG_THREADS) {
-            const int key = A.list[i];
+        const int n_list = sh.n_live;
+        for (int i = tid; i < n_list; i += WG_THREADS) {
+            const int key = A.live_n ? ld_agent(&A.list[i]) : A.list[i];
+            if (key < 0) continue;
             const unsigned long long s = __hip_atomic_load(&W.seq_start[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (s == 0 || s == SEQ_HANDED || s > now || now - s < W.late_ticks) continue;
             if (__hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
@@ -3189,7 +3533,8 @@ __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned 
         }
         __syncthreads();
         if (tid == 0 && sh.pick != ~0ULL) {
-            const int key = A.list[(int)(sh.pick & ((1u << 24) - 1))];
+            const int i = (int)(sh.pick & ((1u << 24) - 1));
+            const int key = A.live_n ? ld_agent(&A.list[i]) : A.list[i];
             sh.key = atomicCAS(&W.taken[key], 0, 1) == 0 ? key : -3;
         }
         __syncthreads();
@@ -3383,6 +3728,12 @@ struct BfsArgs {
     const int64_t *col_val, *col_val2;   // the raw value columns (model values)
     int64_t vmin, init_value;
     int32_t per_key_values;
+    // the streaming heavy-key pass (DfsArgs): `list` is live, *live_n long,
+    // complete once phase 1 has finished; t_span = [first key taken, last
+    // workgroup end] (s_memrealtime), the BFS's own time
+    const int32_t *live_n;
+    const int32_t *p1_done, *p1_tot;
+    unsigned long long *t_span;
 };
 
 struct BfsShared {
@@ -4506,14 +4857,18 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A0) {
     uint64_t *pend = A.pend + (size_t)blockIdx.x * 2 * A.q_cap;
     uint64_t *front = A.front + (size_t)blockIdx.x * 2 * A.q_cap;
     char *gscr = A.scratch + (size_t)blockIdx.x * A.scratch_bytes;
+    bool spanned = false;
     for (;;) {
         if (tid == 0) {
             const int idx = atomicAdd(A.queue, 1);
-            sh.key = idx < A.n_list ? A.list[idx] : -1;
+            if (A.live_n) sh.key = stream_key(A.list, A.live_n, A.p1_done, A.p1_tot, idx, A.src.flags);
+            else sh.key = idx < A.n_list ? A.list[idx] : -1;
         }
         __syncthreads();
         const int key = sh.key;
         if (key < 0) break;
+        if (A.t_span && !spanned && tid == 0) atomicMin(&A.t_span[0], __builtin_amdgcn_s_memrealtime());
+        spanned = true;
         if (wid == 0) {
             KeyInfo K;
             jh_key_verdict v;
@@ -4534,6 +4889,7 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A0) {
             __syncthreads();
         }
     }
+    if (A.t_span && tid == 0) atomicMax(&A.t_span[1], __builtin_amdgcn_s_memrealtime());
 }
 
 // Invalid keys settled by the DFS carry -(tmax + 2): the failing row is the
@@ -4584,6 +4940,7 @@ struct XwArgs {
     int32_t *flags;
     unsigned long long *probes;
     int32_t cause_or;           // :linear mode: CAUSE_BY_WGL on the verdicts (k_frontier)
+    unsigned long long *t_span; // [first key taken, last wave end] (s_memrealtime), or null
 };
 
 struct XwTbl {
@@ -4736,14 +5093,14 @@ __device__ __forceinline__ void xw_store(uint64_t *memo, uint32_t slot, uint32_t
                        __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-__global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
+// one wave of the 65-256-member search: wave wv's tables, nm_sh / ring in LDS
+// (k_lin_xw's own, or the dynamic LDS of k_lin_seq_lwx's xw role)
+__device__ __forceinline__ void xw_waves(const XwArgs &A, size_t wv, unsigned long long *nm_sh, uint64_t *ring) {
     const int lane = threadIdx.x;
-    __shared__ unsigned long long nm_sh[XW_SL];
-    __shared__ uint64_t ring[XW_RING * XW_FW];
     XW_PROF(unsigned long long pf[12] = {0};)
-    char *tb = A.scratch + (size_t)blockIdx.x * A.scratch_bytes;
-    uint64_t *memo = A.memo + (size_t)blockIdx.x * A.memo_cap * XW_EW;
-    uint64_t *stk = A.stack + (size_t)blockIdx.x * A.stack_cap * XW_FW;
+    char *tb = A.scratch + wv * A.scratch_bytes;
+    uint64_t *memo = A.memo + wv * A.memo_cap * XW_EW;
+    uint64_t *stk = A.stack + wv * A.stack_cap * XW_FW;
     const uint32_t cap_mask = A.memo_cap - 1;
     uint64_t zk[XW_SL];          // this lane's members' Zobrist words
 #pragma unroll
@@ -4755,6 +5112,7 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
         idx = readlane(idx, 0);
         if (idx >= A.n_list) break;
         const int key = A.list[idx];
+        if (A.t_span && idx < 64 && lane == 0) atomicMin(&A.t_span[0], __builtin_amdgcn_s_memrealtime());
         const KeyMeta mt = A.meta[key];
         const int n_ops = mt.n_ops, n_ok = mt.n_ok;
         const long long sumW = (long long)(uint32_t)mt.pad;
@@ -4955,7 +5313,25 @@ __global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
     }
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
+    if (A.t_span && lane == 0) atomicMax(&A.t_span[1], __builtin_amdgcn_s_memrealtime());
     XW_PROF(if (lane == 0) for (int k = 0; k < 12; k++) atomicAdd(&g_xw_prof[k], pf[k]);)
+}
+__global__ void __launch_bounds__(64) k_lin_xw(XwArgs A) {
+    __shared__ unsigned long long nm_sh[XW_SL];
+    __shared__ uint64_t ring[XW_RING * XW_FW];
+    xw_waves(A, blockIdx.x, nm_sh, ring);
+}
+// The streaming heavy-key pass's grid behind phase 1 (one stream): the
+// 65-256-member search (blocks 0..n_x-1: first, they are the longest), the
+// deferred WIDE keys, then LEAN waves beyond the early grid's -- three roles
+// so that the pass needs no more streams than the hardware has queues
+struct DfsTriple { XwArgs x; DfsArgs w, l; int32_t n_x, n_w; };
+constexpr int XW_LDS = (int)(XW_SL * 8 + XW_RING * XW_FW * 8);
+__global__ void __launch_bounds__(64) k_lin_seq_lwx(DfsTriple P) {
+    const int b = (int)blockIdx.x;
+    if (b < P.n_x) xw_waves(P.x, (size_t)b, (unsigned long long *)jh_lds, (uint64_t *)(jh_lds + XW_SL * 8));
+    else if (b < P.n_x + P.n_w) lin_dfs_waves<MemoWL, false, true>(P.w);
+    else lin_dfs_waves<MemoM, true>(P.l);
 }
 
 __global__ void __launch_bounds__(256) k_fail_rows(KeySrc S, jh_key_verdict *out, int64_t K) {
@@ -5048,13 +5424,14 @@ __global__ void k_summary(const jh_key_verdict *__restrict__ v, int64_t K, long 
 // history entries of the keys in each of four lists (the deferred keys, LEAN,
 // WIDE, the k_lin_xw keys): each phase's roofline bytes
 struct EntryLists {
-    const int32_t *list[4];
-    int n[4];
-    unsigned long long *sum[4];
+    const int32_t *list[5];
+    int n[5];
+    const int32_t *n_dev[5];       // if set: the list's length, on the device
+    unsigned long long *sum[5];
     const uint32_t *off;
 };
 __global__ void __launch_bounds__(256) k_list_entries(EntryLists L) {
-    const int y = blockIdx.y, n = L.n[y];
+    const int y = blockIdx.y, n = L.n_dev[y] ? *L.n_dev[y] : L.n[y];
     const int32_t *list = L.list[y];
     unsigned long long x = 0;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -5196,22 +5573,36 @@ static int fit_units(jh_ctx *ctx, int want, uint64_t per_unit, std::initializer_
 
 // words of the per-call counter block q (device): queues, list lengths, probe
 // and entry counters of the phases
-constexpr int Q_WORDS = 64;
+constexpr int Q_WORDS = 96;
 constexpr int Q_ENT_ALL = 24, Q_DEFER_L = 29, Q_DEFER_W = 30, Q_DEFER3W = 31;
 constexpr int Q_PROBES_HELP = 32, Q_PROBES_P3 = 34, Q_PROBES_WIDE = 36;
 constexpr int Q_ENT_LEAN = 40, Q_ENT_WIDE = 42, Q_ENT_XW = 44;
 constexpr int Q_T_WIDE = 46;        // [46..47] first WIDE wave start, [48..49] last end (s_memrealtime)
+// the streaming heavy-key pass (round 4): phase 1's finished keys, the LEAN
+// sequential waves of both grids, the BFS's queue, and spans (first key taken,
+// last wave end; s_memrealtime) of the BFS, the LEAN role, the xw role and phase 1
+constexpr int Q_P1_DONE = 64, Q_SEQ_WAVES = 65, Q_BFS_QUEUE = 66;
+constexpr int Q_T_BFS = 68, Q_T_LEAN = 72, Q_T_XW = 76, Q_T_P1 = 80;
+constexpr int Q_ENT_P3 = 84;        // entries of the LEAN keys restarted in phase 3
+// LEAN sequential waves launched with the BFS while phase 1 still runs (the
+// rest start behind phase 1): enough for the keys deferred before it ends
+constexpr int EARLY_LEAN_WAVES = 128;
 static inline int64_t q64(const int32_t *qh, int i) {
     return (int64_t)(((uint64_t)(uint32_t)qh[i + 1] << 32) | (uint32_t)qh[i]);
 }
 
-__global__ void k_mark_deferred(const int32_t *__restrict__ defer, int n, jh_key_verdict *out) {
+// stage 1 of a two-stage check: each deferred key comes back with its quick
+// search's progress (deepest layer / layers, in millionths) as `explored`,
+// the order the stage-2 pool takes them in (least advanced first: the likely
+// longest searches start first, as k_sort_defer orders a device's own pass)
+__global__ void k_mark_deferred(const uint64_t *__restrict__ d64, int n, jh_key_verdict *out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
+        const uint64_t pk = d64[i];
         jh_key_verdict v;
-        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_DEFERRED; v.fail_entry = -1; v.explored = 0;
+        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_DEFERRED; v.fail_entry = -1; v.explored = (int64_t)(pk >> 32);
         v.previous_ok = -1; v.last_op = -1; v.analyzer = JH_ANALYZER_WGL; v.reserved = 0;
-        out[defer[i]] = v;
+        out[(uint32_t)pk] = v;
     }
 }
 
@@ -5372,6 +5763,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     unsigned long long *probes = (unsigned long long *)(q + 4);
     HIP_TRY(hipMemsetAsync(q, 0, Q_WORDS * sizeof(int32_t), st));
     HIP_TRY(hipMemsetAsync(q + Q_T_WIDE, 0xFF, 2 * sizeof(int32_t), st));
+    for (int w : {Q_T_BFS, Q_T_LEAN, Q_T_XW, Q_T_P1}) HIP_TRY(hipMemsetAsync(q + w, 0xFF, 2 * sizeof(int32_t), st));
 
     // per-key search tables for every key (<= 8 B per entry + 32 B per key)
     KeyMeta *meta = ctx->ws<KeyMeta>(WS_META, K);
@@ -5430,76 +5822,17 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     }
     const bool skip_p1 = (lflags & JH_LIN_SKIP_PHASE1) != 0 && !linear_mode;
     const bool p1_only = (lflags & JH_LIN_PHASE1_ONLY) != 0 && !linear_mode && !skip_p1;
-    HIP_TRY(hipEventRecord(ctx->ev[1], st));
-    if (!linear_mode && !skip_p1) {
-        k_lin_dfs<true><<<waves1, 64, MemoQ::LDS, st>>>(a);
-        HIP_TRY(hipGetLastError());
-        DfsArgs aw = a;
-        aw.list = list_w; aw.n_list_dev = q + 13; aw.queue = q + 14;
-        aw.defer_kind = d64 + 2 * (K + 1); aw.defer_kind_count = q + Q_DEFER_W;
-        k_lin_dfs<false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
-        a.prio_ins = 0;                       // the heavy-key passes inherit a: no priorities there
-    } else if (cfgreq) {
-        k_req_lists<<<1, 1, 0, st>>>(cfgreq->keys_dev, cfgreq->n_q, K, defer, defer_l, q);
-    } else {
-        // :linear, or stage 2 of a two-stage check: every key that needs a
-        // search is a heavy key
-        k_linear_lists<<<1, 1024, 0, st>>>(list, q + 12, list_w, q + 13, defer, defer_l, defer_w, q);
-    }
-    a.prio_ins = 0;
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->ev[4], st));
     int32_t qh[Q_WORDS];
-    HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    const int n_defer = qh[1], n_def_l = qh[Q_DEFER_L], n_def_w = qh[Q_DEFER_W];
-    const int n_x = cfgreq ? 0 : qh[19];
-    if (n_def_l + n_def_w != n_defer) throw_jh(JH_EDEVICE, "deferred-key lists disagree");
-    if (n_defer > 0 && !linear_mode && !skip_p1) {
-        // heavy keys, least advanced first (the likely longest searches start
-        // first), sorted on the device: no host round trip between the phases
-        // (stage 1 of a two-stage check reads the list too: k_mark_deferred)
-        SortLists sl{};
-        const int nn[3] = {n_defer, n_def_l, n_def_w};
-        int32_t *outs[3] = {defer, defer_l, defer_w};
-        for (int i = 0; i < 3; i++) { sl.in[i] = d64 + (size_t)i * (K + 1); sl.out[i] = outs[i]; sl.n[i] = nn[i]; }
-        k_sort_defer<<<3, 1024, 0, st>>>(sl);
-        for (int i = 0; i < 3; i++) {
-            if (nn[i] <= SORT_SMALL) continue;
-            uint64_t *tk = ctx->ws<uint64_t>(WS_DEFER64_T, (size_t)K + 1);
-            size_t tbs = 0;
-            HIP_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, tbs, sl.in[i], tk, nn[i], 0, 64, st));
-            HIP_TRY(hipcub::DeviceRadixSort::SortKeys(ctx->ws<char>(WS_LTMP, tbs), tbs, sl.in[i], tk, nn[i], 0, 64, st));
-            k_unpack_keys<<<grid_for(nn[i], 256), 256, 0, st>>>(tk, nn[i], outs[i]);
-        }
-    }
-    if (n_defer > 0 || n_x > 0) {
-        // entries per list: the phases' rooflines (56 B per entry of the keys they search)
-        EntryLists el{};
-        el.list[0] = defer; el.n[0] = n_defer; el.sum[0] = (unsigned long long *)(q + Q_ENT_ALL);
-        el.list[1] = defer_l; el.n[1] = n_def_l; el.sum[1] = (unsigned long long *)(q + Q_ENT_LEAN);
-        el.list[2] = defer_w; el.n[2] = n_def_w; el.sum[2] = (unsigned long long *)(q + Q_ENT_WIDE);
-        el.list[3] = list_x; el.n[3] = n_x; el.sum[3] = (unsigned long long *)(q + Q_ENT_XW);
-        el.off = off;
-        k_list_entries<<<dim3(16, 4), 256, 0, st>>>(el);
-    }
-    if (dbg2) {
-        std::vector<unsigned long long> h((size_t)waves1 * 16);
-        HIP_TRY(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
-        unsigned long long tot[16] = {0}, mx9 = 0;
-        for (int w = 0; w < waves1; w++) { for (int k = 0; k < 16; k++) tot[k] += h[16 * w + k]; mx9 = std::max(mx9, h[16 * w + 9]); }
-        fprintf(stderr, "[jh-dfs] waves=%d keys=%llu search=%.0f cyc/key | steps=%llu inserts=%llu evict=%llu lay-loads=%llu op-loads=%llu spills=%llu refills=%llu slow=%llu hbm-probes=%llu hbm-inserts=%llu | cyc/step=%.0f | wave-busy avg=%.0f max=%llu cyc\n",
-                waves1, tot[3], (double)tot[2] / std::max(1ULL, tot[3]), tot[4], tot[5], tot[6], tot[7], tot[10],
-                tot[11], tot[12], tot[13], tot[14], tot[8], (double)tot[2] / std::max(1ULL, tot[4]), (double)tot[9] / waves1, mx9);
-        HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 512) * 16, st));
-    }
+    int n_defer = 0, n_def_l = 0, n_def_w = 0, n_x = 0;
     int waves_x = 0;
-    // windows wider than 64: k_lin_xw on the third stream, alongside phases 2 and 3
-    if (n_x > 0) {
+    XwArgs xa{};
+    // windows wider than 64 (k_lin_xw): one wave per key, up to four per CU
+    // (round 2 capped this at 128 waves); qw: the queue words after k_key_tables
+    auto prep_xw = [&](const int32_t *qw) {
+        if (n_x <= 0) return;
         uint32_t capx = 1u << 12;
         while ((int64_t)capx < 2 * budget && capx < (1u << 30)) capx <<= 1;
-        const uint64_t scr_x = (((uint64_t)(uint32_t)qh[26] | ((uint64_t)(uint32_t)qh[27] << 32)) + 255) & ~255ULL;
-        // one wave per key, up to four per CU (round 2 capped this at 128 waves)
+        const uint64_t scr_x = (((uint64_t)(uint32_t)qw[26] | ((uint64_t)(uint32_t)qw[27] << 32)) + 255) & ~255ULL;
         int want_x = std::min(n_x, 4 * ctx->n_cu);
         if (opts && opts->xw_waves > 0) want_x = std::min(n_x, opts->xw_waves);
         const uint64_t per_x = (uint64_t)capx * XW_EW * 8 + (uint64_t)stack_cap * XW_FW * 8 + scr_x;
@@ -5507,22 +5840,18 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         const bool freshx = ctx->ws_fresh(WS_MEMO_X) || ctx->bufs[WS_MEMO_X].bytes < (size_t)waves_x * capx * XW_EW * 8;
         uint64_t *memox = ctx->ws<uint64_t>(WS_MEMO_X, (size_t)waves_x * capx * XW_EW, /*zero=*/true);
         if (clear_memo && !freshx) HIP_TRY(hipMemsetAsync(memox, 0, ctx->bufs[WS_MEMO_X].bytes, st));
-        XwArgs x{};
-        x.src = KeySrc{rec, pair, off, rB, viol, rank, q + 2};
-        x.list = list_x; x.n_list = n_x; x.queue = q + 21; x.meta = meta; x.out = out_dev;
-        x.scratch = ctx->ws<char>(WS_SCRATCH_X, (size_t)waves_x * scr_x); x.scratch_bytes = scr_x;
-        x.memo = memox; x.memo_cap = capx;
-        x.stack = ctx->ws<uint64_t>(WS_STACK_X, (size_t)waves_x * stack_cap * XW_FW); x.stack_cap = stack_cap;
-        x.budget = budget; x.init_state = init_state;
-        x.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;   // its own table: any gen range works
-        x.flags = q + 2; x.probes = (unsigned long long *)(q + 22);
-        x.cause_or = linear_mode ? CAUSE_BY_WGL : 0;
-        HIP_TRY(hipEventRecord(ctx->ev[8], st));
-        HIP_TRY(hipStreamWaitEvent(ctx->aux2, ctx->ev[8], 0));
-        k_lin_xw<<<waves_x, 64, 0, ctx->aux2>>>(x);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->ev[9], ctx->aux2));
-    }
+        xa = XwArgs{};
+        xa.src = KeySrc{rec, pair, off, rB, viol, rank, q + 2};
+        xa.list = list_x; xa.n_list = n_x; xa.queue = q + 21; xa.meta = meta; xa.out = out_dev;
+        xa.scratch = ctx->ws<char>(WS_SCRATCH_X, (size_t)waves_x * scr_x); xa.scratch_bytes = scr_x;
+        xa.memo = memox; xa.memo_cap = capx;
+        xa.stack = ctx->ws<uint64_t>(WS_STACK_X, (size_t)waves_x * stack_cap * XW_FW); xa.stack_cap = stack_cap;
+        xa.budget = budget; xa.init_state = init_state;
+        xa.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;   // its own table: any gen range works
+        xa.flags = q + 2; xa.probes = (unsigned long long *)(q + 22);
+        xa.cause_or = linear_mode ? CAUSE_BY_WGL : 0;
+        xa.t_span = (unsigned long long *)(q + Q_T_XW);
+    };
 
     // phase 2 hands a key that reaches P2_BUDGET inserts to phase 3 (when the
     // phase has fewer waves than keys)
@@ -5531,8 +5860,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     uint32_t cap2 = 1u << 16;
     while ((int64_t)cap2 < 2 * budget && cap2 < (1u << 30)) cap2 <<= 1;
     if (const char *e = tune_env("JH_MEMO_CAP_SHIFT")) cap2 <<= std::max(0, std::min(3, atoi(e)));   // experiments
-    int32_t *defer3 = ctx->ws<int32_t>(WS_DEFER3, 2 * (size_t)(n_defer + 1));
-    int32_t *defer3w = defer3 + (n_defer + 1);
+    int32_t *defer3 = ctx->ws<int32_t>(WS_DEFER3, 2 * (size_t)(K + 1));
+    int32_t *defer3w = defer3 + (K + 1);
     int32_t *claim = nullptr;
     int waves_w = 0, waves2 = 0;
     bool split3 = false, split3w = false;
@@ -5659,124 +5988,15 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     // JH_WG=2: the workgroup engine races the BFS in place of the sequential search
     const bool wg_race = wg_env && atoi(wg_env) == 2;
     int wg2 = 0, n_help = 0;
-    if (n_defer > 0 && p1_only) {
-        // stage 1 of a two-stage check: the deferred keys come back unsearched
-        k_mark_deferred<<<grid_for(n_defer, 256), 256, 0, st>>>(defer, n_defer, out_dev);
-        HIP_TRY(hipEventRecord(ctx->ev[6], st));
-        HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        HIP_TRY(hipEventRecord(ctx->ev[10], st));
-        HIP_TRY(hipEventRecord(ctx->ev[7], st));
-    } else if (n_defer > 0 && use_wg) {
-        // Deferred LEAN keys on k_lin_wg (one workgroup per key, stream st),
-        // WIDE keys on the aux stream
-        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
-        WgArgs wa{};
-        if (n_def_l > 0) wa = build_wg(ctx->n_cu, nullptr, q);
-        prep_wide();
-        HIP_TRY(hipEventRecord(ctx->ev[6], st));
-        HIP_TRY(hipEventRecord(ctx->ev[11], st));
-        if (n_def_l > 0) {
-            k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, st>>>(wa);
-            HIP_TRY(hipGetLastError());
-        }
-        HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
-        HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
-        launch_wide(ctx->aux, true);
-        HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
-    } else if (n_defer > 0 && linear_mode) {
-        // :algorithm :linear (checker.clj:141-145): the reachable-set search
-        // (k_lin_bfs in linear mode) is the analysis for every key it can hold
-        // -- JIT linearization's configuration sets, layer by layer -- on every
-        // CU; the keys it cannot (windows over 32 members, >= 4096 states, more
-        // than budget + 1 configurations) are decided by WGL afterwards on the
-        // same stream, and k_frontier reports each key's analyzer.
-        claim = ctx->ws<int32_t>(WS_CLAIM, K);
-        HIP_TRY(hipMemsetAsync(claim, 0, (size_t)K * sizeof(int32_t), st));
-        HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
-        HIP_TRY(hipMemsetAsync(q + 3, 0, sizeof(int32_t), st));
-        HIP_TRY(hipMemsetAsync(q + 6, 0, 2 * sizeof(int32_t), st));
-        const int64_t reach_cap = budget + 1;
-        // no WGL count, nothing to store -- except for a configurations request,
-        // which needs the last layer reached: every node
-        const uint32_t ncap = cfgreq ? (uint32_t)std::min<int64_t>(reach_cap + 64, (int64_t)1 << 30) : 1u << 16;
-        uint32_t set_cap = 1u << 12;
-        while ((int64_t)set_cap < 2 * reach_cap && set_cap < (1u << 30)) set_cap <<= 1;
-        const uint32_t q_cap = (uint32_t)std::min<int64_t>(reach_cap + 64, (int64_t)1 << 30);
-        const uint32_t lcap = (uint32_t)smax + 2;
-        const uint64_t per_bfs = (uint64_t)set_cap * 8 + 4ULL * q_cap * 8 + scr_bytes_bfs + (uint64_t)ncap * 8 +
-                                 (uint64_t)lcap * 4;
-        wg2 = fit_units(ctx, std::min(n_defer, ctx->n_cu), per_bfs, {WS_BFS_SET, WS_BFS_Q, WS_BFS_NODES});
-        BfsArgs c{};
-        c.src = KeySrc{rec, pair, off, rB, viol, rank, q + 2};
-        c.list = defer; c.n_list = n_defer; c.queue = q; c.out = out_dev;
-        c.unres_list = ctx->ws<int32_t>(WS_BFS_META, n_defer + 1); c.unres_count = q + 3;
-        c.gset = ctx->ws<uint64_t>(WS_BFS_SET, (size_t)wg2 * set_cap); c.gset_cap = set_cap;
-        uint64_t *bq = ctx->ws<uint64_t>(WS_BFS_Q, (size_t)wg2 * 4 * q_cap);
-        c.pend = bq; c.front = bq + (size_t)wg2 * 2 * q_cap; c.q_cap = q_cap;
-        c.scratch = ctx->ws<char>(WS_SCRATCH_BFS, (size_t)wg2 * scr_bytes_bfs); c.scratch_bytes = scr_bytes_bfs;
-        c.budget = budget; c.init_state = init_state; c.states_ok = n_states < 4096 ? 1 : 0;
-        c.claim = claim; c.reach_cap = reach_cap; c.linear = 1;
-        c.ncap = ncap; c.hcap = 1u << 17; c.lcap = lcap;
-        if (cfgreq) {
-            c.cfg_slot = cfgreq->slot_dev; c.cfg_out = cfgreq->out_dev; c.cfg_n = cfgreq->n_dev;
-            c.cfg_rows = cfgreq->rows_dev; c.cfg_per = cfgreq->per_key;
-            c.col_val = dh->value; c.col_val2 = dh->value2;
-            c.vmin = vmin; c.init_value = init; c.per_key_values = per_key_values ? 1 : 0;
-        }
-        c.nodes = ctx->ws<uint64_t>(WS_BFS_NODES, (size_t)wg2 * ncap);
-        c.lstart = ctx->ws<uint32_t>(WS_BFS_LSTART, (size_t)wg2 * lcap);
-        if (!ctx->lds_attr) {
-            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_bfs, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        BFS_LDS_BYTES));
-            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        MemoH::LDS));
-            HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        MemoH::LDS));
-            ctx->lds_attr = true;
-        }
-        // WGL for what the analysis cannot hold: LEAN and WIDE kernels over the
-        // unresolved list (each takes its own kind), after the BFS
-        const int want_f = std::min(n_defer, 4 * ctx->n_cu);
-        const uint64_t per_f = (uint64_t)cap2 * 16 + (uint64_t)stack_cap * sizeof(Frame) + scr_bytes_h;
-        waves2 = fit_units(ctx, want_f, per_f, {WS_MEMO_DEEP, WS_STACK_DEEP, WS_SCRATCH_DEEP});
-        const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;
-        uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
-        if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
-        DfsArgs f = a;
-        f.handover_min = 0;
-        f.list = c.unres_list; f.n_list = 0; f.n_list_dev = q + 3; f.queue = q + 6; f.defer = 0;
-        f.defer_list = nullptr; f.defer_count = nullptr;
-        f.defer64 = nullptr; f.defer_kind = nullptr; f.defer_kind_count = nullptr;
-        f.memo = memo2; f.memo_cap = cap2;
-        f.stack = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap);
-        f.scratch = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes_h); f.scratch_bytes = scr_bytes_h;
-        f.budget = budget; f.budget_full = 0; f.claim = nullptr;
-        f.gen_base = ctx->gen_base + (uint32_t)K + 1;
-        f.probes = (unsigned long long *)(q + 8); f.dbg = nullptr; f.defer_time = nullptr;
-        f.seq_start = nullptr; f.exit_count = nullptr; f.cause_or = CAUSE_BY_WGL;
-        HIP_TRY(hipEventRecord(ctx->ev[6], st));
-        k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        if (!cfgreq) {
-            k_lin_seq3<true><<<waves2, 64, MemoM::LDS, st>>>(f);
-            HIP_TRY(hipGetLastError());
-            DfsArgs fw = f;
-            fw.queue = q + 7;
-            k_lin_seqw<<<waves2, 64, SEQW_LDS, st>>>(fw);
-            HIP_TRY(hipGetLastError());
-        }
-        HIP_TRY(hipEventRecord(ctx->ev[10], st));
-        HIP_TRY(hipEventRecord(ctx->ev[7], st));
-    } else if (n_defer > 0) {
-        // Heavy keys: two exact searches race per key and the first to settle
-        // it writes its verdict (emit_verdict), the other abandons it.
-        //  - the workgroup BFS (stream st) settles keys with no reachable
-        //    terminal configuration (invalid) within the budget, and valid
-        //    keys whose reachable set it can store (WGL's exact count);
-        //  - the sequential search with the full budget (aux stream: LEAN
-        //    and WIDE keys in one grid) settles every key.
+    // the heavy-key race's engines for at most nd_all deferred keys (nd_l of
+    // them LEAN): the BFS (c), the sequential search of the LEAN keys (b),
+    // the late helpers (wh) or the workgroup race (wr); allocations only
+    BfsArgs c{};
+    DfsArgs b{};
+    WgArgs wr{}, wh{};
+    unsigned long long *seq_start = nullptr;
+    bool p2_m = true, bfs_only = false;
+    auto prep_race = [&](int nd_all, int nd_l) {
         claim = ctx->ws<int32_t>(WS_CLAIM, K);
         HIP_TRY(hipMemsetAsync(claim, 0, (size_t)K * sizeof(int32_t), st));
         // q[0] (phase 1's queue) becomes the BFS's; q[3] its give-up count; q[6] phase 2's queue
@@ -5801,7 +6021,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // 96 of 256 (round 2, with phase 2 at four waves per CU): C4 shard
         // 230 -> 223 ms, C3 ranks 0 / 3 / 6 flat (32: C4 +9 %, 128: no better)
         const int bfs_cus = std::max(1, std::min(96, ctx->n_cu * 3 / 8));
-        wg2 = std::min(n_defer, tune_env("JH_BFS_CUS") ? std::max(1, atoi(tune_env("JH_BFS_CUS"))) : bfs_cus);
+        wg2 = std::min(nd_all, tune_env("JH_BFS_CUS") ? std::max(1, atoi(tune_env("JH_BFS_CUS"))) : bfs_cus);
         const uint64_t per_bfs = (uint64_t)set_cap * 8 + 4ULL * q_cap * 8 + scr_bytes_bfs + (uint64_t)ncap * 8 +
                                  (uint64_t)lcap * 4 + (uint64_t)hcap * 16 + (uint64_t)ncap * 4 + ((uint64_t)ncap / 32 + 1) * 4 +
                                  (uint64_t)ncap * 4 + (uint64_t)ncap * 8;
@@ -5809,10 +6029,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         uint64_t *bset = ctx->ws<uint64_t>(WS_BFS_SET, (size_t)wg2 * set_cap);
         uint64_t *bq = ctx->ws<uint64_t>(WS_BFS_Q, (size_t)wg2 * 4 * q_cap);
         char *bscr = ctx->ws<char>(WS_SCRATCH_BFS, (size_t)wg2 * scr_bytes_bfs);
-        int32_t *unres = ctx->ws<int32_t>(WS_BFS_META, n_defer + 1);
-        BfsArgs c{};
+        int32_t *unres = ctx->ws<int32_t>(WS_BFS_META, nd_all + 1);
+        c = BfsArgs{};
         c.src = KeySrc{rec, pair, off, rB, viol, rank, q + 2};
-        c.list = defer; c.n_list = n_defer; c.queue = q; c.out = out_dev;
+        c.list = defer; c.n_list = nd_all; c.queue = q; c.out = out_dev;
         c.unres_list = unres; c.unres_count = q + 3;
         c.gset = bset; c.gset_cap = set_cap; c.pend = bq; c.front = bq + (size_t)wg2 * 2 * q_cap;
         c.q_cap = q_cap;
@@ -5826,7 +6046,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // key it can (the others stay unsettled); JH_BFS_DBGV=1 (tuning builds):
         // its valid verdicts carry fail_entry = path length, cause = stored
         // configurations, explored = count
-        const bool bfs_only = (lflags & JH_LIN_BFS_ONLY) != 0;
+        bfs_only = (lflags & JH_LIN_BFS_ONLY) != 0;
         c.dbg_plen = tune_env("JH_BFS_DBGV") && atoi(tune_env("JH_BFS_DBGV")) ? 1 : 0;
         c.ncap = ncap; c.hcap = hcap; c.lcap = lcap;
         c.nodes = ctx->ws<uint64_t>(WS_BFS_NODES, (size_t)wg2 * ncap);
@@ -5849,16 +6069,16 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
 
         // late helpers (k_lin_wg in helper mode, wg_helper_pick): a few CUs
         // taken from the sequential search of the LEAN keys
-        n_help = bfs_only || wg_race || n_def_l == 0 ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 8));
+        n_help = bfs_only || wg_race || nd_l == 0 ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 8));
         if (opts && opts->helpers > 0) n_help = std::min(64, opts->helpers);
         if (lflags & JH_LIN_NO_HELPERS) n_help = 0;
         if (n_help > 0 && ctx->n_cu - wg2 - n_help < 16) n_help = 0;
         // phase 2's sequential search with four waves per CU and the 32 KB memo
         // (k_lin_seq3), p2_waves_per_cu = 1 for one wave per CU and the 128 KB
         // memo (k_lin_seq): measured C4 shard 268 -> 228 ms, C3 / ranks 3, 6 / C5 flat
-        const bool p2_m = !(opts && opts->p2_waves_per_cu == 1);
-        if (n_def_l > 0) {
-            int want2 = std::min(n_def_l, std::max(1, (ctx->n_cu - wg2 - n_help) * (p2_m ? 4 : 1)));
+        p2_m = !(opts && opts->p2_waves_per_cu == 1);
+        if (nd_l > 0) {
+            int want2 = std::min(nd_l, std::max(1, (ctx->n_cu - wg2 - n_help) * (p2_m ? 4 : 1)));
             if (opts && opts->lean_waves > 0) want2 = std::min(want2, opts->lean_waves);
             const uint64_t per2 = (uint64_t)cap2 * 16 + (uint64_t)stack_cap * sizeof(Frame) + scr_bytes_h;
             waves2 = fit_units(ctx, want2, per2, {WS_MEMO_DEEP, WS_STACK_DEEP, WS_SCRATCH_DEEP});
@@ -5870,10 +6090,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
             if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
         }
-        WgArgs wr{};
-        if (wg_race && n_def_l > 0) wr = build_wg(std::max(1, ctx->n_cu - wg2), claim, q + 6);
-        WgArgs wh{};
-        unsigned long long *seq_start = nullptr;
+        wr = WgArgs{};
+        if (wg_race && nd_l > 0) wr = build_wg(std::max(1, ctx->n_cu - wg2), claim, q + 6);
+        wh = WgArgs{};
+        seq_start = nullptr;
         if (n_help > 0) {
             wh = build_wg(n_help, claim, nullptr);
             seq_start = ctx->ws<unsigned long long>(WS_HELP_START, K);
@@ -5890,10 +6110,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         char *scr2 = waves2 > 0 ? ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes_h) : nullptr;
         // a wave per key: one pass at the full budget; fewer waves than keys:
         // phase 2 stops at p2 inserts and phase 3 restarts those keys
-        split3 = waves2 < n_def_l && budget > p2;
-        DfsArgs b = a;
+        split3 = waves2 < nd_l && budget > p2;
+        b = a;
         b.handover_min = 0;
-        b.list = defer_l; b.n_list = n_def_l; b.n_list_dev = nullptr; b.queue = q + 6; b.defer = split3 ? 1 : 0;
+        b.list = defer_l; b.n_list = nd_l; b.n_list_dev = nullptr; b.queue = q + 6; b.defer = split3 ? 1 : 0;
         b.defer_list = defer3; b.defer_count = q + 16;
         b.defer64 = nullptr; b.defer_kind = nullptr; b.defer_kind_count = nullptr;
         b.memo = memo2; b.memo_cap = cap2; b.stack = stack2; b.scratch = scr2; b.scratch_bytes = scr_bytes_h;
@@ -5904,133 +6124,496 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         b.probes = (unsigned long long *)(q + 8);
         b.seq_start = seq_start; b.exit_count = seq_start ? q + 28 : nullptr;
         b.defer_time = nullptr;
-
-        // the fork point: everything the phase-2 searches read (claims, queue
-        // counters, sorted lists, the cleared memo on a generation wrap) is
-        // ordered before it; every table of phases 2 and 3 is allocated above
-        // (an allocation after the fork would synchronise the device)
-        prep_wide();
-        HIP_TRY(hipEventRecord(ctx->ev[6], st));
-        // fork: the BFS on st, the LEAN and WIDE sequential searches on aux
-        // (one grid), helpers on aux3
-        HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
-        k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
+    };
+    // the streaming heavy-key pass (round 4) whenever the default race runs
+    const bool stream_p2 = !linear_mode && !skip_p1 && !p1_only && !use_wg && !wg_race && !dbg2 && !defer_times &&
+                           !(lflags & (JH_LIN_NO_STREAM | JH_LIN_BFS_ONLY));
+    if (stream_p2) {
+        // ---- the streaming heavy-key pass (round 4) --------------------------
+        // Round 3 started the heavy keys when phase 1 ended (~17 ms into C3),
+        // though most were deferred at 9-13 ms. Here phase 1 appends every key
+        // it defers to live lists; once its last kernel's queue is drained (each
+        // of its waves then finishes the key it holds and leaves) the host
+        // launches the consumers -- the BFS (aux2), the late helpers (aux3) and
+        // an early grid of LEAN sequential waves (aux) -- which take CUs as
+        // phase 1 frees them and take keys as they are deferred. A grid behind
+        // phase 1 on st runs the 65-256-member keys, the WIDE keys and more LEAN
+        // waves; phase 3 follows on st. Four streams: the hardware's queues.
+        // Every search is the one the round-3 schedule runs (same verdicts and
+        // counts); only when each starts changes.
+        int32_t qt[Q_WORDS];
+        HIP_TRY(hipMemcpyAsync(qt, q, sizeof qt, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        const int n_l1 = qt[12], n_w1 = qt[13];
+        n_x = qt[19];
+        prep_xw(qt);
+        // bounds: phase 1 defers at most the keys it searches
+        n_def_l = n_l1; n_def_w = n_w1; n_defer = n_l1 + n_w1;
+        int w_early = 0;
+        const bool any = n_defer > 0;
+        if (any) {
+            HIP_TRY(hipMemsetAsync(defer, 0xFF, 3 * sizeof(int32_t) * (size_t)(K + 1), st));   // live lists: -1 = not yet
+            prep_race(n_defer, n_def_l);
+            prep_wide();
+            c.list = defer; c.n_list = 0; c.queue = q + Q_BFS_QUEUE;
+            c.live_n = q + 1; c.p1_done = q + Q_P1_DONE; c.p1_tot = q + 12;
+            c.t_span = (unsigned long long *)(q + Q_T_BFS);
+            b.list = defer_l; b.n_list = 0; b.live_n = q + Q_DEFER_L; b.p1_done = q + Q_P1_DONE; b.p1_tot = q + 12;
+            b.s_all = nullptr; b.s_kind = nullptr; b.drained = nullptr; b.wave_off = 0;
+            b.t_span = (unsigned long long *)(q + Q_T_LEAN);
+            if (waves_w > 0) {
+                bw.list = defer_w; bw.n_list = 0; bw.live_n = q + Q_DEFER_W; bw.p1_done = q + Q_P1_DONE; bw.p1_tot = q + 12;
+                bw.s_all = nullptr; bw.s_kind = nullptr; bw.drained = nullptr;
+            }
+            if (n_help > 0) {
+                wh.d.list = defer_l; wh.d.n_list = 0; wh.d.live_n = q + Q_DEFER_L;
+                wh.d.p1_done = q + Q_P1_DONE; wh.d.p1_tot = q + 12;
+                wh.d.s_all = nullptr; wh.d.s_kind = nullptr; wh.d.drained = nullptr;
+                wh.seq_waves_dev = q + Q_SEQ_WAVES;
+            }
+            // the early LEAN grid: enough waves for the keys deferred while
+            // phase 1 runs (C3: ~120), few enough to leave the BFS whole CUs
+            w_early = std::min(waves2, EARLY_LEAN_WAVES);
+            if (const char *e = tune_env("JH_EARLY_LEAN")) w_early = std::min(waves2, std::max(0, atoi(e)));
+            const int32_t sw = waves2;
+            HIP_TRY(hipMemcpyAsync(q + Q_SEQ_WAVES, &sw, sizeof sw, hipMemcpyHostToDevice, st));
+        }
+        // phase-1 producer side: live lists, finished-key count, drain flag
+        if (!ctx->hflag) {
+            HIP_TRY(hipHostMalloc((void **)&ctx->hflag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+            HIP_TRY(hipHostGetDevicePointer((void **)&ctx->hflag_dev, ctx->hflag, 0));
+        }
+        *(volatile int32_t *)ctx->hflag = 0;
+        a.p1_count = q + Q_P1_DONE;
+        if (any) { a.s_all = defer; a.s_kind = defer_l; }
+        DfsArgs aw = a;
+        aw.list = list_w; aw.n_list_dev = q + 13; aw.queue = q + 14;
+        aw.defer_kind = d64 + 2 * (K + 1); aw.defer_kind_count = q + Q_DEFER_W;
+        if (any) aw.s_kind = defer_w;
+        // the last phase-1 kernel with keys raises the flag (WIDE keys run
+        // after the LEAN kernel: then consumers start at the WIDE drain)
+        a.drained = n_w1 == 0 ? ctx->hflag_dev : nullptr;
+        aw.drained = n_w1 > 0 ? ctx->hflag_dev : nullptr;
+        a.t_span = (unsigned long long *)(q + Q_T_P1);
+        HIP_TRY(hipEventRecord(ctx->ev[6], st));     // fork: tables, lists and counters are ready
+        HIP_TRY(hipEventRecord(ctx->ev[1], st));
+        k_lin_dfs<true><<<waves1, 64, MemoQ::LDS, st>>>(a);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        bool wide_done = bfs_only;
-        if (bfs_only || (waves2 == 0 && waves_w == 0)) {}
-        else if (wg_race) { if (waves2) k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux>>>(wr); }
-        else if (p2_m) {
-            DfsPair pr;
-            pr.l = b; pr.w = bw; pr.n_l = waves2;
-            pr.w.wave_off = waves2;
-            k_lin_seq_lw<<<waves2 + waves_w, 64, SEQLW_LDS, ctx->aux>>>(pr);
-            wide_done = true;
-        } else if (waves2) k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
+        k_lin_dfs<false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
-        if (!bfs_only) launch_wide(ctx->aux, !wide_done);
-        if (n_help > 0) {
-            // every helper leaves once the sequential search has left its
-            // queue (or after HELPER_MAX_TICKS): joined before the verdicts are read
-            HIP_TRY(hipStreamWaitEvent(ctx->aux3, ctx->ev[6], 0));
-            k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux3>>>(wh);
-            HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(ctx->ev[12], ctx->aux3));
-        }
-        if (split3 && !bfs_only && !wg_race) {
-            // phase 3: the LEAN keys phase 2 handed over, full budget, on phase 2's
-            // tables (same stream, phase 2 has ended; a fresh generation range).
-            // Few of them (no more than phase 2's CUs): a lone wave and the 128 KB
-            // LDS memo each, as in phase 2; more: four waves per CU. Both kernels
-            // are launched and the count phase 2 left on the device picks one.
-            DfsArgs c3 = b;
-            c3.list = defer3; c3.n_list = 0; c3.n_list_dev = q + 16; c3.defer = 0;
-            c3.defer_list = nullptr; c3.defer_count = nullptr;
-            c3.seq_start = nullptr; c3.exit_count = nullptr;
-            c3.budget = budget; c3.budget_full = 0;
-            c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
-            c3.dbg = nullptr;
-            c3.probes = (unsigned long long *)(q + Q_PROBES_P3);
-            const int few = std::max(1, ctx->n_cu - wg2);
-            DfsArgs c3a = c3;
-            c3a.queue = q + 17; c3a.n_max = few;
-            k_lin_seq<true><<<std::min(waves2, few), 64, MemoH::LDS, ctx->aux>>>(c3a);
-            HIP_TRY(hipGetLastError());
-            DfsArgs c3b = c3;
-            c3b.queue = q + 18; c3b.n_min = few + 1;
-            k_lin_seq3<true><<<waves2, 64, MemoM::LDS, ctx->aux>>>(c3b);
+        HIP_TRY(hipEventRecord(ctx->ev[4], st));
+        a.prio_ins = 0;
+        // behind phase 1 on st: xw keys, WIDE keys, LEAN waves past the early grid's
+        const int late_l = any ? waves2 - w_early : 0;
+        const int n_late = waves_x + waves_w + late_l;
+        if (n_late > 0) {
+            DfsTriple tr{};
+            tr.x = xa; tr.n_x = waves_x;
+            tr.w = bw; tr.w.wave_off = waves_x; tr.n_w = waves_w;
+            tr.l = b; tr.l.wave_off = waves_x + waves_w - w_early;   // its waves use tables w_early..waves2-1
+            const int lds = std::max(SEQLW_LDS, XW_LDS);
+            k_lin_seq_lwx<<<n_late, 64, lds, st>>>(tr);
             HIP_TRY(hipGetLastError());
         }
-        HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
-        HIP_TRY(hipStreamWaitEvent(st, ctx->ev[7], 0));
-        if (n_help > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[12], 0));
-        if (n_help > 0 && wh.key_prof) {
-            // JH_DEBUG=4: what the late helpers took (end time in us after their start)
-            HIP_TRY(hipStreamSynchronize(st));
-            std::vector<unsigned long long> kp(3 * (size_t)K);
-            HIP_TRY(hipMemcpy(kp.data(), wh.key_prof, kp.size() * 8, hipMemcpyDeviceToHost));
-            for (int64_t k = 0; k < K; k++)
-                if (kp[3 * k])
-                    fprintf(stderr, "[jh-help] key %lld wg %llu verdict %llu won %llu inserts %llu cycles %llu end_us %llu\n",
-                            (long long)k, (kp[3 * k + 2] >> 8) & 0xFFF, kp[3 * k + 2] & 0xFF, (kp[3 * k + 2] >> 20) & 1,
-                            kp[3 * k + 1], kp[3 * k], kp[3 * k + 2] >> 32);
+        HIP_TRY(hipEventRecord(ctx->ev[10], st));
+        if (any) {
+            // the consumers, once phase 1's queue is drained: until then phase
+            // 1 holds every CU, and a consumer launched earlier could take CUs
+            // from it while it still has keys to hand out
+            volatile int32_t *hf = (volatile int32_t *)ctx->hflag;
+            while (!*hf) {
+                const hipError_t e = hipEventQuery(ctx->ev[4]);
+                if (e == hipSuccess) break;
+                if (e != hipErrorNotReady) HIP_TRY(e);
+                std::this_thread::yield();
+            }
+            HIP_TRY(hipStreamWaitEvent(ctx->aux2, ctx->ev[6], 0));
+            k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, ctx->aux2>>>(c);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(ctx->ev[5], ctx->aux2));
+            if (n_help > 0) {
+                HIP_TRY(hipStreamWaitEvent(ctx->aux3, ctx->ev[6], 0));
+                k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux3>>>(wh);
+                HIP_TRY(hipGetLastError());
+                HIP_TRY(hipEventRecord(ctx->ev[12], ctx->aux3));
+            }
+            HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
+            if (w_early > 0) {
+                DfsPair pr{};
+                pr.l = b; pr.n_l = w_early;
+                k_lin_seq_lw<<<w_early, 64, SEQLW_LDS, ctx->aux>>>(pr);
+                HIP_TRY(hipGetLastError());
+            }
+            HIP_TRY(hipEventRecord(ctx->ev[11], ctx->aux));
+            // phase 3 after every phase-2 wave (both grids hand keys to it)
+            HIP_TRY(hipStreamWaitEvent(st, ctx->ev[11], 0));
+            HIP_TRY(hipEventRecord(ctx->ev[13], st));
+            if (split3) {
+                DfsArgs c3 = b;
+                c3.list = defer3; c3.n_list = 0; c3.n_list_dev = q + 16; c3.defer = 0; c3.live_n = nullptr;
+                c3.defer_list = nullptr; c3.defer_count = nullptr;
+                c3.seq_start = nullptr; c3.exit_count = nullptr; c3.t_span = nullptr; c3.wave_off = 0;
+                c3.budget = budget; c3.budget_full = 0;
+                c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
+                c3.dbg = nullptr;
+                c3.probes = (unsigned long long *)(q + Q_PROBES_P3);
+                const int few = std::max(1, ctx->n_cu - wg2);
+                DfsArgs c3a = c3;
+                c3a.queue = q + 17; c3a.n_max = few;
+                k_lin_seq<true><<<std::min(waves2, few), 64, MemoH::LDS, st>>>(c3a);
+                HIP_TRY(hipGetLastError());
+                DfsArgs c3b = c3;
+                c3b.queue = q + 18; c3b.n_min = few + 1;
+                k_lin_seq3<true><<<waves2, 64, MemoM::LDS, st>>>(c3b);
+                HIP_TRY(hipGetLastError());
+            }
+            if (split3w) {
+                DfsArgs c3 = bw;
+                c3.list = defer3w; c3.n_list = 0; c3.n_list_dev = q + Q_DEFER3W; c3.queue = q + 20; c3.defer = 0;
+                c3.live_n = nullptr; c3.t_span = nullptr;
+                c3.defer_list = nullptr; c3.defer_count = nullptr;
+                c3.budget = budget; c3.budget_full = 0; c3.wave_off = 0;
+                c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
+                k_lin_seqw<<<waves_w, 64, SEQW_LDS, st>>>(c3);
+                HIP_TRY(hipGetLastError());
+            }
+            HIP_TRY(hipEventRecord(ctx->ev[7], st));
+            HIP_TRY(hipStreamWaitEvent(st, ctx->ev[5], 0));
+            if (n_help > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[12], 0));
+        } else {
+            HIP_TRY(hipEventRecord(ctx->ev[13], st));
+            HIP_TRY(hipEventRecord(ctx->ev[7], st));
         }
-        if (const char *dp = tune_env("JH_BFS_DUMP")) {
-            // debugging: workgroup 0's stored configurations (t:20 | s:12 | mask:32)
-            HIP_TRY(hipStreamSynchronize(st));
-            std::vector<uint64_t> nd(c.ncap);
-            HIP_TRY(hipMemcpy(nd.data(), c.nodes, nd.size() * 8, hipMemcpyDeviceToHost));
-            if (FILE *fp = fopen(dp, "wb")) { fwrite(nd.data(), 8, nd.size(), fp); fclose(fp); }
+        // entries per list (the phases' rooflines), the lists' lengths on the device
+        EntryLists el{};
+        el.list[0] = defer; el.n_dev[0] = q + 1; el.sum[0] = (unsigned long long *)(q + Q_ENT_ALL);
+        el.list[1] = defer_l; el.n_dev[1] = q + Q_DEFER_L; el.sum[1] = (unsigned long long *)(q + Q_ENT_LEAN);
+        el.list[2] = defer_w; el.n_dev[2] = q + Q_DEFER_W; el.sum[2] = (unsigned long long *)(q + Q_ENT_WIDE);
+        el.list[3] = list_x; el.n[3] = n_x; el.sum[3] = (unsigned long long *)(q + Q_ENT_XW);
+        el.list[4] = defer3; el.n_dev[4] = q + 16; el.sum[4] = (unsigned long long *)(q + Q_ENT_P3);
+        el.off = off;
+        k_list_entries<<<dim3(16, 5), 256, 0, st>>>(el);
+    } else {
+        HIP_TRY(hipEventRecord(ctx->ev[1], st));
+        if (!linear_mode && !skip_p1) {
+            k_lin_dfs<true><<<waves1, 64, MemoQ::LDS, st>>>(a);
+            HIP_TRY(hipGetLastError());
+            DfsArgs aw = a;
+            aw.list = list_w; aw.n_list_dev = q + 13; aw.queue = q + 14;
+            aw.defer_kind = d64 + 2 * (K + 1); aw.defer_kind_count = q + Q_DEFER_W;
+            k_lin_dfs<false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
+            a.prio_ins = 0;                       // the heavy-key passes inherit a: no priorities there
+        } else if (cfgreq) {
+            k_req_lists<<<1, 1, 0, st>>>(cfgreq->keys_dev, cfgreq->n_q, K, defer, defer_l, q);
+        } else {
+            // :linear, or stage 2 of a two-stage check: every key that needs a
+            // search is a heavy key
+            k_linear_lists<<<1, 1024, 0, st>>>(list, q + 12, list_w, q + 13, defer, defer_l, defer_w, q);
+        }
+        a.prio_ins = 0;
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->ev[4], st));
+        HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        n_defer = qh[1]; n_def_l = qh[Q_DEFER_L]; n_def_w = qh[Q_DEFER_W];
+        n_x = cfgreq ? 0 : qh[19];
+        if (n_def_l + n_def_w != n_defer) throw_jh(JH_EDEVICE, "deferred-key lists disagree");
+        if (n_defer > 0 && !linear_mode && !skip_p1) {
+            // heavy keys, least advanced first (the likely longest searches start
+            // first), sorted on the device: no host round trip between the phases
+            // (stage 1 of a two-stage check reads the list too: k_mark_deferred)
+            SortLists sl{};
+            const int nn[3] = {n_defer, n_def_l, n_def_w};
+            int32_t *outs[3] = {defer, defer_l, defer_w};
+            for (int i = 0; i < 3; i++) { sl.in[i] = d64 + (size_t)i * (K + 1); sl.out[i] = outs[i]; sl.n[i] = nn[i]; }
+            k_sort_defer<<<3, 1024, 0, st>>>(sl);
+            for (int i = 0; i < 3; i++) {
+                if (nn[i] <= SORT_SMALL) continue;
+                uint64_t *tk = ctx->ws<uint64_t>(WS_DEFER64_T, (size_t)K + 1);
+                size_t tbs = 0;
+                HIP_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, tbs, sl.in[i], tk, nn[i], 0, 64, st));
+                HIP_TRY(hipcub::DeviceRadixSort::SortKeys(ctx->ws<char>(WS_LTMP, tbs), tbs, sl.in[i], tk, nn[i], 0, 64, st));
+                k_unpack_keys<<<grid_for(nn[i], 256), 256, 0, st>>>(tk, nn[i], outs[i]);
+            }
+        }
+        if (n_defer > 0 || n_x > 0) {
+            // entries per list: the phases' rooflines (56 B per entry of the keys they search)
+            EntryLists el{};
+            el.list[0] = defer; el.n[0] = n_defer; el.sum[0] = (unsigned long long *)(q + Q_ENT_ALL);
+            el.list[1] = defer_l; el.n[1] = n_def_l; el.sum[1] = (unsigned long long *)(q + Q_ENT_LEAN);
+            el.list[2] = defer_w; el.n[2] = n_def_w; el.sum[2] = (unsigned long long *)(q + Q_ENT_WIDE);
+            el.list[3] = list_x; el.n[3] = n_x; el.sum[3] = (unsigned long long *)(q + Q_ENT_XW);
+        el.list[4] = nullptr; el.n[4] = 0;
+            el.off = off;
+            k_list_entries<<<dim3(16, 4), 256, 0, st>>>(el);
         }
         if (dbg2) {
-            HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            n_unres = qh[3];
-            std::vector<unsigned long long> h((size_t)wg2 * 16);
+            std::vector<unsigned long long> h((size_t)waves1 * 16);
             HIP_TRY(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
-            for (int w = 0; w < wg2; w++)
-                if (h[16 * w + 4])
-                    fprintf(stderr, "[jh-bfs] wg %d keys=%llu cycles=%llu rounds=%llu configs=%llu cyc/round=%.0f | "
-                            "count: hash=%llu live=%llu path=%llu closure=%llu cyc | global-set rounds=%llu cyc=%llu "
-                            "configs=%llu, LDS-set rounds cyc=%llu configs=%llu | live: layers=%llu (LDS %llu) head-cyc=%llu LDS-layers-cyc=%llu\n",
-                            w, h[16 * w + 4], h[16 * w], h[16 * w + 1], h[16 * w + 3],
-                            (double)h[16 * w] / std::max(1ULL, h[16 * w + 1]), h[16 * w + 5], h[16 * w + 6],
-                            h[16 * w + 7], h[16 * w + 8], h[16 * w + 10], h[16 * w + 9], h[16 * w + 11],
-                            h[16 * w + 12], h[16 * w + 13], h[16 * w + 14] & 0xFFFFFFFF, h[16 * w + 14] >> 32, h[16 * w + 15], h[16 * w + 2]);
-#ifdef JH_BFS_PROF
-            {
-                unsigned long long bp[8];
-                HIP_TRY(hipMemcpyFromSymbol(bp, HIP_SYMBOL(g_bfs_prof), sizeof bp));
-                const double nr = (double)std::max(1ULL, bp[4]), nl = (double)std::max(1ULL, bp[6]);
-                unsigned long long bx[4];
-                HIP_TRY(hipMemcpyFromSymbol(bx, HIP_SYMBOL(g_bfs_prof_x), sizeof bx));
-                const double ni = (double)std::max(1ULL, bx[2]);
-                fprintf(stderr, "[jh-bfs-prof] rounds=%llu cyc/round: claim+barrier %.0f items %.0f barrier %.0f tail %.0f | "
-                        "layers=%llu formation cyc/layer %.0f | tid0 items=%llu cyc/item: load+children %.0f insert8 %.0f record8 %.0f\n",
-                        bp[4], bp[0] / nr, bp[1] / nr, bp[2] / nr, bp[3] / nr, bp[6], bp[5] / nl, bx[2], bp[7] / ni, bx[0] / ni, bx[1] / ni);
-                memset(bx, 0, sizeof bx);
-                HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bfs_prof_x), bx, sizeof bx));
-                memset(bp, 0, sizeof bp);
-                HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bfs_prof), bp, sizeof bp));
-            }
-#endif
-            std::vector<unsigned long long> g((size_t)waves2 * 16);
-            HIP_TRY(hipMemcpy(g.data(), dbg + 16 * 256, g.size() * 8, hipMemcpyDeviceToHost));
-            for (int w = 0; w < waves2; w++)
-                if (g[16 * w + 4] > 0)
-                    fprintf(stderr, "[jh-seq] wave %d keys=%llu search=%llu cyc busy=%llu | steps=%llu inserts=%llu evict=%llu lay-loads=%llu op-loads=%llu spills=%llu refills=%llu slow=%llu hbm-probes=%llu | cyc/step=%.0f\n",
-                            w, g[16 * w + 3], g[16 * w + 2], g[16 * w + 9], g[16 * w + 4], g[16 * w + 5], g[16 * w + 6],
-                            g[16 * w + 7], g[16 * w + 10], g[16 * w + 11], g[16 * w + 12], g[16 * w + 13], g[16 * w + 14],
-                            (double)g[16 * w + 2] / std::max(1ULL, g[16 * w + 4]));
+            unsigned long long tot[16] = {0}, mx9 = 0;
+            for (int w = 0; w < waves1; w++) { for (int k = 0; k < 16; k++) tot[k] += h[16 * w + k]; mx9 = std::max(mx9, h[16 * w + 9]); }
+            fprintf(stderr, "[jh-dfs] waves=%d keys=%llu search=%.0f cyc/key | steps=%llu inserts=%llu evict=%llu lay-loads=%llu op-loads=%llu spills=%llu refills=%llu slow=%llu hbm-probes=%llu hbm-inserts=%llu | cyc/step=%.0f | wave-busy avg=%.0f max=%llu cyc\n",
+                    waves1, tot[3], (double)tot[2] / std::max(1ULL, tot[3]), tot[4], tot[5], tot[6], tot[7], tot[10],
+                    tot[11], tot[12], tot[13], tot[14], tot[8], (double)tot[2] / std::max(1ULL, tot[4]), (double)tot[9] / waves1, mx9);
+            HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 512) * 16, st));
         }
-    } else {
-        HIP_TRY(hipEventRecord(ctx->ev[6], st));
-        HIP_TRY(hipEventRecord(ctx->ev[5], st));
-        HIP_TRY(hipEventRecord(ctx->ev[10], st));
-        HIP_TRY(hipEventRecord(ctx->ev[7], st));
+        // windows wider than 64: k_lin_xw on the third stream, alongside phases 2 and 3
+        if (n_x > 0) {
+            prep_xw(qh);
+            xa.t_span = nullptr;
+            HIP_TRY(hipEventRecord(ctx->ev[8], st));
+            HIP_TRY(hipStreamWaitEvent(ctx->aux2, ctx->ev[8], 0));
+            k_lin_xw<<<waves_x, 64, 0, ctx->aux2>>>(xa);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(ctx->ev[9], ctx->aux2));
+        }
+        if (n_defer > 0 && p1_only) {
+            // stage 1 of a two-stage check: the deferred keys come back unsearched
+            k_mark_deferred<<<grid_for(n_defer, 256), 256, 0, st>>>(d64, n_defer, out_dev);
+            HIP_TRY(hipEventRecord(ctx->ev[6], st));
+            HIP_TRY(hipEventRecord(ctx->ev[5], st));
+            HIP_TRY(hipEventRecord(ctx->ev[10], st));
+            HIP_TRY(hipEventRecord(ctx->ev[7], st));
+        } else if (n_defer > 0 && use_wg) {
+            // Deferred LEAN keys on k_lin_wg (one workgroup per key, stream st),
+            // WIDE keys on the aux stream
+            HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
+            WgArgs wa{};
+            if (n_def_l > 0) wa = build_wg(ctx->n_cu, nullptr, q);
+            prep_wide();
+            HIP_TRY(hipEventRecord(ctx->ev[6], st));
+            HIP_TRY(hipEventRecord(ctx->ev[11], st));
+            if (n_def_l > 0) {
+                k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, st>>>(wa);
+                HIP_TRY(hipGetLastError());
+            }
+            HIP_TRY(hipEventRecord(ctx->ev[5], st));
+            HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
+            HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
+            launch_wide(ctx->aux, true);
+            HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
+        } else if (n_defer > 0 && linear_mode) {
+            // :algorithm :linear (checker.clj:141-145): the reachable-set search
+            // (k_lin_bfs in linear mode) is the analysis for every key it can hold
+            // -- JIT linearization's configuration sets, layer by layer -- on every
+            // CU; the keys it cannot (windows over 32 members, >= 4096 states, more
+            // than budget + 1 configurations) are decided by WGL afterwards on the
+            // same stream, and k_frontier reports each key's analyzer.
+            claim = ctx->ws<int32_t>(WS_CLAIM, K);
+            HIP_TRY(hipMemsetAsync(claim, 0, (size_t)K * sizeof(int32_t), st));
+            HIP_TRY(hipMemsetAsync(q, 0, sizeof(int32_t), st));
+            HIP_TRY(hipMemsetAsync(q + 3, 0, sizeof(int32_t), st));
+            HIP_TRY(hipMemsetAsync(q + 6, 0, 2 * sizeof(int32_t), st));
+            const int64_t reach_cap = budget + 1;
+            // no WGL count, nothing to store -- except for a configurations request,
+            // which needs the last layer reached: every node
+            const uint32_t ncap = cfgreq ? (uint32_t)std::min<int64_t>(reach_cap + 64, (int64_t)1 << 30) : 1u << 16;
+            uint32_t set_cap = 1u << 12;
+            while ((int64_t)set_cap < 2 * reach_cap && set_cap < (1u << 30)) set_cap <<= 1;
+            const uint32_t q_cap = (uint32_t)std::min<int64_t>(reach_cap + 64, (int64_t)1 << 30);
+            const uint32_t lcap = (uint32_t)smax + 2;
+            const uint64_t per_bfs = (uint64_t)set_cap * 8 + 4ULL * q_cap * 8 + scr_bytes_bfs + (uint64_t)ncap * 8 +
+                                     (uint64_t)lcap * 4;
+            wg2 = fit_units(ctx, std::min(n_defer, ctx->n_cu), per_bfs, {WS_BFS_SET, WS_BFS_Q, WS_BFS_NODES});
+            BfsArgs c{};
+            c.src = KeySrc{rec, pair, off, rB, viol, rank, q + 2};
+            c.list = defer; c.n_list = n_defer; c.queue = q; c.out = out_dev;
+            c.unres_list = ctx->ws<int32_t>(WS_BFS_META, n_defer + 1); c.unres_count = q + 3;
+            c.gset = ctx->ws<uint64_t>(WS_BFS_SET, (size_t)wg2 * set_cap); c.gset_cap = set_cap;
+            uint64_t *bq = ctx->ws<uint64_t>(WS_BFS_Q, (size_t)wg2 * 4 * q_cap);
+            c.pend = bq; c.front = bq + (size_t)wg2 * 2 * q_cap; c.q_cap = q_cap;
+            c.scratch = ctx->ws<char>(WS_SCRATCH_BFS, (size_t)wg2 * scr_bytes_bfs); c.scratch_bytes = scr_bytes_bfs;
+            c.budget = budget; c.init_state = init_state; c.states_ok = n_states < 4096 ? 1 : 0;
+            c.claim = claim; c.reach_cap = reach_cap; c.linear = 1;
+            c.ncap = ncap; c.hcap = 1u << 17; c.lcap = lcap;
+            if (cfgreq) {
+                c.cfg_slot = cfgreq->slot_dev; c.cfg_out = cfgreq->out_dev; c.cfg_n = cfgreq->n_dev;
+                c.cfg_rows = cfgreq->rows_dev; c.cfg_per = cfgreq->per_key;
+                c.col_val = dh->value; c.col_val2 = dh->value2;
+                c.vmin = vmin; c.init_value = init; c.per_key_values = per_key_values ? 1 : 0;
+            }
+            c.nodes = ctx->ws<uint64_t>(WS_BFS_NODES, (size_t)wg2 * ncap);
+            c.lstart = ctx->ws<uint32_t>(WS_BFS_LSTART, (size_t)wg2 * lcap);
+            if (!ctx->lds_attr) {
+                HIP_TRY(hipFuncSetAttribute((const void *)k_lin_bfs, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            BFS_LDS_BYTES));
+                HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            MemoH::LDS));
+                HIP_TRY(hipFuncSetAttribute((const void *)k_lin_seq<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            MemoH::LDS));
+                ctx->lds_attr = true;
+            }
+            // WGL for what the analysis cannot hold: LEAN and WIDE kernels over the
+            // unresolved list (each takes its own kind), after the BFS
+            const int want_f = std::min(n_defer, 4 * ctx->n_cu);
+            const uint64_t per_f = (uint64_t)cap2 * 16 + (uint64_t)stack_cap * sizeof(Frame) + scr_bytes_h;
+            waves2 = fit_units(ctx, want_f, per_f, {WS_MEMO_DEEP, WS_STACK_DEEP, WS_SCRATCH_DEEP});
+            const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;
+            uint64_t *memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
+            if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
+            DfsArgs f = a;
+            f.handover_min = 0;
+            f.list = c.unres_list; f.n_list = 0; f.n_list_dev = q + 3; f.queue = q + 6; f.defer = 0;
+            f.defer_list = nullptr; f.defer_count = nullptr;
+            f.defer64 = nullptr; f.defer_kind = nullptr; f.defer_kind_count = nullptr;
+            f.memo = memo2; f.memo_cap = cap2;
+            f.stack = ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap);
+            f.scratch = ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes_h); f.scratch_bytes = scr_bytes_h;
+            f.budget = budget; f.budget_full = 0; f.claim = nullptr;
+            f.gen_base = ctx->gen_base + (uint32_t)K + 1;
+            f.probes = (unsigned long long *)(q + 8); f.dbg = nullptr; f.defer_time = nullptr;
+            f.seq_start = nullptr; f.exit_count = nullptr; f.cause_or = CAUSE_BY_WGL;
+            HIP_TRY(hipEventRecord(ctx->ev[6], st));
+            k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(ctx->ev[5], st));
+            if (!cfgreq) {
+                k_lin_seq3<true><<<waves2, 64, MemoM::LDS, st>>>(f);
+                HIP_TRY(hipGetLastError());
+                DfsArgs fw = f;
+                fw.queue = q + 7;
+                k_lin_seqw<<<waves2, 64, SEQW_LDS, st>>>(fw);
+                HIP_TRY(hipGetLastError());
+            }
+            HIP_TRY(hipEventRecord(ctx->ev[10], st));
+            HIP_TRY(hipEventRecord(ctx->ev[7], st));
+        } else if (n_defer > 0) {
+            // Heavy keys: two exact searches race per key and the first to settle
+            // it writes its verdict (emit_verdict), the other abandons it.
+            //  - the workgroup BFS (stream st) settles keys with no reachable
+            //    terminal configuration (invalid) within the budget, and valid
+            //    keys whose reachable set it can store (WGL's exact count);
+            //  - the sequential search with the full budget (aux stream: LEAN
+            //    and WIDE keys in one grid) settles every key.
+            prep_race(n_defer, n_def_l);
+
+            // the fork point: everything the phase-2 searches read (claims, queue
+            // counters, sorted lists, the cleared memo on a generation wrap) is
+            // ordered before it; every table of phases 2 and 3 is allocated above
+            // (an allocation after the fork would synchronise the device)
+            prep_wide();
+            HIP_TRY(hipEventRecord(ctx->ev[6], st));
+            // fork: the BFS on st, the LEAN and WIDE sequential searches on aux
+            // (one grid), helpers on aux3
+            HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
+            k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, st>>>(c);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(ctx->ev[5], st));
+            bool wide_done = bfs_only;
+            if (bfs_only || (waves2 == 0 && waves_w == 0)) {}
+            else if (wg_race) { if (waves2) k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux>>>(wr); }
+            else if (p2_m) {
+                DfsPair pr;
+                pr.l = b; pr.w = bw; pr.n_l = waves2;
+                pr.w.wave_off = waves2;
+                k_lin_seq_lw<<<waves2 + waves_w, 64, SEQLW_LDS, ctx->aux>>>(pr);
+                wide_done = true;
+            } else if (waves2) k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(ctx->ev[10], ctx->aux));
+            if (!bfs_only) launch_wide(ctx->aux, !wide_done);
+            if (n_help > 0) {
+                // every helper leaves once the sequential search has left its
+                // queue (or after HELPER_MAX_TICKS): joined before the verdicts are read
+                HIP_TRY(hipStreamWaitEvent(ctx->aux3, ctx->ev[6], 0));
+                k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux3>>>(wh);
+                HIP_TRY(hipGetLastError());
+                HIP_TRY(hipEventRecord(ctx->ev[12], ctx->aux3));
+            }
+            if (split3 && !bfs_only && !wg_race) {
+                // phase 3: the LEAN keys phase 2 handed over, full budget, on phase 2's
+                // tables (same stream, phase 2 has ended; a fresh generation range).
+                // Few of them (no more than phase 2's CUs): a lone wave and the 128 KB
+                // LDS memo each, as in phase 2; more: four waves per CU. Both kernels
+                // are launched and the count phase 2 left on the device picks one.
+                DfsArgs c3 = b;
+                c3.list = defer3; c3.n_list = 0; c3.n_list_dev = q + 16; c3.defer = 0;
+                c3.defer_list = nullptr; c3.defer_count = nullptr;
+                c3.seq_start = nullptr; c3.exit_count = nullptr;
+                c3.budget = budget; c3.budget_full = 0;
+                c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
+                c3.dbg = nullptr;
+                c3.probes = (unsigned long long *)(q + Q_PROBES_P3);
+                const int few = std::max(1, ctx->n_cu - wg2);
+                DfsArgs c3a = c3;
+                c3a.queue = q + 17; c3a.n_max = few;
+                k_lin_seq<true><<<std::min(waves2, few), 64, MemoH::LDS, ctx->aux>>>(c3a);
+                HIP_TRY(hipGetLastError());
+                DfsArgs c3b = c3;
+                c3b.queue = q + 18; c3b.n_min = few + 1;
+                k_lin_seq3<true><<<waves2, 64, MemoM::LDS, ctx->aux>>>(c3b);
+                HIP_TRY(hipGetLastError());
+            }
+            HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
+            HIP_TRY(hipStreamWaitEvent(st, ctx->ev[7], 0));
+            if (n_help > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[12], 0));
+            if (n_help > 0 && wh.key_prof) {
+                // JH_DEBUG=4: what the late helpers took (end time in us after their start)
+                HIP_TRY(hipStreamSynchronize(st));
+                std::vector<unsigned long long> kp(3 * (size_t)K);
+                HIP_TRY(hipMemcpy(kp.data(), wh.key_prof, kp.size() * 8, hipMemcpyDeviceToHost));
+                for (int64_t k = 0; k < K; k++)
+                    if (kp[3 * k])
+                        fprintf(stderr, "[jh-help] key %lld wg %llu verdict %llu won %llu inserts %llu cycles %llu end_us %llu\n",
+                                (long long)k, (kp[3 * k + 2] >> 8) & 0xFFF, kp[3 * k + 2] & 0xFF, (kp[3 * k + 2] >> 20) & 1,
+                                kp[3 * k + 1], kp[3 * k], kp[3 * k + 2] >> 32);
+            }
+            if (const char *dp = tune_env("JH_BFS_DUMP")) {
+                // debugging: workgroup 0's stored configurations (t:20 | s:12 | mask:32)
+                HIP_TRY(hipStreamSynchronize(st));
+                std::vector<uint64_t> nd(c.ncap);
+                HIP_TRY(hipMemcpy(nd.data(), c.nodes, nd.size() * 8, hipMemcpyDeviceToHost));
+                if (FILE *fp = fopen(dp, "wb")) { fwrite(nd.data(), 8, nd.size(), fp); fclose(fp); }
+            }
+            if (dbg2) {
+                HIP_TRY(hipMemcpyAsync(qh, q, sizeof qh, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                n_unres = qh[3];
+                std::vector<unsigned long long> h((size_t)wg2 * 16);
+                HIP_TRY(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+                for (int w = 0; w < wg2; w++)
+                    if (h[16 * w + 4])
+                        fprintf(stderr, "[jh-bfs] wg %d keys=%llu cycles=%llu rounds=%llu configs=%llu cyc/round=%.0f | "
+                                "count: hash=%llu live=%llu path=%llu closure=%llu cyc | global-set rounds=%llu cyc=%llu "
+                                "configs=%llu, LDS-set rounds cyc=%llu configs=%llu | live: layers=%llu (LDS %llu) head-cyc=%llu LDS-layers-cyc=%llu\n",
+                                w, h[16 * w + 4], h[16 * w], h[16 * w + 1], h[16 * w + 3],
+                                (double)h[16 * w] / std::max(1ULL, h[16 * w + 1]), h[16 * w + 5], h[16 * w + 6],
+                                h[16 * w + 7], h[16 * w + 8], h[16 * w + 10], h[16 * w + 9], h[16 * w + 11],
+                                h[16 * w + 12], h[16 * w + 13], h[16 * w + 14] & 0xFFFFFFFF, h[16 * w + 14] >> 32, h[16 * w + 15], h[16 * w + 2]);
+    #ifdef JH_BFS_PROF
+                {
+                    unsigned long long bp[8];
+                    HIP_TRY(hipMemcpyFromSymbol(bp, HIP_SYMBOL(g_bfs_prof), sizeof bp));
+                    const double nr = (double)std::max(1ULL, bp[4]), nl = (double)std::max(1ULL, bp[6]);
+                    unsigned long long bx[4];
+                    HIP_TRY(hipMemcpyFromSymbol(bx, HIP_SYMBOL(g_bfs_prof_x), sizeof bx));
+                    const double ni = (double)std::max(1ULL, bx[2]);
+                    fprintf(stderr, "[jh-bfs-prof] rounds=%llu cyc/round: claim+barrier %.0f items %.0f barrier %.0f tail %.0f | "
+                            "layers=%llu formation cyc/layer %.0f | tid0 items=%llu cyc/item: load+children %.0f insert8 %.0f record8 %.0f\n",
+                            bp[4], bp[0] / nr, bp[1] / nr, bp[2] / nr, bp[3] / nr, bp[6], bp[5] / nl, bx[2], bp[7] / ni, bx[0] / ni, bx[1] / ni);
+                    memset(bx, 0, sizeof bx);
+                    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bfs_prof_x), bx, sizeof bx));
+                    memset(bp, 0, sizeof bp);
+                    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bfs_prof), bp, sizeof bp));
+                }
+    #endif
+                std::vector<unsigned long long> g((size_t)waves2 * 16);
+                HIP_TRY(hipMemcpy(g.data(), dbg + 16 * 256, g.size() * 8, hipMemcpyDeviceToHost));
+                for (int w = 0; w < waves2; w++)
+                    if (g[16 * w + 4] > 0)
+                        fprintf(stderr, "[jh-seq] wave %d keys=%llu search=%llu cyc busy=%llu | steps=%llu inserts=%llu evict=%llu lay-loads=%llu op-loads=%llu spills=%llu refills=%llu slow=%llu hbm-probes=%llu | cyc/step=%.0f\n",
+                                w, g[16 * w + 3], g[16 * w + 2], g[16 * w + 9], g[16 * w + 4], g[16 * w + 5], g[16 * w + 6],
+                                g[16 * w + 7], g[16 * w + 10], g[16 * w + 11], g[16 * w + 12], g[16 * w + 13], g[16 * w + 14],
+                                (double)g[16 * w + 2] / std::max(1ULL, g[16 * w + 4]));
+            }
+        } else {
+            HIP_TRY(hipEventRecord(ctx->ev[6], st));
+            HIP_TRY(hipEventRecord(ctx->ev[5], st));
+            HIP_TRY(hipEventRecord(ctx->ev[10], st));
+            HIP_TRY(hipEventRecord(ctx->ev[7], st));
+        }
+        if (n_x > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[9], 0));
     }
-    if (n_x > 0) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[9], 0));
     HIP_TRY(hipEventRecord(ctx->ev[2], st));
     if (defer_times && n_defer > 0) {
         // timeline: when each deferred key was handed on (us after phase 1's
@@ -6082,6 +6665,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     HIP_TRY(hipStreamSynchronize(st));
     if (qh[2] & 2) throw_jh(JH_EDEVICE, "per-key table exceeded the scratch reservation");
     if (qh[2] & 4) throw_jh(JH_EDEVICE, "DFS stack overflow");
+    if (qh[2] & FLAG_BLK_FULL) throw_jh(JH_EDEVICE, "phase-1 memo blocks exhausted without a heavy-key pass");
     if ((qh[2] & 0x1F0) && acc_stats && ctx->bufs.size() > WS_DEBUG && ctx->bufs[WS_DEBUG].p && n_wg > 0 &&
         dbgenv && atoi(dbgenv) >= 3) {
         std::vector<unsigned long long> tr((size_t)n_wg * 256);
@@ -6102,11 +6686,16 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 fprintf(stderr, "[jh-acc] wg %d LOST ITEM pos %llu tail %llu cap_total %llu\n", g, l8[0], l8[1], l8[2]);
         }
     }
-    if (qh[2] & 0x1F0) {
-        char m[160];
+    if (qh[2] & 0x3F0) {
+        char m[192];
         snprintf(m, sizeof m, "search watchdog tripped (flags 0x%x: 16 lost work item, 32 idle enumeration, "
-                 "64 full set, 128 step limit, 256 bad window)", qh[2]);
+                 "64 full set, 128 step limit, 256 bad window, 512 stream wait)", qh[2]);
         throw_jh(JH_EDEVICE, m);
+    }
+    if (stream_p2) {
+        // the live lists' final lengths (the bounds used to size the pass above)
+        n_defer = qh[1]; n_def_l = qh[Q_DEFER_L]; n_def_w = qh[Q_DEFER_W];
+        if (n_def_l + n_def_w != n_defer) throw_jh(JH_EDEVICE, "deferred-key lists disagree");
     }
     if (sum) {
         sum->valid = sh[0]; sum->n_invalid = sh[1]; sum->n_unknown = sh[2];
@@ -6121,7 +6710,29 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         sum->deferred_entries = q64(qh, Q_ENT_ALL);
         sum->seq_probes = q64(qh, 8);
         sum->seq_ms = 0; sum->bfs_ms = 0; sum->p3_ms = 0; sum->wide_ms = 0; sum->xw_ms = 0;
-        if (n_defer > 0) {
+        sum->streamed = stream_p2 ? 1 : 0;
+        sum->p3_entries = q64(qh, Q_ENT_P3);
+        sum->p2_start_ms = -1; sum->p1_span_ms = 0;
+        // an engine's own span from its s_memrealtime words (100 MHz): [first key, last wave end]
+        auto span_ms = [&](int w) {
+            const int64_t t0 = q64(qh, w), t1 = q64(qh, w + 2);
+            return (t0 != -1 && t1 > t0) ? (t1 - t0) / 1e5 : 0.0;
+        };
+        if (stream_p2) {
+            sum->p1_span_ms = span_ms(Q_T_P1);
+            sum->seq_ms = span_ms(Q_T_LEAN);
+            sum->bfs_ms = span_ms(Q_T_BFS);
+            sum->xw_ms = span_ms(Q_T_XW);
+            if (waves_w > 0) sum->wide_ms = span_ms(Q_T_WIDE);
+            if (split3) { float c2 = 0; HIP_TRY(hipEventElapsedTime(&c2, ctx->ev[13], ctx->ev[7])); sum->p3_ms = c2; }
+            const int64_t p1s = q64(qh, Q_T_P1);
+            int64_t first = -1;
+            for (int w : {Q_T_BFS, Q_T_LEAN}) {
+                const int64_t t = q64(qh, w);
+                if (t != -1 && (first == -1 || t < first)) first = t;
+            }
+            if (first != -1 && p1s != -1) sum->p2_start_ms = (first - p1s) / 1e5;
+        } else if (n_defer > 0) {
             float a2 = 0, b2 = 0;
             if (use_wg) HIP_TRY(hipEventElapsedTime(&a2, ctx->ev[11], ctx->ev[5]));
             else HIP_TRY(hipEventElapsedTime(&a2, ctx->ev[6], ctx->ev[10]));
@@ -6131,7 +6742,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             // the WIDE waves' own span (they share a grid with the LEAN ones)
             if (waves_w > 0 && q64(qh, Q_T_WIDE + 2) > q64(qh, Q_T_WIDE)) sum->wide_ms = (q64(qh, Q_T_WIDE + 2) - q64(qh, Q_T_WIDE)) / 1e5;
         }
-        if (n_x > 0) { float e2 = 0; HIP_TRY(hipEventElapsedTime(&e2, ctx->ev[8], ctx->ev[9])); sum->xw_ms = e2; }
+        if (n_x > 0 && !stream_p2) { float e2 = 0; HIP_TRY(hipEventElapsedTime(&e2, ctx->ev[8], ctx->ev[9])); sum->xw_ms = e2; }
 #ifdef JH_XW_PROF
         if (n_x > 0) {
             unsigned long long x[12];

@@ -50,7 +50,7 @@ def main():
     # the phase whose kernel this is (bench.PHASES): its entries and probes in each pass's run
     alg = {}
     for log, d in run.items():
-        for name, (tf, pf, ef, kern) in PHASES.items():
+        for name, (tf, pf, ef, kf, kern) in PHASES.items():
             if kern.split("<")[0] in kernel and (("<" not in kernel) or kern in kernel) and d.get(tf, 0) > 0:
                 ent = d["entries"] if ef is None else d[ef]
                 alg[log] = BYTES_PER_ENTRY * ent + BYTES_PER_PROBE * d[pf]

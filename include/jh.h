@@ -283,13 +283,15 @@ int jh_key_index(jh_ctx *ctx, const jh_history *h, int64_t *key_off, int64_t *ro
  * last layer its search reaches -- the ways of linearizing the ops before the
  * failing :ok op from which that op cannot be linearized -- in a canonical
  * order: register value (nil first, then ascending), then the linearized
- * members of the window as a bit mask in call order. n_out[i] = the count for
- * keys[i], or -1 (not invalid, or outside the reachable-set engine: windows
- * over 32 members, >= 4096 states, more than budget + 1 configurations).
+ * members of the window as a bit mask in call order (a JH_MAX_WINDOW-bit
+ * number). n_out[i] = the count for keys[i], or -1 (not invalid, a window
+ * over JH_MAX_WINDOW members, or more than budget configurations reachable).
+ * Windows up to 32 members with < 4096 states come from the reachable-set
+ * engine, wider ones (round 4) from the 65-256-member search's table.
  * out[i * per_key + j] describes configuration j of keys[i]; its rows are
  * rows_out[rows_off .. rows_off + n_linearized + n_pending): the invocation
  * rows of the linearized ops, then of the pending ones (knossos' :pending),
- * each in call order; rows_cap >= n_keys_q * per_key * 64. knossos is not
+ * each in call order; rows_cap >= n_keys_q * per_key * JH_MAX_WINDOW. knossos is not
  * vendored: this order, the cut and the layer are this library's
  * definitions (parity unpinned; the oracle restates them). */
 typedef struct jh_lin_config {

@@ -254,7 +254,7 @@ class Context:
         nq = len(keys)
         out = (A.JhLinConfig * max(nq * per_key, 1))()
         n_out = np.zeros(max(nq, 1), np.int32)
-        rows = np.zeros(max(nq * per_key * 64, 1), np.int64)
+        rows = np.zeros(max(nq * per_key * A.MAX_WINDOW, 1), np.int64)
         err = C.create_string_buffer(1024)
         rc = lib().jh_lin_configs(self._h, C.byref(h), C.byref(_opts(init, budget, **tune)),
                                   keys.ctypes.data_as(C.POINTER(C.c_int64)), nq, per_key, out,

@@ -220,49 +220,107 @@ class Linearizable(Checker):
 
 def add_configs(result, configs, cols, model=None):
     """:configs and :final-paths of an invalid result (checker.clj:146-158
-    keeps (take 10 ...) of each), from jh_lin_configs: every configuration of
-    the frontier as {:model, :linearized ops, :pending ops}. Its final path is
-    the step no configuration gets past: from the configuration's model, the
-    result's :op, whose step is inconsistent from every frontier model (a
-    model it could step from would have a successor past :op's completion).
-    The knossos maps these restate are not vendored: parity unpinned."""
+    keeps (take 10 ...) of each), from jh_lin_configs: the frontier -- the
+    configurations at the last layer any search reaches, first 10 in the
+    canonical order (include/jh.h).
+
+    A configuration is shaped as knossos 0.3.x's Config record [K] (model,
+    last-op, pending): the model, the last op linearized (the linearized
+    window member invoked last; nil when the window has none: the order in
+    which the rest were linearized is not part of a configuration) and the
+    pending ops in call order. A final path starts at the configuration
+    ({:op last-op :model model}), linearizes the pending ops that step
+    consistently, in call order, each with the model after it, and ends in
+    the failing :op, inconsistent from every frontier model (a model it could
+    step from would have a successor past the op's completion) -- one path
+    per configuration. knossos is not vendored: the shape follows its record
+    from memory and the path choice is this library's, parity unpinned."""
     if configs is None:
         return result
-    def model_map(v):
-        return {"value": None if v == A.NIL else int(v)}
-    cf = [{"model": model_map(v), "linearized": [H.decode_op(cols, x) for x in lin],
-           "pending": [H.decode_op(cols, x) for x in pend]} for v, lin, pend in configs]
-    result["configs"] = cf[:A.CONFIGS_PER_KEY]
+    cf = []
+    for v, lin, pend in configs:
+        val = None if v == A.NIL else int(v)
+        if val is not None and cols.values_interned and 0 <= val < len(cols.value_table):
+            val = cols.value_table[val]          # interned history: the state is a value-table id
+        m = _model_of(model, val)
+        cf.append({"model": _model_map(m),
+                   "last-op": _completed_op(cols, max(lin)) if lin else None,
+                   "pending": [_completed_op(cols, x) for x in sorted(pend)],
+                   "_m": m})
     op = result.get("op")
-    result["final-paths"] = [[{"op": None, "model": c["model"]},
-                              {"op": op, "model": _final_step(model, c["model"]["value"], op)}]
-                             for c in cf][:A.CONFIGS_PER_KEY]
+    paths = []
+    for c in cf[:A.CONFIGS_PER_KEY]:
+        m = c["_m"]
+        path = [{"op": c["last-op"], "model": _model_map(m)}]
+        for p in c["pending"]:
+            r = _step(m, p)
+            if r is None or is_inconsistent(r):
+                continue
+            m = r
+            path.append({"op": p, "model": _model_map(m)})
+        if op is not None:
+            r = _step(m, op)
+            path.append({"op": op, "model": ({"inconsistent": r.msg} if is_inconsistent(r) else
+                                             {"error": "no step"} if r is None else _model_map(r))})
+        paths.append(path)
+    for c in cf:
+        del c["_m"]
+    result["configs"] = cf[:A.CONFIGS_PER_KEY]
+    result["final-paths"] = paths
     return result
 
 
-def _final_step(model, value, op):
-    """knossos.model/step of a frontier model on the failing op, as the
-    {:inconsistent msg} map the path ends in (model.py's messages)."""
-    if op is None:
-        return None
+def _completed_op(cols, row):
+    """The invocation at `row` as knossos.history/complete leaves it [K]
+    (cassandra/src/cassandra/checker.clj:29-31): an :ok completion fills a
+    nil :value -- the next row of the same process completes it."""
+    op = H.decode_op(cols, int(row))
+    v = op.get("value")
+    if v is None or (hasattr(v, "value") and hasattr(v, "key") and v.value is None):
+        p = int(cols.process[row])
+        if p >= 0:
+            nxt = np.nonzero(cols.process[row + 1:] == p)[0]
+            if len(nxt):
+                c = H.decode_op(cols, int(row + 1 + nxt[0]))
+                if c.get("type") == "ok":
+                    op = dict(op, value=c.get("value"))
+    return op
+
+
+def _unwrap(op):
     v = op.get("value")
     if hasattr(v, "key") and hasattr(v, "value"):       # an independent tuple
         op = dict(op, value=v.value)
+    return op
+
+
+def _model_of(model, value):
+    """The model object for a configuration's interned state value."""
     if isinstance(model, Mutex):
-        m = Mutex(bool(value))
+        return Mutex(bool(value))
+    if isinstance(model, Register):
+        return Register(value)
+    return CASRegister(value)
+
+
+def _model_map(m):
+    if isinstance(m, Mutex):
+        return {"locked": m.locked}
+    return {"value": getattr(m, "value", None)}
+
+
+def _step(m, op):
+    """knossos.model/step of model m on a history op map (mutex ops arrive as
+    the cas they were searched as, model.to_device_ops); None if no clause."""
+    op = _unwrap(op)
+    if isinstance(m, Mutex):
         cas = op.get("value")
-        op = dict(op, f="acquire" if list(cas or []) == [0, 1] else "release")
-    elif isinstance(model, Register):
-        m = Register(value)
-    else:
-        m = CASRegister(value)
+        if op.get("f") == "cas":
+            op = dict(op, f="acquire" if list(cas or []) == [0, 1] else "release")
     try:
-        r = m.step(op)
-    except (ValueError, TypeError) as e:
-        return {"error": str(e)}
-    if is_inconsistent(r):
-        return {"inconsistent": r.msg}
-    return {"value": getattr(r, "value", None)}
+        return m.step(op)
+    except (ValueError, TypeError):
+        return None
 
 
 def _algorithm(a):

@@ -178,7 +178,7 @@ int jh_lin_configs(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts, co
     if (!ctx || !keys || !out || !n_out || !rows_out) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
     if (per_key < 1 || per_key > 16) { set_err(err, errlen, "per_key must be in 1..16"); return JH_EINVAL; }
     if (n_keys_q < 0 || n_keys_q > (1 << 20)) { set_err(err, errlen, "bad number of keys"); return JH_EINVAL; }
-    if (rows_cap < n_keys_q * per_key * 64) { set_err(err, errlen, "rows_cap < n_keys_q * per_key * 64"); return JH_EINVAL; }
+    if (rows_cap < n_keys_q * per_key * JH_MAX_WINDOW) { set_err(err, errlen, "rows_cap < n_keys_q * per_key * JH_MAX_WINDOW"); return JH_EINVAL; }
     ctx = primary(ctx);
     std::lock_guard<std::mutex> g(ctx->mu);
     return guarded(err, errlen, [&] {
@@ -196,7 +196,7 @@ int jh_lin_configs(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts, co
         int64_t *kd = ctx->ws<int64_t>(WS_CFG_KEYS, nq);
         jh_lin_config *co = ctx->ws<jh_lin_config>(WS_CFG_OUT, (size_t)nq * per_key);
         int32_t *cn = ctx->ws<int32_t>(WS_CFG_N, nq);
-        int64_t *cr = ctx->ws<int64_t>(WS_CFG_ROWS, (size_t)nq * per_key * 64);
+        int64_t *cr = ctx->ws<int64_t>(WS_CFG_ROWS, (size_t)nq * per_key * JH_MAX_WINDOW);
         HIP_TRY(hipMemsetAsync(slot, 0xFF, sizeof(int32_t) * K, st));
         HIP_TRY(hipMemsetAsync(cn, 0xFF, sizeof(int32_t) * nq, st));
         HIP_TRY(hipMemcpyAsync(kd, keys, sizeof(int64_t) * nq, hipMemcpyHostToDevice, st));
@@ -205,7 +205,7 @@ int jh_lin_configs(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts, co
         LinCfgReq req{kd, nq, per_key, slot, co, cn, cr};
         lin_check_independent(ctx, &d, opts, keyed, dv, nullptr, st, &req);
         std::vector<jh_lin_config> hc((size_t)nq * per_key);
-        std::vector<int64_t> hr((size_t)nq * per_key * 64);
+        std::vector<int64_t> hr((size_t)nq * per_key * JH_MAX_WINDOW);
         HIP_TRY(hipMemcpyAsync(n_out, cn, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(hc.data(), co, sizeof(jh_lin_config) * hc.size(), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(hr.data(), cr, sizeof(int64_t) * hr.size(), hipMemcpyDeviceToHost, st));

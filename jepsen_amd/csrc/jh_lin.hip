@@ -354,7 +354,9 @@ struct DfsArgs {
     const int32_t *p1_tot;
     int32_t *drained;
     const int32_t *live_n;
+    unsigned long long *tl;     // -DJH_TUNING timeline (JH_DEFER_TIMES): per key [2] search start, [3] end
 };
+constexpr int TL_W = 6;         // timeline words per key: BFS, sequential, helper (start, end)
 constexpr unsigned long long SEQ_HANDED = ~0ULL;
 
 __device__ __forceinline__ int ld_agent(const int32_t *p) {
@@ -1034,40 +1036,38 @@ __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint32_t *bcnt, uin
 // Here a key's evicted entries (8-byte LEAN keys, no generation tag: the
 // blocks are the key's own) fill 8 KB blocks of 1 024 slots to at most half,
 // one block after the other, so an eviction writes whole lines of a few
-// blocks. Lane b of the wave holds block b's layer range [tlo, thi]; a probe
-// of a Bloom-positive child reads one 64-byte group of every block whose range
-// holds the child's layer, all lanes at once: one round trip, as before.
-// The entries are staged in registers (no global stage either).
+// blocks. Block b's layer range [tlo, thi] is kept in LDS beside the memo; a
+// probe of a Bloom-positive child reads one 64-byte group of every block
+// whose range holds the child's layer, lane b for block b: one round trip,
+// as before. The entries are compacted in place (no stage in global memory).
 constexpr int BLK_SLOTS = 1024;          // 8-byte slots per block (8 KB)
 constexpr int BLK_FILL = 512;            // entries per block at most (load 1/2)
 constexpr int BLK_MAX = 64;              // blocks per key (lane b: block b); 32 K entries
 constexpr int BLK_GROUPS = BLK_SLOTS / 8;
 constexpr int32_t FLAG_BLK_FULL = 2048;  // flags: a key needed more than BLK_MAX blocks
-struct BlkState {
-    uint32_t nblk, fill;      // blocks used; entries in the last one (wave-uniform)
-    uint32_t tlo, thi;        // lane b: block b's layer range
-    uint32_t ovf;             // a block beyond BLK_MAX was needed: the key's memo is incomplete
+// per wave, in LDS after its memo (kept out of registers: the search's loop
+// is at its register budget, and state passed through calls inflates it)
+struct BlkLds {
+    uint32_t nblk, fill, ovf, pad;       // blocks used, entries in the last one, over BLK_MAX
+    uint32_t tlo[BLK_MAX], thi[BLK_MAX];
 };
+constexpr int BLK_LDS = (int)sizeof(BlkLds);
 __device__ __forceinline__ uint32_t blk_group(uint64_t k) {
     return (uint32_t)(jh_mix64(k) >> 40) & (BLK_GROUPS - 1);
 }
-// one lane: k (unique in the key's memo) into block blk, from its hash group
-// on; the group is read first so the CAS goes to its first empty slot
+// one lane: k (unique in the key's memo) into block blk, from its hash
+// group on, slot by slot: a CAS per slot, the slots of a group filling front
+// to back (one round trip per occupied slot passed; few registers, as the
+// eviction runs inside the search's register budget)
 __device__ __forceinline__ void blk_put(uint64_t *blk, uint64_t k) {
-    uint32_t g = blk_group(k);
-    for (int it = 0; it < BLK_GROUPS; it++) {
-        unsigned long long *p = (unsigned long long *)(blk + 8 * g);
-        int j0 = 8;
-#pragma unroll
-        for (int j = 7; j >= 0; j--)
-            if (__hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) j0 = j;
-        for (int j = j0; j < 8; j++) {
-            unsigned long long exp = 0;
-            if (__hip_atomic_compare_exchange_strong(p + j, &exp, (unsigned long long)k, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                return;
-        }
-        g = (g + 1) & (BLK_GROUPS - 1);
+    const uint32_t g0 = blk_group(k) * 8;
+#pragma unroll 1
+    for (uint32_t it = 0; it < BLK_SLOTS; it++) {
+        unsigned long long exp = 0;
+        if (__hip_atomic_compare_exchange_strong((unsigned long long *)(blk + ((g0 + it) & (BLK_SLOTS - 1))), &exp,
+                                                 (unsigned long long)k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            return;
     }
 }
 // one lane: is k in block blk (a group with an empty slot ends the probe)
@@ -1100,15 +1100,16 @@ __device__ __forceinline__ uint32_t wave_max_in(uint64_t m, int lane, uint32_t v
 }
 // the lanes' entries x (where v) into the key's blocks: the last block up to
 // BLK_FILL, then a fresh one (zeroed first); their layer ranges widen
-__device__ __forceinline__ void blk_add(uint64_t *region, BlkState &s, uint64_t x, bool v, int lane) {
+__device__ __forceinline__ void blk_add(uint64_t *region, BlkLds *bl, uint64_t x, bool v, int lane) {
     const uint64_t m = ballot(v);
     if (!m) return;
+    const uint32_t nb = rflu(bl->nblk), fill = rflu(bl->fill);
     const uint32_t cnt = (uint32_t)__popcll(m);
     const uint32_t rank = (uint32_t)mbcnt(m);
-    const uint32_t room = s.nblk ? BLK_FILL - s.fill : 0;
-    const uint32_t cur = s.nblk - 1, nb = s.nblk;
+    const uint32_t room = nb ? BLK_FILL - fill : 0;
+    const uint32_t cur = nb - 1;
     if (cnt > room) {
-        if (nb >= BLK_MAX) { s.ovf = 1; return; }
+        if (nb >= BLK_MAX) { if (lane == 0) bl->ovf = 1; wave_sync(); return; }
         uint4 *z = (uint4 *)(region + (size_t)nb * BLK_SLOTS);
 #pragma unroll
         for (int r = 0; r < BLK_SLOTS * 8 / 16 / 64; r++) z[lane + 64 * r] = make_uint4(0, 0, 0, 0);
@@ -1122,26 +1123,24 @@ __device__ __forceinline__ void blk_add(uint64_t *region, BlkState &s, uint64_t 
     const uint64_t mc = ballot(v && in_cur), mn = m & ~mc;
     if (mc) {
         const uint32_t lo = wave_min_in(mc, lane, xt), hi = wave_max_in(mc, lane, xt);
-        if (lane == (int)cur) { s.tlo = min(s.tlo, lo); s.thi = max(s.thi, hi); }
+        if (lane == 0) { bl->tlo[cur] = min(bl->tlo[cur], lo); bl->thi[cur] = max(bl->thi[cur], hi); }
     }
     if (mn) {
         const uint32_t lo = wave_min_in(mn, lane, xt), hi = wave_max_in(mn, lane, xt);
-        if (lane == (int)nb) { s.tlo = lo; s.thi = hi; }
-        s.nblk = nb + 1;
-        s.fill = cnt - room;
-    } else {
-        s.fill += cnt;
+        if (lane == 0) { bl->tlo[nb] = lo; bl->thi[nb] = hi; bl->nblk = nb + 1; bl->fill = cnt - room; }
+    } else if (lane == 0) {
+        bl->fill = fill + cnt;
     }
+    wave_sync();
 }
 // memo_evict for the block memo: the same theta rule; the LDS table is not
 // rebuilt but compacted bucket by bucket in place (a lane owns whole buckets:
 // the entries at or above theta keep their slots' order, the others go to the
 // blocks), so nothing is staged and no entry can fail to find a place.
-// Returns the blocks, the new theta and the entries kept.
-struct EvictBlk { BlkState s; uint32_t theta; int kept; };
+// Returns theta << 32 | kept, like memo_evict.
 template <class M>
-__device__ __forceinline__ EvictBlk memo_evict_blk(uint64_t *lmemo, uint32_t *bcnt, uint32_t *bloom, uint64_t *region,
-                                                BlkState s, uint32_t t_cur, uint32_t theta_old, int lane) {
+__device__ __noinline__ uint64_t memo_evict_blk(uint64_t *lmemo, uint32_t *bcnt, uint32_t *bloom, uint64_t *region,
+                                                BlkLds *bl, uint32_t t_cur, uint32_t theta_old, int lane) {
     int bins = 0;                                  // lane b < 16 holds bin b
 #pragma unroll 1
     for (int r = 0; r < M::SLOTS / 64; r++) {
@@ -1174,29 +1173,25 @@ __device__ __forceinline__ EvictBlk memo_evict_blk(uint64_t *lmemo, uint32_t *bc
     for (int bb = 0; bb < M::BKT / 64; bb++) {
         const uint32_t b = (uint32_t)lane + 64u * (uint32_t)bb;
         const uint32_t n = bcnt8[b];
-        uint64_t e[4];
-        bool ev[4];
         uint32_t w = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            e[j] = (uint32_t)j < n ? lmemo[4 * b + j] : 0;
-            const bool keep = (uint32_t)j < n && lk_t(e[j]) >= th2;
-            ev[j] = (uint32_t)j < n && !keep;
-            if (keep) { lmemo[4 * b + w] = e[j]; w++; }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) if ((uint32_t)j >= w) lmemo[4 * b + j] = 0;
-        bcnt8[b] = (uint8_t)w;
-        kept += (int)w;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            blk_add(region, s, e[j], ev[j], lane);
-            if (ev[j]) {
+        // slot by slot (a kept entry moves to slot w <= j: no unread slot is overwritten)
+#pragma unroll 1
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint64_t x = j < n ? lmemo[4 * b + j] : 0;
+            const bool keep = j < n && lk_t(x) >= th2;
+            const bool ev = j < n && !keep;
+            if (keep) { lmemo[4 * b + w] = x; w++; }
+            blk_add(region, bl, x, ev, lane);
+            if (ev) {
                 uint32_t h1, h2;
-                lk_hash((uint32_t)e[j], (uint32_t)(e[j] >> 32), h1, h2);
+                lk_hash((uint32_t)x, (uint32_t)(x >> 32), h1, h2);
                 bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
             }
         }
+#pragma unroll 1
+        for (uint32_t j = w; j < 4; j++) lmemo[4 * b + j] = 0;
+        bcnt8[b] = (uint8_t)w;
+        kept += (int)w;
     }
     for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o);
     // the LDS rewrite and the block writes (stores, L2 atomics) done before
@@ -1205,42 +1200,39 @@ __device__ __forceinline__ EvictBlk memo_evict_blk(uint64_t *lmemo, uint32_t *bc
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     wave_sync();
-    EvictBlk r;
-    r.s = s; r.theta = th2; r.kept = kept;
-    return r;
+    return ((uint64_t)th2 << 32) | (uint32_t)kept;
 }
-// one child into the blocks (both its LDS buckets full). Inlined like
-// memo_evict_blk: as calls they kept 122 VGPRs live in phase 1's loop (4
-// waves per SIMD instead of 5); inline 90, no scratch
+// one child into the blocks (both its LDS buckets full), out of line
 template <class M>
-__device__ __forceinline__ BlkState blk_add_one(uint64_t *region, BlkState s, uint64_t x, bool v, uint32_t *bloom,
-                                             uint32_t bl1, uint32_t bl2, int lane) {
-    blk_add(region, s, x, v, lane);
+__device__ __noinline__ void blk_add_one(uint64_t *region, BlkLds *bl, uint64_t x, bool v, uint32_t *bloom,
+                                         uint32_t bl1, uint32_t bl2, int lane) {
+    blk_add(region, bl, x, v, lane);
     if (v) bloom_set2<M>(bloom, bl1, bl2);
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     wave_sync();
-    return s;
 }
 // the Bloom-positive lanes (maybe) of a step: which children are in the
 // blocks. One round trip per such lane: every block whose layer range holds
 // the child's layer is probed at once (lane b: block b).
-struct BlkFind { uint64_t found; uint32_t probes; };
-__device__ __forceinline__ BlkFind blk_find(const uint64_t *region, BlkState s, uint64_t maybe, uint64_t k, uint32_t kt,
-                                         int lane) {
-    BlkFind f{0, 0};
+__device__ __forceinline__ uint64_t blk_find(const uint64_t *region, const BlkLds *bl, uint64_t maybe, uint64_t k,
+                                             uint32_t kt, int lane, unsigned long long &probes) {
+    uint64_t found = 0;
+    const uint32_t nb = rflu(bl->nblk);
+    const bool blk = (uint32_t)lane < nb;
+    const uint32_t lo = blk ? bl->tlo[lane] : 1u, hi = blk ? bl->thi[lane] : 0u;
     while (maybe) {
         const int i = __builtin_ctzll(maybe);
         maybe &= maybe - 1;
         const uint64_t ki = readlane64(k, i);
         const uint32_t ti = (uint32_t)readlane((int)kt, i);
-        const bool mine = (uint32_t)lane < s.nblk && s.tlo <= ti && ti <= s.thi;
-        f.probes += (uint32_t)__popcll(ballot(mine));
+        const bool mine = lo <= ti && ti <= hi;
+        probes += (unsigned long long)__popcll(ballot(mine));
         const bool hit = mine && blk_has(region + (size_t)lane * BLK_SLOTS, ki);
-        if (ballot(hit)) f.found |= 1ULL << i;
+        if (ballot(hit)) found |= 1ULL << i;
     }
-    return f;
+    return found;
 }
 
 __device__ __forceinline__ uint64_t drop_bit(uint64_t m, uint32_t r) {
@@ -1613,7 +1605,11 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
     uint32_t n_steps = 0, n_lay = 0, n_up = 0, n_spill = 0, n_refill = 0, n_slow = 0, n_evict = 0, n_hbm = 0;
     const unsigned long long probes0 = my_probes;
     // BLK (phase 1): the HBM part of the memo is this key's blocks in `memo`
-    BlkState blks{0u, 0u, 0xFFFFFFFFu, 0u, 0u};
+    BlkLds *blks = (BlkLds *)(jh_lds + M::LDS);
+    if constexpr (BLK) {
+        if (lane == 0) { blks->nblk = 0; blks->fill = 0; blks->ovf = 0; }
+        blks->tlo[lane] = 0xFFFFFFFFu; blks->thi[lane] = 0;
+    }
 
     // layer-table window: lane j holds lay[tb0 + j]
     uint32_t tb0 = 0, drq = 0, dhi = 0;
@@ -1723,11 +1719,7 @@ expand:
             const bool maybe = ((low >> lane) & 1) && bloom_test2<M>(bloom, lk_bl(h1), lk_bl(h2));
             if constexpr (BLK) {
                 const uint64_t mm = ballot(maybe);
-                if (mm) {
-                    const BlkFind fr = blk_find(memo, blks, mm, k, kt, lane);
-                    absent &= ~fr.found;
-                    my_probes += fr.probes;
-                }
+                if (mm) absent &= ~blk_find(memo, blks, mm, k, kt, lane, my_probes);
             } else {
                 bool found = false;
                 if (maybe) found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
@@ -1773,11 +1765,10 @@ insert:
                 if (++lcount >= M::EVICT) {
                     DFS_STAT(n_evict++);
                     if constexpr (BLK) {
-                        const EvictBlk e = memo_evict_blk<M>(lmemo, bcnt, bloom, memo, blks, nt, theta, lane);
-                        blks = e.s;
-                        DFS_STAT(n_hbm += (uint32_t)lcount - (uint32_t)e.kept);
-                        lcount = rfl(e.kept);
-                        theta = rflu(e.theta);
+                        const uint64_t er = memo_evict_blk<M>(lmemo, bcnt, bloom, memo, blks, nt, theta, lane);
+                        DFS_STAT(n_hbm += (uint32_t)lcount - (uint32_t)er);
+                        lcount = rfl((int)(uint32_t)er);
+                        theta = rflu((uint32_t)(er >> 32));
                     } else {
                         const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
                         DFS_STAT(n_hbm += (uint32_t)lcount - (uint32_t)er);
@@ -1788,7 +1779,7 @@ insert:
             } else {
                 // both buckets full: HBM, and theta rises above the layer
                 if constexpr (BLK) {
-                    blks = blk_add_one<M>(memo, blks, ((uint64_t)khi << 32) | klo, lane == i, bloom, lk_bl(h1), lk_bl(h2), lane);
+                    blk_add_one<M>(memo, blks, ((uint64_t)khi << 32) | klo, lane == i, bloom, lk_bl(h1), lk_bl(h2), lane);
                 } else {
                     const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
                     if (lane == i) {
@@ -1802,7 +1793,7 @@ insert:
                 DFS_STAT(n_hbm++);
             }
             if constexpr (BLK) {
-                if (blks.ovf) {
+                if (rflu(blks->ovf)) {
                     // more blocks than BLK_MAX (only with a quick budget over 32 K
                     // inserts): the memo is incomplete, so the key goes to the
                     // heavy-key pass, which restarts it
@@ -2413,6 +2404,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         }
         if (A.t_span && !spanned && lane == 0) atomicMin(&A.t_span[0], __builtin_amdgcn_s_memrealtime());
         spanned = true;
+        if (A.tl && lane == 0) A.tl[TL_W * (size_t)key + 2] = __builtin_amdgcn_s_memrealtime();
         const KeyMeta mt = A.meta[key];
         KeyInfo K;
         K.n_ops = mt.n_ops; K.n_ok = mt.n_ok; K.sumW = 0;
@@ -2434,7 +2426,11 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         else if constexpr (WL) verdict = dfs_lean_w<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         if (A.dbg && lane == 0) { A.dbg[16 * wv + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * wv + 3] += 1; }
-        if (verdict == JH_CANCELLED) { p1_key_done(); continue; }
+        if (verdict == JH_CANCELLED) {
+            if (A.tl && lane == 0) A.tl[TL_W * (size_t)key + 3] = __builtin_amdgcn_s_memrealtime();
+            p1_key_done();
+            continue;
+        }
         if (verdict == JH_UNKNOWN && A.defer && inserts >= A.budget &&
             (A.budget_full == 0 || inserts < A.budget_full)) {
             if (lane == 0) {
@@ -2466,6 +2462,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         // an invalid key's failing row is resolved by k_fail_rows from tmax
         if (verdict == JH_INVALID) v.fail_entry = -(int64_t)tmax - 2;
         if (lane == 0) emit_verdict(A.out, A.claim, key, v);
+        if (A.tl && lane == 0) A.tl[TL_W * (size_t)key + 3] = __builtin_amdgcn_s_memrealtime();
         p1_key_done();
     }
     if (A.dbg && lane == 0) A.dbg[16 * wv + 9] = __builtin_amdgcn_s_memtime() - t_begin;
@@ -2502,9 +2499,17 @@ __global__ void __launch_bounds__(256) k_list_cost(const int32_t *__restrict__ l
 // phase 1: every key under the quick budget
 // (five waves per SIMD: phase 1's 20 resident waves per CU; the block memo's
 // out-of-line calls would otherwise take the register allocation past it)
+#ifndef JH_P1_BLK
+#define JH_P1_BLK 1
+#endif
+#ifdef JH_P1_WPE
+#define JH_P1_ATTR __attribute__((amdgpu_waves_per_eu(JH_P1_WPE)))
+#else
+#define JH_P1_ATTR
+#endif
 template <bool LEAN>
-__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
-    lin_dfs_waves<MemoQ, LEAN, false, LEAN>(A);
+__global__ void __launch_bounds__(64) JH_P1_ATTR k_lin_dfs(DfsArgs A) {
+    lin_dfs_waves<MemoQ, LEAN, false, LEAN && JH_P1_BLK>(A);
 }
 // heavy keys: the full-budget sequential search racing k_lin_bfs, one wave
 // per CU with a 128 KB LDS memo
@@ -3580,8 +3585,10 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
             long long inserts = 0;
             uint32_t tmax = 0;
             const unsigned long long ck0 = __builtin_amdgcn_s_memtime();
+            if (A.tl && lane == 0) A.tl[TL_W * (size_t)key + 4] = __builtin_amdgcn_s_memrealtime();
             const int verdict = dfs_acc<MemoW>(W, sh, K, A.tables + mt.off, key, lane, memo, stack, stage, gset,
                                                work, wtab, pend, inserts, tmax, my_probes);
+            if (A.tl && lane == 0) A.tl[TL_W * (size_t)key + 5] = __builtin_amdgcn_s_memrealtime();
             jh_key_verdict v;
             v.valid = verdict;
             v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
@@ -3734,6 +3741,7 @@ struct BfsArgs {
     const int32_t *live_n;
     const int32_t *p1_done, *p1_tot;
     unsigned long long *t_span;
+    unsigned long long *tl;     // -DJH_TUNING timeline: per key [0] BFS start, [1] end
 };
 
 struct BfsShared {
@@ -4339,6 +4347,30 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
 // is not vendored, so this order and cut are this library's (oracle:
 // orc_lin_configs).
 constexpr int CFG_MAX = 16;
+constexpr int CFG_ROWS = JH_MAX_WINDOW;     // row slots per configuration (the widest window)
+// A configuration's register value from its interned state id (one wave):
+// 0 is nil; one global range: vmin + id - 1; per-key ids (k_iassign): 1 the
+// initial value, the others the raw value of a record of the key carrying it
+__device__ long long cfg_state_value(uint32_t st, int per_key_values, long long vmin, long long init_value,
+                                     const KeySrc &S, uint32_t s0, uint32_t s1, const int64_t *col_val,
+                                     const int64_t *col_val2, int lane) {
+    if (st == 0) return JH_NIL;
+    if (!per_key_values) return vmin + (long long)st - 1;
+    if (st == 1 && init_value != JH_NIL) return init_value;
+    for (uint32_t base = s0; base < s1; base += 64) {
+        const uint32_t p = base + lane;
+        long long v = JH_NIL;
+        if (p < s1) {
+            const Rec x = S.rec[p];
+            const long long row = (long long)S.rows[p];
+            if (x.proc >= 0 && x.v1 == (int32_t)st) v = col_val[row];
+            else if (x.proc >= 0 && x.f == F_CAS && x.v2 == (int32_t)st) v = col_val2[row];
+        }
+        const uint64_t hit = ballot(v != JH_NIL);
+        if (hit) return (long long)readlane64((uint64_t)v, __builtin_ctzll(hit));
+    }
+    return JH_NIL;
+}
 __device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int key, const int32_t *woff,
                                  const uint16_t *W, uint32_t n_ok) {
     const int slot = A.cfg_slot[key];
@@ -4381,29 +4413,9 @@ __device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int k
     wave_sync();
     for (int i = 0; i < nsel; i++) {
         const uint32_t st = (uint32_t)(sel[i] >> 32) & 0xFFF, mask = (uint32_t)sel[i];
-        long long val = JH_NIL;
-        if (st != 0) {
-            if (!A.per_key_values) val = A.vmin + (long long)st - 1;
-            else if (st == 1 && A.init_value != JH_NIL) val = A.init_value;
-            else {
-                // per-key ids: the raw value of a record of this key carrying the id
-                long long got = JH_NIL;
-                for (uint32_t base = sh.K.s0; base < sh.K.s1; base += 64) {
-                    const uint32_t p = base + lane;
-                    long long v = JH_NIL;
-                    if (p < sh.K.s1) {
-                        const Rec x = A.src.rec[p];
-                        const long long row = (long long)A.src.rows[p];
-                        if (x.proc >= 0 && x.v1 == (int32_t)st) v = A.col_val[row];
-                        else if (x.proc >= 0 && x.f == F_CAS && x.v2 == (int32_t)st) v = A.col_val2[row];
-                    }
-                    const uint64_t hit = ballot(v != JH_NIL);
-                    if (hit) { got = readlane64((uint64_t)v, __builtin_ctzll(hit)); break; }
-                }
-                val = got;
-            }
-        }
-        const int64_t o = ((int64_t)slot * A.cfg_per + i) * 64;
+        const long long val = cfg_state_value(st, A.per_key_values, A.vmin, A.init_value, A.src, sh.K.s0, sh.K.s1,
+                                              A.col_val, A.col_val2, lane);
+        const int64_t o = ((int64_t)slot * A.cfg_per + i) * CFG_ROWS;
         const bool in = lane < w, lin = in && ((mask >> lane) & 1);
         const uint64_t bl = ballot(lin), bp = ballot(in && !lin);
         const int nl = __popcll(bl);
@@ -4869,6 +4881,7 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A0) {
         if (key < 0) break;
         if (A.t_span && !spanned && tid == 0) atomicMin(&A.t_span[0], __builtin_amdgcn_s_memrealtime());
         spanned = true;
+        if (A.tl && tid == 0) A.tl[TL_W * (size_t)key] = __builtin_amdgcn_s_memrealtime();
         if (wid == 0) {
             KeyInfo K;
             jh_key_verdict v;
@@ -4888,6 +4901,7 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A0) {
             if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
             __syncthreads();
         }
+        if (A.tl && tid == 0) A.tl[TL_W * (size_t)key + 1] = __builtin_amdgcn_s_memrealtime();
     }
     if (A.t_span && tid == 0) atomicMax(&A.t_span[1], __builtin_amdgcn_s_memrealtime());
 }
@@ -4941,6 +4955,16 @@ struct XwArgs {
     unsigned long long *probes;
     int32_t cause_or;           // :linear mode: CAUSE_BY_WGL on the verdicts (k_frontier)
     unsigned long long *t_span; // [first key taken, last wave end] (s_memrealtime), or null
+    // jh_lin_configs for the keys the reachable-set engine cannot hold: the
+    // frontier of each requested invalid key, from this search's table
+    const int32_t *cfg_slot;
+    jh_lin_config *cfg_out;
+    int32_t *cfg_n;
+    int64_t *cfg_rows;
+    int32_t cfg_per;
+    const int64_t *col_val, *col_val2;
+    int64_t vmin, init_value;
+    int32_t per_key_values;
 };
 
 struct XwTbl {
@@ -5091,6 +5115,99 @@ __device__ __forceinline__ void xw_store(uint64_t *memo, uint32_t slot, uint32_t
         __hip_atomic_store(&e[w], m[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __hip_atomic_store(&e[4], ((uint64_t)gen << 40) | ((uint64_t)t << 20) | s, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// jh_lin_configs beyond the reachable-set engine (windows over 32 members,
+// >= 4096 states): for an invalid key this search's table holds every
+// configuration it reached (WGL's cache is the whole reachable set), so the
+// frontier is the table's entries of the key's generation at layer tmax (and
+// the root when tmax is 0, which is never inserted). The first cfg_per of them
+// in the canonical order -- state id (= register value order), then the
+// window mask as a 256-bit number -- by repeated wave minima, each written as
+// bfs_dump_configs writes its own: value, then the invocation rows of the
+// linearized and the pending members of W(tmax) in call order.
+struct Cfg5 { uint32_t s; uint64_t m3, m2, m1, m0; };
+__device__ __forceinline__ bool cfg_less(const Cfg5 &a, const Cfg5 &b) {
+    if (a.s != b.s) return a.s < b.s;
+    if (a.m3 != b.m3) return a.m3 < b.m3;
+    if (a.m2 != b.m2) return a.m2 < b.m2;
+    if (a.m1 != b.m1) return a.m1 < b.m1;
+    return a.m0 < b.m0;
+}
+__device__ void xw_dump_configs(const XwArgs &A, const uint64_t *memo, uint32_t gen, uint32_t tmax, int key,
+                                const XwTbl &T, int lane) {
+    const int slot = A.cfg_slot[key];
+    if (slot < 0) return;
+    const uint32_t s0 = A.src.off[key], s1 = A.src.off[key + 1];
+    const int wo = T.woff[tmax], w = T.woff[tmax + 1] - wo;
+    // the invocation row of every member of W(tmax): member 64 c + lane in wrow[c]
+    long long wrow[XW_SL];
+#pragma unroll
+    for (int c = 0; c < XW_SL; c++) {
+        wrow[c] = -1;
+        const int j = 64 * c + lane;
+        if (j < w) {
+            const int32_t id = (int32_t)T.W[wo + j];
+            for (uint32_t p = s0; p < s1; p++)
+                if (A.src.rank[p] == id) { wrow[c] = (long long)A.src.rows[p]; break; }
+        }
+    }
+    const int per = min(A.cfg_per, CFG_MAX);
+    Cfg5 prev{0, 0, 0, 0, 0};
+    int n = 0;
+    for (int i = 0; i < per; i++) {
+        Cfg5 best{0xFFFFFFFFu, ~0ULL, ~0ULL, ~0ULL, ~0ULL};
+        bool have = false;
+        auto offer = [&](const Cfg5 &c) {
+            if ((i == 0 || cfg_less(prev, c)) && (!have || cfg_less(c, best))) { best = c; have = true; }
+        };
+        if (tmax == 0 && lane == 0) offer(Cfg5{(uint32_t)A.init_state, 0, 0, 0, 0});
+        for (uint32_t j = (uint32_t)lane; j < A.memo_cap; j += 64) {
+            const uint64_t *e = memo + (size_t)j * XW_EW;
+            const uint64_t e4 = e[4];
+            if ((uint32_t)(e4 >> 40) != gen || ((uint32_t)(e4 >> 20) & T_MASK) != tmax) continue;
+            offer(Cfg5{(uint32_t)e4 & STATE_MASK, e[3], e[2], e[1], e[0]});
+        }
+        // wave minimum of the lanes' best
+        for (int o = 32; o > 0; o >>= 1) {
+            Cfg5 x;
+            x.s = (uint32_t)__shfl_xor((int)best.s, o);
+            x.m3 = (uint64_t)__shfl_xor((long long)best.m3, o); x.m2 = (uint64_t)__shfl_xor((long long)best.m2, o);
+            x.m1 = (uint64_t)__shfl_xor((long long)best.m1, o); x.m0 = (uint64_t)__shfl_xor((long long)best.m0, o);
+            const bool xh = __shfl_xor((int)have, o) != 0;
+            if (xh && (!have || cfg_less(x, best))) { best = x; have = true; }
+        }
+        if (!have) break;
+        prev = best;
+        n = i + 1;
+        const long long val = cfg_state_value(best.s, A.per_key_values, A.vmin, A.init_value, A.src, s0, s1,
+                                              A.col_val, A.col_val2, lane);
+        const int64_t o = ((int64_t)slot * A.cfg_per + i) * CFG_ROWS;
+        const uint64_t mw[XW_SL] = {best.m0, best.m1, best.m2, best.m3};
+        int nl = 0, np = 0;
+#pragma unroll
+        for (int c = 0; c < XW_SL; c++) nl += __popcll(ballot(64 * c + lane < w && ((mw[c] >> lane) & 1)));
+#pragma unroll
+        for (int c = 0; c < XW_SL; c++) {
+            const bool in = 64 * c + lane < w, lin = in && ((mw[c] >> lane) & 1);
+            const uint64_t bl = ballot(lin), bp = ballot(in && !lin);
+            int lo = 0, po = 0;
+            for (int c2 = 0; c2 < c; c2++) {
+                const bool in2 = 64 * c2 + lane < w, lin2 = in2 && ((mw[c2] >> lane) & 1);
+                lo += __popcll(ballot(lin2));
+                po += __popcll(ballot(in2 && !lin2));
+            }
+            if (lin) A.cfg_rows[o + lo + mbcnt(bl)] = wrow[c];
+            if (in && !lin) A.cfg_rows[o + nl + po + mbcnt(bp)] = wrow[c];
+            np += __popcll(bp);
+        }
+        if (lane == 0) {
+            jh_lin_config cf;
+            cf.key = key; cf.model_value = val; cf.n_linearized = nl; cf.n_pending = np; cf.rows_off = o;
+            A.cfg_out[(int64_t)slot * A.cfg_per + i] = cf;
+        }
+    }
+    if (lane == 0) A.cfg_n[slot] = n;
 }
 
 // one wave of the 65-256-member search: wave wv's tables, nm_sh / ring in LDS
@@ -5310,6 +5427,10 @@ __device__ __forceinline__ void xw_waves(const XwArgs &A, size_t wv, unsigned lo
         v.explored = ins;
         v.fail_entry = verdict == JH_INVALID ? -(int64_t)tmax - 2 : -1;
         if (lane == 0) A.out[key] = v;
+        if (A.cfg_slot && verdict == JH_INVALID) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            xw_dump_configs(A, memo, gen, tmax, key, T, lane);
+        }
     }
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
@@ -5606,6 +5727,17 @@ __global__ void k_mark_deferred(const uint64_t *__restrict__ d64, int n, jh_key_
     }
 }
 
+// jh_lin_configs: the k_lin_xw table bytes of the keys the reachable-set
+// engine gave up (their configurations come from that search)
+__global__ void k_xw_need(const int32_t *__restrict__ list, const int32_t *n, const KeyMeta *__restrict__ meta,
+                          unsigned long long *need) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < *n) {
+        const KeyMeta m = meta[list[i]];
+        atomicMax(need, (unsigned long long)xw_bytes(m.n_ops, m.n_ok, (long long)(uint32_t)m.pad));
+    }
+}
+
 // jh_lin_configs: the requested keys are the whole heavy list, all LEAN
 __global__ void k_req_lists(const int64_t *__restrict__ keys, int n, int64_t K, int32_t *defer, int32_t *defer_l,
                             int32_t *q) {
@@ -5742,7 +5874,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     int64_t quick = std::min<int64_t>(budget, QUICK_BUDGET);
     if (opts && opts->quick_budget > 0)
         quick = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(budget, memo_cap1 / 2), opts->quick_budget));
-    int p1_per_cu = 163840 / MemoQ::LDS;
+    int p1_per_cu = 163840 / (MemoQ::LDS + BLK_LDS);
     if (opts && opts->p1_waves_per_cu > 0) p1_per_cu = std::min(p1_per_cu, (int)opts->p1_waves_per_cu);
     const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * p1_per_cu);
     uint64_t *memo = ctx->ws<uint64_t>(WS_MEMO, (size_t)waves1 * memo_cap1 * 2, /*zero=*/true);
@@ -6126,7 +6258,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         b.defer_time = nullptr;
     };
     // the streaming heavy-key pass (round 4) whenever the default race runs
-    const bool stream_p2 = !linear_mode && !skip_p1 && !p1_only && !use_wg && !wg_race && !dbg2 && !defer_times &&
+    const bool stream_p2 = !linear_mode && !skip_p1 && !p1_only && !use_wg && !wg_race && !dbg2 &&
                            !(lflags & (JH_LIN_NO_STREAM | JH_LIN_BFS_ONLY));
     if (stream_p2) {
         // ---- the streaming heavy-key pass (round 4) --------------------------
@@ -6177,6 +6309,13 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             if (const char *e = tune_env("JH_EARLY_LEAN")) w_early = std::min(waves2, std::max(0, atoi(e)));
             const int32_t sw = waves2;
             HIP_TRY(hipMemcpyAsync(q + Q_SEQ_WAVES, &sw, sizeof sw, hipMemcpyHostToDevice, st));
+            if (defer_times) {
+                // tuning builds: per key [BFS start, BFS end, sequential start, end]
+                unsigned long long *tl = ctx->ws<unsigned long long>(WS_TL, TL_W * (size_t)K);
+                HIP_TRY(hipMemsetAsync(tl, 0, TL_W * sizeof(unsigned long long) * K, st));
+                c.tl = tl; b.tl = tl;
+                if (n_help > 0) wh.d.tl = tl;
+            }
         }
         // phase-1 producer side: live lists, finished-key count, drain flag
         if (!ctx->hflag) {
@@ -6197,7 +6336,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         a.t_span = (unsigned long long *)(q + Q_T_P1);
         HIP_TRY(hipEventRecord(ctx->ev[6], st));     // fork: tables, lists and counters are ready
         HIP_TRY(hipEventRecord(ctx->ev[1], st));
-        k_lin_dfs<true><<<waves1, 64, MemoQ::LDS, st>>>(a);
+        k_lin_dfs<true><<<waves1, 64, MemoQ::LDS + BLK_LDS, st>>>(a);
         HIP_TRY(hipGetLastError());
         k_lin_dfs<false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
         HIP_TRY(hipGetLastError());
@@ -6296,7 +6435,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     } else {
         HIP_TRY(hipEventRecord(ctx->ev[1], st));
         if (!linear_mode && !skip_p1) {
-            k_lin_dfs<true><<<waves1, 64, MemoQ::LDS, st>>>(a);
+            k_lin_dfs<true><<<waves1, 64, MemoQ::LDS + BLK_LDS, st>>>(a);
             HIP_TRY(hipGetLastError());
             DfsArgs aw = a;
             aw.list = list_w; aw.n_list_dev = q + 13; aw.queue = q + 14;
@@ -6474,6 +6613,30 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 fw.queue = q + 7;
                 k_lin_seqw<<<waves2, 64, SEQW_LDS, st>>>(fw);
                 HIP_TRY(hipGetLastError());
+            } else {
+                // configurations of the requested keys the reachable-set
+                // engine cannot hold (windows over 32 members, >= 4096 states):
+                // the 65-256-member search (4-word masks, every configuration
+                // in its table, any window up to JH_MAX_WINDOW) and the
+                // frontier from its table (xw_dump_configs)
+                HIP_TRY(hipMemsetAsync(q + 26, 0, 2 * sizeof(int32_t), st));
+                k_xw_need<<<grid_for(n_defer, 256), 256, 0, st>>>(c.unres_list, q + 3, meta,
+                                                                 (unsigned long long *)(q + 26));
+                int32_t qx[Q_WORDS];
+                HIP_TRY(hipMemcpyAsync(qx, q, sizeof qx, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                n_x = qx[3];
+                if (n_x > 0) {
+                    prep_xw(qx);
+                    xa.list = c.unres_list; xa.n_list = n_x; xa.t_span = nullptr;
+                    xa.cfg_slot = cfgreq->slot_dev; xa.cfg_out = cfgreq->out_dev; xa.cfg_n = cfgreq->n_dev;
+                    xa.cfg_rows = cfgreq->rows_dev; xa.cfg_per = cfgreq->per_key;
+                    xa.col_val = dh->value; xa.col_val2 = dh->value2;
+                    xa.vmin = vmin; xa.init_value = init; xa.per_key_values = per_key_values ? 1 : 0;
+                    k_lin_xw<<<waves_x, 64, 0, st>>>(xa);
+                    HIP_TRY(hipGetLastError());
+                }
+                n_x = 0;
             }
             HIP_TRY(hipEventRecord(ctx->ev[10], st));
             HIP_TRY(hipEventRecord(ctx->ev[7], st));
@@ -6620,6 +6783,11 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // first wave), when phase 1 ended, when the sequential search took the
         // key (if helpers ran), and the key's final insert count
         HIP_TRY(hipStreamSynchronize(st));
+        if (stream_p2) {
+            int32_t nd = 0;
+            HIP_TRY(hipMemcpy(&nd, q + 1, sizeof nd, hipMemcpyDeviceToHost));
+            n_defer = nd;
+        }
         std::vector<unsigned long long> dt((size_t)K + 2);
         HIP_TRY(hipMemcpy(dt.data(), a.defer_time, dt.size() * 8, hipMemcpyDeviceToHost));
         std::vector<int32_t> dk(n_defer);
@@ -6637,12 +6805,40 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         std::vector<std::pair<long long, int>> heavy;
         for (int d = 0; d < n_defer; d++) heavy.push_back({vv[dk[d]].explored, dk[d]});
         std::sort(heavy.rbegin(), heavy.rend());
+        std::vector<unsigned long long> tl;
+        if (stream_p2 && ctx->bufs.size() > WS_TL && ctx->bufs[WS_TL].p) {
+            tl.resize(TL_W * (size_t)K);
+            HIP_TRY(hipMemcpy(tl.data(), ctx->bufs[WS_TL].p, 8 * tl.size(), hipMemcpyDeviceToHost));
+        }
+        auto us = [&](unsigned long long t) { return t ? (double)(t - dt[0]) / 100.0 : -1.0; };
         for (int i = 0; i < std::min(n_defer, 12); i++) {
             const int k = heavy[i].second;
             double st_us = -1;
             if (!ss.empty() && ss[k] && ss[k] != SEQ_HANDED) st_us = ((ss[k] & ~1ULL) - dt[0]) / 100.0;
-            fprintf(stderr, "[jh-defer] key %d explored %lld valid %d deferred %.1f us seq-start %.1f us\n", k,
+            fprintf(stderr, "[jh-defer] key %d explored %lld valid %d deferred %.1f us seq-start %.1f us", k,
                     heavy[i].first, vv[k].valid, (dt[2 + k] - dt[0]) / 100.0, st_us);
+            if (!tl.empty())
+                fprintf(stderr, " | bfs %.1f-%.1f us seq %.1f-%.1f us", us(tl[TL_W * k]), us(tl[TL_W * k + 1]),
+                        us(tl[TL_W * k + 2]), us(tl[TL_W * k + 3]));
+            fprintf(stderr, "\n");
+        }
+        if (!tl.empty()) {
+            // the keys that ended last (the step's critical path)
+            std::vector<std::pair<unsigned long long, int>> last;
+            for (int d = 0; d < n_defer; d++) {
+                const int k = dk[d];
+                unsigned long long e = 0;
+                for (int w = 1; w < TL_W; w += 2) e = std::max(e, tl[TL_W * k + w]);
+                last.push_back({e, k});
+            }
+            std::sort(last.rbegin(), last.rend());
+            for (int i = 0; i < std::min(n_defer, 8); i++) {
+                const int k = last[i].second;
+                fprintf(stderr, "[jh-last] key %d explored %lld valid %d deferred %.1f | bfs %.1f-%.1f seq %.1f-%.1f help %.1f-%.1f us\n",
+                        k, (long long)vv[k].explored, vv[k].valid, (dt[2 + k] - dt[0]) / 100.0, us(tl[TL_W * k]),
+                        us(tl[TL_W * k + 1]), us(tl[TL_W * k + 2]), us(tl[TL_W * k + 3]), us(tl[TL_W * k + 4]),
+                        us(tl[TL_W * k + 5]));
+            }
         }
         int q5[5] = {0, 0, 0, 0, 0};
         for (auto &e2 : ev) q5[std::min(4, (int)(e2.first / (std::max(1.0, (dt[1] - dt[0]) / 100.0) / 5)))]++;

@@ -61,13 +61,11 @@ def render_analysis(cols, result, path):
     :final-paths (checker.add_configs). Returns the path written."""
     op = result.get("op")
     configs = result.get("configs") or []
-    lin_all = None
+    lin_all = {int(c["last-op"]["index"]) for c in configs if c.get("last-op")}
     pend = set()
     for c in configs:
-        lin = {o["index"] for o in c["linearized"]}
-        lin_all = lin if lin_all is None else lin_all & lin
         pend |= {o["index"] for o in c["pending"]}
-    lin_all = lin_all or set()
+    lin_all -= pend
     rows = {}
     for r in sorted(lin_all | pend):
         rows[_span(cols, r)] = "#8c8" if r in lin_all else "#bbb"

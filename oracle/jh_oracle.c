@@ -427,19 +427,30 @@ static int linear_domain(const orc_key *k) {
     return k->max_window <= 32 && orc_linear_states_ok && k->n_ok < (1 << 20) - 2;
 }
 
-typedef struct { int64_t bucket, v; uint64_t m; } cfg_ord;
+/* the frontier's order: value bucket (nil, then with per-key value
+ * numbering the initial value, then the rest), value, then the window mask
+ * as a JH_MAX_WINDOW-bit number (high word first) */
+typedef struct { int64_t bucket, v; uint64_t m[MW]; } cfg_ord;
 static int cmp_cfg_ord(const void *a, const void *b) {
     const cfg_ord *x = (const cfg_ord *)a, *y = (const cfg_ord *)b;
     if (x->bucket != y->bucket) return x->bucket < y->bucket ? -1 : 1;
     if (x->v != y->v) return x->v < y->v ? -1 : 1;
-    return x->m < y->m ? -1 : x->m > y->m;
+    for (int w = MW - 1; w >= 0; w--)
+        if (x->m[w] != y->m[w]) return x->m[w] < y->m[w] ? -1 : 1;
+    return 0;
+}
+/* :configs are defined wherever the reachable set can be enumerated: any
+ * window up to JH_MAX_WINDOW (libjh: the reachable-set engine up to 32
+ * members, the 65-256-member search's table beyond) */
+static int configs_domain(const orc_key *k) {
+    return !k->status && k->max_window <= JH_MAX_WINDOW && k->n_ok < (1 << 20) - 2;
 }
 static int configs_one(const jh_history *h, const int64_t *sel, int64_t m, int64_t init, int64_t budget,
                        int per_key, int per_key_values, jh_lin_config *out, int64_t *rows) {
     orc_key k;
     orc_key_prepare(h, sel, m, &k);
     int n = -1;
-    if (!k.status && linear_domain(&k)) {
+    if (configs_domain(&k)) {
         cvec front = {0, 0, 0};
         int64_t explored; uint32_t tmax;
         if (orc_linear(&k, init, budget, &explored, &tmax, &front) == JH_INVALID) {
@@ -447,7 +458,7 @@ static int configs_one(const jh_history *h, const int64_t *sel, int64_t m, int64
             for (int64_t i = 0; i < front.n; i++) {
                 const int64_t v = front.e[i].s;
                 o[i].bucket = v == JH_NIL ? 0 : (per_key_values && init != JH_NIL && v == init) ? 1 : 2;
-                o[i].v = v; o[i].m = front.e[i].m[0];
+                o[i].v = v; memcpy(o[i].m, front.e[i].m, sizeof o[i].m);
             }
             qsort(o, front.n, sizeof(cfg_ord), cmp_cfg_ord);
             n = (int)(front.n < per_key ? front.n : per_key);
@@ -456,10 +467,10 @@ static int configs_one(const jh_history *h, const int64_t *sel, int64_t m, int64
             for (int i = 0; i < n; i++) {
                 jh_lin_config *c = &out[i];
                 c->key = 0; c->model_value = o[i].v; c->n_linearized = 0; c->n_pending = 0;
-                c->rows_off = (int64_t)i * 64;
-                int64_t *r = rows + (int64_t)i * 64;
-                for (int j = 0; j < w; j++) if ((o[i].m >> j) & 1) r[c->n_linearized++] = k.ops[W[j]].call;
-                for (int j = 0; j < w; j++) if (!((o[i].m >> j) & 1)) r[c->n_linearized + c->n_pending++] = k.ops[W[j]].call;
+                c->rows_off = (int64_t)i * JH_MAX_WINDOW;
+                int64_t *r = rows + (int64_t)i * JH_MAX_WINDOW;
+                for (int j = 0; j < w; j++) if (bit_get(o[i].m, j)) r[c->n_linearized++] = k.ops[W[j]].call;
+                for (int j = 0; j < w; j++) if (!bit_get(o[i].m, j)) r[c->n_linearized + c->n_pending++] = k.ops[W[j]].call;
             }
             free(o);
         }
@@ -480,10 +491,10 @@ int orc_lin_configs(const jh_history *h, int64_t init, int64_t budget, const int
             if (kk == keys[q] || kk < 0) sel[m++] = r;
         }
         n_out[q] = configs_one(h, sel, m, init, budget, per_key, per_key_values, out + q * per_key,
-                               rows + q * per_key * 64);
+                               rows + q * per_key * JH_MAX_WINDOW);
         for (int i = 0; i < per_key; i++) {
             out[q * per_key + i].key = keys[q];
-            out[q * per_key + i].rows_off += q * per_key * 64;
+            out[q * per_key + i].rows_off += q * per_key * JH_MAX_WINDOW;
         }
     }
     free(sel);

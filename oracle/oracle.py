@@ -123,7 +123,7 @@ def lin_configs(cols, keys, per_key=A.CONFIGS_PER_KEY, init=A.NIL, budget=A.DEFA
     nq = len(keys)
     out = (A.JhLinConfig * max(nq * per_key, 1))()
     n_out = np.zeros(max(nq, 1), np.int32)
-    rows = np.zeros(max(nq * per_key * 64, 1), np.int64)
+    rows = np.zeros(max(nq * per_key * A.MAX_WINDOW, 1), np.int64)
     lib().orc_lin_configs(C.byref(h), init, budget, A.ptr64(keys), nq, per_key,
                           1 if per_key_values(cols, init) else 0, out,
                           n_out.ctypes.data_as(C.POINTER(C.c_int32)), A.ptr64(rows))

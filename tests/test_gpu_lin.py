@@ -440,9 +440,11 @@ def test_frontier_configs_host_map(ctx):
     r = checker.Linearizable({"model": model.CASRegister(None)}).check(None, d["history"], {})
     assert r["valid?"] is False and 0 < len(r["configs"]) <= 10 and len(r["final-paths"]) == len(r["configs"])
     for cfg in r["configs"]:
-        assert all(op["type"] == "invoke" for op in cfg["pending"] + cfg["linearized"])
+        assert set(cfg) == {"model", "last-op", "pending"}
+        assert all(op["type"] == "invoke" for op in cfg["pending"])
+        assert cfg["last-op"] is None or cfg["last-op"]["type"] == "invoke"
     for p in r["final-paths"]:
-        assert p[-1]["op"] == r["op"] and p[-1]["model"] == {"inconsistent": "can't read 0 from register "}
+        assert p[-1]["op"] == r["op"] and "inconsistent" in p[-1]["model"]
 
 
 @pytest.mark.parametrize("seed", [3, 3 + 7919 * 3])
@@ -473,3 +475,50 @@ def test_phase1_block_memo(ctx, quick):
     g, gs = ctx.check_cas_independent(cols, quick_budget=quick)
     c, _ = oracle.check_cas_independent(cols, threads=8)
     _same(g, c)
+
+
+def _wide_failure_history(widths):
+    """One key per width P: a read of a never-written value fails at the
+    sixth row (three writes concurrent with it), after which P crashed
+    writes stay open to the end -- the key's widest window is P + 1 members,
+    so the whole key runs in the 33-64 (P < 64) or 65-256-member engine
+    while its frontier is small and exact."""
+    h = []
+    for k, p in enumerate(widths):
+        t = lambda v: H.tuple_(k, v)  # noqa: E731
+        h += [H.invoke_op(0, "write", t(1)), H.ok_op(0, "write", t(1)),
+              H.invoke_op(1, "write", t(2)), H.invoke_op(2, "write", t(3)), H.invoke_op(3, "read", t(None)),
+              H.ok_op(3, "read", t(4)), H.ok_op(1, "write", t(2)), H.ok_op(2, "write", t(3))]
+        h += [H.invoke_op(100 + i, "write", t(1 + i % 3)) for i in range(p)]
+        h += [H.invoke_op(4, "read", t(None)), H.ok_op(4, "read", t(1))]
+        h += [H.info_op(100 + i, "write", t(1 + i % 3)) for i in range(p)]
+    return H.encode(h)
+
+
+def test_frontier_configs_wide_windows(ctx):
+    """:configs beyond the reachable-set engine (round 4, row f1): keys whose
+    windows exceed 32 members take their frontier from the WIDE / 65-256
+    member search's table; the configurations equal the oracle's
+    (orc_linear's frontier, any window) key by key. Two histories: synthetic
+    keys of 40 threads (windows 36-40, invalid deep in the history) and
+    hand-made keys whose windows reach 41, 71, 131 and 251 members."""
+    cols, _ = synth.cas_register(n_keys=48, ops_per_key=40, threads_per_key=40, readers=20, n_values=5,
+                                 process_limit=320, groups=10, init_nil=True, p_info=0.3, p_invalid=0.6,
+                                 nemesis_every=10000, seed=556)
+    budget = 1 << 18
+    c, _ = oracle.check_cas_independent(cols, budget=budget, threads=16)
+    bad = np.nonzero(c["valid"] == A.INVALID)[0]
+    assert len(bad) >= 3
+    g = ctx.lin_configs(cols, bad, budget=budget)
+    o = oracle.lin_configs(cols, bad, budget=budget)
+    assert g == o
+    assert all(g[int(k)] for k in bad)
+
+    cols = _wide_failure_history([40, 70, 130, 250])
+    keys = np.arange(4)
+    c, _ = oracle.check_cas_independent(cols, budget=1 << 16, threads=4)
+    assert (c["valid"] == A.INVALID).all()
+    g = ctx.lin_configs(cols, keys, budget=1 << 16)
+    o = oracle.lin_configs(cols, keys, budget=1 << 16)
+    assert g == o
+    assert all(len(g[k]) == 5 for k in range(4))

@@ -160,9 +160,20 @@ def test_final_paths_end_inconsistent(built):
                              r["previous_ok"], r["last_op"], r["analyzer"])
     checker.add_configs(out, oracle.lin_configs(cols, [0], init=A.NIL)[0], cols, M.CASRegister(None))
     assert 0 < len(out["final-paths"]) == len(out["configs"]) <= 10
-    for p in out["final-paths"]:
-        assert p[0]["op"] is None and p[-1]["op"] == out["op"]
-        assert p[-1]["model"] == {"inconsistent": "can't read 0 from register "}
+    for cfg, p in zip(out["configs"], out["final-paths"]):
+        # knossos' Config record [K]: model, last-op, pending
+        assert set(cfg) == {"model", "last-op", "pending"}
+        assert all(op["type"] == "invoke" for op in cfg["pending"])
+        assert [o["index"] for o in cfg["pending"]] == sorted(o["index"] for o in cfg["pending"])
+        # from the configuration through consistent pending steps to the failing op
+        assert p[0]["op"] == cfg["last-op"] and p[0]["model"] == cfg["model"] and p[-1]["op"] == out["op"]
+        m = M.CASRegister(cfg["model"]["value"])
+        for st in p[1:-1]:
+            assert st["op"] in cfg["pending"]
+            m = m.step(st["op"])
+            assert not M.is_inconsistent(m) and st["model"] == {"value": m.value}
+        assert M.is_inconsistent(m.step(out["op"]))
+        assert p[-1]["model"] == {"inconsistent": m.step(out["op"]).msg}
     assert M.CASRegister(1).step({"f": "cas", "value": [2, None]}).msg == "can't CAS 1 from 2 to "
 
 

@@ -137,9 +137,11 @@ typedef struct jh_history {
 /* Phase 1 keeps every key it started until the quick budget (no hand-over of
  * long searches to the heavy-key pass once its queue is empty). */
 #define JH_LIN_NO_HANDOVER   128
-/* The heavy-key pass starts after phase 1 has ended (the round-3 schedule)
- * instead of consuming phase 1's deferrals as they are made. Same verdicts. */
-#define JH_LIN_NO_STREAM     256
+/* The streaming heavy-key pass: its engines consume phase 1's deferrals as
+ * they are made instead of starting after phase 1. Same verdicts; measured
+ * slower on C3 (the heavy keys' searches share CUs with phase
+ * 1 and start without helpers), so it is off by default. */
+#define JH_LIN_STREAM        256
 
 typedef struct jh_lin_opts {
     int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */
@@ -225,8 +227,8 @@ typedef struct jh_summary {
     int64_t wide_entries;      /* entries of the deferred WIDE keys */
     int64_t xw_entries;        /* entries of the k_lin_xw keys */
     int64_t waves[4];          /* launched waves: phase-2 LEAN, WIDE, phase-3 LEAN, xw */
-    /* ABI 5 (round 4): the streaming heavy-key pass (JH_LIN_NO_STREAM turns it
-     * off). When streamed, seq_ms / bfs_ms / xw_ms are the engines' own spans
+    /* ABI 5 (round 4): the streaming heavy-key pass (JH_LIN_STREAM turns it
+     * on). When streamed, seq_ms / bfs_ms / xw_ms are the engines' own spans
      * (first key taken to last wave end), p3_ms runs from the end of phase 2. */
     int64_t streamed;          /* 1: heavy keys started while phase 1 still ran */
     int64_t p3_entries;        /* entries of the LEAN keys restarted in phase 3 */
@@ -410,6 +412,20 @@ int jh_check_set_full(jh_ctx *ctx, const jh_history *h, const int64_t *time,
                       int32_t linearizable, jh_set_full_result *res,
                       int64_t *lost, int64_t *never_read, int64_t *stale, int64_t list_cap,
                       char *err, size_t errlen);
+
+/* jh_check_set_full with options (zero-initialise; the call above is this
+ * with only `linearizable` set). */
+typedef struct jh_set_full_opts {
+    int32_t linearizable;      /* {:linearizable? true}: stale elements make the result invalid */
+    int32_t pad;
+    int64_t read_batch;        /* :ok reads per bitmap batch, 0 = automatic (<= 2 GiB of bitmap,
+                                  <= 65535 reads); tests use 1 and 3 to cross batch edges */
+    int64_t reserved[4];
+} jh_set_full_opts;
+int jh_check_set_full_opts(jh_ctx *ctx, const jh_history *h, const int64_t *time,
+                           const jh_set_full_opts *opts, jh_set_full_result *res,
+                           int64_t *lost, int64_t *never_read, int64_t *stale, int64_t list_cap,
+                           char *err, size_t errlen);
 
 /* Queues. Values are the :value of :enqueue / :dequeue ops and the elements
  * of :ok :drain ops (integers, or ids the shim interned; JH_NIL = nil).

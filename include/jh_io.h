@@ -46,6 +46,15 @@ extern "C" {
 
 typedef struct jh_ingest jh_ingest;
 
+/* Options of the _opts entry points (zero-initialise; the plain entry points
+ * below are these with only `threads` set). */
+typedef struct jh_ingest_opts {
+    int32_t threads;      /* EDN host threads, 0 = all cores */
+    int32_t debug;        /* nonzero: per-chunk parse timings on stderr */
+    int64_t min_chunk;    /* smallest EDN chunk in bytes, 0 = 1 MiB (tests split small texts) */
+    int64_t reserved[4];
+} jh_ingest_opts;
+
 /* Parses a history file (EDN: `threads` host threads, 0 = all cores, split at
  * line starts and verified; fressian: one pass, its caches are sequential). */
 int jh_ingest_file(const char *path, int format, int independent, int threads,
@@ -53,6 +62,10 @@ int jh_ingest_file(const char *path, int format, int independent, int threads,
 /* The same over bytes in memory (not retained). */
 int jh_ingest_buffer(const char *buf, size_t len, int format, int independent, int threads,
                      jh_ingest **out, char *err, size_t errlen);
+int jh_ingest_file_opts(const char *path, int format, int independent, const jh_ingest_opts *opts,
+                        jh_ingest **out, char *err, size_t errlen);
+int jh_ingest_buffer_opts(const char *buf, size_t len, int format, int independent, const jh_ingest_opts *opts,
+                          jh_ingest **out, char *err, size_t errlen);
 /* Host columns owned by the handle (valid until jh_ingest_free), on_device 0. */
 void jh_ingest_history(const jh_ingest *g, jh_history *h);
 /* The :time column (JH_NIL where absent), for jh_check_set_full. */

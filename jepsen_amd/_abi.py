@@ -59,7 +59,7 @@ ALGORITHMS = {"competition": ALGO_COMPETITION, "wgl": ALGO_WGL, "linear": ALGO_L
 LIN_BFS_ONLY, LIN_GEN_JUMP, LIN_INTERN_PER_KEY, LIN_NO_HELPERS, LIN_HELPERS_NOW = 1, 2, 4, 8, 16
 LIN_PHASE1_ONLY, LIN_SKIP_PHASE1 = 32, 64
 LIN_NO_HANDOVER = 128
-LIN_NO_STREAM = 256
+LIN_STREAM = 256
 CAUSE_DEFERRED = 9
 
 
@@ -142,6 +142,17 @@ class JhSetFullResult(C.Structure):
                 ("n_worst", C.c_int64), ("worst_stale", JhSetFullElem * SF_WORST),
                 ("n_reads", C.c_int64), ("read_elements", C.c_int64),
                 ("device_ms", C.c_double)]
+
+
+class JhSetFullOpts(C.Structure):
+    _fields_ = [("linearizable", C.c_int32), ("pad", C.c_int32), ("read_batch", C.c_int64),
+                ("reserved", C.c_int64 * 4)]
+
+
+class JhIngestOpts(C.Structure):
+    """include/jh_io.h jh_ingest_opts."""
+    _fields_ = [("threads", C.c_int32), ("debug", C.c_int32), ("min_chunk", C.c_int64),
+                ("reserved", C.c_int64 * 4)]
 
 
 class JhQueueResult(C.Structure):

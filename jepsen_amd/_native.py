@@ -61,6 +61,9 @@ def lib():
                                                C.c_int64, p64, p64, C.c_char_p, C.c_size_t]
             L.jh_check_set_full.argtypes = [C.c_void_p, H, p64, C.c_int32, C.POINTER(A.JhSetFullResult),
                                             p64, p64, p64, C.c_int64, C.c_char_p, C.c_size_t]
+            L.jh_check_set_full_opts.argtypes = [C.c_void_p, H, p64, C.POINTER(A.JhSetFullOpts),
+                                                 C.POINTER(A.JhSetFullResult), p64, p64, p64, C.c_int64,
+                                                 C.c_char_p, C.c_size_t]
             L.jh_check_total_queue.argtypes = [C.c_void_p, H, C.POINTER(A.JhQueueResult), p64, p64, p64, p64,
                                                C.c_int64, C.c_char_p, C.c_size_t]
             L.jh_check_queue.argtypes = [C.c_void_p, H, C.POINTER(A.JhQueueResult), p64, C.c_int64,
@@ -72,6 +75,10 @@ def lib():
             L.jh_ingest_file.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, pp, C.c_char_p, C.c_size_t]
             L.jh_ingest_buffer.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.c_int, pp,
                                            C.c_char_p, C.c_size_t]
+            io = C.POINTER(A.JhIngestOpts)
+            L.jh_ingest_file_opts.argtypes = [C.c_char_p, C.c_int, C.c_int, io, pp, C.c_char_p, C.c_size_t]
+            L.jh_ingest_buffer_opts.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, io, pp,
+                                                C.c_char_p, C.c_size_t]
             L.jh_ingest_history.argtypes = [C.c_void_p, H]
             L.jh_ingest_history.restype = None
             L.jh_ingest_time.argtypes = [C.c_void_p]
@@ -92,10 +99,10 @@ def lib():
 EXPORTED_SYMBOLS = ["jh_version", "jh_open", "jh_open_multi", "jh_open_devices", "jh_n_devices", "jh_key_costs", "jh_key_index",
                     "jh_close", "jh_check_cas_independent",
                     "jh_check_cas", "jh_check_cas_independent_device", "jh_lin_configs", "jh_check_counter",
-                    "jh_check_set", "jh_check_set_bitmaps", "jh_check_set_full", "jh_check_total_queue", "jh_check_queue",
+                    "jh_check_set", "jh_check_set_bitmaps", "jh_check_set_full", "jh_check_set_full_opts", "jh_check_total_queue", "jh_check_queue",
                     "jh_host_alloc", "jh_host_free",
                     # include/jh_io.h
-                    "jh_ingest_file", "jh_ingest_buffer", "jh_ingest_history", "jh_ingest_time",
+                    "jh_ingest_file", "jh_ingest_buffer", "jh_ingest_file_opts", "jh_ingest_buffer_opts", "jh_ingest_history", "jh_ingest_time",
                     "jh_ingest_values_interned", "jh_ingest_table_size", "jh_ingest_table_entry", "jh_ingest_free"]
 
 
@@ -350,17 +357,19 @@ class Context:
         out["bits"] = [b[:min(nw.value, cap)] for b in bits]
         return out
 
-    def check_set_full(self, cols, time, linearizable=False, list_cap=None, on_device=False):
+    def check_set_full(self, cols, time, linearizable=False, list_cap=None, on_device=False, read_batch=0):
         """(checker/set-full {:linearizable? linearizable}). `time` is the :time
-        column (numpy int64, or a device pointer when on_device)."""
+        column (numpy int64, or a device pointer when on_device); read_batch > 0
+        caps the :ok reads per bitmap batch (jh_set_full_opts, tests)."""
         h = A.make_history(cols, on_device=on_device)
         cap = int(cols.n) if list_cap is None else list_cap
         lists = [np.zeros(max(cap, 1), np.int64) for _ in range(3)]
         r = A.JhSetFullResult()
         err = C.create_string_buffer(1024)
         tp = C.cast(C.c_void_p(int(time)), C.POINTER(C.c_int64)) if on_device else A.ptr64(time)
-        rc = lib().jh_check_set_full(self._h, C.byref(h), tp, int(bool(linearizable)), C.byref(r),
-                                     *[A.ptr64(x) for x in lists], cap, err, len(err))
+        o = A.JhSetFullOpts(linearizable=int(bool(linearizable)), read_batch=int(read_batch))
+        rc = lib().jh_check_set_full_opts(self._h, C.byref(h), tp, C.byref(o), C.byref(r),
+                                          *[A.ptr64(x) for x in lists], cap, err, len(err))
         _raise(rc, err)
         out = {name: getattr(r, name) for name, _ in A.JhSetFullResult._fields_}
         out["stable_latencies"] = list(r.stable_latencies)

@@ -325,7 +325,17 @@ int jh_host_free(void *p) {
 int jh_check_set_full(jh_ctx *ctx, const jh_history *h, const int64_t *time, int32_t linearizable,
                       jh_set_full_result *res, int64_t *lost, int64_t *never_read, int64_t *stale,
                       int64_t list_cap, char *err, size_t errlen) {
-    if (!ctx || !res) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    jh_set_full_opts o;
+    memset(&o, 0, sizeof o);
+    o.linearizable = linearizable;
+    return jh_check_set_full_opts(ctx, h, time, &o, res, lost, never_read, stale, list_cap, err, errlen);
+}
+
+int jh_check_set_full_opts(jh_ctx *ctx, const jh_history *h, const int64_t *time, const jh_set_full_opts *opts,
+                           jh_set_full_result *res, int64_t *lost, int64_t *never_read, int64_t *stale,
+                           int64_t list_cap, char *err, size_t errlen) {
+    if (!ctx || !res || !opts) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    if (opts->read_batch < 0) { set_err(err, errlen, "read_batch < 0"); return JH_EINVAL; }
     ctx = primary(ctx);
     std::lock_guard<std::mutex> g(ctx->mu);
     return guarded(err, errlen, [&] {
@@ -335,7 +345,8 @@ int jh_check_set_full(jh_ctx *ctx, const jh_history *h, const int64_t *time, int
         jh_history d = stage_history(ctx, h, false, true);
         const int64_t *dt = h->on_device ? time : stage_col(ctx, WS_SF_TIME, time, h->n, ctx->stream);
         int64_t *lists[3] = {lost, never_read, stale};
-        set_full_check(ctx, &d, dt, linearizable != 0, res, lists, list_cap < 0 ? 0 : list_cap, ctx->stream);
+        set_full_check(ctx, &d, dt, opts->linearizable != 0, opts->read_batch, res, lists, list_cap < 0 ? 0 : list_cap,
+                       ctx->stream);
     });
 }
 

@@ -173,7 +173,7 @@ void set_check(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, int64_t *r
 void set_check_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, uint32_t *bits_out[4],
                        int64_t words_cap, int64_t *base, int64_t *n_words, hipStream_t stream);
 // set-full (jh_setfull.hip); lists_out = {lost, never-read, stale}
-void set_full_check(jh_ctx *ctx, const jh_history *dh, const int64_t *time_dev, bool linearizable,
+void set_full_check(jh_ctx *ctx, const jh_history *dh, const int64_t *time_dev, bool linearizable, int64_t read_batch,
                     jh_set_full_result *res, int64_t *lists_out[3], int64_t list_cap, hipStream_t stream);
 // queues (jh_queue.hip); outs = {lost, unexpected, duplicated, recovered}
 void total_queue_check(jh_ctx *ctx, const jh_history *dh, jh_queue_result *res, int64_t *outs[4],

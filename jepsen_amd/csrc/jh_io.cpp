@@ -1321,8 +1321,9 @@ void merge_table(std::vector<Rows> &rs, LocalTable Rows::*tbl, Merge &M, int64_t
     }
 }
 
-int run_chunks(const char *buf, size_t len, int format, bool independent, int threads, bool intern,
+int run_chunks(const char *buf, size_t len, int format, bool independent, const jh_ingest_opts &o, bool intern,
                std::vector<Rows> &rs, IoErr &err) {
+    const int threads = o.threads;
     if (format == JH_FMT_FRESSIAN) {
         rs.assign(1, Rows());
         parse_fressian((const uint8_t *)buf, len, independent, intern, rs[0]);
@@ -1350,9 +1351,8 @@ int run_chunks(const char *buf, size_t len, int format, bool independent, int th
     }
     const size_t n = (size_t)(e - b);
     int T = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
-    // chunks of >= 1 MiB (JH_INGEST_CHUNK: smaller, for the boundary tests)
-    size_t min_chunk = 1 << 20;
-    if (const char *ev = getenv("JH_INGEST_CHUNK")) min_chunk = (size_t)std::max(1L, atol(ev));
+    // chunks of >= 1 MiB (jh_ingest_opts.min_chunk: smaller, for the boundary tests)
+    const size_t min_chunk = o.min_chunk > 0 ? (size_t)o.min_chunk : (size_t)1 << 20;
     T = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, n / min_chunk + 1));
     std::vector<const char *> st(T + 1);
     st[0] = b;
@@ -1370,7 +1370,7 @@ int run_chunks(const char *buf, size_t len, int format, bool independent, int th
             th.emplace_back([&, i]() {
                 auto t0 = std::chrono::steady_clock::now();
                 parse_edn_chunk(buf, st[i], st[i + 1], e, independent, intern, rs[i]);
-                if (getenv("JH_INGEST_DEBUG"))
+                if (o.debug)
                     fprintf(stderr, "[jh-ingest] chunk %d: %zu bytes, %zu rows, %.3f s\n", i, (size_t)(st[i + 1] - st[i]),
                             rs[i].proc.size(), std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
             });
@@ -1388,7 +1388,7 @@ int run_chunks(const char *buf, size_t len, int format, bool independent, int th
             while (q < st[i + 1] && (edn_ws((unsigned char)*q))) q++;
             if (q == st[i + 1] && !rs[i + 1].err.code) continue;
             if (rs[i].err.code) { err = rs[i].err; return err.code; }
-            if (getenv("JH_INGEST_DEBUG"))
+            if (o.debug)
                 fprintf(stderr, "[jh-ingest] chunk %d ends at %zu, chunk %d starts at %zu (err %d: %s): sequential re-parse\n", i,
                         rs[i].end, i + 1, (size_t)(st[i + 1] - buf), rs[i + 1].err.code, rs[i + 1].err.msg.c_str());
             Rows tail;
@@ -1402,8 +1402,8 @@ int run_chunks(const char *buf, size_t len, int format, bool independent, int th
     return JH_OK;
 }
 
-int ingest(const char *buf, size_t len, int format, int independent, int threads, jh_ingest **out, char *err,
-           size_t errlen) {
+int ingest(const char *buf, size_t len, int format, int independent, const jh_ingest_opts &o, jh_ingest **out,
+           char *err, size_t errlen) {
     if (!out) { set_err(err, errlen, "null out"); return JH_EINVAL; }
     *out = nullptr;
     if (format == JH_FMT_AUTO) {
@@ -1415,12 +1415,12 @@ int ingest(const char *buf, size_t len, int format, int independent, int threads
     }
     if (format != JH_FMT_EDN && format != JH_FMT_FRESSIAN) { set_err(err, errlen, "unknown format"); return JH_EINVAL; }
     try {
-        const bool dbg = getenv("JH_INGEST_DEBUG") != nullptr;
+        const bool dbg = o.debug != 0;
         auto now = []() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
         double t0 = now();
         std::vector<Rows> rs;
         IoErr e;
-        int rc = run_chunks(buf, len, format, independent != 0, threads, false, rs, e);
+        int rc = run_chunks(buf, len, format, independent != 0, o, false, rs, e);
         bool ints_only = true;
         int64_t coll_row = -1, rowbase = 0;
         if (rc == JH_OK)
@@ -1429,7 +1429,7 @@ int ingest(const char *buf, size_t len, int format, int independent, int threads
                 if (coll_row < 0 && r.coll_row >= 0) coll_row = rowbase + r.coll_row;
                 rowbase += (int64_t)r.proc.size();
             }
-        if (rc == JH_OK && !ints_only) rc = run_chunks(buf, len, format, independent != 0, threads, true, rs, e);
+        if (rc == JH_OK && !ints_only) rc = run_chunks(buf, len, format, independent != 0, o, true, rs, e);
         if (rc != JH_OK) {
             char m[96];
             snprintf(m, sizeof m, "%s byte %zu: ", format == JH_FMT_EDN ? "EDN" : "fressian", e.at);
@@ -1507,32 +1507,53 @@ int ingest(const char *buf, size_t len, int format, int independent, int threads
     }
 }
 
+jh_ingest_opts plain_opts(int threads) {
+    jh_ingest_opts o;
+    memset(&o, 0, sizeof o);
+    o.threads = threads;
+    return o;
+}
+
 }  // namespace
 
 extern "C" {
 
-int jh_ingest_buffer(const char *buf, size_t len, int format, int independent, int threads, jh_ingest **out,
-                     char *err, size_t errlen) {
+int jh_ingest_buffer_opts(const char *buf, size_t len, int format, int independent, const jh_ingest_opts *opts,
+                          jh_ingest **out, char *err, size_t errlen) {
     if (!buf && len) { set_err(err, errlen, "null buffer"); return JH_EINVAL; }
-    return ingest(buf ? buf : "", len, format, independent, threads, out, err, errlen);
+    const jh_ingest_opts o = opts ? *opts : plain_opts(0);
+    return ingest(buf ? buf : "", len, format, independent, o, out, err, errlen);
 }
 
-int jh_ingest_file(const char *path, int format, int independent, int threads, jh_ingest **out, char *err,
-                   size_t errlen) {
+int jh_ingest_file_opts(const char *path, int format, int independent, const jh_ingest_opts *opts, jh_ingest **out,
+                        char *err, size_t errlen) {
     if (!path) { set_err(err, errlen, "null path"); return JH_EINVAL; }
+    const jh_ingest_opts o = opts ? *opts : plain_opts(0);
     int fd = open(path, O_RDONLY);
     if (fd < 0) { set_err(err, errlen, std::string("cannot open ") + path); return JH_EINVAL; }
     struct stat sb;
     if (fstat(fd, &sb) != 0) { close(fd); set_err(err, errlen, "cannot stat the history file"); return JH_EINVAL; }
     size_t len = (size_t)sb.st_size;
-    if (len == 0) { close(fd); return ingest("", 0, format, independent, threads, out, err, errlen); }
+    if (len == 0) { close(fd); return ingest("", 0, format, independent, o, out, err, errlen); }
     void *m = mmap(nullptr, len, PROT_READ, MAP_PRIVATE, fd, 0);
     close(fd);
     if (m == MAP_FAILED) { set_err(err, errlen, "cannot map the history file"); return JH_EINVAL; }
     madvise(m, len, MADV_SEQUENTIAL);
-    int rc = ingest((const char *)m, len, format, independent, threads, out, err, errlen);
+    int rc = ingest((const char *)m, len, format, independent, o, out, err, errlen);
     munmap(m, len);
     return rc;
+}
+
+int jh_ingest_buffer(const char *buf, size_t len, int format, int independent, int threads, jh_ingest **out,
+                     char *err, size_t errlen) {
+    const jh_ingest_opts o = plain_opts(threads);
+    return jh_ingest_buffer_opts(buf, len, format, independent, &o, out, err, errlen);
+}
+
+int jh_ingest_file(const char *path, int format, int independent, int threads, jh_ingest **out, char *err,
+                   size_t errlen) {
+    const jh_ingest_opts o = plain_opts(threads);
+    return jh_ingest_file_opts(path, format, independent, &o, out, err, errlen);
 }
 
 void jh_ingest_history(const jh_ingest *g, jh_history *h) {

@@ -357,6 +357,12 @@ struct DfsArgs {
     unsigned long long *tl;     // -DJH_TUNING timeline (JH_DEFER_TIMES): per key [2] search start, [3] end
 };
 constexpr int TL_W = 6;         // timeline words per key: BFS, sequential, helper (start, end)
+#ifdef JH_TUNING
+#define TL_REC(tl, key, w) \
+    do { if ((tl) && (threadIdx.x & 63) == 0) (tl)[TL_W * (size_t)(key) + (w)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define TL_REC(tl, key, w) do { } while (0)
+#endif
 constexpr unsigned long long SEQ_HANDED = ~0ULL;
 
 __device__ __forceinline__ int ld_agent(const int32_t *p) {
@@ -1027,213 +1033,6 @@ __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint32_t *bcnt, uin
     return ((uint64_t)th2 << 32) | (uint32_t)kept;
 }
 
-// ---------------------------------------------------------------------------
-// Phase 1's HBM memo in blocks (round 4). The hash table above costs every
-// evicted entry a random 128-byte line: its bucket read, then the CAS and the
-// store write the line back -- phase 1 moved 2.0 GB in and 3.2 GB out for
-// 0.6 GB of algorithmic bytes (profiles/r03/traffic_c3_s3_k_lin_dfs_true.json)
-// though its searches probe HBM rarely (~1 Bloom-positive lane per 300 steps).
-// Here a key's evicted entries (8-byte LEAN keys, no generation tag: the
-// blocks are the key's own) fill 8 KB blocks of 1 024 slots to at most half,
-// one block after the other, so an eviction writes whole lines of a few
-// blocks. Block b's layer range [tlo, thi] is kept in LDS beside the memo; a
-// probe of a Bloom-positive child reads one 64-byte group of every block
-// whose range holds the child's layer, lane b for block b: one round trip,
-// as before. The entries are compacted in place (no stage in global memory).
-constexpr int BLK_SLOTS = 1024;          // 8-byte slots per block (8 KB)
-constexpr int BLK_FILL = 512;            // entries per block at most (load 1/2)
-constexpr int BLK_MAX = 64;              // blocks per key (lane b: block b); 32 K entries
-constexpr int BLK_GROUPS = BLK_SLOTS / 8;
-constexpr int32_t FLAG_BLK_FULL = 2048;  // flags: a key needed more than BLK_MAX blocks
-// per wave, in LDS after its memo (kept out of registers: the search's loop
-// is at its register budget, and state passed through calls inflates it)
-struct BlkLds {
-    uint32_t nblk, fill, ovf, pad;       // blocks used, entries in the last one, over BLK_MAX
-    uint32_t tlo[BLK_MAX], thi[BLK_MAX];
-};
-constexpr int BLK_LDS = (int)sizeof(BlkLds);
-__device__ __forceinline__ uint32_t blk_group(uint64_t k) {
-    return (uint32_t)(jh_mix64(k) >> 40) & (BLK_GROUPS - 1);
-}
-// one lane: k (unique in the key's memo) into block blk, from its hash
-// group on, slot by slot: a CAS per slot, the slots of a group filling front
-// to back (one round trip per occupied slot passed; few registers, as the
-// eviction runs inside the search's register budget)
-__device__ __forceinline__ void blk_put(uint64_t *blk, uint64_t k) {
-    const uint32_t g0 = blk_group(k) * 8;
-#pragma unroll 1
-    for (uint32_t it = 0; it < BLK_SLOTS; it++) {
-        unsigned long long exp = 0;
-        if (__hip_atomic_compare_exchange_strong((unsigned long long *)(blk + ((g0 + it) & (BLK_SLOTS - 1))), &exp,
-                                                 (unsigned long long)k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-            return;
-    }
-}
-// one lane: is k in block blk (a group with an empty slot ends the probe)
-__device__ __forceinline__ bool blk_has(const uint64_t *blk, uint64_t k) {
-    uint32_t g = blk_group(k);
-    for (int it = 0; it < BLK_GROUPS; it++) {
-        const unsigned long long *p = (const unsigned long long *)(blk + 8 * g);
-        unsigned long long e[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) e[j] = __hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bool hit = false, room = false;
-#pragma unroll
-        for (int j = 0; j < 8; j++) { hit |= e[j] == k; room |= e[j] == 0; }
-        if (hit) return true;
-        if (room) return false;
-        g = (g + 1) & (BLK_GROUPS - 1);
-    }
-    return false;
-}
-// wave min / max of a per-lane value over the lanes in m (m != 0)
-__device__ __forceinline__ uint32_t wave_min_in(uint64_t m, int lane, uint32_t v) {
-    uint32_t x = ((m >> lane) & 1) ? v : 0xFFFFFFFFu;
-    for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o));
-    return x;
-}
-__device__ __forceinline__ uint32_t wave_max_in(uint64_t m, int lane, uint32_t v) {
-    uint32_t x = ((m >> lane) & 1) ? v : 0u;
-    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
-    return x;
-}
-// the lanes' entries x (where v) into the key's blocks: the last block up to
-// BLK_FILL, then a fresh one (zeroed first); their layer ranges widen
-__device__ __forceinline__ void blk_add(uint64_t *region, BlkLds *bl, uint64_t x, bool v, int lane) {
-    const uint64_t m = ballot(v);
-    if (!m) return;
-    const uint32_t nb = rflu(bl->nblk), fill = rflu(bl->fill);
-    const uint32_t cnt = (uint32_t)__popcll(m);
-    const uint32_t rank = (uint32_t)mbcnt(m);
-    const uint32_t room = nb ? BLK_FILL - fill : 0;
-    const uint32_t cur = nb - 1;
-    if (cnt > room) {
-        if (nb >= BLK_MAX) { if (lane == 0) bl->ovf = 1; wave_sync(); return; }
-        uint4 *z = (uint4 *)(region + (size_t)nb * BLK_SLOTS);
-#pragma unroll
-        for (int r = 0; r < BLK_SLOTS * 8 / 16 / 64; r++) z[lane + 64 * r] = make_uint4(0, 0, 0, 0);
-        // the zeros in L2 before the CAS inserts (L2 atomics) of other lanes
-        __builtin_amdgcn_s_waitcnt(0);
-        wave_sync();
-    }
-    const bool in_cur = rank < room;
-    if (v) blk_put(region + (size_t)(in_cur ? cur : nb) * BLK_SLOTS, x);
-    const uint32_t xt = lk_t(x);
-    const uint64_t mc = ballot(v && in_cur), mn = m & ~mc;
-    if (mc) {
-        const uint32_t lo = wave_min_in(mc, lane, xt), hi = wave_max_in(mc, lane, xt);
-        if (lane == 0) { bl->tlo[cur] = min(bl->tlo[cur], lo); bl->thi[cur] = max(bl->thi[cur], hi); }
-    }
-    if (mn) {
-        const uint32_t lo = wave_min_in(mn, lane, xt), hi = wave_max_in(mn, lane, xt);
-        if (lane == 0) { bl->tlo[nb] = lo; bl->thi[nb] = hi; bl->nblk = nb + 1; bl->fill = cnt - room; }
-    } else if (lane == 0) {
-        bl->fill = fill + cnt;
-    }
-    wave_sync();
-}
-// memo_evict for the block memo: the same theta rule; the LDS table is not
-// rebuilt but compacted bucket by bucket in place (a lane owns whole buckets:
-// the entries at or above theta keep their slots' order, the others go to the
-// blocks), so nothing is staged and no entry can fail to find a place.
-// Returns theta << 32 | kept, like memo_evict.
-template <class M>
-__device__ __noinline__ uint64_t memo_evict_blk(uint64_t *lmemo, uint32_t *bcnt, uint32_t *bloom, uint64_t *region,
-                                                BlkLds *bl, uint32_t t_cur, uint32_t theta_old, int lane) {
-    int bins = 0;                                  // lane b < 16 holds bin b
-#pragma unroll 1
-    for (int r = 0; r < M::SLOTS / 64; r++) {
-        const uint64_t x = lmemo[lane + 64 * r];
-        const uint32_t xt = lk_t(x);
-        const int d = x == 0 ? 99 : (xt >= t_cur ? 0 : (int)min(t_cur - xt, 15u));
-#pragma unroll
-        for (int b = 0; b < 16; b++) {
-            const int cnt = __popcll(ballot(d == b));
-            if (lane == b) bins += cnt;
-        }
-    }
-    int acc = 0, dstar = -1;
-#pragma unroll 1
-    for (int b = 0; b < 16; b++) {
-        acc += readlane(bins, b);
-        if (acc > M::EVICT / 2) break;
-        dstar = b;
-    }
-    uint32_t th2;
-    if (dstar < 0) th2 = t_cur + 1;
-    else {
-        th2 = t_cur > (uint32_t)dstar ? t_cur - (uint32_t)dstar : 0u;
-        if (dstar == 15) th2 = t_cur - min(t_cur, 15u);
-    }
-    th2 = max(th2, theta_old);
-    uint8_t *bcnt8 = (uint8_t *)bcnt;
-    int kept = 0;
-#pragma unroll 1
-    for (int bb = 0; bb < M::BKT / 64; bb++) {
-        const uint32_t b = (uint32_t)lane + 64u * (uint32_t)bb;
-        const uint32_t n = bcnt8[b];
-        uint32_t w = 0;
-        // slot by slot (a kept entry moves to slot w <= j: no unread slot is overwritten)
-#pragma unroll 1
-        for (uint32_t j = 0; j < 4; j++) {
-            const uint64_t x = j < n ? lmemo[4 * b + j] : 0;
-            const bool keep = j < n && lk_t(x) >= th2;
-            const bool ev = j < n && !keep;
-            if (keep) { lmemo[4 * b + w] = x; w++; }
-            blk_add(region, bl, x, ev, lane);
-            if (ev) {
-                uint32_t h1, h2;
-                lk_hash((uint32_t)x, (uint32_t)(x >> 32), h1, h2);
-                bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
-            }
-        }
-#pragma unroll 1
-        for (uint32_t j = w; j < 4; j++) lmemo[4 * b + j] = 0;
-        bcnt8[b] = (uint8_t)w;
-        kept += (int)w;
-    }
-    for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o);
-    // the LDS rewrite and the block writes (stores, L2 atomics) done before
-    // the search goes on
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    wave_sync();
-    return ((uint64_t)th2 << 32) | (uint32_t)kept;
-}
-// one child into the blocks (both its LDS buckets full), out of line
-template <class M>
-__device__ __noinline__ void blk_add_one(uint64_t *region, BlkLds *bl, uint64_t x, bool v, uint32_t *bloom,
-                                         uint32_t bl1, uint32_t bl2, int lane) {
-    blk_add(region, bl, x, v, lane);
-    if (v) bloom_set2<M>(bloom, bl1, bl2);
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    wave_sync();
-}
-// the Bloom-positive lanes (maybe) of a step: which children are in the
-// blocks. One round trip per such lane: every block whose layer range holds
-// the child's layer is probed at once (lane b: block b).
-__device__ __forceinline__ uint64_t blk_find(const uint64_t *region, const BlkLds *bl, uint64_t maybe, uint64_t k,
-                                             uint32_t kt, int lane, unsigned long long &probes) {
-    uint64_t found = 0;
-    const uint32_t nb = rflu(bl->nblk);
-    const bool blk = (uint32_t)lane < nb;
-    const uint32_t lo = blk ? bl->tlo[lane] : 1u, hi = blk ? bl->thi[lane] : 0u;
-    while (maybe) {
-        const int i = __builtin_ctzll(maybe);
-        maybe &= maybe - 1;
-        const uint64_t ki = readlane64(k, i);
-        const uint32_t ti = (uint32_t)readlane((int)kt, i);
-        const bool mine = lo <= ti && ti <= hi;
-        probes += (unsigned long long)__popcll(ballot(mine));
-        const bool hit = mine && blk_has(region + (size_t)lane * BLK_SLOTS, ki);
-        if (ballot(hit)) found |= 1ULL << i;
-    }
-    return found;
-}
 
 __device__ __forceinline__ uint64_t drop_bit(uint64_t m, uint32_t r) {
     const uint64_t lo = (1ULL << r) - 1;
@@ -1582,7 +1381,7 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
 // Search order and memo contents are exactly WGL's (orc_wgl_canonical,
 // oracle/jh_oracle.c, which does probe after a backtrack and never finds the
 // child present): explored counts stay identical.
-template <class M, bool BLK = false>
+template <class M>
 __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, const char *tb, int key, int lane,
                         uint64_t *memo, Frame *stack, uint64_t *stage,
                         long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes) {
@@ -1604,12 +1403,6 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
     int lcount = 0;
     uint32_t n_steps = 0, n_lay = 0, n_up = 0, n_spill = 0, n_refill = 0, n_slow = 0, n_evict = 0, n_hbm = 0;
     const unsigned long long probes0 = my_probes;
-    // BLK (phase 1): the HBM part of the memo is this key's blocks in `memo`
-    BlkLds *blks = (BlkLds *)(jh_lds + M::LDS);
-    if constexpr (BLK) {
-        if (lane == 0) { blks->nblk = 0; blks->fill = 0; blks->ovf = 0; }
-        blks->tlo[lane] = 0xFFFFFFFFu; blks->thi[lane] = 0;
-    }
 
     // layer-table window: lane j holds lay[tb0 + j]
     uint32_t tb0 = 0, drq = 0, dhi = 0;
@@ -1717,14 +1510,9 @@ expand:
             const uint32_t kt = khi >> 16 & 0x7FFF, ks = (khi >> 8) & 0xFF;
             const uint64_t km = k & ((1ULL << 40) - 1);
             const bool maybe = ((low >> lane) & 1) && bloom_test2<M>(bloom, lk_bl(h1), lk_bl(h2));
-            if constexpr (BLK) {
-                const uint64_t mm = ballot(maybe);
-                if (mm) absent &= ~blk_find(memo, blks, mm, k, kt, lane, my_probes);
-            } else {
-                bool found = false;
-                if (maybe) found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
-                absent &= ~ballot(found);
-            }
+            bool found = false;
+            if (maybe) found = (hbm_probe(memo, cap_mask, gen, kt, ks, km, my_probes) >> 32) == 0;
+            absent &= ~ballot(found);
         }
     }
     if (!absent) goto pop;
@@ -1764,44 +1552,22 @@ insert:
                 }
                 if (++lcount >= M::EVICT) {
                     DFS_STAT(n_evict++);
-                    if constexpr (BLK) {
-                        const uint64_t er = memo_evict_blk<M>(lmemo, bcnt, bloom, memo, blks, nt, theta, lane);
-                        DFS_STAT(n_hbm += (uint32_t)lcount - (uint32_t)er);
-                        lcount = rfl((int)(uint32_t)er);
-                        theta = rflu((uint32_t)(er >> 32));
-                    } else {
-                        const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
-                        DFS_STAT(n_hbm += (uint32_t)lcount - (uint32_t)er);
-                        lcount = rfl((int)(uint32_t)er);
-                        theta = rflu((uint32_t)(er >> 32));
-                    }
+                    const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
+                    DFS_STAT(n_hbm += (uint32_t)lcount - (uint32_t)er);
+                    lcount = rfl((int)(uint32_t)er);
+                    theta = rflu((uint32_t)(er >> 32));
                 }
             } else {
                 // both buckets full: HBM, and theta rises above the layer
-                if constexpr (BLK) {
-                    blk_add_one<M>(memo, blks, ((uint64_t)khi << 32) | klo, lane == i, bloom, lk_bl(h1), lk_bl(h2), lane);
-                } else {
-                    const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
-                    if (lane == i) {
-                        hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
-                        bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
+                if (lane == i) {
+                    hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
+                    bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
                 }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 theta = max(theta, nt + 1);
                 DFS_STAT(n_hbm++);
-            }
-            if constexpr (BLK) {
-                if (rflu(blks->ovf)) {
-                    // more blocks than BLK_MAX (only with a quick budget over 32 K
-                    // inserts): the memo is incomplete, so the key goes to the
-                    // heavy-key pass, which restarts it
-                    if (!A.defer && lane == 0) atomicOr(A.flags, FLAG_BLK_FULL);
-                    ins = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
-                    verdict = JH_UNKNOWN;
-                    goto done;
-                }
             }
         }
         // push the parent; a full ring spills its oldest half to HBM
@@ -2365,7 +2131,10 @@ __global__ void __launch_bounds__(256) k_key_tables(TblArgs A) {
 
 // LEAN: dfs_lean (8-byte LDS keys); else WL: dfs_lean_w (16-byte LDS keys),
 // else dfs_search (every configuration in the HBM table)
-template <class M, bool LEAN, bool WL = false, bool BLK = false>
+// STREAM: the kernel takes part in the streaming heavy-key pass (phase 1 as
+// the producer of the live lists, or a consumer of them); without it the
+// streaming code is compiled out (it costs phase 1 registers and occupancy).
+template <class M, bool LEAN, bool WL = false, bool STREAM = false>
 __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     const int lane = threadIdx.x;
     const size_t wv = (size_t)(blockIdx.x - A.wave_off);
@@ -2380,14 +2149,15 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     if (A.defer_time && lane == 0) atomicMin(&A.defer_time[0], __builtin_amdgcn_s_memrealtime());
     // phase 1 (streaming): this key is finished -- after its list entries
     auto p1_key_done = [&]() {
-        if (A.p1_count && lane == 0) __hip_atomic_fetch_add(A.p1_count, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (STREAM)
+            if (A.p1_count && lane == 0) __hip_atomic_fetch_add(A.p1_count, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     };
     for (;;) {
         int idx = 0;
         if (lane == 0) idx = atomicAdd(A.queue, 1);
         idx = readlane(idx, 0);
         int key;
-        if (A.live_n) {
+        if (STREAM && A.live_n) {
             int k = -1;
             if (lane == 0) k = stream_key(A.list, A.live_n, A.p1_done, A.p1_tot, idx, A.flags);
             key = readlane(k, 0);
@@ -2396,7 +2166,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
             if (idx >= n_list) {
                 // the first wave to find the queue empty: the host may launch
                 // the streaming consumers now (system scope: host-mapped)
-                if (A.drained && idx == n_list && lane == 0)
+                if (STREAM && A.drained && idx == n_list && lane == 0)
                     __hip_atomic_store(A.drained, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
             }
@@ -2404,7 +2174,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         }
         if (A.t_span && !spanned && lane == 0) atomicMin(&A.t_span[0], __builtin_amdgcn_s_memrealtime());
         spanned = true;
-        if (A.tl && lane == 0) A.tl[TL_W * (size_t)key + 2] = __builtin_amdgcn_s_memrealtime();
+        TL_REC(A.tl, key, 2);
         const KeyMeta mt = A.meta[key];
         KeyInfo K;
         K.n_ops = mt.n_ops; K.n_ok = mt.n_ok; K.sumW = 0;
@@ -2422,12 +2192,12 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
             __hip_atomic_store(&A.seq_start[key], __builtin_amdgcn_s_memrealtime() | 1ULL, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         int verdict;
-        if constexpr (LEAN) verdict = dfs_lean<M, BLK>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
+        if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else if constexpr (WL) verdict = dfs_lean_w<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         if (A.dbg && lane == 0) { A.dbg[16 * wv + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * wv + 3] += 1; }
         if (verdict == JH_CANCELLED) {
-            if (A.tl && lane == 0) A.tl[TL_W * (size_t)key + 3] = __builtin_amdgcn_s_memrealtime();
+            TL_REC(A.tl, key, 3);
             p1_key_done();
             continue;
         }
@@ -2444,9 +2214,9 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
                 if (A.defer_kind) {
                     const int dk = atomicAdd(A.defer_kind_count, 1);
                     A.defer_kind[dk] = pk;
-                    if (A.s_kind) __hip_atomic_store(&A.s_kind[dk], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (STREAM && A.s_kind) __hip_atomic_store(&A.s_kind[dk], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                if (A.s_all) __hip_atomic_store(&A.s_all[d], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (STREAM && A.s_all) __hip_atomic_store(&A.s_all[d], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (A.defer_time) A.defer_time[2 + key] = __builtin_amdgcn_s_memrealtime();
                 if (A.seq_start)
                     __hip_atomic_store(&A.seq_start[key], SEQ_HANDED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2462,7 +2232,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         // an invalid key's failing row is resolved by k_fail_rows from tmax
         if (verdict == JH_INVALID) v.fail_entry = -(int64_t)tmax - 2;
         if (lane == 0) emit_verdict(A.out, A.claim, key, v);
-        if (A.tl && lane == 0) A.tl[TL_W * (size_t)key + 3] = __builtin_amdgcn_s_memrealtime();
+        TL_REC(A.tl, key, 3);
         p1_key_done();
     }
     if (A.dbg && lane == 0) A.dbg[16 * wv + 9] = __builtin_amdgcn_s_memtime() - t_begin;
@@ -2496,20 +2266,11 @@ __global__ void __launch_bounds__(256) k_list_cost(const int32_t *__restrict__ l
     }
 }
 
-// phase 1: every key under the quick budget
-// (five waves per SIMD: phase 1's 20 resident waves per CU; the block memo's
-// out-of-line calls would otherwise take the register allocation past it)
-#ifndef JH_P1_BLK
-#define JH_P1_BLK 1
-#endif
-#ifdef JH_P1_WPE
-#define JH_P1_ATTR __attribute__((amdgpu_waves_per_eu(JH_P1_WPE)))
-#else
-#define JH_P1_ATTR
-#endif
-template <bool LEAN>
-__global__ void __launch_bounds__(64) JH_P1_ATTR k_lin_dfs(DfsArgs A) {
-    lin_dfs_waves<MemoQ, LEAN, false, LEAN && JH_P1_BLK>(A);
+// phase 1: every key under the quick budget (STREAM: the producer of the
+// streaming heavy-key pass's live lists)
+template <bool LEAN, bool STREAM>
+__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
+    lin_dfs_waves<MemoQ, LEAN, false, STREAM>(A);
 }
 // heavy keys: the full-budget sequential search racing k_lin_bfs, one wave
 // per CU with a 128 KB LDS memo
@@ -2534,9 +2295,10 @@ __global__ void __launch_bounds__(64) k_lin_seqw(DfsArgs A) { lin_dfs_waves<Memo
 // no more streams than the hardware has queues
 struct DfsPair { DfsArgs l, w; int32_t n_l; };
 constexpr int SEQLW_LDS = MemoM::LDS > SEQW_LDS ? MemoM::LDS : SEQW_LDS;
+template <bool STREAM>
 __global__ void __launch_bounds__(64) k_lin_seq_lw(DfsPair P) {
-    if ((int)blockIdx.x < P.n_l) lin_dfs_waves<MemoM, true>(P.l);
-    else lin_dfs_waves<MemoWL, false, true>(P.w);
+    if ((int)blockIdx.x < P.n_l) lin_dfs_waves<MemoM, true, false, STREAM>(P.l);
+    else lin_dfs_waves<MemoWL, false, true, STREAM>(P.w);
 }
 
 // Deferred keys, least advanced first (phase 1's progress, ties by key: the
@@ -3585,10 +3347,10 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
             long long inserts = 0;
             uint32_t tmax = 0;
             const unsigned long long ck0 = __builtin_amdgcn_s_memtime();
-            if (A.tl && lane == 0) A.tl[TL_W * (size_t)key + 4] = __builtin_amdgcn_s_memrealtime();
+            TL_REC(A.tl, key, 4);
             const int verdict = dfs_acc<MemoW>(W, sh, K, A.tables + mt.off, key, lane, memo, stack, stage, gset,
                                                work, wtab, pend, inserts, tmax, my_probes);
-            if (A.tl && lane == 0) A.tl[TL_W * (size_t)key + 5] = __builtin_amdgcn_s_memrealtime();
+            TL_REC(A.tl, key, 5);
             jh_key_verdict v;
             v.valid = verdict;
             v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
@@ -4449,7 +4211,9 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
     const uint32_t n_ok = (uint32_t)K.n_ok;
     uint64_t *lset = (uint64_t *)(jh_lds + BFS_HDR + BFS_TBL);
     const uint32_t gmask = A.gset_cap - 1;
-    if (sh.maxw > 64) {
+    if (sh.maxw > 64 && !A.cfg_slot) {
+        // (a configurations request hands such a key to the 65-256-member
+        // search below, with the other keys this engine cannot hold)
         if (tid == 0) {
             jh_key_verdict v;
             v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_WINDOW; v.fail_entry = -1; v.explored = 0;
@@ -4881,7 +4645,7 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A0) {
         if (key < 0) break;
         if (A.t_span && !spanned && tid == 0) atomicMin(&A.t_span[0], __builtin_amdgcn_s_memrealtime());
         spanned = true;
-        if (A.tl && tid == 0) A.tl[TL_W * (size_t)key] = __builtin_amdgcn_s_memrealtime();
+        TL_REC(A.tl, key, 0);
         if (wid == 0) {
             KeyInfo K;
             jh_key_verdict v;
@@ -4901,7 +4665,7 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A0) {
             if (tid == 0) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
             __syncthreads();
         }
-        if (A.tl && tid == 0) A.tl[TL_W * (size_t)key + 1] = __builtin_amdgcn_s_memrealtime();
+        TL_REC(A.tl, key, 1);
     }
     if (A.t_span && tid == 0) atomicMax(&A.t_span[1], __builtin_amdgcn_s_memrealtime());
 }
@@ -5451,8 +5215,8 @@ constexpr int XW_LDS = (int)(XW_SL * 8 + XW_RING * XW_FW * 8);
 __global__ void __launch_bounds__(64) k_lin_seq_lwx(DfsTriple P) {
     const int b = (int)blockIdx.x;
     if (b < P.n_x) xw_waves(P.x, (size_t)b, (unsigned long long *)jh_lds, (uint64_t *)(jh_lds + XW_SL * 8));
-    else if (b < P.n_x + P.n_w) lin_dfs_waves<MemoWL, false, true>(P.w);
-    else lin_dfs_waves<MemoM, true>(P.l);
+    else if (b < P.n_x + P.n_w) lin_dfs_waves<MemoWL, false, true, true>(P.w);
+    else lin_dfs_waves<MemoM, true, false, true>(P.l);
 }
 
 __global__ void __launch_bounds__(256) k_fail_rows(KeySrc S, jh_key_verdict *out, int64_t K) {
@@ -5874,7 +5638,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     int64_t quick = std::min<int64_t>(budget, QUICK_BUDGET);
     if (opts && opts->quick_budget > 0)
         quick = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(budget, memo_cap1 / 2), opts->quick_budget));
-    int p1_per_cu = 163840 / (MemoQ::LDS + BLK_LDS);
+    int p1_per_cu = 163840 / MemoQ::LDS;
     if (opts && opts->p1_waves_per_cu > 0) p1_per_cu = std::min(p1_per_cu, (int)opts->p1_waves_per_cu);
     const int waves1 = (int)std::min<int64_t>(K, (int64_t)ctx->n_cu * p1_per_cu);
     uint64_t *memo = ctx->ws<uint64_t>(WS_MEMO, (size_t)waves1 * memo_cap1 * 2, /*zero=*/true);
@@ -6259,7 +6023,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     };
     // the streaming heavy-key pass (round 4) whenever the default race runs
     const bool stream_p2 = !linear_mode && !skip_p1 && !p1_only && !use_wg && !wg_race && !dbg2 &&
-                           !(lflags & (JH_LIN_NO_STREAM | JH_LIN_BFS_ONLY));
+                           (lflags & JH_LIN_STREAM) && !(lflags & JH_LIN_BFS_ONLY);
     if (stream_p2) {
         // ---- the streaming heavy-key pass (round 4) --------------------------
         // Round 3 started the heavy keys when phase 1 ended (~17 ms into C3),
@@ -6336,9 +6100,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         a.t_span = (unsigned long long *)(q + Q_T_P1);
         HIP_TRY(hipEventRecord(ctx->ev[6], st));     // fork: tables, lists and counters are ready
         HIP_TRY(hipEventRecord(ctx->ev[1], st));
-        k_lin_dfs<true><<<waves1, 64, MemoQ::LDS + BLK_LDS, st>>>(a);
+        k_lin_dfs<true, true><<<waves1, 64, MemoQ::LDS, st>>>(a);
         HIP_TRY(hipGetLastError());
-        k_lin_dfs<false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
+        k_lin_dfs<false, true><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[4], st));
         a.prio_ins = 0;
@@ -6380,7 +6144,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             if (w_early > 0) {
                 DfsPair pr{};
                 pr.l = b; pr.n_l = w_early;
-                k_lin_seq_lw<<<w_early, 64, SEQLW_LDS, ctx->aux>>>(pr);
+                k_lin_seq_lw<true><<<w_early, 64, SEQLW_LDS, ctx->aux>>>(pr);
                 HIP_TRY(hipGetLastError());
             }
             HIP_TRY(hipEventRecord(ctx->ev[11], ctx->aux));
@@ -6435,12 +6199,12 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     } else {
         HIP_TRY(hipEventRecord(ctx->ev[1], st));
         if (!linear_mode && !skip_p1) {
-            k_lin_dfs<true><<<waves1, 64, MemoQ::LDS + BLK_LDS, st>>>(a);
+            k_lin_dfs<true, false><<<waves1, 64, MemoQ::LDS, st>>>(a);
             HIP_TRY(hipGetLastError());
             DfsArgs aw = a;
             aw.list = list_w; aw.n_list_dev = q + 13; aw.queue = q + 14;
             aw.defer_kind = d64 + 2 * (K + 1); aw.defer_kind_count = q + Q_DEFER_W;
-            k_lin_dfs<false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
+            k_lin_dfs<false, false><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
             a.prio_ins = 0;                       // the heavy-key passes inherit a: no priorities there
         } else if (cfgreq) {
             k_req_lists<<<1, 1, 0, st>>>(cfgreq->keys_dev, cfgreq->n_q, K, defer, defer_l, q);
@@ -6669,7 +6433,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 DfsPair pr;
                 pr.l = b; pr.w = bw; pr.n_l = waves2;
                 pr.w.wave_off = waves2;
-                k_lin_seq_lw<<<waves2 + waves_w, 64, SEQLW_LDS, ctx->aux>>>(pr);
+                k_lin_seq_lw<false><<<waves2 + waves_w, 64, SEQLW_LDS, ctx->aux>>>(pr);
                 wide_done = true;
             } else if (waves2) k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
             HIP_TRY(hipGetLastError());
@@ -6861,7 +6625,6 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     HIP_TRY(hipStreamSynchronize(st));
     if (qh[2] & 2) throw_jh(JH_EDEVICE, "per-key table exceeded the scratch reservation");
     if (qh[2] & 4) throw_jh(JH_EDEVICE, "DFS stack overflow");
-    if (qh[2] & FLAG_BLK_FULL) throw_jh(JH_EDEVICE, "phase-1 memo blocks exhausted without a heavy-key pass");
     if ((qh[2] & 0x1F0) && acc_stats && ctx->bufs.size() > WS_DEBUG && ctx->bufs[WS_DEBUG].p && n_wg > 0 &&
         dbgenv && atoi(dbgenv) >= 3) {
         std::vector<unsigned long long> tr((size_t)n_wg * 256);

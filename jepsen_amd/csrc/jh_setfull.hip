@@ -385,7 +385,7 @@ __global__ void k_sf_worst(const long long *__restrict__ lat_sorted, const int32
 
 }  // namespace
 
-void set_full_check(jh_ctx *ctx, const jh_history *dh, const int64_t *time_dev, bool linearizable,
+void set_full_check(jh_ctx *ctx, const jh_history *dh, const int64_t *time_dev, bool linearizable, int64_t read_batch,
                     jh_set_full_result *res, int64_t *lists_out[3], int64_t list_cap, hipStream_t st) {
     memset(res, 0, sizeof *res);
     const int64_t n = dh->n;
@@ -469,7 +469,7 @@ void set_full_check(jh_ctx *ctx, const jh_history *dh, const int64_t *time_dev, 
         const int64_t W = (M + 63) / 64;
         int64_t batch = std::max<int64_t>(1, ((int64_t)2 << 30) / (W * 8));
         batch = std::min<int64_t>({batch, (int64_t)65535, R});
-        if (const char *eb = getenv("JH_SF_BATCH")) batch = std::max<int64_t>(1, std::min<int64_t>(batch, atoll(eb)));
+        if (read_batch > 0) batch = std::min(batch, read_batch);
         unsigned long long *bits = ctx->ws<unsigned long long>(WS_SF_BITS, batch * W);   // [W][batch]
         const unsigned gx = (unsigned)std::max<int64_t>(1, (mh.max_cnt + BITS_CHUNK - 1) / BITS_CHUNK);
         for (int64_t r0 = 0; r0 < R; r0 += batch) {

@@ -23,6 +23,7 @@ from ._native import JhError, lib
 
 FMT = {"auto": 0, "edn": 1, "fressian": 2}
 TBL_KEYS, TBL_F, TBL_VALUES = 0, 1, 2
+DEFAULT_MIN_CHUNK = 0        # jh_ingest_opts.min_chunk when a call gives none (0 = 1 MiB)
 
 
 def _table(L, g, which):
@@ -66,25 +67,33 @@ def _load(L, rc, g, err, with_time):
         L.jh_ingest_free(g)
 
 
-def load_columns(path, independent=False, fmt="auto", threads=0, with_time=False):
+def _opts(threads, min_chunk, debug):
+    mc = DEFAULT_MIN_CHUNK if min_chunk is None else min_chunk
+    return A.JhIngestOpts(threads=int(threads), debug=int(bool(debug)), min_chunk=int(mc))
+
+
+def load_columns(path, independent=False, fmt="auto", threads=0, with_time=False, min_chunk=None, debug=False):
     """history.edn / test.fressian file -> history.Columns (include/jh.h
     layout); keyed by independent tuple when independent=True. threads=0: all
-    cores (EDN; fressian is one sequential pass)."""
+    cores (EDN; fressian is one sequential pass). min_chunk / debug:
+    jh_ingest_opts (smallest EDN chunk, 0 = 1 MiB; per-chunk timings)."""
     L = lib()
     g = C.c_void_p()
     err = C.create_string_buffer(512)
-    rc = L.jh_ingest_file(str(path).encode(), FMT[fmt], 1 if independent else 0, int(threads), C.byref(g),
-                          err, len(err))
+    o = _opts(threads, min_chunk, debug)
+    rc = L.jh_ingest_file_opts(str(path).encode(), FMT[fmt], 1 if independent else 0, C.byref(o), C.byref(g),
+                               err, len(err))
     return _load(L, rc, g, err, with_time)
 
 
-def parse_columns(data, independent=False, fmt="auto", threads=0, with_time=False):
+def parse_columns(data, independent=False, fmt="auto", threads=0, with_time=False, min_chunk=None, debug=False):
     """The same over bytes (or str) in memory."""
     if isinstance(data, str):
         data = data.encode("utf-8")
     L = lib()
     g = C.c_void_p()
     err = C.create_string_buffer(512)
-    rc = L.jh_ingest_buffer(data, len(data), FMT[fmt], 1 if independent else 0, int(threads), C.byref(g),
-                            err, len(err))
+    o = _opts(threads, min_chunk, debug)
+    rc = L.jh_ingest_buffer_opts(data, len(data), FMT[fmt], 1 if independent else 0, C.byref(o), C.byref(g),
+                                 err, len(err))
     return _load(L, rc, g, err, with_time)

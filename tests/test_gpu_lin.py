@@ -449,15 +449,15 @@ def test_frontier_configs_host_map(ctx):
 
 @pytest.mark.parametrize("seed", [3, 3 + 7919 * 3])
 def test_streamed_equals_round3_schedule(ctx, seed):
-    """The streaming heavy-key pass (consumers start while phase 1 still
-    defers keys) and the round-3 schedule (JH_LIN_NO_STREAM: after phase 1)
+    """The streaming heavy-key pass (JH_LIN_STREAM: consumers start while
+    phase 1 still defers keys) and the default schedule (after phase 1)
     decide every key identically, and both equal the oracle; a 2 000-key slice
     of the C3 workload (rank 0 / rank 3 seeds) has keys in every engine."""
     cols, _ = synth.cas_register(n_keys=2000, ops_per_key=500, threads_per_key=10, readers=5, n_values=5,
                                  process_limit=20, groups=10, p_info=0.02, p_invalid=0.01, nemesis_every=10000,
                                  seed=seed)
-    g, gs = ctx.check_cas_independent(cols)
-    l, ls = ctx.check_cas_independent(cols, flags=A.LIN_NO_STREAM)
+    g, gs = ctx.check_cas_independent(cols, flags=A.LIN_STREAM)
+    l, ls = ctx.check_cas_independent(cols)
     assert gs.streamed == 1 and ls.streamed == 0
     assert gs.n_deferred == ls.n_deferred > 0
     _same(g, l)
@@ -466,10 +466,10 @@ def test_streamed_equals_round3_schedule(ctx, seed):
 
 
 @pytest.mark.parametrize("quick", [300, 2000, 30000])
-def test_phase1_block_memo(ctx, quick):
-    """Phase 1's HBM memo is per-key blocks (round 4): quick budgets from one
-    eviction's worth to ~60 blocks per key, keys past them deferred -- every
-    field equal to the oracle."""
+def test_phase1_quick_budgets(ctx, quick):
+    """Phase 1 at quick budgets from one LDS eviction's worth to past the
+    heavy keys' size (keys past it deferred): every field equal to the
+    oracle."""
     cols, _ = synth.cas_register(n_keys=300, ops_per_key=400, threads_per_key=10, readers=5, groups=10,
                                  p_info=0.05, p_invalid=0.1, seed=4242)
     g, gs = ctx.check_cas_independent(cols, quick_budget=quick)

@@ -74,16 +74,15 @@ def _with_time(cols, time):
     return cols
 
 
-@pytest.mark.parametrize("batch", [None, "1", "3"])
-def test_set_full_large_vs_numpy_oracle(ctx, batch, monkeypatch):
+@pytest.mark.parametrize("batch", [0, 1, 3])
+def test_set_full_large_vs_numpy_oracle(ctx, batch):
     """200 K elements, 40 whole-set reads (~3.8 M read elements), read batches
-    of 1 and 3 reads (JH_SF_BATCH) as well as the default single batch."""
-    if batch:
-        monkeypatch.setenv("JH_SF_BATCH", batch)
+    of 1 and 3 reads (jh_set_full_opts.read_batch) as well as the default
+    single batch."""
     cols, time = synth.set_full_history(n_adds=200_000, n_procs=20, read_every=250, n_lost=300,
                                         n_stale=500, seed=11)
     want = SN.set_full_cols(cols, time)
-    r = ctx.check_set_full(cols, time)
+    r = ctx.check_set_full(cols, time, read_batch=batch)
     got = checker.set_full_result(r, cols, time)
     assert _flat_worst(got) == want
     n_ok_reads = int(((cols.f == 0) & (cols.type == 1) & (cols.process >= 0)).sum())

@@ -59,7 +59,7 @@ def _same(a, b, what=""):
 @pytest.fixture(autouse=True)
 def small_chunks(monkeypatch):
     # 4 KiB chunks so that even small texts are split over every thread
-    monkeypatch.setenv("JH_INGEST_CHUNK", "4096")
+    monkeypatch.setattr(ingest, "DEFAULT_MIN_CHUNK", 4096)
 
 
 def _check_edn(ops_or_text, independent=False, threads=(1, 3, 8)):

@@ -28,11 +28,11 @@ BYTES_PER_ENTRY = 56           # 7 x int64 columns read once
 BYTES_PER_PROBE = 16           # one memo entry {mask, t|state|gen}
 # HBM bytes per launch of a kernel from the rocprofv3 FETCH_SIZE and
 # WRITE_SIZE passes over the SAME history (tools/gpu_pmc.sh + pmc_traffic.py),
-# one file per (workload, seed, kernel) under profiles/r03/: PMC counters
+# one file per (workload, seed, kernel) under profiles/r04/: PMC counters
 # cannot be read inside a timed run, and a file of another history (another
 # workload, seed or rank) is never used. The file also holds the algorithmic
 # bytes of the profiled run itself, so traffic / algorithmic is a same-run ratio.
-TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r03")
+TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r04")
 
 
 def traffic_name(workload, seed, kernel):
@@ -52,14 +52,15 @@ def pmc_traffic(workload, seed, kernel):
 
 # the search phases a bench line reports a roofline for: (summary field of
 # the time, of the memo probes, of the entries of the keys searched, of the
-# number of keys searched, kernel). Streamed (ABI 5), the phase-2 LEAN role,
-# the WIDE role and xw each have their own span (first key to last wave end).
+# number of keys searched, kernel). The default schedule's kernels; the
+# phase-2 LEAN and WIDE roles share the k_lin_seq_lw grid but keep their own
+# timers (the WIDE waves' span, ABI 4).
 PHASES = {
-    "phase1": ("dfs_ms", "memo_probes", None, None, "k_lin_dfs<true>"),
-    "phase2_lean": ("seq_ms", "seq_probes", "lean_entries", "n_lean_deferred", "k_lin_seq_lw"),
+    "phase1": ("dfs_ms", "memo_probes", None, None, "k_lin_dfs<true, false>"),
+    "phase2_lean": ("seq_ms", "seq_probes", "lean_entries", "n_lean_deferred", "k_lin_seq_lw<false>"),
     "phase3_lean": ("p3_ms", "p3_probes", "p3_entries", "n_phase3", "k_lin_seq3<true>"),
-    "wide": ("wide_ms", "wide_probes", "wide_entries", "n_deferred_wide", "k_lin_seq_lwx"),
-    "xw": ("xw_ms", "xw_probes", "xw_entries", "n_xw", "k_lin_seq_lwx"),
+    "wide": ("wide_ms", "wide_probes", "wide_entries", "n_deferred_wide", "k_lin_seq_lw<false>"),
+    "xw": ("xw_ms", "xw_probes", "xw_entries", "n_xw", "k_lin_xw"),
 }
 
 
@@ -122,6 +123,7 @@ def parse():
                     help="c3 (default, BASELINE.json's metric): 10k keys per GPU; c4: a 125k-key "
                          "shard of the 1M-key history (1/8 per GPU); c5: 50 threads per key, many :info")
     ap.add_argument("--keys", type=int, default=None)
+    ap.add_argument("--budget", type=int, default=None, help="insert budget per key (default per workload)")
     ap.add_argument("--ops-per-key", type=int, default=500)
     ap.add_argument("--cpu-sample-keys", type=int, default=None,
                     help="keys of the rank-0 history timed on the CPU (default per workload)")
@@ -130,6 +132,10 @@ def parse():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--seed-rank", type=int, default=None,
                     help="generate the history rank R of a multi-GPU run would check (rehearsal on one GPU)")
+    ap.add_argument("--pool", type=int, default=1,
+                    help="N > 1: the two-stage pool (phase 1 per rank, deferred keys exchanged over RCCL "
+                         "and dealt by phase-1 progress, one stage-2 call per rank; shard.two_stage_resident); "
+                         "0: each rank checks its shard in one call")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=INT",
                     help="a jh_lin_opts tuning field for A/B runs (e.g. handover_min=2048); "
                          "recorded in config.opts")
@@ -167,7 +173,7 @@ def main():
     # ---- workload: this rank's shard of the C3 configuration -------------
     wl = WORKLOADS[args.workload]
     n_keys = args.keys or wl["keys"]
-    budget = wl.get("budget", A.DEFAULT_BUDGET)
+    budget = args.budget or wl.get("budget", A.DEFAULT_BUDGET)
     shard_info = None
     if wl.get("global_history"):
         # C4: one global history (every rank generates the same one, 16 host
@@ -212,8 +218,52 @@ def main():
 
     red_max = torch.zeros(2, dtype=torch.int64, device=dev)
     red_sum = torch.zeros(4, dtype=torch.int64, device=dev)
+    use_pool = dist is not None and args.pool
+    pool_stats = []
+    if use_pool:
+        from jepsen_amd import shard as _shard
+        key_rows = _shard.KeyRows(cols.key, cols.n_keys)
+        tune = dict(args.tune)
+        flags0 = tune.pop("flags", 0)
+
+        def _dev_view(t, n, k):
+            class V:
+                pass
+            v = V()
+            v.n, v.n_keys, v.aux, v.n_aux = n, k, 0, 0
+            for c in _shard.COLS:
+                setattr(v, c, t[c].data_ptr())
+            return v
+
+        def step_pool():
+            got = {}
+
+            def stage1():
+                got[1] = ctx.check_cas_independent_device(DCols, verd.data_ptr(), budget=budget,
+                                                          flags=flags0 | A.LIN_PHASE1_ONLY, **tune)
+                return np.frombuffer(verd.cpu().numpy().tobytes(), dtype=A.VERDICT_DTYPE).copy()
+
+            def stage2(sub, m):
+                v2 = torch.empty(m * A.VERDICT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+                got[2] = ctx.check_cas_independent_device(_dev_view(sub, int(sub["key"].numel()), m), v2.data_ptr(),
+                                                          budget=budget, flags=flags0 | A.LIN_SKIP_PHASE1, **tune)
+                return np.frombuffer(v2.cpu().numpy().tobytes(), dtype=A.VERDICT_DTYPE).copy()
+
+            g, st = _shard.two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=dev)
+            pool_stats.append(st)
+            # one jh_summary for the report: phase 1 from stage 1, the heavy-key
+            # pass from stage 2 (explored / counts are the all-reduced ones)
+            s = got.get(2) or got[1]
+            if 2 in got:
+                for f in ("dfs_ms", "memo_probes"):
+                    setattr(s, f, getattr(got[1], f))
+            s.valid, s.n_invalid, s.n_unknown = g["valid"], g["n_invalid"], g["n_unknown"]
+            s.explored = g["explored"]
+            return s
 
     def step():
+        if use_pool:
+            return step_pool()
         s = ctx.check_cas_independent_device(DCols, verd.data_ptr(), budget=budget, **args.tune)
         if dist is not None:
             # RCCL verdict summary all-reduce over xGMI: merge-valid (MAX),
@@ -285,6 +335,9 @@ def main():
         parity = None
         if not args.no_parity:
             from oracle import oracle
+            if use_pool:
+                # the pool's verdicts are spread over the ranks: rank 0's shard once more in one call
+                ctx.check_cas_independent_device(DCols, verd.data_ptr(), budget=budget, **args.tune)
             hv = np.frombuffer(verd.cpu().numpy().tobytes(), dtype=A.VERDICT_DTYPE)
             ov, os_ = oracle.check_cas_independent(cols, budget=budget, threads=min(16, len(os.sched_getaffinity(0))))
             # verdict, cause, failing row and WGL's cache size of every key
@@ -321,6 +374,10 @@ def main():
                        "phase1_span_ms": float(np.mean([x["p1_span_ms"] for x in sums])),
                        "phases": phase_table(sums), "opts": args.tune or None},
             "shard": shard_info,
+            "pool": ({"mode": "two-stage (shard.two_stage_resident): phase 1 per rank, deferred keys' rows "
+                              "all-gathered over RCCL, dealt round-robin least phase-1 progress first, one "
+                              "stage-2 call per rank", "rank0_last_step": pool_stats[-1]}
+                     if use_pool and pool_stats else None),
             "value_kind": "history resident in HBM, verdicts left in HBM (kernel pipeline only); "
                           "host-to-host rate in e2e_host_buffers",
             "e2e_host_buffers": e2e,

@@ -232,7 +232,7 @@ typedef struct jh_summary {
      * (first key taken to last wave end), p3_ms runs from the end of phase 2. */
     int64_t streamed;          /* 1: heavy keys started while phase 1 still ran */
     int64_t p3_entries;        /* entries of the LEAN keys restarted in phase 3 */
-    double  p2_start_ms;       /* first heavy key taken, ms after phase 1's first wave (-1: none) */
+    double  p2_start_ms;       /* heavy-key pass start (streamed: its first key taken), ms after phase 1 began (-1: none) */
     double  p1_span_ms;        /* phase 1's first wave to its last wave's end (streamed) */
 } jh_summary;
 

@@ -6413,6 +6413,13 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             //  - the sequential search with the full budget (aux stream: LEAN
             //    and WIDE keys in one grid) settles every key.
             prep_race(n_defer, n_def_l);
+            if (defer_times) {
+                // tuning builds: per key [BFS start, end, sequential start, end, helper start, end]
+                unsigned long long *tl = ctx->ws<unsigned long long>(WS_TL, TL_W * (size_t)K);
+                HIP_TRY(hipMemsetAsync(tl, 0, TL_W * sizeof(unsigned long long) * K, st));
+                c.tl = tl; b.tl = tl; bw.tl = tl;
+                if (n_help > 0) wh.d.tl = tl;
+            }
 
             // the fork point: everything the phase-2 searches read (claims, queue
             // counters, sorted lists, the cleared memo on a generation wrap) is
@@ -6570,7 +6577,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         for (int d = 0; d < n_defer; d++) heavy.push_back({vv[dk[d]].explored, dk[d]});
         std::sort(heavy.rbegin(), heavy.rend());
         std::vector<unsigned long long> tl;
-        if (stream_p2 && ctx->bufs.size() > WS_TL && ctx->bufs[WS_TL].p) {
+        if (ctx->bufs.size() > WS_TL && ctx->bufs[WS_TL].p) {
             tl.resize(TL_W * (size_t)K);
             HIP_TRY(hipMemcpy(tl.data(), ctx->bufs[WS_TL].p, 8 * tl.size(), hipMemcpyDeviceToHost));
         }
@@ -6698,6 +6705,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             sum->seq_ms = a2;
             if (!use_wg) { HIP_TRY(hipEventElapsedTime(&b2, ctx->ev[6], ctx->ev[5])); sum->bfs_ms = b2; }
             if (split3) { float c2 = 0; HIP_TRY(hipEventElapsedTime(&c2, ctx->ev[10], ctx->ev[7])); sum->p3_ms = c2; }
+            // the heavy-key pass's start (the fork), after phase 1's start
+            if (!use_wg && !p1_only) { float g2 = 0; HIP_TRY(hipEventElapsedTime(&g2, ctx->ev[1], ctx->ev[6])); sum->p2_start_ms = g2; }
             // the WIDE waves' own span (they share a grid with the LEAN ones)
             if (waves_w > 0 && q64(qh, Q_T_WIDE + 2) > q64(qh, Q_T_WIDE)) sum->wide_ms = (q64(qh, Q_T_WIDE + 2) - q64(qh, Q_T_WIDE)) / 1e5;
         }

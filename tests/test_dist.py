@@ -141,3 +141,81 @@ def test_two_stage_pool(built):
     assert pool > 10 and res[0][4]["pool"] == res[1][4]["pool"]
     assert res[0][4]["pulled"] + res[1][4]["pulled"] == pool
     assert min(res[0][4]["pulled"], res[1][4]["pulled"]) > 0
+
+
+def _worker3(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from jepsen_amd import history as H
+        from jepsen_amd import shard, synth
+        from oracle import oracle
+        # weak scaling as bench.py runs it: each rank its own history
+        cols, _ = synth.cas_register(n_keys=160, ops_per_key=120, p_invalid=0.1, p_info=0.05, seed=31 + rank)
+        dcols = {c: torch.from_numpy(getattr(cols, c).copy()) for c in shard.COLS}
+        kr = shard.KeyRows(cols.key, cols.n_keys)
+
+        def stage1():
+            # libjh's JH_LIN_PHASE1_ONLY contract: keys past the quick budget
+            # come back deferred with their progress as `explored`
+            v, _ = oracle.check_cas_independent(cols)
+            v = v.copy()
+            d = v["explored"] > 300
+            v["valid"][d] = A.UNKNOWN
+            v["cause"][d] = A.CAUSE_DEFERRED
+            v["explored"][d] = 1000 - (v["explored"][d] % 997)
+            v["fail_entry"][d] = -1
+            return v
+
+        got = []
+
+        def stage2(sub, m):
+            c = H.Columns(n=int(sub["key"].numel()), n_keys=m, aux=np.zeros(1, np.int64),
+                          **{k: sub[k].numpy().copy() for k in shard.COLS})
+            v, _ = oracle.check_cas_independent(c)
+            got.append(int(c.n))
+            return v
+
+        g, st = shard.two_stage_resident(rank, world, dcols, kr, stage1, stage2)
+        q.put((rank, g, st))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_stage_resident_pool(built):
+    """bench.py --gpus N's own path (shard.two_stage_resident), world 2 over
+    gloo: phase 1 on each rank's own history, the deferred keys' rows
+    exchanged with all_gather, the pool ordered by phase-1 progress and dealt
+    round-robin, one stage-2 call per rank. The all-reduced summary equals
+    the two histories checked whole, and both ranks take a share."""
+    from jepsen_amd import synth
+    from oracle import oracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker3, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = {"valid": 0, "n_invalid": 0, "n_unknown": 0, "n_keys": 0, "explored": 0}
+    ffs = []
+    for r in range(world):
+        cols, _ = synth.cas_register(n_keys=160, ops_per_key=120, p_invalid=0.1, p_info=0.05, seed=31 + r)
+        _, s = oracle.check_cas_independent(cols)
+        want["valid"] = max(want["valid"], s.valid)
+        for f in ("n_invalid", "n_unknown", "n_keys", "explored"):
+            want[f] += getattr(s, f)
+        if s.first_fail_entry >= 0:
+            ffs.append(s.first_fail_entry)
+    for rank, g, st in res:
+        for f, x in want.items():
+            assert g[f] == x, (rank, f, g[f], x)
+        assert g["first_fail_entry"] == (min(ffs) if ffs else -1)
+        assert st["pool"] > 4 and st["checked_here"] >= st["pool"] // 2
+    assert sum(st["checked_here"] for _, _, st in res) == res[0][2]["pool"]

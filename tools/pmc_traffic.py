@@ -5,7 +5,7 @@ written as the JSON bench.py puts into its roofline object (`traffic`,
 
     python tools/pmc_traffic.py <pmc-dir> <kernel-substring> <workload> <seed>
 
--> profiles/r03/traffic_<workload>_s<seed>_<kernel>.json (bench.traffic_name).
+-> profiles/r04/traffic_<workload>_s<seed>_<kernel>.json (bench.traffic_name).
 Both counters are in KiB. The guide's gfx950 calibration: FETCH_SIZE reports
 1/2 of the bytes of wide (16 B/lane) coalesced streaming reads, WRITE_SIZE is
 exact for 16 B/lane streaming stores; other access widths are uncalibrated.

@@ -2268,8 +2268,13 @@ __global__ void __launch_bounds__(256) k_list_cost(const int32_t *__restrict__ l
 
 // phase 1: every key under the quick budget (STREAM: the producer of the
 // streaming heavy-key pass's live lists)
+#ifdef JH_P1_WPE
+#define JH_P1_ATTR __attribute__((amdgpu_waves_per_eu(JH_P1_WPE)))
+#else
+#define JH_P1_ATTR
+#endif
 template <bool LEAN, bool STREAM>
-__global__ void __launch_bounds__(64) k_lin_dfs(DfsArgs A) {
+__global__ void __launch_bounds__(64) JH_P1_ATTR k_lin_dfs(DfsArgs A) {
     lin_dfs_waves<MemoQ, LEAN, false, STREAM>(A);
 }
 // heavy keys: the full-budget sequential search racing k_lin_bfs, one wave
@@ -4686,7 +4691,11 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A0) {
 // its frame from LDS; the frame carries the layer's window offset and width).
 constexpr int XW_SL = JH_MAX_WINDOW / 64;        // mask words / member slices
 constexpr uint32_t XW_HB = 4;                    // entries per bucket
-constexpr int XW_EW = 6;                         // words per entry
+constexpr int XW_EW = 6;                         // words per entry (the four-slice layout; the buffer's stride)
+// Entries per search instantiation: SL mask words, then gen|t|state; the
+// two-slice search (windows of 65-128 members, round 4) packs 4 words (32 B:
+// a bucket is one 128-byte line), the four-slice one 6
+template <int SL> struct XwL { static constexpr int EW = SL == 2 ? 4 : 6; };
 constexpr int XW_FW = 8;                         // words per stack frame
 // LDS ring of the top stack frames: 1.5 KB, under what k_lin_bfs's 157 KB
 // leaves of a CU (the two share CUs in C5)
@@ -4694,8 +4703,10 @@ constexpr int XW_RING = 24;
 // JH_XW_PROF builds: where a step's time goes (s_memtime, summed over waves)
 #ifdef JH_XW_PROF
 #define XW_PROF(x) x
+#define XW_PROFA(x) , x
 #else
 #define XW_PROF(x)
+#define XW_PROFA(x)
 #endif
 __device__ unsigned long long g_xw_prof[12];
 
@@ -4838,33 +4849,38 @@ __device__ __forceinline__ uint64_t xw_zw(int b) { return jh_mix64(0x9E3779B97F4
 __device__ __forceinline__ uint64_t xw_hash(uint32_t t, uint32_t s, uint64_t hm) {
     return jh_mix64(hm ^ (((uint64_t)t << 32) | s));
 }
+template <int SL>
 __device__ __forceinline__ uint64_t xw_zsum(const uint64_t *m, const uint64_t *zk, int lane) {
     uint64_t x = 0;
 #pragma unroll
-    for (int q = 0; q < XW_SL; q++) x ^= ((m[q] >> lane) & 1) ? zk[q] : 0ULL;
+    for (int q = 0; q < SL; q++) x ^= ((m[q] >> lane) & 1) ? zk[q] : 0ULL;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
     return rfl64(x);
 }
 
 // probe: slot | absent << 32 (absent: the slot an insert of this key takes)
+template <int SL>
 __device__ uint64_t xw_probe(const uint64_t *memo, uint32_t cap_mask, uint32_t gen, uint32_t t,
                              uint32_t s, const uint64_t *m, uint64_t hm, unsigned long long &probes) {
+    constexpr int EW = XwL<SL>::EW, E2 = EW / 2;           // 16-byte pairs per entry
     const uint64_t want = ((uint64_t)gen << 40) | ((uint64_t)t << 20) | s;
     uint32_t b = (uint32_t)xw_hash(t, s, hm) & cap_mask & ~(XW_HB - 1);
     for (;;) {
-        const ulonglong2 *B = (const ulonglong2 *)(memo + (size_t)b * XW_EW);
-        ulonglong2 e[XW_HB * 3];
+        const ulonglong2 *B = (const ulonglong2 *)(memo + (size_t)b * EW);
+        ulonglong2 e[XW_HB * E2];
 #pragma unroll
-        for (uint32_t j = 0; j < XW_HB * 3; j++) e[j] = B[j];
+        for (uint32_t j = 0; j < XW_HB * E2; j++) e[j] = B[j];
         probes++;
         int empty = -1, hit = -1;
 #pragma unroll
         for (int j = XW_HB - 1; j >= 0; j--) {
-            const uint64_t w1 = e[3 * j + 2].x;
+            const ulonglong2 *x = e + E2 * j;
+            const uint64_t w1 = SL == 2 ? x[1].x : x[2].x;
             if ((w1 >> 40) != gen) empty = j;
-            if (w1 == want && e[3 * j].x == m[0] && e[3 * j].y == m[1] && e[3 * j + 1].x == m[2] &&
-                e[3 * j + 1].y == m[3]) hit = j;
+            bool eq = w1 == want && x[0].x == m[0] && x[0].y == m[1];
+            if constexpr (SL == 4) eq = eq && x[1].x == m[2] && x[1].y == m[3];
+            if (eq) hit = j;
         }
         if (hit >= 0 && (empty < 0 || hit < empty)) return b + (uint32_t)hit;
         if (empty >= 0) return (1ULL << 32) | (b + (uint32_t)empty);
@@ -4872,12 +4888,13 @@ __device__ uint64_t xw_probe(const uint64_t *memo, uint32_t cap_mask, uint32_t g
     }
 }
 
+template <int SL>
 __device__ __forceinline__ void xw_store(uint64_t *memo, uint32_t slot, uint32_t gen, uint32_t t,
                                          uint32_t s, const uint64_t *m) {
-    uint64_t *e = memo + (size_t)slot * XW_EW;
-    for (int w = 0; w < XW_SL; w++)
+    uint64_t *e = memo + (size_t)slot * XwL<SL>::EW;
+    for (int w = 0; w < SL; w++)
         __hip_atomic_store(&e[w], m[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_store(&e[4], ((uint64_t)gen << 40) | ((uint64_t)t << 20) | s, __ATOMIC_RELAXED,
+    __hip_atomic_store(&e[SL], ((uint64_t)gen << 40) | ((uint64_t)t << 20) | s, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -4898,6 +4915,7 @@ __device__ __forceinline__ bool cfg_less(const Cfg5 &a, const Cfg5 &b) {
     if (a.m1 != b.m1) return a.m1 < b.m1;
     return a.m0 < b.m0;
 }
+template <int SL>
 __device__ void xw_dump_configs(const XwArgs &A, const uint64_t *memo, uint32_t gen, uint32_t tmax, int key,
                                 const XwTbl &T, int lane) {
     const int slot = A.cfg_slot[key];
@@ -4927,10 +4945,10 @@ __device__ void xw_dump_configs(const XwArgs &A, const uint64_t *memo, uint32_t 
         };
         if (tmax == 0 && lane == 0) offer(Cfg5{(uint32_t)A.init_state, 0, 0, 0, 0});
         for (uint32_t j = (uint32_t)lane; j < A.memo_cap; j += 64) {
-            const uint64_t *e = memo + (size_t)j * XW_EW;
-            const uint64_t e4 = e[4];
+            const uint64_t *e = memo + (size_t)j * XwL<SL>::EW;
+            const uint64_t e4 = e[SL];
             if ((uint32_t)(e4 >> 40) != gen || ((uint32_t)(e4 >> 20) & T_MASK) != tmax) continue;
-            offer(Cfg5{(uint32_t)e4 & STATE_MASK, e[3], e[2], e[1], e[0]});
+            offer(Cfg5{(uint32_t)e4 & STATE_MASK, SL == 4 ? e[3] : 0ULL, SL == 4 ? e[2] : 0ULL, e[1], e[0]});
         }
         // wave minimum of the lanes' best
         for (int o = 32; o > 0; o >>= 1) {
@@ -4976,13 +4994,220 @@ __device__ void xw_dump_configs(const XwArgs &A, const uint64_t *memo, uint32_t 
 
 // one wave of the 65-256-member search: wave wv's tables, nm_sh / ring in LDS
 // (k_lin_xw's own, or the dynamic LDS of k_lin_seq_lwx's xw role)
+// One key's search once its tables are built (xw_fill): SL mask words, the
+// two-slice instantiation for windows of 65-128 members, the four-slice one
+// for 129-256. Same search order and memo contents either way.
+template <int SL>
+__device__ __forceinline__ void xw_search(const XwArgs &A, int key, const XwTbl &T, int n_ok, uint64_t *memo,
+                                          uint64_t *stk, const uint64_t *zk, unsigned long long *nm_sh,
+                                          uint64_t *ring, unsigned long long &my_probes
+                                          XW_PROFA(unsigned long long *pf)) {
+    const int lane = threadIdx.x;
+    const uint32_t cap_mask = A.memo_cap - 1;
+    jh_key_verdict v;
+    {
+        const uint32_t gen = (A.gen_base + (uint32_t)key + 1) & ((1u << GEN_BITS) - 1);
+        const uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
+
+        // the current layer's members: member 64k + lane in slice k
+        uint32_t t = 0, tmax = 0, s = (uint32_t)A.init_state, ins = 0, depth = 0;
+        uint64_t mask[SL];
+#pragma unroll
+        for (int q = 0; q < SL; q++) mask[q] = 0;
+        uint32_t mrq[SL];
+        int32_t mrr[SL];
+        int w = 0, r = 0, start = 0, lo = 0;
+        // after a pop: the popped member's slice and which of its children
+        // were absent when the parent took that member. The table never
+        // drops an entry, so the others are still present: only these are
+        // probed again (none left: no round trip for the slice)
+        int k_known = -1;
+        uint64_t abs_known = 0;
+        // layer t's members: W(t) = P[o .. o + w)
+        auto load_layer = [&](int o, int wt) {
+            XW_PROF(const unsigned long long l0 = __builtin_amdgcn_s_memtime();)
+            lo = o; w = wt;
+            r = 0;
+#pragma unroll
+            for (int k = 0; k < SL; k++) {
+                const int j = 64 * k + lane;
+                mrq[k] = RQ_EMPTY; mrr[k] = -2;
+                if (j < w) { const uint2 pr = T.P[o + j]; mrq[k] = pr.x; mrr[k] = (int32_t)pr.y; }
+                const uint64_t b = ballot(j < w && mrr[k] == (int32_t)t);
+                if (b) r = 64 * k + __builtin_ctzll(b);
+            }
+            XW_PROF(pf[2] += __builtin_amdgcn_s_memtime() - l0; pf[7]++;)
+        };
+        load_layer(T.woff[0], T.woff[1] - T.woff[0]);
+        uint32_t rlo = 0;      // the LDS ring holds frames [rlo, depth)
+        uint64_t hm = 0;       // Zobrist sum of the configuration's mask
+        XW_PROF(const unsigned long long k0 = __builtin_amdgcn_s_memtime();)
+        int verdict = -1;
+        for (;;) {
+            // expand: candidates from `start` on, in call order, slice by slice
+            bool took = false;
+            uint32_t u_r = t;
+            uint64_t nm_r[SL], hr = 0;
+#pragma unroll
+            for (int q = 0; q < SL; q++) nm_r[q] = 0;
+            bool lifted = false;
+            int wo0 = 0, wo1 = 0;          // woff[u_r], woff[u_r + 1]: loaded beside the probes
+            // unrolled: static slice indices (no register-array selects, no
+            // SGPR spills: 4.02 -> 3.37 s of C5's k_lin_xw)
+#pragma unroll
+            for (int k = 0; k < SL && !took; k++) {
+                if (64 * k >= w) break;
+                const int j = 64 * k + lane;
+                const uint32_t req = mrq[k] & 0xFFFF;
+                const bool cl = j < w && j >= start && !((mask[k] >> lane) & 1) && (req == s || req == RQ_ANY) &&
+                                (k != k_known || ((abs_known >> lane) & 1));
+                const uint64_t cand = ballot(cl);
+                if (!cand) continue;
+                if (!lifted && (r >> 6) == k && ((cand >> (r & 63)) & 1)) {
+                    // the RET child: lift RET[t], keep lifting while the next
+                    // layer's RET op is already linearized, compact onto W(u)
+                    XW_PROF(const unsigned long long f0 = __builtin_amdgcn_s_memtime();)
+                    lifted = true;
+                    uint64_t lin[SL];
+#pragma unroll
+                    for (int q = 0; q < SL; q++) lin[q] = mask[q];
+                    lin[r >> 6] |= 1ULL << (r & 63);
+                    uint32_t u = t + 1;
+                    while (u < (uint32_t)n_ok) {
+                        bool hit = false;
+#pragma unroll
+                        for (int q = 0; q < SL; q++) hit |= ((lin[q] >> lane) & 1) && mrr[q] == (int32_t)u;
+                        if (!ballot(hit)) break;
+                        u++;
+                    }
+                    u_r = u;
+                    if (u < (uint32_t)n_ok) {
+                        wo0 = T.woff[u]; wo1 = T.woff[u + 1];
+                        if (lane < SL) nm_sh[lane] = 0;
+                        wave_sync();
+                        int base = 0;
+#pragma unroll
+                        for (int q = 0; q < SL; q++) {
+                            const bool kept = 64 * q + lane < w && (mrr[q] < 0 || mrr[q] >= (int32_t)u);
+                            const uint64_t bk = ballot(kept);
+                            const int pos = base + mbcnt(bk);
+                            if (kept && ((lin[q] >> lane) & 1)) atomicOr(&nm_sh[pos >> 6], 1ULL << (pos & 63));
+                            base += __popcll(bk);
+                        }
+                        wave_sync();
+#pragma unroll
+                        for (int q = 0; q < SL; q++) nm_r[q] = rfl64(nm_sh[q]);
+                        wave_sync();
+                        hr = xw_zsum<SL>(nm_r, zk, lane);
+                    }
+                    XW_PROF(pf[9] += __builtin_amdgcn_s_memtime() - f0;)
+                }
+                // every candidate lane probes its child
+                const bool is_r = j == r;
+                uint64_t cm[SL];
+#pragma unroll
+                for (int q = 0; q < SL; q++) cm[q] = is_r ? nm_r[q] : (mask[q] | (q == k ? (1ULL << lane) : 0ULL));
+                const uint32_t ct = is_r ? u_r : t, cs = mrq[k] >> 16;
+                const uint64_t chm = is_r ? hr : (hm ^ zk[k]);
+                bool found = false;
+                uint32_t slot = 0;
+                XW_PROF(const unsigned long long q0 = __builtin_amdgcn_s_memtime();)
+                if (cl) {
+                    const uint64_t pr = xw_probe<SL>(memo, cap_mask, gen, ct, cs, cm, chm, my_probes);
+                    found = (pr >> 32) == 0;
+                    slot = (uint32_t)pr;
+                }
+                const uint64_t absent = cand & ~ballot(found);
+                XW_PROF(pf[1] += __builtin_amdgcn_s_memtime() - q0; pf[6]++;)
+                if (!absent) continue;
+                const int i = __builtin_ctzll(absent);
+                if (ins >= budget) { verdict = JH_UNKNOWN; break; }
+                ins++;
+                XW_PROF(const unsigned long long h0 = __builtin_amdgcn_s_memtime();)
+                if (lane == i) xw_store<SL>(memo, slot, gen, ct, cs, cm);
+                // push the parent (t, its window, member, s, mask): HBM, and
+                // the LDS ring slot a pop reads while the frame stays in it
+                if (lane == 0) {
+                    uint64_t *f = stk + (size_t)depth * XW_FW;
+                    uint64_t *g = ring + (depth % XW_RING) * XW_FW;
+                    const uint64_t f4 = ((uint64_t)t << 32) | ((uint32_t)w << 16) | (uint32_t)(64 * k + i);
+                    const uint64_t f5 = ((uint64_t)(uint32_t)lo << 32) | s;
+#pragma unroll
+                    for (int q = 0; q < SL; q++) { f[q] = mask[q]; g[q] = mask[q]; }
+                    f[4] = f4; f[5] = f5; f[6] = hm; f[7] = absent;
+                    g[4] = f4; g[5] = f5; g[6] = hm; g[7] = absent;
+                }
+                depth++;
+                if (depth - rlo > (uint32_t)XW_RING) rlo = depth - XW_RING;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                XW_PROF(pf[4] += __builtin_amdgcn_s_memtime() - h0; pf[5]++;)
+                s = (uint32_t)readlane((int)cs, i);
+                hm = readlane64(chm, i);
+                const uint32_t nt = (uint32_t)readlane((int)ct, i);
+#pragma unroll
+                for (int q = 0; q < SL; q++) mask[q] = readlane64(cm[q], i);
+                took = true;
+                start = 0;
+                k_known = -1;
+                if (nt != t) {
+                    t = nt;
+                    tmax = max(tmax, t);
+                    if (t >= (uint32_t)n_ok) { verdict = JH_VALID; break; }
+                    load_layer(wo0, wo1 - wo0);     // nt != t only for the RET child: t == u_r
+                }
+            }
+            if (verdict >= 0) break;
+            if (took) continue;
+            // pop
+            if (depth == 0) { verdict = JH_INVALID; break; }
+            XW_PROF(const unsigned long long o0 = __builtin_amdgcn_s_memtime();)
+            depth--;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            uint64_t ti, f5;
+            if (depth >= rlo) {
+                const uint64_t *g = ring + (depth % XW_RING) * XW_FW;
+#pragma unroll
+                for (int q = 0; q < SL; q++) mask[q] = rfl64(g[q]);
+                ti = rfl64(g[4]); f5 = rfl64(g[5]); hm = rfl64(g[6]); abs_known = rfl64(g[7]);
+            } else {
+                const uint64_t *f = stk + (size_t)depth * XW_FW;
+#pragma unroll
+                for (int q = 0; q < SL; q++) mask[q] = rfl64(f[q]);
+                ti = rfl64(f[4]); f5 = rfl64(f[5]); hm = rfl64(f[6]); abs_known = rfl64(f[7]);
+                rlo = depth;
+                XW_PROF(pf[10]++;)
+            }
+            s = (uint32_t)f5;
+            start = (int)(ti & 0xFFFF) + 1;
+            k_known = (int)(ti & 0xFFFF) >> 6;
+            const uint32_t pt = (uint32_t)(ti >> 32);
+            XW_PROF(pf[3] += __builtin_amdgcn_s_memtime() - o0; pf[8]++;)
+            if (pt != t) { t = pt; load_layer((int)(f5 >> 32), (int)((ti >> 16) & 0xFFFF)); }
+        }
+        XW_PROF(pf[0] += __builtin_amdgcn_s_memtime() - k0; pf[11]++;)
+        v.valid = verdict;
+        v.cause = (verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0) | A.cause_or;
+        v.explored = ins;
+        v.fail_entry = verdict == JH_INVALID ? -(int64_t)tmax - 2 : -1;
+        if (lane == 0) A.out[key] = v;
+        if (A.cfg_slot && verdict == JH_INVALID) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            xw_dump_configs<SL>(A, memo, gen, tmax, key, T, lane);
+        }
+    }
+}
+
+#ifndef JH_XW_SL2
+#define JH_XW_SL2 1     // the two-slice search for windows of 65-128 members (0: four slices for all)
+#endif
 __device__ __forceinline__ void xw_waves(const XwArgs &A, size_t wv, unsigned long long *nm_sh, uint64_t *ring) {
     const int lane = threadIdx.x;
     XW_PROF(unsigned long long pf[12] = {0};)
     char *tb = A.scratch + wv * A.scratch_bytes;
     uint64_t *memo = A.memo + wv * A.memo_cap * XW_EW;
     uint64_t *stk = A.stack + wv * A.stack_cap * XW_FW;
-    const uint32_t cap_mask = A.memo_cap - 1;
     uint64_t zk[XW_SL];          // this lane's members' Zobrist words
 #pragma unroll
     for (int k = 0; k < XW_SL; k++) zk[k] = xw_zw(64 * k + lane);
@@ -5009,192 +5234,8 @@ __device__ __forceinline__ void xw_waves(const XwArgs &A, size_t wv, unsigned lo
             if (lane == 0) A.out[key] = v;
             continue;
         }
-        const uint32_t gen = (A.gen_base + (uint32_t)key + 1) & ((1u << GEN_BITS) - 1);
-        const uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
-
-        // the current layer's members: member 64k + lane in slice k
-        uint32_t t = 0, tmax = 0, s = (uint32_t)A.init_state, ins = 0, depth = 0;
-        uint64_t mask[XW_SL] = {0, 0, 0, 0};
-        uint32_t mrq[XW_SL];
-        int32_t mrr[XW_SL];
-        int w = 0, r = 0, start = 0, lo = 0;
-        // after a pop: the popped member's slice and which of its children
-        // were absent when the parent took that member. The table never
-        // drops an entry, so the others are still present: only these are
-        // probed again (none left: no round trip for the slice)
-        int k_known = -1;
-        uint64_t abs_known = 0;
-        // layer t's members: W(t) = P[o .. o + w)
-        auto load_layer = [&](int o, int wt) {
-            XW_PROF(const unsigned long long l0 = __builtin_amdgcn_s_memtime();)
-            lo = o; w = wt;
-            r = 0;
-#pragma unroll
-            for (int k = 0; k < XW_SL; k++) {
-                const int j = 64 * k + lane;
-                mrq[k] = RQ_EMPTY; mrr[k] = -2;
-                if (j < w) { const uint2 pr = T.P[o + j]; mrq[k] = pr.x; mrr[k] = (int32_t)pr.y; }
-                const uint64_t b = ballot(j < w && mrr[k] == (int32_t)t);
-                if (b) r = 64 * k + __builtin_ctzll(b);
-            }
-            XW_PROF(pf[2] += __builtin_amdgcn_s_memtime() - l0; pf[7]++;)
-        };
-        load_layer(T.woff[0], T.woff[1] - T.woff[0]);
-        uint32_t rlo = 0;      // the LDS ring holds frames [rlo, depth)
-        uint64_t hm = 0;       // Zobrist sum of the configuration's mask
-        XW_PROF(const unsigned long long k0 = __builtin_amdgcn_s_memtime();)
-        int verdict = -1;
-        for (;;) {
-            // expand: candidates from `start` on, in call order, slice by slice
-            bool took = false;
-            uint32_t u_r = t;
-            uint64_t nm_r[XW_SL] = {0, 0, 0, 0}, hr = 0;
-            bool lifted = false;
-            int wo0 = 0, wo1 = 0;          // woff[u_r], woff[u_r + 1]: loaded beside the probes
-            // unrolled: static slice indices (no register-array selects, no
-            // SGPR spills: 4.02 -> 3.37 s of C5's k_lin_xw)
-#pragma unroll
-            for (int k = 0; k < XW_SL && !took; k++) {
-                if (64 * k >= w) break;
-                const int j = 64 * k + lane;
-                const uint32_t req = mrq[k] & 0xFFFF;
-                const bool cl = j < w && j >= start && !((mask[k] >> lane) & 1) && (req == s || req == RQ_ANY) &&
-                                (k != k_known || ((abs_known >> lane) & 1));
-                const uint64_t cand = ballot(cl);
-                if (!cand) continue;
-                if (!lifted && (r >> 6) == k && ((cand >> (r & 63)) & 1)) {
-                    // the RET child: lift RET[t], keep lifting while the next
-                    // layer's RET op is already linearized, compact onto W(u)
-                    XW_PROF(const unsigned long long f0 = __builtin_amdgcn_s_memtime();)
-                    lifted = true;
-                    uint64_t lin[XW_SL];
-#pragma unroll
-                    for (int q = 0; q < XW_SL; q++) lin[q] = mask[q];
-                    lin[r >> 6] |= 1ULL << (r & 63);
-                    uint32_t u = t + 1;
-                    while (u < (uint32_t)n_ok) {
-                        bool hit = false;
-#pragma unroll
-                        for (int q = 0; q < XW_SL; q++) hit |= ((lin[q] >> lane) & 1) && mrr[q] == (int32_t)u;
-                        if (!ballot(hit)) break;
-                        u++;
-                    }
-                    u_r = u;
-                    if (u < (uint32_t)n_ok) {
-                        wo0 = T.woff[u]; wo1 = T.woff[u + 1];
-                        if (lane < XW_SL) nm_sh[lane] = 0;
-                        wave_sync();
-                        int base = 0;
-#pragma unroll
-                        for (int q = 0; q < XW_SL; q++) {
-                            const bool kept = 64 * q + lane < w && (mrr[q] < 0 || mrr[q] >= (int32_t)u);
-                            const uint64_t bk = ballot(kept);
-                            const int pos = base + mbcnt(bk);
-                            if (kept && ((lin[q] >> lane) & 1)) atomicOr(&nm_sh[pos >> 6], 1ULL << (pos & 63));
-                            base += __popcll(bk);
-                        }
-                        wave_sync();
-#pragma unroll
-                        for (int q = 0; q < XW_SL; q++) nm_r[q] = rfl64(nm_sh[q]);
-                        wave_sync();
-                        hr = xw_zsum(nm_r, zk, lane);
-                    }
-                    XW_PROF(pf[9] += __builtin_amdgcn_s_memtime() - f0;)
-                }
-                // every candidate lane probes its child
-                const bool is_r = j == r;
-                uint64_t cm[XW_SL];
-#pragma unroll
-                for (int q = 0; q < XW_SL; q++) cm[q] = is_r ? nm_r[q] : (mask[q] | (q == k ? (1ULL << lane) : 0ULL));
-                const uint32_t ct = is_r ? u_r : t, cs = mrq[k] >> 16;
-                const uint64_t chm = is_r ? hr : (hm ^ zk[k]);
-                bool found = false;
-                uint32_t slot = 0;
-                XW_PROF(const unsigned long long q0 = __builtin_amdgcn_s_memtime();)
-                if (cl) {
-                    const uint64_t pr = xw_probe(memo, cap_mask, gen, ct, cs, cm, chm, my_probes);
-                    found = (pr >> 32) == 0;
-                    slot = (uint32_t)pr;
-                }
-                const uint64_t absent = cand & ~ballot(found);
-                XW_PROF(pf[1] += __builtin_amdgcn_s_memtime() - q0; pf[6]++;)
-                if (!absent) continue;
-                const int i = __builtin_ctzll(absent);
-                if (ins >= budget) { verdict = JH_UNKNOWN; break; }
-                ins++;
-                XW_PROF(const unsigned long long h0 = __builtin_amdgcn_s_memtime();)
-                if (lane == i) xw_store(memo, slot, gen, ct, cs, cm);
-                // push the parent (t, its window, member, s, mask): HBM, and
-                // the LDS ring slot a pop reads while the frame stays in it
-                if (lane == 0) {
-                    uint64_t *f = stk + (size_t)depth * XW_FW;
-                    uint64_t *g = ring + (depth % XW_RING) * XW_FW;
-                    const uint64_t f4 = ((uint64_t)t << 32) | ((uint32_t)w << 16) | (uint32_t)(64 * k + i);
-                    const uint64_t f5 = ((uint64_t)(uint32_t)lo << 32) | s;
-                    f[0] = mask[0]; f[1] = mask[1]; f[2] = mask[2]; f[3] = mask[3]; f[4] = f4; f[5] = f5; f[6] = hm;
-                    f[7] = absent;
-                    g[0] = mask[0]; g[1] = mask[1]; g[2] = mask[2]; g[3] = mask[3]; g[4] = f4; g[5] = f5; g[6] = hm;
-                    g[7] = absent;
-                }
-                depth++;
-                if (depth - rlo > (uint32_t)XW_RING) rlo = depth - XW_RING;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                XW_PROF(pf[4] += __builtin_amdgcn_s_memtime() - h0; pf[5]++;)
-                s = (uint32_t)readlane((int)cs, i);
-                hm = readlane64(chm, i);
-                const uint32_t nt = (uint32_t)readlane((int)ct, i);
-#pragma unroll
-                for (int q = 0; q < XW_SL; q++) mask[q] = readlane64(cm[q], i);
-                took = true;
-                start = 0;
-                k_known = -1;
-                if (nt != t) {
-                    t = nt;
-                    tmax = max(tmax, t);
-                    if (t >= (uint32_t)n_ok) { verdict = JH_VALID; break; }
-                    load_layer(wo0, wo1 - wo0);     // nt != t only for the RET child: t == u_r
-                }
-            }
-            if (verdict >= 0) break;
-            if (took) continue;
-            // pop
-            if (depth == 0) { verdict = JH_INVALID; break; }
-            XW_PROF(const unsigned long long o0 = __builtin_amdgcn_s_memtime();)
-            depth--;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            uint64_t ti, f5;
-            if (depth >= rlo) {
-                const uint64_t *g = ring + (depth % XW_RING) * XW_FW;
-#pragma unroll
-                for (int q = 0; q < XW_SL; q++) mask[q] = rfl64(g[q]);
-                ti = rfl64(g[4]); f5 = rfl64(g[5]); hm = rfl64(g[6]); abs_known = rfl64(g[7]);
-            } else {
-                const uint64_t *f = stk + (size_t)depth * XW_FW;
-#pragma unroll
-                for (int q = 0; q < XW_SL; q++) mask[q] = rfl64(f[q]);
-                ti = rfl64(f[4]); f5 = rfl64(f[5]); hm = rfl64(f[6]); abs_known = rfl64(f[7]);
-                rlo = depth;
-                XW_PROF(pf[10]++;)
-            }
-            s = (uint32_t)f5;
-            start = (int)(ti & 0xFFFF) + 1;
-            k_known = (int)(ti & 0xFFFF) >> 6;
-            const uint32_t pt = (uint32_t)(ti >> 32);
-            XW_PROF(pf[3] += __builtin_amdgcn_s_memtime() - o0; pf[8]++;)
-            if (pt != t) { t = pt; load_layer((int)(f5 >> 32), (int)((ti >> 16) & 0xFFFF)); }
-        }
-        XW_PROF(pf[0] += __builtin_amdgcn_s_memtime() - k0; pf[11]++;)
-        v.valid = verdict;
-        v.cause = (verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0) | A.cause_or;
-        v.explored = ins;
-        v.fail_entry = verdict == JH_INVALID ? -(int64_t)tmax - 2 : -1;
-        if (lane == 0) A.out[key] = v;
-        if (A.cfg_slot && verdict == JH_INVALID) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            xw_dump_configs(A, memo, gen, tmax, key, T, lane);
-        }
+        if (JH_XW_SL2 && maxw <= 128) xw_search<2>(A, key, T, n_ok, memo, stk, zk, nm_sh, ring, my_probes XW_PROFA(pf));
+        else xw_search<4>(A, key, T, n_ok, memo, stk, zk, nm_sh, ring, my_probes XW_PROFA(pf));
     }
     for (int o = 32; o > 0; o >>= 1) my_probes += __shfl_xor(my_probes, o);
     if (lane == 0 && A.probes) atomicAdd(A.probes, my_probes);
@@ -5488,6 +5529,18 @@ __global__ void k_mark_deferred(const uint64_t *__restrict__ d64, int n, jh_key_
         v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_DEFERRED; v.fail_entry = -1; v.explored = (int64_t)(pk >> 32);
         v.previous_ok = -1; v.last_op = -1; v.analyzer = JH_ANALYZER_WGL; v.reserved = 0;
         out[(uint32_t)pk] = v;
+    }
+}
+
+// stage 1 of a two-stage check: keys of a list (the 65-256-member keys) come
+// back deferred with progress 0
+__global__ void k_mark_list_deferred(const int32_t *__restrict__ list, int n, jh_key_verdict *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        jh_key_verdict v;
+        v.valid = JH_UNKNOWN; v.cause = JH_CAUSE_DEFERRED; v.fail_entry = -1; v.explored = 0;
+        v.previous_ok = -1; v.last_op = -1; v.analyzer = JH_ANALYZER_WGL; v.reserved = 0;
+        out[list[i]] = v;
     }
 }
 
@@ -6259,6 +6312,13 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                     waves1, tot[3], (double)tot[2] / std::max(1ULL, tot[3]), tot[4], tot[5], tot[6], tot[7], tot[10],
                     tot[11], tot[12], tot[13], tot[14], tot[8], (double)tot[2] / std::max(1ULL, tot[4]), (double)tot[9] / waves1, mx9);
             HIP_TRY(hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * (waves1 + 512) * 16, st));
+        }
+        // stage 1 of a two-stage check: the 65-256-member keys are heavy keys
+        // too -- they come back deferred (progress 0) for the pool, unsearched
+        if (n_x > 0 && p1_only) {
+            k_mark_list_deferred<<<grid_for(n_x, 256), 256, 0, st>>>(list_x, n_x, out_dev);
+            HIP_TRY(hipGetLastError());
+            n_x = 0;
         }
         // windows wider than 64: k_lin_xw on the third stream, alongside phases 2 and 3
         if (n_x > 0) {

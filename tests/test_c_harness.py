@@ -143,3 +143,24 @@ def test_multi_context_pooled_heavy_keys(built, tmp_path, devs):
     out = _check_vs_oracle(tmp_path, cols, devs, quick=40)
     summ = dict(kv.split("=") for kv in out.split("\n")[1].split())
     assert int(summ["n_deferred"]) > 50
+
+
+@pytest.mark.gpu
+def test_multi_context_pools_wide_window_keys(built, tmp_path):
+    """stage 1 of the two-stage check hands the 65-256-member
+    keys back deferred too (they are the heaviest), so stage 2 pools them
+    with the rest. C5-shaped keys (50 threads per key, many :info) on two
+    contexts: several windows over 64 members, every verdict field equal to
+    the oracle's."""
+    from jepsen_amd import synth
+    cols = synth.cas_register(n_keys=24, ops_per_key=160, threads_per_key=50, readers=25, n_values=5,
+                              process_limit=100, groups=10, init_nil=True, p_info=0.2, p_invalid=0.05,
+                              nemesis_every=10000, seed=23)[0]
+    from jepsen_amd import _abi as A
+    wide = 0
+    for k in range(cols.n_keys):
+        t = cols.type[cols.key == k]
+        opened = np.cumsum(np.where(t == A.TYPE_INVOKE, 1, np.where((t == A.TYPE_OK) | (t == A.TYPE_FAIL), -1, 0)))
+        wide += int(opened.max() > 64)
+    assert wide >= 2
+    _check_vs_oracle(tmp_path, cols, "0,0")

@@ -219,6 +219,23 @@ def test_c5_full(ctx):
            (cs.valid, cs.n_invalid, cs.n_unknown, cs.first_fail_entry)
 
 
+@pytest.mark.parametrize("budget", [1 << 20, 1 << 22])
+def test_c5_budget_subset(ctx, budget):
+    """C5's budget sweep, held to the oracle on a bounded
+    subset at each budget: eight C5 keys that end :unknown at 2^20 (deep
+    searches, windows over 64 members among them), checked at 2^20 and 2^22
+    inserts per key -- verdict, cause and WGL count equal key by key."""
+    cols, _ = synth.cas_register(n_keys=1000, threads_per_key=50, readers=25, process_limit=100,
+                                 p_info=0.2, p_invalid=0.01, seed=5)
+    own = np.ones(cols.n_keys, np.int64)
+    own[[3, 17, 42, 101, 256, 512, 777, 999]] = 0
+    sub, _, _ = shard.shard_history(cols, own, 0)
+    g, gs = ctx.check_cas_independent(sub, budget=budget)
+    c, cs = oracle.check_cas_independent(sub, budget=budget, threads=8)
+    _same(g, c)
+    assert gs.n_unknown == cs.n_unknown
+
+
 # --------------------------------------------------- independent o compose --
 class _Recorder(CK.Checker):
     """A non-linearizable member of the composition (the timeline/html slot of

@@ -274,6 +274,9 @@ def main():
                                        dtype=torch.int64))
             dist.all_reduce(red_max, op=dist.ReduceOp.MAX)
             dist.all_reduce(red_sum, op=dist.ReduceOp.SUM)
+            # the line reports the whole job's verdict counts
+            mx, sm = red_max.tolist(), red_sum.tolist()
+            s.valid, s.n_invalid, s.n_unknown, s.explored = mx[0], sm[0], sm[1], sm[3]
         return s
 
     for _ in range(args.warmup):

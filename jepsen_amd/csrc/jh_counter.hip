@@ -134,32 +134,7 @@ constexpr int PER = CHUNK / PACK_THREADS;   // rows per thread per chunk (row k 
 // chunk already showed every later row of its process in the chunk to be
 // :info, so the walk starts at the chunk's end (a crashed op's walk then ends
 // at once: its process' last row lies inside the chunk).
-#ifndef PACK_BLOCKS_PER_CU
-#define PACK_BLOCKS_PER_CU 2
-#endif
-// A block-wide barrier over LDS only: the next tile's column loads stay in
-// flight across it (__syncthreads' workgroup fence would wait for them).
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// Round 4: a software pipeline over the block's tiles (tile, tile + grid, ...):
-// the four columns of the next tile are loaded into registers while this
-// tile's LDS passes run, so a block always has a tile's loads in flight
-// (round 3 ran one tile per block and its loads waited on its LDS passes).
-// four waves per SIMD (two blocks per CU, 128 VGPRs): the pipeline's second
-// tile in registers costs the occupancy round 3 had (four blocks at 62 VGPRs)
-#ifndef JH_PACK_WPE
-#define JH_PACK_WPE 4
-#endif
-#if JH_PACK_WPE > 0
-#define JH_PACK_ATTR __attribute__((amdgpu_waves_per_eu(JH_PACK_WPE)))
-#else
-#define JH_PACK_ATTR
-#endif
-__global__ void __launch_bounds__(PACK_THREADS) JH_PACK_ATTR k_cnt_pack(const int64_t *__restrict__ proc,
+__global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__restrict__ proc,
                                                   const int64_t *__restrict__ type,
                                                   const int64_t *__restrict__ f,
                                                   const int64_t *__restrict__ val, int64_t n,
@@ -175,48 +150,33 @@ __global__ void __launch_bounds__(PACK_THREADS) JH_PACK_ATTR k_cnt_pack(const in
     __shared__ int16_t rs[CHUNK];                   // each row's hash slot (-1: none)
     __shared__ unsigned long long M[PAIR_GROUPS][PAIR_PROCS];
     __shared__ int nd, nls;
-    __shared__ long long sh[3][PACK_THREADS / 64];
+    __shared__ long long sh[5][PACK_THREADS / 64];
     const int tid = threadIdx.x;
-    const int64_t n_tiles = (n + CHUNK - 1) / CHUNK;
     long long am = 0, na = 0;
-    // the tile's rows in flight, row k * PACK_THREADS + tid: the low words of
-    // process (offset < 2^28 from pmin), type and f, and the whole value
-    // (the lines are fetched whole either way; half the registers in flight)
-    const int32_t *proc32 = (const int32_t *)proc, *type32 = (const int32_t *)type, *f32 = (const int32_t *)f;
-    const int32_t *val32 = (const int32_t *)val;
-    int32_t rp[PER], rt[PER], rf[PER];
-    long long cv[PER];
-    auto load_tile = [&](int64_t tile) {
-        const int64_t c0 = tile * CHUNK;
+    long long t_lo = 0, t_hi = 0, t_nr = 0;          // this tile's sums
+    {
+        const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
+        const int nc = (int)min<int64_t>(CHUNK, n - c0);
+        // every row of the thread in flight at once, then compacted
+        // (process offset, f2 << 2 | type, value)
+        long long rp[PER], rt[PER], rf[PER], cv[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const int64_t r = c0 + k * PACK_THREADS + tid;
-            const uint32_t o = 2u * (uint32_t)r;          // rows < 2^31 (jh_check_counter)
-            if (tile < n_tiles && r < n) { rp[k] = proc32[o]; rt[k] = type32[o]; rf[k] = f32[o]; cv[k] = *(const long long *)(val32 + o); }
-            else { rp[k] = (int32_t)pmin; rt[k] = T_INFO; rf[k] = 0; cv[k] = 0; }
+            if (r < n) { rp[k] = proc[r]; rt[k] = type[r]; rf[k] = f[r]; cv[k] = val[r]; }
+            else { rp[k] = pmin; rt[k] = T_INFO; rf[k] = 0; cv[k] = 0; }
         }
-    };
-    load_tile(blockIdx.x);
-    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        const int64_t c0 = tile * CHUNK;
-        const int nc = (int)min<int64_t>(CHUNK, n - c0);
-        long long t_lo = 0, t_hi = 0, t_nr = 0;          // this tile's sums
-        // compacted (process offset, f2 << 2 | type) and the value, then the
-        // next tile's loads issued into the freed registers
         uint32_t cp[PER], cx[PER];
-        long long vv[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            cp[k] = (uint32_t)rp[k] - (uint32_t)pmin;                              // span < 2^28
+            cp[k] = (uint32_t)(rp[k] - pmin);                                      // span < 2^28
             const uint32_t f2 = rf[k] == JH_F_ADD ? F2_ADD : rf[k] == JH_F_READ ? F2_READ : F2_OTHER;
             cx[k] = (f2 << 2) | (uint32_t)(rt[k] & 3);
-            vv[k] = cv[k];
         }
-        load_tile(tile + gridDim.x);
         for (int i = tid; i < HSLOTS; i += PACK_THREADS) { hk[i] = 0; hv[i] = -1; hc[i] = -1; }
         for (int i = tid; i < PAIR_GROUPS * PAIR_PROCS; i += PACK_THREADS) (&M[0][0])[i] = 0;
         if (tid == 0) { nd = 0; nls = 0; }
-        lds_barrier();
+        __syncthreads();
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const int i = k * PACK_THREADS + tid;
@@ -227,7 +187,7 @@ __global__ void __launch_bounds__(PACK_THREADS) JH_PACK_ATTR k_cnt_pack(const in
             sc[i] = (uint8_t)cx[k];
             sp[i] = -1;
             if (f2 == F2_ADD && (ty == T_INVOKE || ty == T_OK)) {
-                const long long v = vv[k];
+                const long long v = cv[k];
                 if (v != JH_NIL) am = max(am, v < 0 ? (v == LLONG_MIN ? LLONG_MAX : -v) : v);
                 na++;
             }
@@ -254,7 +214,7 @@ __global__ void __launch_bounds__(PACK_THREADS) JH_PACK_ATTR k_cnt_pack(const in
             else atomicMax(&last[pk], (int)r);
             rs[i] = (int16_t)slot;
         }
-        lds_barrier();
+        __syncthreads();
         // compact process index of every row (the hash is complete now), and the
         // group masks of non-:info rows
         int8_t rc[PER];
@@ -268,7 +228,7 @@ __global__ void __launch_bounds__(PACK_THREADS) JH_PACK_ATTR k_cnt_pack(const in
             rc[k] = (int8_t)c;
             if (c >= 0 && (sc[i] & 3) != T_INFO) atomicOr(&M[i >> 6][c], 1ULL << (i & 63));
         }
-        lds_barrier();
+        __syncthreads();
         bool walk_from_end[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
@@ -295,7 +255,7 @@ __global__ void __launch_bounds__(PACK_THREADS) JH_PACK_ATTR k_cnt_pack(const in
             sp[i] = (int16_t)got;                      // -1: spill (no completion in the chunk)
             if (got >= 0) sp[got] = (int16_t)i;
         }
-        lds_barrier();
+        __syncthreads();
         // the contribution words
 #pragma unroll
         for (int k = 0; k < PER; k++) {
@@ -308,6 +268,7 @@ __global__ void __launch_bounds__(PACK_THREADS) JH_PACK_ATTR k_cnt_pack(const in
             uint32_t w = CW_NONE;
             if (ty == T_INVOKE) {
                 if (c == -1) {
+                    // spills gather in LDS: one global atomic per chunk
                     // the chunk's own spill region: no global atomic
                     spill[c0 + atomicAdd(&nls, 1)] = walk_from_end[k] ? ~(int32_t)r : (int32_t)r;
                     w = f2 == F2_READ ? CW_INVREAD : f2 == F2_ADD ? CW_PEND : CW_NONE;
@@ -315,7 +276,7 @@ __global__ void __launch_bounds__(PACK_THREADS) JH_PACK_ATTR k_cnt_pack(const in
                     w = CW_INVREAD;
                 } else if (f2 == F2_ADD && c >= 0 && (sc[c] & 3) != T_FAIL) {
                     // (remove :fails?) keeps it: upper += (or inv ok)
-                    long long v = vv[k];
+                    long long v = cv[k];
                     bool own = true;
                     if (v == JH_NIL) { v = val[c0 + c]; own = false; }
                     if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
@@ -328,7 +289,7 @@ __global__ void __launch_bounds__(PACK_THREADS) JH_PACK_ATTR k_cnt_pack(const in
             } else if (ty == T_OK || ty == T_FAIL) {
                 const uint32_t u = c < 0 ? CW_U : 0u;      // no invocation in the chunk (yet)
                 if (ty == T_OK && f2 == F2_ADD) {
-                    const long long v = vv[k];
+                    const long long v = cv[k];
                     if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
                     else { w = cw_make(CW_LO, v); t_lo += v; }
                 } else if (ty == T_OK && f2 == F2_READ) {
@@ -344,29 +305,29 @@ __global__ void __launch_bounds__(PACK_THREADS) JH_PACK_ATTR k_cnt_pack(const in
             }
             cw[r] = w;
         }
-        for (int o = 32; o > 0; o >>= 1) {
-            t_lo += (long long)__shfl_xor(t_lo, o); t_hi += (long long)__shfl_xor(t_hi, o); t_nr += (long long)__shfl_xor(t_nr, o);
-        }
-        if ((tid & 63) == 0) { sh[0][tid >> 6] = t_lo; sh[1][tid >> 6] = t_hi; sh[2][tid >> 6] = t_nr; }
-        lds_barrier();                                    // (also orders every nls increment)
-        if (tid == 0) {
-            for (int w = 1; w < PACK_THREADS / 64; w++) { t_lo += sh[0][w]; t_hi += sh[1][w]; t_nr += sh[2][w]; }
-            agg[tile] = CntAcc{t_lo, t_hi, (int)t_nr, 0};
-            spill_n[tile] = nls;
-        }
-        // the last row of each of the chunk's processes (these few atomics hit
-        // the same addresses from every block: no barrier waits on them)
-        for (int i = tid; i < HSLOTS; i += PACK_THREADS)
-            if (hk[i]) atomicMax(&last[hk[i] - 1], hv[i]);
-        lds_barrier();                                    // the next tile clears the LDS tables
     }
     for (int o = 32; o > 0; o >>= 1) {
         am = max(am, (long long)__shfl_xor(am, o)); na += (long long)__shfl_xor(na, o);
+        t_lo += (long long)__shfl_xor(t_lo, o); t_hi += (long long)__shfl_xor(t_hi, o); t_nr += (long long)__shfl_xor(t_nr, o);
     }
     if ((tid & 63) == 0) {
+        sh[0][tid >> 6] = am; sh[1][tid >> 6] = na; sh[2][tid >> 6] = t_lo; sh[3][tid >> 6] = t_hi; sh[4][tid >> 6] = t_nr;
+    }
+    __syncthreads();                                  // (also orders every nls increment)
+    if (tid == 0) {
+        for (int w = 1; w < PACK_THREADS / 64; w++) {
+            am = max(am, sh[0][w]); na += sh[1][w]; t_lo += sh[2][w]; t_hi += sh[3][w]; t_nr += sh[4][w];
+        }
+        agg[blockIdx.x] = CntAcc{t_lo, t_hi, (int)t_nr, 0};
+        spill_n[blockIdx.x] = nls;
         if (am) atomicMax(&m->amax_abs, am);
         if (na) atomicAdd((unsigned long long *)&m->n_add, (unsigned long long)na);
     }
+    // the last row of each of the chunk's processes, after the last barrier
+    // (these few atomics hit the same addresses from every block: no barrier
+    // waits on them)
+    for (int i = tid; i < HSLOTS; i += PACK_THREADS)
+        if (hk[i]) atomicMax(&last[hk[i] - 1], hv[i]);
 }
 
 // the spilled invocations: one thread each walks its process' rows forward
@@ -568,9 +529,7 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
     int32_t *spill_n = ctx->ws<int32_t>(WS_C_FLAG, n_tiles);       // likewise
     CntAcc *pre = agg + n_tiles;
     CntAcc *total = pre + n_tiles;
-    // the resident blocks, each pipelining its tiles (k_cnt_pack)
-    const int pack_grid = (int)std::min<int64_t>(n_tiles, (int64_t)ctx->n_cu * PACK_BLOCKS_PER_CU);
-    k_cnt_pack<<<pack_grid, PACK_THREADS, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
+    k_cnt_pack<<<(int)n_tiles, PACK_THREADS, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
                                                      mh.pmin, last, cw, pair, spill, spill_n, m, agg);
     k_cnt_pair_spill<<<grid_for(n_tiles * 16, 256, 16384), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
                                                                       mh.pmin, last, spill, spill_n, n_tiles, cw, pair, m, agg);

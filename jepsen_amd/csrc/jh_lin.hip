@@ -2268,7 +2268,12 @@ __global__ void __launch_bounds__(256) k_list_cost(const int32_t *__restrict__ l
 
 // phase 1: every key under the quick budget (STREAM: the producer of the
 // streaming heavy-key pass's live lists)
-#ifdef JH_P1_WPE
+// six waves per SIMD (<= 80 VGPRs, 24 per CU; LDS allows 26): phase 1
+// 16.5 -> 15.7 ms on C3 (round 4, profiles/r04); JH_P1_WPE=0: no cap
+#ifndef JH_P1_WPE
+#define JH_P1_WPE 6
+#endif
+#if JH_P1_WPE > 0
 #define JH_P1_ATTR __attribute__((amdgpu_waves_per_eu(JH_P1_WPE)))
 #else
 #define JH_P1_ATTR
@@ -4309,9 +4314,33 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                 int room = 1;
                 if (lane == 0) {
                     const uint32_t old = atomicAdd(&sh.lcount, cand);
-                    if (old + cand > (uint32_t)(LSET * 3 / 4)) { atomicSub(&sh.lcount, cand); sh.ovf = 1; room = 0; }
+                    if (old + cand > (uint32_t)(LSET * 3 / 4)) { atomicSub(&sh.lcount, cand); room = 0; }
                 }
-                if (!readlane(room, 0)) return;
+                if (!readlane(room, 0)) {
+                    // the batch's reservation counts its duplicates too (and the
+                    // other waves' batches in flight): near the limit, room is
+                    // taken per new configuration instead, so a layer moves to
+                    // the global set only when the set is really 3/4 full
+                    // (round 3's batched reservation alone moved C4's layers
+                    // early: C4 222.7 -> 245 ms, round 4)
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        if (!ck[q]) continue;
+                        const uint64_t kq = ck[q] + 1;
+                        for (uint32_t hh = lset_hash(kq);; hh = (hh + 1) & (LSET - 1)) {
+                            const unsigned long long x = lset[hh];
+                            if (x == kq) break;                          // present
+                            if (x != 0) continue;
+                            const uint32_t old = atomicAdd(&sh.lcount, 1u);
+                            if (old + 1 > (uint32_t)(LSET * 3 / 4)) { atomicSub(&sh.lcount, 1u); sh.ovf = 1; break; }
+                            const unsigned long long y = atomicCAS((unsigned long long *)&lset[hh], 0ULL, kq);
+                            if (y == 0) { nw[q] = true; break; }
+                            atomicSub(&sh.lcount, 1u);                   // lost the slot
+                            if (y == kq) break;
+                        }
+                    }
+                    return;
+                }
                 uint64_t k[8];
                 uint32_t h[8];
                 unsigned long long pv[8];

@@ -26,6 +26,11 @@ timeout -k 10 300 $B --workload c5 --steps 1 --warmup 0 --budget 4194304 > $O/c5
 exit 0
 fi
 C="python -u bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 --no-parity"
+# C4 on this box: rounds 2 and 3 (git worktrees r2ref/, r3ref/) against HEAD
+for t in r2ref r3ref; do
+  (cd $R/$t && timeout -k 10 300 python -u bench.py --workload c4 --steps 3 --warmup 1 --no-cpu --e2e 0 --no-parity > $R/$O/c4_$t.json 2> $R/$O/c4_$t.err) || exit 1
+done
+timeout -k 10 300 python -u bench.py --workload c4 --steps 3 --warmup 1 --no-cpu --e2e 0 --no-parity > $O/c4_head.json 2> $O/c4_head.err || exit 1
 for rep in 1 2; do
   timeout -k 10 120 $C > $O/c3_head_$rep.json 2> $O/c3_head_$rep.err || exit 1
   JH_LIB=$V/libjh_p1w6.so timeout -k 10 120 $C > $O/c3_p1w6_$rep.json 2> $O/c3_p1w6_$rep.err || exit 1

@@ -4202,6 +4202,9 @@ __device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int k
     if (lane == 0) A.cfg_n[slot] = nsel;
 }
 
+#ifndef JH_BFS_ITEMS
+#define JH_BFS_ITEMS 0
+#endif
 template <bool L>
 __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, uint64_t *gset,
                         uint64_t *pend, uint64_t *front) {
@@ -4526,9 +4529,13 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             if (A.dbg && tid == 0) { pt = __builtin_amdgcn_s_memtime(); atomicAdd(&g_bfs_prof[0], pt - rt0); atomicAdd(&g_bfs_prof[4], 1ULL); })
             if (sh.status & 4) break;
             for (;;) {
-            // one item per (frontier configuration, 8 members): a round's work
-            // spread over every wave, not one configuration's members in series
-            const unsigned ng = (unsigned)(w + 7) >> 3;
+            // one configuration per lane, its members eight at a time in series
+            // (round 2's layout; round 3 split a round into (configuration, 8
+            // members) items over every wave, JH_BFS_ITEMS=1: measured in round
+            // 4 on one box, C4 250 -> 222 ms, C3 ranks 0 / 3 / 6 43.3 / 72.7 /
+            // 82.6 -> 41.3 / 70.8 / 78.3 ms with this layout; the bisect of
+            // round 3's C4 regression pointed at that change, profiles/r04/)
+            const unsigned ng = JH_BFS_ITEMS ? (unsigned)(w + 7) >> 3 : 1u;
             const unsigned items = nf * ng;
             for (unsigned i0 = tid - lane; i0 < items; i0 += BFS_THREADS) {
                 const unsigned it = i0 + lane;
@@ -4536,8 +4543,9 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                 const unsigned i = it < items ? it / ng : 0;
                 const uint64_t c = it < items ? fcur[i] : 0xFFFFFFFFull;    // past the end: every member taken
                 const uint32_t s = (uint32_t)(c >> 32), mask = (uint32_t)c;
-                {
-                    const int j0 = it < items ? (int)(it - i * ng) * 8 : 0;
+                const int jb = JH_BFS_ITEMS && it < items ? (int)(it - i * ng) * 8 : 0;
+                const int je = JH_BFS_ITEMS ? jb + 8 : w;
+                for (int j0 = jb; j0 < je; j0 += 8) {
                     uint64_t ck[8];       // same-layer children of members j0..j0+7: s2 << 32 | mask'
                     Win8 wn;
                     win8(sh, j0, wn);

@@ -4205,6 +4205,14 @@ __device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int k
 #ifndef JH_BFS_ITEMS
 #define JH_BFS_ITEMS 0
 #endif
+// JH_BFS_ROOM_EXACT=1: a refused batch reservation (it counts duplicates and
+// other waves' batches) retries per new configuration before the layer moves
+// to the global set. Measured in round 4 (profiles/r04/bfs_room/): slower --
+// C4 222 vs 215 ms, C3 ranks 0 / 3 / 6 42.5 / 71.3 / 78.1 vs 40.4 / 70.3 /
+// 77.3 ms -- so off.
+#ifndef JH_BFS_ROOM_EXACT
+#define JH_BFS_ROOM_EXACT 0
+#endif
 template <bool L>
 __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, uint64_t *gset,
                         uint64_t *pend, uint64_t *front) {
@@ -4320,6 +4328,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                     if (old + cand > (uint32_t)(LSET * 3 / 4)) { atomicSub(&sh.lcount, cand); room = 0; }
                 }
                 if (!readlane(room, 0)) {
+                    if (!JH_BFS_ROOM_EXACT) { if (lane == 0) sh.ovf = 1; return; }
                     // the batch's reservation counts its duplicates too (and the
                     // other waves' batches in flight): near the limit, room is
                     // taken per new configuration instead, so a layer moves to

@@ -269,15 +269,19 @@ def two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=None
             base += int(n)
     pool.sort()
     mine = [e for i, e in enumerate(pool) if i % world == rank]
-    # my share's columns: each key's rows, keys renumbered densely
-    parts = []
-    for j, (_, r, k, base, n) in enumerate(mine):
-        blk = packs[r].reshape(len(COLS) + 1, -1)[:, base:base + n].clone()
-        blk[COLS.index("key")] = j
-        parts.append(blk)
+    # my share's columns: each key's rows (one gather over every rank's
+    # offer), keys renumbered densely
     v2 = None
     if mine:
-        allc = torch.cat(parts, 1)
+        nc = len(COLS) + 1
+        width = [p.numel() // nc for p in packs]
+        start = np.concatenate([[0], np.cumsum(width)[:-1]]).astype(np.int64)
+        idx = np.concatenate([np.arange(start[r] + base, start[r] + base + n, dtype=np.int64)
+                              for _, r, _, base, n in mine])
+        kid = np.repeat(np.arange(len(mine), dtype=np.int64), [e[4] for e in mine])
+        allp = torch.cat([p.reshape(nc, -1) for p in packs], 1)
+        allc = allp.index_select(1, torch.from_numpy(idx).to(allp.device))
+        allc[COLS.index("key")] = torch.from_numpy(kid).to(allp.device)
         sub = {c: allc[i].contiguous() for i, c in enumerate(COLS)}
         src_row = allc[len(COLS)].cpu().numpy()
         v2 = stage2(sub, len(mine)).copy()

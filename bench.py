@@ -79,7 +79,7 @@ def phase_rooflines(sums, n_entries):
     out = {}
     for name, (tf, pf, ef, kf, kern) in PHASES.items():
         ms = float(np.mean([x[tf] for x in sums]))
-        keys = float(np.mean([_field(x, kf) for x in sums])) if kf else 1.0
+        keys = float(np.mean([_field(x, kf) for x in sums])) if kf else float(np.mean([x["n_keys"] for x in sums]))
         if ms <= 0 or keys <= 0:
             continue
         probes = float(np.mean([x[pf] for x in sums]))

@@ -3619,6 +3619,12 @@ __device__ __forceinline__ void bfs_lookup_batch(const ulonglong2 *ent, uint32_t
     }
 }
 
+// the count pass's same-layer liveness: one item per (node, 8 members) (1,
+// kept) or one node per thread with its members in series (0: measured in
+// round 4, ranks 3 / 4 / 6 1.5-2.7 ms slower, profiles/r04/bfs_lv/)
+#ifndef JH_BFS_LV_ITEMS
+#define JH_BFS_LV_ITEMS 1
+#endif
 // the window's operations of members j0 .. j0+7 (j0 a multiple of 8 below
 // 64): four 16-byte LDS reads issued together, instead of one dependent LDS
 // round trip per member inside the children's branches
@@ -3823,16 +3829,22 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
                 ord[atomicAdd(&hist[35 + __popc((uint32_t)lk[i])], 1u)] = (uint16_t)i;
             __syncthreads();
             const int pmin = (int)hist[0], pmax = (int)hist[1];
-            const uint32_t nb = (uint32_t)(w + 7) / 8;
+            // JH_BFS_LV_ITEMS: one item per (node, 8 members) (round 3); else
+            // one node per thread, its members eight at a time until a live
+            // child is found (round 4)
+            const uint32_t nb = JH_BFS_LV_ITEMS ? (uint32_t)(w + 7) / 8 : 1u;
             for (int p = pmax; p >= pmin; p--) {
-                // one item per (node, 8 members): the 8 children's LDS probes issue together
+                // the 8 children's LDS probes issue together
                 const uint32_t cnt = hist[2 + p], b0 = hist[35 + p] - cnt;
                 for (uint32_t q = tid; q < cnt * nb; q += BFS_THREADS) {
                     const uint32_t i = ord[b0 + q / nb];
-                    const int j0 = (int)(q % nb) * 8;
                     if (lv[i]) continue;
                     const uint64_t x = lk[i];
                     const uint32_t s0 = (uint32_t)(x >> 32) & 0xFFF, m0 = (uint32_t)x;
+                    const int jb = JH_BFS_LV_ITEMS ? (int)(q % nb) * 8 : 0;
+                    const int je = JH_BFS_LV_ITEMS ? jb + 8 : w;
+                    bool live = false;
+                    for (int j0 = jb; j0 < je && !live; j0 += 8) {
                     uint64_t ck[8];
                     uint32_t h[8], e[8];
                     Win8 wn;
@@ -3852,7 +3864,6 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
                     uint64_t kk[8];
 #pragma unroll
                     for (int u = 0; u < 8; u++) kk[u] = e[u] ? lk[e[u] - 1] : 0;
-                    bool live = false;
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
                         if (!ck[u] || !e[u]) continue;
@@ -3865,6 +3876,7 @@ __device__ void bfs_wgl_count(const BfsArgs &A, BfsShared &sh, int tid, int key,
                                 if (lk[ee - 1] == ck[u]) { idx = ee; break; }
                             }
                         if (idx && lv[idx - 1]) live = true;
+                    }
                     }
                     if (live) lv[i] = 1;
                 }

@@ -147,7 +147,6 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
     __shared__ int8_t hc[HSLOTS];                   // its compact index, -1 beyond PAIR_PROCS
     __shared__ uint8_t sc[CHUNK];                   // the chunk's rows: f2 << 2 | type
     __shared__ int16_t sp[CHUNK];                   // each row's partner in the chunk (-1: none)
-    __shared__ int16_t rs[CHUNK];                   // each row's hash slot (-1: none)
     __shared__ unsigned long long M[PAIR_GROUPS][PAIR_PROCS];
     __shared__ int nd, nls;
     __shared__ long long sh[5][PACK_THREADS / 64];
@@ -177,6 +176,11 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
         for (int i = tid; i < PAIR_GROUPS * PAIR_PROCS; i += PACK_THREADS) (&M[0][0])[i] = 0;
         if (tid == 0) { nd = 0; nls = 0; }
         __syncthreads();
+        // each row's hash slot (-1: none) and kind stay in this thread's
+        // registers: only the pairing reads other rows' (round 4)
+        int rsl[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) rsl[k] = -1;
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const int i = k * PACK_THREADS + tid;
@@ -185,7 +189,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
             const uint32_t pk = cp[k];
             const uint32_t ty = cx[k] & 3, f2 = cx[k] >> 2;
             sc[i] = (uint8_t)cx[k];
-            sp[i] = -1;
+            if (ty != T_INVOKE) sp[i] = -1;            // an invocation's partner stays in registers
             if (f2 == F2_ADD && (ty == T_INVOKE || ty == T_OK)) {
                 const long long v = cv[k];
                 if (v != JH_NIL) am = max(am, v < 0 ? (v == LLONG_MIN ? LLONG_MAX : -v) : v);
@@ -212,7 +216,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
             // (lane + 1 holds row i + 1: past the chunk's end it is inactive)
             if (slot >= 0) { if ((tid & 63) == 63 || i + 1 >= nc || nxt != slot) atomicMax(&hv[slot], (int)r); }
             else atomicMax(&last[pk], (int)r);
-            rs[i] = (int16_t)slot;
+            rsl[k] = slot;
         }
         __syncthreads();
         // compact process index of every row (the hash is complete now), and the
@@ -223,19 +227,21 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
             const int i = k * PACK_THREADS + tid;
             rc[k] = -1;
             if (i >= nc) continue;
-            const int slot = rs[i];
+            const int slot = rsl[k];
             const int c = slot >= 0 ? hc[slot] : -1;
             rc[k] = (int8_t)c;
-            if (c >= 0 && (sc[i] & 3) != T_INFO) atomicOr(&M[i >> 6][c], 1ULL << (i & 63));
+            if (c >= 0 && (cx[k] & 3) != T_INFO) atomicOr(&M[i >> 6][c], 1ULL << (i & 63));
         }
         __syncthreads();
         bool walk_from_end[PER];
+        int gotk[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const int i = k * PACK_THREADS + tid;
             walk_from_end[k] = false;
+            gotk[k] = -1;
             if (i >= nc) continue;
-            const uint32_t x = sc[i];
+            const uint32_t x = cx[k];
             if ((x & 3) != T_INVOKE) continue;
             const int c = rc[k];
             int got = -1;
@@ -252,7 +258,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
                 atomicMin(&m->viol1, ((unsigned long long)(c0 + got) << 4) | JH_CAUSE_DOUBLE_INVOKE);
                 got = -2;
             }
-            sp[i] = (int16_t)got;                      // -1: spill (no completion in the chunk)
+            gotk[k] = got;                             // -1: spill (no completion in the chunk)
             if (got >= 0) sp[got] = (int16_t)i;
         }
         __syncthreads();
@@ -261,10 +267,10 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
         for (int k = 0; k < PER; k++) {
             const int i = k * PACK_THREADS + tid;
             if (i >= nc) continue;
-            const uint32_t x = sc[i];
+            const uint32_t x = cx[k];
             const uint32_t ty = x & 3, f2 = x >> 2;
             const int64_t r = c0 + i;
-            const int c = sp[i];
+            const int c = ty == T_INVOKE ? gotk[k] : (int)sp[i];
             uint32_t w = CW_NONE;
             if (ty == T_INVOKE) {
                 if (c == -1) {

@@ -3278,6 +3278,9 @@ done:
 // the whole step on one wave. Sets sh.key (-1: the sequential search has
 // left its queue, or the helper has waited HELPER_MAX_TICKS: done).
 constexpr unsigned long long HELPER_MAX_TICKS = 500000000ULL;   // 5 s of s_memrealtime (100 MHz)
+#ifndef JH_HELP_BY_ORDER
+#define JH_HELP_BY_ORDER 0
+#endif
 __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned long long t_enter) {
     const DfsArgs &A = W.d;
     for (;;) {
@@ -3306,7 +3309,11 @@ __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned 
                 __hip_atomic_load(&W.taken[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                 continue;
             const unsigned long long run = min(now - s, (1ULL << 40) - 1);
-            atomicMin(&sh.pick, (((1ULL << 40) - 1 - run) << 24) | (unsigned long long)i);
+            // JH_HELP_BY_ORDER: the first key in the list's order (least
+            // phase-1 progress first) among those past the delay; else the
+            // key the sequential search has been on longest
+            atomicMin(&sh.pick, JH_HELP_BY_ORDER ? (unsigned long long)i
+                                                 : (((1ULL << 40) - 1 - run) << 24) | (unsigned long long)i);
         }
         __syncthreads();
         if (tid == 0 && sh.pick != ~0ULL) {

@@ -37,6 +37,22 @@
 
 namespace {
 
+#ifndef JH_CNT_BALLOT
+#define JH_CNT_BALLOT 0      // group masks by per-wave ballots instead of LDS atomics (A/B)
+#endif
+#ifndef JH_SPILL_VEC
+#define JH_SPILL_VEC 8       // rows per step of the spill walk (0 or 1: one row per step)
+#endif
+constexpr int SPILL_VEC = JH_SPILL_VEC > 1 ? JH_SPILL_VEC : 1;
+#ifndef JH_SPILL_LANES
+#define JH_SPILL_LANES 32    // lanes per chunk in k_cnt_pair_spill (~20 spills per C2 chunk)
+#endif
+constexpr int SPILL_LANES = JH_SPILL_LANES;
+static_assert(SPILL_LANES >= 1 && SPILL_LANES <= 256 && (SPILL_LANES & (SPILL_LANES - 1)) == 0, "power of two");
+#ifndef JH_CNT_HASH32
+#define JH_CNT_HASH32 0      // a 32-bit multiplicative slot hash instead of jh_mix64 (A/B)
+#endif
+
 constexpr int T_INVOKE = 0, T_OK = 1, T_FAIL = 2, T_INFO = 3;
 constexpr int CHUNK = 2048, HSLOTS = 1024;
 
@@ -140,7 +156,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
                                                   const int64_t *__restrict__ val, int64_t n,
                                                   long long pmin, int32_t *__restrict__ last,
                                                   uint32_t *__restrict__ cw, int32_t *__restrict__ pair,
-                                                  int32_t *__restrict__ spill, int32_t *__restrict__ spill_n,
+                                                  uint2 *__restrict__ spill, int32_t *__restrict__ spill_n,
                                                   CntMeta *m, CntAcc *__restrict__ agg) {
     __shared__ uint32_t hk[HSLOTS];                 // process - pmin + 1 (0: empty)
     __shared__ int hv[HSLOTS];                      // its last row
@@ -195,7 +211,11 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
                 if (v != JH_NIL) am = max(am, v < 0 ? (v == LLONG_MIN ? LLONG_MAX : -v) : v);
                 na++;
             }
+#if JH_CNT_HASH32
+            uint32_t h = (pk * 0x9E3779B1u) >> (32 - 10);               // HSLOTS = 2^10
+#else
             uint32_t h = (uint32_t)jh_mix64((uint64_t)pk) & (HSLOTS - 1);
+#endif
             int slot = -1;
             for (int probe = 0; probe < 64; probe++) {
                 uint32_t cur = hk[h];
@@ -226,11 +246,29 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
         for (int k = 0; k < PER; k++) {
             const int i = k * PACK_THREADS + tid;
             rc[k] = -1;
+#if JH_CNT_BALLOT
+            // a wave's 64 lanes are the 64 rows of group i >> 6 (PACK_THREADS
+            // is a multiple of 64), and no other wave writes that group's
+            // masks: one ballot per distinct process, one plain LDS store
+            int c = -1;
+            if (i < nc) { const int slot = rsl[k]; c = slot >= 0 ? hc[slot] : -1; }
+            rc[k] = (int8_t)c;
+            const bool on = c >= 0 && (cx[k] & 3) != T_INFO;
+            unsigned long long todo = __ballot(on);
+            while (todo) {
+                const int l0 = __builtin_ctzll(todo);
+                const int cc = __shfl(c, l0);
+                const unsigned long long mm = __ballot(on && c == cc);
+                if ((tid & 63) == l0) M[i >> 6][cc] = mm;
+                todo &= ~mm;
+            }
+#else
             if (i >= nc) continue;
             const int slot = rsl[k];
             const int c = slot >= 0 ? hc[slot] : -1;
             rc[k] = (int8_t)c;
             if (c >= 0 && (cx[k] & 3) != T_INFO) atomicOr(&M[i >> 6][c], 1ULL << (i & 63));
+#endif
         }
         __syncthreads();
         bool walk_from_end[PER];
@@ -276,7 +314,8 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
                 if (c == -1) {
                     // spills gather in LDS: one global atomic per chunk
                     // the chunk's own spill region: no global atomic
-                    spill[c0 + atomicAdd(&nls, 1)] = walk_from_end[k] ? ~(int32_t)r : (int32_t)r;
+                    spill[c0 + atomicAdd(&nls, 1)] = make_uint2((uint32_t)(walk_from_end[k] ? ~(int32_t)r : (int32_t)r),
+                                                                cp[k] | (f2 << 28));
                     w = f2 == F2_READ ? CW_INVREAD : f2 == F2_ADD ? CW_PEND : CW_NONE;
                 } else if (f2 == F2_READ) {
                     w = CW_INVREAD;
@@ -339,56 +378,84 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
 // the spilled invocations: one thread each walks its process' rows forward
 // to the completion, or past the process' last row (no completion: a crashed
 // op, which stays in), and completes the invocation's word (and claims the
-// completion's)
+// completion's). A spill carries its row and its process offset | f2 << 28
+// (span < 2^28), so the walk starts after one dependent load (last[]).
 __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restrict__ proc,
                                                         const int64_t *__restrict__ type,
                                                         const int64_t *__restrict__ f,
                                                         const int64_t *__restrict__ val, int64_t n,
                                                         long long pmin, const int32_t *__restrict__ last,
-                                                        const int32_t *__restrict__ spill,
+                                                        const uint2 *__restrict__ spill,
                                                         const int32_t *__restrict__ spill_n, int64_t n_chunks,
                                                         uint32_t *__restrict__ cw, int32_t *__restrict__ pair,
                                                         CntMeta *m, CntAcc *__restrict__ agg) {
-    // 16 lanes per chunk: its spills are spill[chunk * CHUNK ..][0 .. spill_n[chunk])
-    const int sl = threadIdx.x & 15;
-    for (int64_t ch = (int64_t)blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4); ch < n_chunks;
-         ch += (int64_t)gridDim.x * (blockDim.x >> 4))
-    for (int s = sl; s < spill_n[ch]; s += 16) {
-        const int32_t se = spill[ch * CHUNK + s];
+    // SPILL_LANES lanes per chunk: its spills are spill[chunk * CHUNK ..][0 .. spill_n[chunk])
+    const int sl = threadIdx.x & (SPILL_LANES - 1);
+    const int cpb = 256 / SPILL_LANES;
+    for (int64_t ch = (int64_t)blockIdx.x * cpb + threadIdx.x / SPILL_LANES; ch < n_chunks;
+         ch += (int64_t)gridDim.x * cpb)
+    for (int s = sl; s < spill_n[ch]; s += SPILL_LANES) {
+        const uint2 e = spill[ch * CHUNK + s];
+        const int32_t se = (int32_t)e.x;
         const int64_t r = se >= 0 ? se : ~se;
-        const long long p = proc[r];
-        const int64_t ff = f[r];
-        const int64_t lr = last[p - pmin];
+        const uint32_t pk = e.y & ((1u << 28) - 1), f2 = e.y >> 28;
+        const long long p = pmin + (long long)pk;
+        const int64_t lr = last[pk];
+        const long long vr = f2 == F2_ADD ? (long long)val[r] : 0;    // issued with last[]
         int64_t got = -1;
+        int gty = -1;                                                  // the completion's type
         // from the chunk's end when the chunk held only :info rows of p after r
         const int64_t j0 = se >= 0 ? r + 1 : (r / CHUNK + 1) * CHUNK;
+#if JH_SPILL_VEC > 1
+        // SPILL_VEC rows per step: their process and type loads are issued
+        // together, so a long walk waits on one memory latency per step, not
+        // per row (lr < n: every load is in bounds)
+        for (int64_t j = j0; j <= lr && got == -1; j += SPILL_VEC) {
+            long long pv[SPILL_VEC], tv[SPILL_VEC];
+#pragma unroll
+            for (int q = 0; q < SPILL_VEC; q++) {
+                const int64_t jq = min(j + q, lr);
+                pv[q] = proc[jq]; tv[q] = type[jq];
+            }
+#pragma unroll
+            for (int q = 0; q < SPILL_VEC; q++) {
+                const int64_t jq = j + q;
+                if (got != -1 || jq > lr || pv[q] != p) continue;
+                const int64_t ty = tv[q] & 3;
+                if (ty == T_INFO) continue;
+                if (ty == T_INVOKE) { atomicMin(&m->viol1, ((unsigned long long)jq << 4) | JH_CAUSE_DOUBLE_INVOKE); got = -2; }
+                else { got = jq; gty = (int)ty; }
+            }
+        }
+#else
         for (int64_t j = j0; j <= lr; j++) {
             if (proc[j] != p) continue;
             const int64_t ty = type[j] & 3;
             if (ty == T_INFO) continue;
             if (ty == T_INVOKE) { atomicMin(&m->viol1, ((unsigned long long)j << 4) | JH_CAUSE_DOUBLE_INVOKE); got = -2; }
-            else got = j;
+            else { got = j; gty = (int)ty; }
             break;
         }
+#endif
         if (got >= 0) atomicAnd(&cw[got], ~CW_U);
-        const bool got_okread = got >= 0 && (type[got] & 3) == T_OK && f[got] == JH_F_READ;
+        const bool got_okread = got >= 0 && gty == T_OK && f[got] == JH_F_READ;
         if (got_okread) {
             // an :ok :read counts in its tile as a read row only when it
             // completes an [:invoke :read] (checker.clj:713-716); completing
             // anything else it has no pending read: an orphan, stripped of its
             // kind as the in-chunk pairing does (k_cnt_pack), so no later pass
             // reads its pair[] (never written for it)
-            if (ff == JH_F_READ) atomicAdd(&agg[got / CNT_TILE].nr, 1);
+            if (f2 == F2_READ) atomicAdd(&agg[got / CNT_TILE].nr, 1);
             else {
                 atomicMin(&m->viol2, ((unsigned long long)got << 4) | JH_CAUSE_ORPHAN);
                 atomicAnd(&cw[got], ~7u);
             }
         }
-        if (ff == JH_F_ADD) {
+        if (f2 == F2_ADD) {
             uint32_t w = CW_NONE;
-            const bool failed = got >= 0 && (type[got] & 3) == T_FAIL;
+            const bool failed = got >= 0 && gty == T_FAIL;
             if (got != -2 && !failed) {
-                long long v = val[r];
+                long long v = vr;
                 bool own = true;
                 if (v == JH_NIL && got >= 0) { v = val[got]; own = false; }
                 if (v == JH_NIL) atomicMin(&m->viol2, ((unsigned long long)r << 4) | JH_CAUSE_NIL_VALUE);
@@ -399,7 +466,7 @@ __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restric
                 }
             }
             cw[r] = w;
-        } else if (ff == JH_F_READ && got_okread) {
+        } else if (f2 == F2_READ && got_okread) {
             pair[got] = (int32_t)r;
         }
     }
@@ -416,6 +483,7 @@ __global__ void __launch_bounds__(256) k_cnt_tile_scan(const uint32_t *__restric
                                                        int64_t *__restrict__ lo_at, CntAcc *total, CntMeta *m) {
     __shared__ long long sc[3][4];
     const int tid = threadIdx.x;
+    const CntAcc p = pre[blockIdx.x];         // issued first: its latency overlaps the words'
     const int64_t base = (int64_t)blockIdx.x * CNT_TILE;
     const int64_t r0 = base + (int64_t)tid * CNT_PER;
     uint32_t w[CNT_PER];
@@ -450,7 +518,6 @@ __global__ void __launch_bounds__(256) k_cnt_tile_scan(const uint32_t *__restric
     if (lane == 63) { sc[0][wv] = il; sc[1][wv] = ih; sc[2][wv] = in; }
     __syncthreads();
     for (int v = 0; v < wv; v++) { il += sc[0][v]; ih += sc[1][v]; in += sc[2][v]; }
-    const CntAcc p = pre[blockIdx.x];
     long long rl = p.lo + il - lo, rh = p.hi + ih - hi, rn = p.nr + in - nr;
 #pragma unroll
     for (int j = 0; j < CNT_PER; j++) {
@@ -529,7 +596,7 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
     int32_t *pair = ctx->ws<int32_t>(WS_C_PAIR, n);
     uint32_t *cw = ctx->ws<uint32_t>(WS_C_PT, n + 8);
     HIP_TRY(hipMemsetAsync(last, 0xFF, sizeof(int32_t) * (span + 1), st));
-    int32_t *spill = ctx->ws<int32_t>(WS_C_IDX, n);          // reused for the read rows below
+    uint2 *spill = ctx->ws<uint2>(WS_C_IDX, n);              // reused for the read rows below
     const int64_t n_tiles = (n + CNT_TILE - 1) / CNT_TILE;
     CntAcc *agg = ctx->ws<CntAcc>(WS_C_OUT2, 2 * n_tiles + 1);     // written by every pack block
     int32_t *spill_n = ctx->ws<int32_t>(WS_C_FLAG, n_tiles);       // likewise
@@ -537,7 +604,7 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
     CntAcc *total = pre + n_tiles;
     k_cnt_pack<<<(int)n_tiles, PACK_THREADS, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
                                                      mh.pmin, last, cw, pair, spill, spill_n, m, agg);
-    k_cnt_pair_spill<<<grid_for(n_tiles * 16, 256, 16384), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
+    k_cnt_pair_spill<<<grid_for(n_tiles * SPILL_LANES, 256, 16384), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
                                                                       mh.pmin, last, spill, spill_n, n_tiles, cw, pair, m, agg);
 
     // reduce-then-scan over tiles of contribution words

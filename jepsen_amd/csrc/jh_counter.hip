@@ -473,61 +473,98 @@ __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restric
 }
 
 
-// thread t takes rows CNT_PER*t .. of the tile in order, from the tile's
-// exclusive prefix; writes only at read rows
-__global__ void __launch_bounds__(256) k_cnt_tile_scan(const uint32_t *__restrict__ cw,
+// thread t takes rows CNT_PER*t .. of each of the block's TS_TILES tiles in
+// order, from the tile's exclusive prefix; writes only at read rows. Every
+// tile's words are loaded before any is scanned, and one barrier serves them
+// all. Measured (profiles/r04/c2_spill/): 1 tile 207 us per 100 M rows, 2
+// tiles (122 VGPRs) 263, 4 tiles 458; one tile per block stays.
+#ifndef JH_TS_TILES
+#define JH_TS_TILES 1
+#endif
+constexpr int TS_TILES = JH_TS_TILES;
+#ifdef JH_TS_WPE
+#define TS_ATTR __attribute__((amdgpu_waves_per_eu(JH_TS_WPE, JH_TS_WPE)))
+#else
+#define TS_ATTR
+#endif
+__global__ void TS_ATTR __launch_bounds__(256) k_cnt_tile_scan(const uint32_t *__restrict__ cw,
                                                        const int32_t *__restrict__ pair,
                                                        const int64_t *__restrict__ val, int64_t n,
-                                                       const CntAcc *__restrict__ pre,
+                                                       int64_t n_tiles, const CntAcc *__restrict__ pre,
                                                        int32_t *__restrict__ rd_row, int64_t *__restrict__ rd_hi,
                                                        int64_t *__restrict__ lo_at, CntAcc *total, CntMeta *m) {
-    __shared__ long long sc[3][4];
+    __shared__ long long sc[TS_TILES][3][4];
     const int tid = threadIdx.x;
-    const CntAcc p = pre[blockIdx.x];         // issued first: its latency overlaps the words'
-    const int64_t base = (int64_t)blockIdx.x * CNT_TILE;
-    const int64_t r0 = base + (int64_t)tid * CNT_PER;
-    uint32_t w[CNT_PER];
-    if (r0 + CNT_PER <= n) {
-        const uint4 a = *(const uint4 *)(cw + r0), b = *(const uint4 *)(cw + r0 + 4);
-        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
-    } else {
+    const int lane = tid & 63, wv = tid >> 6;
+    const int64_t t0 = (int64_t)blockIdx.x * TS_TILES;
+    CntAcc p[TS_TILES];
+    uint32_t w[TS_TILES][CNT_PER];
 #pragma unroll
-        for (int j = 0; j < CNT_PER; j++) w[j] = r0 + j < n ? cw[r0 + j] : 0u;
+    for (int t = 0; t < TS_TILES; t++) {
+        const int64_t r0 = (t0 + t) * CNT_TILE + (int64_t)tid * CNT_PER;
+        p[t] = t0 + t < n_tiles ? pre[t0 + t] : CntAcc{0, 0, 0, 0};
+        if (r0 + CNT_PER <= n) {
+            const uint4 a = *(const uint4 *)(cw + r0), b = *(const uint4 *)(cw + r0 + 4);
+            w[t][0] = a.x; w[t][1] = a.y; w[t][2] = a.z; w[t][3] = a.w;
+            w[t][4] = b.x; w[t][5] = b.y; w[t][6] = b.z; w[t][7] = b.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < CNT_PER; j++) w[t][j] = r0 + j < n ? cw[r0 + j] : 0u;
+        }
     }
-    long long lo = 0, hi = 0, nr = 0;
+    long long lo[TS_TILES], hi[TS_TILES], il[TS_TILES], ih[TS_TILES];
+    int nr[TS_TILES], in[TS_TILES];
     unsigned long long orphan = ~0ULL;        // a completion no invocation claimed
 #pragma unroll
-    for (int j = 0; j < CNT_PER; j++) {
-        const uint32_t k = w[j] & 7;
-        if (w[j] & CW_U) orphan = min(orphan, (unsigned long long)(r0 + j));
-        if (k == CW_LO) lo += cw_val(w[j], val, pair, r0 + j);
-        else if (k == CW_HI) hi += cw_val(w[j], val, pair, r0 + j);
-        else if (k == CW_OKREAD && !(w[j] & CW_U)) nr++;
+    for (int t = 0; t < TS_TILES; t++) {
+        const int64_t r0 = (t0 + t) * CNT_TILE + (int64_t)tid * CNT_PER;
+        lo[t] = 0; hi[t] = 0; nr[t] = 0;
+#pragma unroll
+        for (int j = 0; j < CNT_PER; j++) {
+            const uint32_t k = w[t][j] & 7;
+            if (w[t][j] & CW_U) orphan = min(orphan, (unsigned long long)(r0 + j));
+            if (k == CW_LO) lo[t] += cw_val(w[t][j], val, pair, r0 + j);
+            else if (k == CW_HI) hi[t] += cw_val(w[t][j], val, pair, r0 + j);
+            else if (k == CW_OKREAD && !(w[t][j] & CW_U)) nr[t]++;
+        }
+        il[t] = lo[t]; ih[t] = hi[t]; in[t] = nr[t];
     }
-    for (int o = 32; o > 0; o >>= 1) orphan = min(orphan, (unsigned long long)__shfl_xor(orphan, o));
-    if ((tid & 63) == 0 && orphan != ~0ULL) atomicMin(&m->viol1, (orphan << 4) | JH_CAUSE_ORPHAN);
-    // block exclusive scan of the per-thread sums: wave shuffles, then the
-    // totals of the waves before
-    long long il = lo, ih = hi, in = nr;
-    const int lane = tid & 63, wv = tid >> 6;
+    if (__any(orphan != ~0ULL)) {
+        for (int o = 32; o > 0; o >>= 1) orphan = min(orphan, (unsigned long long)__shfl_xor(orphan, o));
+        if (lane == 0) atomicMin(&m->viol1, (orphan << 4) | JH_CAUSE_ORPHAN);
+    }
+    // block exclusive scans of the per-thread sums: wave shuffles, then the
+    // totals of the waves before (one barrier for every tile)
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const long long a0 = __shfl_up(il, o), a1 = __shfl_up(ih, o), a2 = __shfl_up(in, o);
-        if (lane >= o) { il += a0; ih += a1; in += a2; }
-    }
-    if (lane == 63) { sc[0][wv] = il; sc[1][wv] = ih; sc[2][wv] = in; }
-    __syncthreads();
-    for (int v = 0; v < wv; v++) { il += sc[0][v]; ih += sc[1][v]; in += sc[2][v]; }
-    long long rl = p.lo + il - lo, rh = p.hi + ih - hi, rn = p.nr + in - nr;
 #pragma unroll
-    for (int j = 0; j < CNT_PER; j++) {
-        const uint32_t k = w[j] & 7;
-        const int64_t r = r0 + j;
-        if (k == CW_LO) rl += cw_val(w[j], val, pair, r);
-        else if (k == CW_HI) rh += cw_val(w[j], val, pair, r);
-        else if (k == CW_OKREAD && !(w[j] & CW_U)) { rn++; rd_row[rn - 1] = (int32_t)r; rd_hi[rn - 1] = rh; }
-        else if (k == CW_INVREAD) lo_at[r] = rl;
-        if (r == n - 1) *total = CntAcc{rl, rh, (int)rn, 0};
+        for (int t = 0; t < TS_TILES; t++) {
+            const long long a0 = __shfl_up(il[t], o), a1 = __shfl_up(ih[t], o);
+            const int a2 = __shfl_up(in[t], o);
+            if (lane >= o) { il[t] += a0; ih[t] += a1; in[t] += a2; }
+        }
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int t = 0; t < TS_TILES; t++) { sc[t][0][wv] = il[t]; sc[t][1][wv] = ih[t]; sc[t][2][wv] = in[t]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TS_TILES; t++) {
+        const int64_t r0 = (t0 + t) * CNT_TILE + (int64_t)tid * CNT_PER;
+        long long el = il[t], eh = ih[t], en = in[t];
+        for (int v = 0; v < wv; v++) { el += sc[t][0][v]; eh += sc[t][1][v]; en += sc[t][2][v]; }
+        long long rl = p[t].lo + el - lo[t], rh = p[t].hi + eh - hi[t], rn = p[t].nr + en - nr[t];
+#pragma unroll
+        for (int j = 0; j < CNT_PER; j++) {
+            const uint32_t k = w[t][j] & 7;
+            const int64_t r = r0 + j;
+            if (k == CW_LO) rl += cw_val(w[t][j], val, pair, r);
+            else if (k == CW_HI) rh += cw_val(w[t][j], val, pair, r);
+            else if (k == CW_OKREAD && !(w[t][j] & CW_U)) { rn++; rd_row[rn - 1] = (int32_t)r; rd_hi[rn - 1] = rh; }
+            else if (k == CW_INVREAD) lo_at[r] = rl;
+            if (r == n - 1) *total = CntAcc{rl, rh, (int)rn, 0};
+        }
     }
 }
 
@@ -615,7 +652,8 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
     HIP_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, tb, agg, pre, CntSumOp(), CntAcc{0, 0, 0, 0}, (int)n_tiles, st));
     void *tmp = ctx->ws<char>(WS_S_TMP, tb);
     HIP_TRY(hipcub::DeviceScan::ExclusiveScan(tmp, tb, agg, pre, CntSumOp(), CntAcc{0, 0, 0, 0}, (int)n_tiles, st));
-    k_cnt_tile_scan<<<(unsigned)n_tiles, 256, 0, st>>>(cw, pair, dh->value, n, pre, rd_row, rd_hi, lo_at, total, m);
+    k_cnt_tile_scan<<<(unsigned)((n_tiles + TS_TILES - 1) / TS_TILES), 256, 0, st>>>(cw, pair, dh->value, n, n_tiles, pre,
+                                                                                      rd_row, rd_hi, lo_at, total, m);
     // the triples of every :ok :read (their count stays on the device: the
     // kernel reads it), then one host round trip for the verdict
     const int64_t cap = std::min(n, reads_cap);

@@ -72,21 +72,34 @@ __global__ void __launch_bounds__(256) k_set_scan(const int64_t *__restrict__ ty
 }
 
 // the final read's element range (its first element need not be 16-byte
-// aligned: the pairs start at the aligned address below it)
+// aligned: the aligned pairs inside it go four per thread per step, so four
+// 16-byte loads are in flight; the odd elements at either end, thread 0).
+// Round 4 (profiles/r04/c2_spill/r4unroll_*): 128 -> 119 us per 47 M
+// elements; the same unrolling of k_cnt_prange and of k_set_scan (two row
+// pairs per step) measured flat / slower, not kept.
+#ifndef JH_RANGE_UNROLL
+#define JH_RANGE_UNROLL 4
+#endif
 __global__ void __launch_bounds__(256) k_set_range(const int64_t *__restrict__ aux, int64_t off, int64_t cnt, int vec, SetMeta *m) {
     long long lo = LLONG_MAX, hi = LLONG_MIN;
-    const int64_t a0 = off & ~1LL, np = (off + cnt - a0 + 1) / 2;
-    const longlong2 *p2 = (const longlong2 *)(aux + a0);
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t j = a0 + 2 * i;
-        if (vec && j >= off && j + 1 < off + cnt) {
-            const longlong2 x = p2[i];
-            lo = min(lo, min(x.x, x.y)); hi = max(hi, max(x.x, x.y));
-        } else {
-            for (int k = 0; k < 2; k++)
-                if (j + k >= off && j + k < off + cnt) { const long long v = aux[j + k]; lo = min(lo, v); hi = max(hi, v); }
+    const int64_t gt = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, gs = (int64_t)gridDim.x * blockDim.x;
+    if (vec) {
+        const int64_t a0 = (off + 1) & ~1LL, a1 = (off + cnt) & ~1LL;
+        const int64_t np = a1 > a0 ? (a1 - a0) / 2 : 0;
+        const longlong2 *p2 = (const longlong2 *)(aux + a0);
+        for (int64_t i = gt; i < np; i += JH_RANGE_UNROLL * gs) {
+            longlong2 x[JH_RANGE_UNROLL];
+#pragma unroll
+            for (int u = 0; u < JH_RANGE_UNROLL; u++) x[u] = p2[i + u * gs < np ? i + u * gs : i];   // (a repeat is harmless)
+#pragma unroll
+            for (int u = 0; u < JH_RANGE_UNROLL; u++) { lo = min(lo, min(x[u].x, x[u].y)); hi = max(hi, max(x[u].x, x[u].y)); }
         }
+        if (gt == 0) {
+            if (a0 > off && cnt > 0) { const long long v = aux[off]; lo = min(lo, v); hi = max(hi, v); }
+            if (a1 < off + cnt && a1 >= a0) { const long long v = aux[a1]; lo = min(lo, v); hi = max(hi, v); }
+        }
+    } else {
+        for (int64_t j = off + gt; j < off + cnt; j += gs) { const long long v = aux[j]; lo = min(lo, v); hi = max(hi, v); }
     }
     __shared__ long long sh[4];
     lo = block_reduce256(lo, RedMin(), sh);

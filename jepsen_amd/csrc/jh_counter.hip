@@ -49,6 +49,9 @@ constexpr int SPILL_VEC = JH_SPILL_VEC > 1 ? JH_SPILL_VEC : 1;
 #endif
 constexpr int SPILL_LANES = JH_SPILL_LANES;
 static_assert(SPILL_LANES >= 1 && SPILL_LANES <= 256 && (SPILL_LANES & (SPILL_LANES - 1)) == 0, "power of two");
+#ifndef JH_SPILL_TAB
+#define JH_SPILL_TAB 2       // chunks publish their processes' first non-:info rows (2: built by ballots, 1: by wave 0; 0: walk only)
+#endif
 #ifndef JH_CNT_HASH32
 #define JH_CNT_HASH32 0      // a 32-bit multiplicative slot hash instead of jh_mix64 (A/B)
 #endif
@@ -157,6 +160,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
                                                   long long pmin, int32_t *__restrict__ last,
                                                   uint32_t *__restrict__ cw, int32_t *__restrict__ pair,
                                                   uint2 *__restrict__ spill, int32_t *__restrict__ spill_n,
+                                                  uint2 *__restrict__ tab, int32_t *__restrict__ tab_n,
                                                   CntMeta *m, CntAcc *__restrict__ agg) {
     __shared__ uint32_t hk[HSLOTS];                 // process - pmin + 1 (0: empty)
     __shared__ int hv[HSLOTS];                      // its last row
@@ -165,6 +169,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
     __shared__ int16_t sp[CHUNK];                   // each row's partner in the chunk (-1: none)
     __shared__ unsigned long long M[PAIR_GROUPS][PAIR_PROCS];
     __shared__ int nd, nls;
+    __shared__ uint32_t cproc[PAIR_PROCS];            // compact index -> process offset
     __shared__ long long sh[5][PACK_THREADS / 64];
     const int tid = threadIdx.x;
     long long am = 0, na = 0;
@@ -224,6 +229,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
                     if (cur == 0) {
                         const int c = atomicAdd(&nd, 1);
                         hc[h] = (int8_t)(c < PAIR_PROCS ? c : -1);
+                        if (c < PAIR_PROCS) cproc[c] = pk;
                         cur = pk + 1;
                     }
                 }
@@ -271,6 +277,56 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
 #endif
         }
         __syncthreads();
+#if JH_SPILL_TAB
+        // the chunk's table for k_cnt_pair_spill: per tracked process its
+        // first non-:info row here (flag << 31 | sc << 16 | row in chunk), so a
+        // walk from an earlier chunk reads one table instead of these rows
+#if JH_SPILL_TAB == 2
+        // every wave takes four processes, two per step (a half-wave per
+        // process, a lane per 64-row group): the first group with a set bit by
+        // one ballot, no lane walks the groups
+        {
+            const int lane = tid & 63, wv = tid >> 6, half = lane >> 5, g = lane & 31;
+            const int ndc = min(nd, PAIR_PROCS);
+            static_assert(PAIR_GROUPS == 32 && PAIR_PROCS == 32 && PACK_THREADS == 512, "table layout");
+#pragma unroll
+            for (int st = 0; st < 2; st++) {
+                const int c = (st * 8 + wv) * 2 + half;
+                const unsigned long long mg = (c < ndc && (g << 6) < nc) ? M[g][c] : 0ULL;
+                const unsigned long long b = __ballot(mg != 0ULL);
+                const uint32_t bh = half ? (uint32_t)(b >> 32) : (uint32_t)b;
+                if (g == 0) {
+                    uint2 e = make_uint2(0u, 0u);
+                    if (c < ndc) {
+                        e.x = cproc[c] + 1;
+                        if (bh) {
+                            const int g0 = __builtin_ctz(bh);
+                            const int first = (g0 << 6) + __builtin_ctzll(M[g0][c]);
+                            e.y = (1u << 31) | ((uint32_t)sc[first] << 16) | (uint32_t)first;
+                        }
+                    }
+                    tab[(int64_t)blockIdx.x * PAIR_PROCS + c] = e;
+                }
+            }
+            if (tid == 0) tab_n[blockIdx.x] = nd;
+        }
+#else
+        if (tid < PAIR_PROCS) {
+            uint2 e = make_uint2(0u, 0u);
+            if (tid < min(nd, PAIR_PROCS)) {
+                int first = -1;
+                for (int g = 0; g < PAIR_GROUPS && (g << 6) < nc; g++) {
+                    const unsigned long long mg = M[g][tid];
+                    if (mg) { first = (g << 6) + __builtin_ctzll(mg); break; }
+                }
+                e.x = cproc[tid] + 1;
+                e.y = first < 0 ? 0u : (1u << 31) | ((uint32_t)sc[first] << 16) | (uint32_t)first;
+            }
+            tab[(int64_t)blockIdx.x * PAIR_PROCS + tid] = e;
+            if (tid == 0) tab_n[blockIdx.x] = nd;
+        }
+#endif
+#endif
         bool walk_from_end[PER];
         int gotk[PER];
 #pragma unroll
@@ -387,6 +443,7 @@ __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restric
                                                         long long pmin, const int32_t *__restrict__ last,
                                                         const uint2 *__restrict__ spill,
                                                         const int32_t *__restrict__ spill_n, int64_t n_chunks,
+                                                        const uint2 *__restrict__ tab, const int32_t *__restrict__ tab_n,
                                                         uint32_t *__restrict__ cw, int32_t *__restrict__ pair,
                                                         CntMeta *m, CntAcc *__restrict__ agg) {
     // SPILL_LANES lanes per chunk: its spills are spill[chunk * CHUNK ..][0 .. spill_n[chunk])
@@ -406,7 +463,53 @@ __global__ void __launch_bounds__(256) k_cnt_pair_spill(const int64_t *__restric
         int gty = -1;                                                  // the completion's type
         // from the chunk's end when the chunk held only :info rows of p after r
         const int64_t j0 = se >= 0 ? r + 1 : (r / CHUNK + 1) * CHUNK;
-#if JH_SPILL_VEC > 1
+#if JH_SPILL_TAB
+        // at each chunk boundary the chunk's table gives p's first non-:info
+        // row there (or says it has none); inside a chunk (r's own, or one
+        // with more than PAIR_PROCS processes) SPILL_VEC rows per step, their
+        // process and type loads issued together
+        for (int64_t j = j0; got == -1 && j <= lr;) {
+            const int64_t cj = j / CHUNK;
+            if (j == cj * CHUNK && tab_n[cj] <= PAIR_PROCS) {
+                const uint4 *t4 = (const uint4 *)(tab + cj * PAIR_PROCS);
+                uint32_t ey = 0;
+#pragma unroll
+                for (int q0 = 0; q0 < PAIR_PROCS / 2; q0 += 4) {
+                    uint4 x[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) x[u] = t4[q0 + u];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (x[u].x == pk + 1) ey = x[u].y;
+                        if (x[u].z == pk + 1) ey = x[u].w;
+                    }
+                }
+                if (!(ey >> 31)) { j = (cj + 1) * CHUNK; continue; }     // no non-:info row of p in chunk cj
+                const int64_t jq = cj * CHUNK + (ey & 0xFFFF);
+                const int ty = (int)((ey >> 16) & 3);
+                if (ty == T_INVOKE) { atomicMin(&m->viol1, ((unsigned long long)jq << 4) | JH_CAUSE_DOUBLE_INVOKE); got = -2; }
+                else { got = jq; gty = ty; }
+                break;
+            }
+            const int64_t jend = min(lr, (cj + 1) * CHUNK - 1);
+            long long pv[SPILL_VEC], tv[SPILL_VEC];
+#pragma unroll
+            for (int q = 0; q < SPILL_VEC; q++) {
+                const int64_t jq = min(j + q, jend);
+                pv[q] = proc[jq]; tv[q] = type[jq];
+            }
+#pragma unroll
+            for (int q = 0; q < SPILL_VEC; q++) {
+                const int64_t jq = j + q;
+                if (got != -1 || jq > jend || pv[q] != p) continue;
+                const int64_t ty = tv[q] & 3;
+                if (ty == T_INFO) continue;
+                if (ty == T_INVOKE) { atomicMin(&m->viol1, ((unsigned long long)jq << 4) | JH_CAUSE_DOUBLE_INVOKE); got = -2; }
+                else { got = jq; gty = (int)ty; }
+            }
+            j = min(j + SPILL_VEC, jend + 1);
+        }
+#elif JH_SPILL_VEC > 1
         // SPILL_VEC rows per step: their process and type loads are issued
         // together, so a long walk waits on one memory latency per step, not
         // per row (lr < n: every load is in bounds)
@@ -638,11 +741,13 @@ void counter_check(jh_ctx *ctx, const jh_history *dh, int64_t *reads_out, int64_
     CntAcc *agg = ctx->ws<CntAcc>(WS_C_OUT2, 2 * n_tiles + 1);     // written by every pack block
     int32_t *spill_n = ctx->ws<int32_t>(WS_C_FLAG, n_tiles);       // likewise
     CntAcc *pre = agg + n_tiles;
+    uint2 *tab = ctx->ws<uint2>(WS_C_TAB, (size_t)n_tiles * (PAIR_PROCS + 1));   // + tab_n
+    int32_t *tab_n = (int32_t *)(tab + (size_t)n_tiles * PAIR_PROCS);
     CntAcc *total = pre + n_tiles;
     k_cnt_pack<<<(int)n_tiles, PACK_THREADS, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
-                                                     mh.pmin, last, cw, pair, spill, spill_n, m, agg);
+                                                     mh.pmin, last, cw, pair, spill, spill_n, tab, tab_n, m, agg);
     k_cnt_pair_spill<<<grid_for(n_tiles * SPILL_LANES, 256, 16384), 256, 0, st>>>(dh->process, dh->type, dh->f, dh->value, n,
-                                                                      mh.pmin, last, spill, spill_n, n_tiles, cw, pair, m, agg);
+                                                                      mh.pmin, last, spill, spill_n, n_tiles, tab, tab_n, cw, pair, m, agg);
 
     // reduce-then-scan over tiles of contribution words
     int32_t *rd_row = ctx->ws<int32_t>(WS_C_IDX, n);

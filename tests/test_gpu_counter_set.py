@@ -263,3 +263,36 @@ def test_set_sparse_span(ctx):
     c = oracle.check_set(cols)
     _set_same(ctx.check_set(cols), c)
     _bits_same(ctx.check_set_bitmaps(cols, words_cap=1 << 22), c)
+
+
+@pytest.mark.parametrize("n_procs", [6, 40])
+@pytest.mark.parametrize("tail", ["ok", "info-then-ok", "fail", "double-invoke", "crash"])
+def test_counter_walk_across_chunks(ctx, n_procs, tail):
+    """A spilled invocation whose process is silent for several 2048-row
+    chunks: k_cnt_pair_spill jumps chunk to chunk on their first-row tables
+    (or walks chunks with more than 32 processes), past :info rows of the
+    process, to the completion, a double invocation, or nothing (a crash)."""
+    inv = lambda p, f, v: {"process": p, "type": "invoke", "f": f, "value": v}
+    ok = lambda p, f, v: {"process": p, "type": "ok", "f": f, "value": v}
+
+    def filler(h, rows, k0):
+        for k in range(rows // 2):
+            q = 1 + ((k0 + k) % (n_procs - 1))
+            h += [inv(q, "add", 1), ok(q, "add", 1)]
+    h = []
+    filler(h, 1500, 0)
+    h.append(inv(0, "add", 3))                       # process 0's invocation in chunk 0
+    filler(h, 5000, 7)                               # chunks 1 and 2: no row of process 0
+    if tail == "info-then-ok":
+        h.append({"process": 0, "type": "info", "f": "add", "value": 3})
+        filler(h, 900, 3)
+    if tail in ("ok", "info-then-ok"):
+        h.append(ok(0, "add", 3))
+    elif tail == "fail":
+        h.append({"process": 0, "type": "fail", "f": "add", "value": 3})
+    elif tail == "double-invoke":
+        h.append(inv(0, "add", 1))
+    filler(h, 300, 5)
+    h += [inv(1, "read", None), ok(1, "read", 7)]
+    cols = H.encode(h, keyed=False)
+    _counter_same(ctx.check_counter(cols), oracle.check_counter(cols))

@@ -55,6 +55,8 @@ struct jh_ctx {
     hipStream_t aux = nullptr;     // second stream for racing searches (jh_lin.hip)
     hipStream_t aux2 = nullptr;    // third stream: windows wider than 64 (jh_lin.hip)
     hipStream_t aux3 = nullptr;    // fourth stream: phase-2 late helpers (jh_lin.hip)
+    hipStream_t msk[4] = {};       // tuning builds: CU-masked streams of the streamed pass (JH_CU_SPLIT)
+    int msk_split = 0;
     std::mutex mu;
     std::vector<Buf> bufs;
     hipEvent_t ev[24] = {};

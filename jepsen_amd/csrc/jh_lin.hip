@@ -6155,6 +6155,23 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // waves; phase 3 follows on st. Four streams: the hardware's queues.
         // Every search is the one the round-3 schedule runs (same verdicts and
         // counts); only when each starts changes.
+        // tuning builds: JH_CU_SPLIT=R gives phase 1 the first n_cu - R CUs and
+        // the consumers the last R (CU-masked streams), and starts the
+        // consumers with phase 1 instead of at its drain
+        hipStream_t p1s = st, cs1 = ctx->aux, cs2 = ctx->aux2, cs3 = ctx->aux3;
+        const int cu_split = tune_env("JH_CU_SPLIT") ? std::max(0, std::min(ctx->n_cu - 8, atoi(tune_env("JH_CU_SPLIT")))) : 0;
+        if (cu_split > 0) {
+            if (ctx->msk_split != cu_split) {
+                for (hipStream_t &m : ctx->msk) if (m) { HIP_TRY(hipStreamDestroy(m)); m = nullptr; }
+                const int nw = (ctx->n_cu + 31) / 32;
+                std::vector<uint32_t> m1(nw, 0u), m2(nw, 0u);
+                for (int i = 0; i < ctx->n_cu; i++) (i < ctx->n_cu - cu_split ? m1 : m2)[i >> 5] |= 1u << (i & 31);
+                HIP_TRY(hipExtStreamCreateWithCUMask(&ctx->msk[0], (uint32_t)nw, m1.data()));
+                for (int i = 1; i < 4; i++) HIP_TRY(hipExtStreamCreateWithCUMask(&ctx->msk[i], (uint32_t)nw, m2.data()));
+                ctx->msk_split = cu_split;
+            }
+            p1s = ctx->msk[0]; cs1 = ctx->msk[1]; cs2 = ctx->msk[2]; cs3 = ctx->msk[3];
+        }
         int32_t qt[Q_WORDS];
         HIP_TRY(hipMemcpyAsync(qt, q, sizeof qt, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
@@ -6218,11 +6235,13 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         a.t_span = (unsigned long long *)(q + Q_T_P1);
         HIP_TRY(hipEventRecord(ctx->ev[6], st));     // fork: tables, lists and counters are ready
         HIP_TRY(hipEventRecord(ctx->ev[1], st));
-        k_lin_dfs<true, true><<<waves1, 64, MemoQ::LDS, st>>>(a);
+        if (p1s != st) HIP_TRY(hipStreamWaitEvent(p1s, ctx->ev[6], 0));
+        k_lin_dfs<true, true><<<waves1, 64, MemoQ::LDS, p1s>>>(a);
         HIP_TRY(hipGetLastError());
-        k_lin_dfs<false, true><<<std::min(waves1, 1024), 64, MemoQ::LDS, st>>>(aw);
+        k_lin_dfs<false, true><<<std::min(waves1, 1024), 64, MemoQ::LDS, p1s>>>(aw);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->ev[4], st));
+        HIP_TRY(hipEventRecord(ctx->ev[4], p1s));
+        if (p1s != st) HIP_TRY(hipStreamWaitEvent(st, ctx->ev[4], 0));
         a.prio_ins = 0;
         // behind phase 1 on st: xw keys, WIDE keys, LEAN waves past the early grid's
         const int late_l = any ? waves2 - w_early : 0;
@@ -6242,30 +6261,30 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             // 1 holds every CU, and a consumer launched earlier could take CUs
             // from it while it still has keys to hand out
             volatile int32_t *hf = (volatile int32_t *)ctx->hflag;
-            while (!*hf) {
+            while (!cu_split && !*hf) {
                 const hipError_t e = hipEventQuery(ctx->ev[4]);
                 if (e == hipSuccess) break;
                 if (e != hipErrorNotReady) HIP_TRY(e);
                 std::this_thread::yield();
             }
-            HIP_TRY(hipStreamWaitEvent(ctx->aux2, ctx->ev[6], 0));
-            k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, ctx->aux2>>>(c);
+            HIP_TRY(hipStreamWaitEvent(cs2, ctx->ev[6], 0));
+            k_lin_bfs<<<wg2, BFS_THREADS, BFS_LDS_BYTES, cs2>>>(c);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(ctx->ev[5], ctx->aux2));
+            HIP_TRY(hipEventRecord(ctx->ev[5], cs2));
             if (n_help > 0) {
-                HIP_TRY(hipStreamWaitEvent(ctx->aux3, ctx->ev[6], 0));
-                k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, ctx->aux3>>>(wh);
+                HIP_TRY(hipStreamWaitEvent(cs3, ctx->ev[6], 0));
+                k_lin_wg<<<n_wg, WG_THREADS, WG_LDS, cs3>>>(wh);
                 HIP_TRY(hipGetLastError());
-                HIP_TRY(hipEventRecord(ctx->ev[12], ctx->aux3));
+                HIP_TRY(hipEventRecord(ctx->ev[12], cs3));
             }
-            HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev[6], 0));
+            HIP_TRY(hipStreamWaitEvent(cs1, ctx->ev[6], 0));
             if (w_early > 0) {
                 DfsPair pr{};
                 pr.l = b; pr.n_l = w_early;
-                k_lin_seq_lw<true><<<w_early, 64, SEQLW_LDS, ctx->aux>>>(pr);
+                k_lin_seq_lw<true><<<w_early, 64, SEQLW_LDS, cs1>>>(pr);
                 HIP_TRY(hipGetLastError());
             }
-            HIP_TRY(hipEventRecord(ctx->ev[11], ctx->aux));
+            HIP_TRY(hipEventRecord(ctx->ev[11], cs1));
             // phase 3 after every phase-2 wave (both grids hand keys to it)
             HIP_TRY(hipStreamWaitEvent(st, ctx->ev[11], 0));
             HIP_TRY(hipEventRecord(ctx->ev[13], st));

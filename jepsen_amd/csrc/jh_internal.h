@@ -102,7 +102,7 @@ enum WsSlot {
     WS_S_BITS, WS_S_RUNS, WS_S_TMP, WS_S_CNT,
     WS_BFS_SET, WS_BFS_Q, WS_BFS_META, WS_CLAIM, WS_SCRATCH_BFS, WS_DEBUG, WS_META, WS_ARENA, WS_DEFER_PROG, WS_LIST_W, WS_C_PT,
     WS_DEFER3, WS_MEMO_P3, WS_STACK_P3, WS_SCRATCH_P3,
-    WS_LIST_X, WS_MEMO_X, WS_STACK_X, WS_SCRATCH_X, WS_C_OUT2, WS_C_TAB,
+    WS_LIST_X, WS_MEMO_X, WS_STACK_X, WS_SCRATCH_X, WS_C_OUT2, WS_C_TAB, WS_S_CODE,
     WS_SF_META, WS_SF_FLAG, WS_SF_LUT, WS_SF_TMP, WS_SF_ELEM, WS_SF_STATE, WS_SF_RFLAG, WS_SF_READS,
     WS_SF_BITS, WS_SF_OUT, WS_SF_FL, WS_SF_SEL, WS_SF_TIME, WS_SF_PART,
     WS_Q_META, WS_Q_PART, WS_Q_HIST, WS_Q_FLAG, WS_Q_ROWS, WS_Q_TMP, WS_Q_MULT, WS_Q_MFLAG, WS_Q_POS,

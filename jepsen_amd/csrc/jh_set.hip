@@ -34,15 +34,26 @@ __device__ __forceinline__ longlong2 ld_pair(const int64_t *__restrict__ c, int6
     return make_longlong2(c[2 * i], 0);
 }
 
+#ifndef JH_SET_CODE
+#define JH_SET_CODE 1        // the scan leaves a byte per row (1 :invoke :add, 2 :ok :add) for the byte-map pass
+#endif
 __global__ void __launch_bounds__(256) k_set_scan(const int64_t *__restrict__ type, const int64_t *__restrict__ f,
-                           const int64_t *__restrict__ val, int64_t n, int vec, SetMeta *m) {
+                           const int64_t *__restrict__ val, int64_t n, int vec, SetMeta *m,
+                           uint16_t *__restrict__ code) {
     long long lo = LLONG_MAX, hi = LLONG_MIN, fr = -1;
     int na = 0, nd = 0;
     const int64_t np = (n + 1) / 2;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const longlong2 t2 = ld_pair(type, i, n, vec), f2 = ld_pair(f, i, n, vec), v2 = ld_pair(val, i, n, vec);
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    // software-pipelined: the next pair's loads are issued before this pair's
+    // code store (stores and loads share one in-order counter on CDNA: a store
+    // issued before a load would make the wait for that load wait for it too)
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    longlong2 t2 = make_longlong2(0, 0), f2 = t2, v2 = t2;
+    if (i < np) { t2 = ld_pair(type, i, n, vec); f2 = ld_pair(f, i, n, vec); v2 = ld_pair(val, i, n, vec); }
+    for (; i < np; i += gs) {
         const int64_t tt[2] = {t2.x, t2.y}, ffs[2] = {f2.x, f2.y}, vv[2] = {v2.x, v2.y};
+        if (i + gs < np) { t2 = ld_pair(type, i + gs, n, vec); f2 = ld_pair(f, i + gs, n, vec); v2 = ld_pair(val, i + gs, n, vec); }
+        uint32_t cc = 0;
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const int64_t r = 2 * i + k;
@@ -52,8 +63,10 @@ __global__ void __launch_bounds__(256) k_set_scan(const int64_t *__restrict__ ty
                 const int64_t v = vv[k];
                 if (v == JH_NIL) { if (ty == T_INVOKE) na = 1; else nd = 1; }
                 else { lo = min(lo, (long long)v); hi = max(hi, (long long)v); }
+                cc |= (ty == T_INVOKE ? 1u : 2u) << (8 * k);
             } else if (ff == JH_F_READ && ty == T_OK) fr = max(fr, (long long)r);
         }
+        if (code) code[i] = (uint16_t)cc;
     }
     __shared__ long long sh[4];
     __shared__ int shi[4];
@@ -400,6 +413,42 @@ __global__ void __launch_bounds__(256) k_set_bytes_rows(const int64_t *__restric
     if ((threadIdx.x & 63) == 0 && best != ~0ULL) atomicMin(&m->first_lost_row, best);
 }
 
+// the same from the scan's row codes: 2 + 16 bytes per row pair instead of 48
+__global__ void __launch_bounds__(256) k_set_bytes_code(const uint16_t *__restrict__ code,
+                                                        const int64_t *__restrict__ val, int64_t n, long long vmin,
+                                                        uint8_t *__restrict__ Ab, uint8_t *__restrict__ Db,
+                                                        const uint32_t *__restrict__ R, int vec, SetMeta *m) {
+    unsigned long long best = ~0ULL;
+    const int64_t np = (n + 1) / 2;
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    // software-pipelined like k_set_scan: the next pair's code and values are
+    // loaded before this pair's byte stores
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    uint32_t ccn = 0;
+    longlong2 v2n = make_longlong2(0, 0);
+    if (i < np) { ccn = code[i]; v2n = ld_pair(val, i, n, vec); }
+    for (; i < np; i += gs) {
+        const uint32_t cc = ccn;
+        const int64_t vv[2] = {v2n.x, v2n.y};
+        if (i + gs < np) { ccn = code[i + gs]; v2n = ld_pair(val, i + gs, n, vec); }
+        if (!cc) continue;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint32_t c = (cc >> (8 * k)) & 0xFF;       // rows past n carry code 0
+            if (!c) continue;
+            const int64_t r = 2 * i + k;
+            const int64_t b = vv[k] - vmin;
+            if (c == 1) Ab[b] = 1;
+            else {
+                Db[b] = 1;
+                if (!((R[b >> 5] >> (b & 31)) & 1)) best = min(best, (unsigned long long)r);
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o));
+    if ((threadIdx.x & 63) == 0 && best != ~0ULL) atomicMin(&m->first_lost_row, best);
+}
+
 // 32 bytes -> one bitmap word, for each of A and D
 __global__ void __launch_bounds__(256) k_set_pack_bits(const uint8_t *__restrict__ bytes, int64_t span_pad, int64_t nw,
                                                        uint32_t *__restrict__ bits) {
@@ -541,7 +590,8 @@ static bool set_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, S
     mi.vmin = LLONG_MAX; mi.vmax = LLONG_MIN; mi.final_row = -1; mi.first_lost_row = ~0ULL;
     HIP_TRY(hipMemcpyAsync(m, &mi, sizeof mi, hipMemcpyHostToDevice, st));
     const int vec = ((uintptr_t)dh->type | (uintptr_t)dh->f | (uintptr_t)dh->value) % 16 == 0;
-    if (n > 0) k_set_scan<<<grid_for((n + 1) / 2, 256, 4096), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vec, m);
+    uint16_t *code = JH_SET_CODE ? ctx->ws<uint16_t>(WS_S_CODE, (size_t)(n + 1) / 2 + 1) : nullptr;
+    if (n > 0) k_set_scan<<<grid_for((n + 1) / 2, 256, 4096), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vec, m, code);
     HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     res->final_read_entry = mh.final_row;
@@ -595,7 +645,10 @@ static bool set_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, S
         const int64_t span_pad = nw * 32;
         uint8_t *bytes = ctx->ws<uint8_t>(WS_S_BYTES, 2 * span_pad);
         HIP_TRY(hipMemsetAsync(bytes, 0, 2 * span_pad, st));
-        if (n > 0)
+        if (n > 0 && code)
+            k_set_bytes_code<<<grid_for((n + 1) / 2, 256, 16384), 256, 0, st>>>(code, dh->value, n, vmin, bytes,
+                                                                               bytes + span_pad, R, vec, m);
+        else if (n > 0)
             k_set_bytes_rows<<<grid_for((n + 1) / 2, 256, 16384), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, bytes,
                                                                                bytes + span_pad, R, vec, m);
         k_set_pack_bits<<<grid_for(2 * nw, 256, 16384), 256, 0, st>>>(bytes, span_pad, nw, bits);

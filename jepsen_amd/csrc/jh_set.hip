@@ -34,6 +34,9 @@ __device__ __forceinline__ longlong2 ld_pair(const int64_t *__restrict__ c, int6
     return make_longlong2(c[2 * i], 0);
 }
 
+#ifndef JH_SET_CODE_WIDE
+#define JH_SET_CODE_WIDE 0   // eight lanes' codes in one 16-byte store (A/B)
+#endif
 #ifndef JH_SET_CODE
 #define JH_SET_CODE 1        // the scan leaves a byte per row (1 :invoke :add, 2 :ok :add) for the byte-map pass
 #endif
@@ -50,14 +53,24 @@ __global__ void __launch_bounds__(256) k_set_scan(const int64_t *__restrict__ ty
     int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     longlong2 t2 = make_longlong2(0, 0), f2 = t2, v2 = t2;
     if (i < np) { t2 = ld_pair(type, i, n, vec); f2 = ld_pair(f, i, n, vec); v2 = ld_pair(val, i, n, vec); }
+#if JH_SET_CODE_WIDE
+    // the loop runs while any lane of the wave has a pair (every lane takes
+    // part in the shuffles that gather eight lanes' codes into one 16-byte
+    // store; a lane past the end carries code 0)
+    const int64_t i_lane0 = i - (threadIdx.x & 63);
+    for (int64_t w0 = i_lane0; w0 < np; w0 += gs, i += gs) {
+        const bool live = i < np;
+#else
     for (; i < np; i += gs) {
+        const bool live = true;
+#endif
         const int64_t tt[2] = {t2.x, t2.y}, ffs[2] = {f2.x, f2.y}, vv[2] = {v2.x, v2.y};
         if (i + gs < np) { t2 = ld_pair(type, i + gs, n, vec); f2 = ld_pair(f, i + gs, n, vec); v2 = ld_pair(val, i + gs, n, vec); }
         uint32_t cc = 0;
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const int64_t r = 2 * i + k;
-            if (r >= n) break;
+            if (!live || r >= n) break;
             const int64_t ty = tt[k], ff = ffs[k];
             if (ff == JH_F_ADD && (ty == T_INVOKE || ty == T_OK)) {
                 const int64_t v = vv[k];
@@ -66,7 +79,16 @@ __global__ void __launch_bounds__(256) k_set_scan(const int64_t *__restrict__ ty
                 cc |= (ty == T_INVOKE ? 1u : 2u) << (8 * k);
             } else if (ff == JH_F_READ && ty == T_OK) fr = max(fr, (long long)r);
         }
+#if JH_SET_CODE_WIDE
+        if (code) {
+            const uint32_t x = cc | ((uint32_t)__shfl_down((int)cc, 1) << 16);     // lanes l, l + 1
+            const uint32_t y1 = (uint32_t)__shfl_down((int)x, 2), y2 = (uint32_t)__shfl_down((int)x, 4),
+                           y3 = (uint32_t)__shfl_down((int)x, 6);
+            if ((threadIdx.x & 7) == 0 && live) ((uint4 *)code)[i >> 3] = make_uint4(x, y1, y2, y3);
+        }
+#else
         if (code) code[i] = (uint16_t)cc;
+#endif
     }
     __shared__ long long sh[4];
     __shared__ int shi[4];
@@ -590,7 +612,7 @@ static bool set_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, S
     mi.vmin = LLONG_MAX; mi.vmax = LLONG_MIN; mi.final_row = -1; mi.first_lost_row = ~0ULL;
     HIP_TRY(hipMemcpyAsync(m, &mi, sizeof mi, hipMemcpyHostToDevice, st));
     const int vec = ((uintptr_t)dh->type | (uintptr_t)dh->f | (uintptr_t)dh->value) % 16 == 0;
-    uint16_t *code = JH_SET_CODE ? ctx->ws<uint16_t>(WS_S_CODE, (size_t)(n + 1) / 2 + 1) : nullptr;
+    uint16_t *code = JH_SET_CODE ? ctx->ws<uint16_t>(WS_S_CODE, (size_t)(n + 1) / 2 + 16) : nullptr;   // + a 16-byte tail
     if (n > 0) k_set_scan<<<grid_for((n + 1) / 2, 256, 4096), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vec, m, code);
     HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));

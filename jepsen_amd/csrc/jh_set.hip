@@ -34,6 +34,12 @@ __device__ __forceinline__ longlong2 ld_pair(const int64_t *__restrict__ c, int6
     return make_longlong2(c[2 * i], 0);
 }
 
+#ifndef JH_SCAN_GRID
+#define JH_SCAN_GRID 8192     // grid caps of the scan and the byte-map pass (profiles/r04/c2_spill/r4sgrid_*: scan 2048 / 4096 / 8192 / 16384 blocks 493 / 483-501 / 456-458 / 509-516 us)
+#endif
+#ifndef JH_BYTES_GRID
+#define JH_BYTES_GRID 16384
+#endif
 #ifndef JH_SET_CODE_WIDE
 #define JH_SET_CODE_WIDE 0   // eight lanes' codes in one 16-byte store (A/B)
 #endif
@@ -613,7 +619,7 @@ static bool set_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, S
     HIP_TRY(hipMemcpyAsync(m, &mi, sizeof mi, hipMemcpyHostToDevice, st));
     const int vec = ((uintptr_t)dh->type | (uintptr_t)dh->f | (uintptr_t)dh->value) % 16 == 0;
     uint16_t *code = JH_SET_CODE ? ctx->ws<uint16_t>(WS_S_CODE, (size_t)(n + 1) / 2 + 16) : nullptr;   // + a 16-byte tail
-    if (n > 0) k_set_scan<<<grid_for((n + 1) / 2, 256, 4096), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vec, m, code);
+    if (n > 0) k_set_scan<<<grid_for((n + 1) / 2, 256, JH_SCAN_GRID), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vec, m, code);
     HIP_TRY(hipMemcpyAsync(&mh, m, sizeof mh, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     res->final_read_entry = mh.final_row;
@@ -668,7 +674,7 @@ static bool set_bitmaps(jh_ctx *ctx, const jh_history *dh, jh_set_result *res, S
         uint8_t *bytes = ctx->ws<uint8_t>(WS_S_BYTES, 2 * span_pad);
         HIP_TRY(hipMemsetAsync(bytes, 0, 2 * span_pad, st));
         if (n > 0 && code)
-            k_set_bytes_code<<<grid_for((n + 1) / 2, 256, 16384), 256, 0, st>>>(code, dh->value, n, vmin, bytes,
+            k_set_bytes_code<<<grid_for((n + 1) / 2, 256, JH_BYTES_GRID), 256, 0, st>>>(code, dh->value, n, vmin, bytes,
                                                                                bytes + span_pad, R, vec, m);
         else if (n > 0)
             k_set_bytes_rows<<<grid_for((n + 1) / 2, 256, 16384), 256, 0, st>>>(dh->type, dh->f, dh->value, n, vmin, bytes,

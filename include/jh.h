@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define JH_ABI_VERSION 5
+#define JH_ABI_VERSION 6
 
 /* Return codes. Anything non-zero also writes a NUL-terminated message into
  * the caller's err buffer; the JNA shim throws ex-info and check-safe turns
@@ -279,29 +279,44 @@ int jh_check_cas_independent(jh_ctx *ctx, const jh_history *h,
 int jh_key_index(jh_ctx *ctx, const jh_history *h, int64_t *key_off, int64_t *rows,
                  char *err, size_t errlen);
 
-/* The frontier of invalid keys: knossos' :configs (checker.clj:146-158
- * passes the analysis through and keeps (take 10 ...) of them). For each
- * requested key that is invalid, up to per_key (<= 16) configurations of the
- * last layer its search reaches -- the ways of linearizing the ops before the
- * failing :ok op from which that op cannot be linearized -- in a canonical
- * order: register value (nil first, then ascending), then the linearized
- * members of the window as a bit mask in call order (a JH_MAX_WINDOW-bit
- * number). n_out[i] = the count for keys[i], or -1 (not invalid, a window
- * over JH_MAX_WINDOW members, or more than budget configurations reachable).
+/* knossos' :configs (checker.clj:146-158 passes the analysis through and
+ * keeps (take 10 ...) of them), from the JIT-linearization analysis
+ * (:algorithm :linear; doc/tutorial/04-checker.md:126-138 prints one).
+ *  - An invalid key: its frontier -- the configurations of the last layer
+ *    its search reaches, the ways of linearizing the ops before the failing
+ *    :ok op from which that op cannot be.
+ *  - A valid key (ABI 6): its final configurations -- the configurations the
+ *    analysis holds after the key's last :ok completion: every way the
+ *    crashed ops may stand once every :ok op is linearized (the register
+ *    value, and which crashed ops were linearized).
+ * For each requested key, up to per_key (<= 16) configurations in a
+ * canonical order: register value (nil first, then ascending), then the
+ * linearized members as a bit mask in call order (a JH_MAX_WINDOW-bit
+ * number). n_out[i] = the count for keys[i], or -1 (no search was needed, a
+ * window over JH_MAX_WINDOW members, more than budget configurations
+ * reachable, or a valid key the reachable-set engine cannot hold: WGL
+ * decides those, and a WGL analysis carries no configurations).
  * Windows up to 32 members with < 4096 states come from the reachable-set
- * engine, wider ones (round 4) from the 65-256-member search's table.
+ * engine, wider invalid ones (round 4) from the 65-256-member search's table.
  * out[i * per_key + j] describes configuration j of keys[i]; its rows are
  * rows_out[rows_off .. rows_off + n_linearized + n_pending): the invocation
  * rows of the linearized ops, then of the pending ones (knossos' :pending),
- * each in call order; rows_cap >= n_keys_q * per_key * JH_MAX_WINDOW. knossos is not
- * vendored: this order, the cut and the layer are this library's
- * definitions (parity unpinned; the oracle restates them). */
+ * each in call order -- for a frontier the members of the window, for final
+ * configurations the crashed ops (their :info completion or none) the search
+ * keeps; rows_cap >= n_keys_q * per_key * JH_MAX_WINDOW. last_row (ABI 6) is
+ * the configuration's :last-op as knossos' analysis prints it: the row of the
+ * key's last client :ok completion before the configurations' point (the
+ * failing op's completion for a frontier, the end of the history for final
+ * configurations), -1 if there is none. knossos is not vendored: this order,
+ * the cut and the layer are this library's definitions (parity unpinned; the
+ * oracle restates them). */
 typedef struct jh_lin_config {
     int64_t key;
     int64_t model_value;       /* the register's value in this configuration (JH_NIL: nil) */
     int32_t n_linearized;
     int32_t n_pending;
     int64_t rows_off;
+    int64_t last_row;          /* ABI 6: the :ok completion that is this configuration's :last-op, or -1 */
 } jh_lin_config;
 
 int jh_lin_configs(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts,

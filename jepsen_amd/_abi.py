@@ -6,7 +6,7 @@ every struct layout.
 """
 import ctypes as C
 
-JH_ABI_VERSION = 5
+JH_ABI_VERSION = 6
 
 JH_OK, JH_EINVAL, JH_EUNSUPPORTED, JH_EDEVICE, JH_ENOMEM = 0, 1, 2, 3, 4
 TYPE_INVOKE, TYPE_OK, TYPE_FAIL, TYPE_INFO = 0, 1, 2, 3
@@ -106,7 +106,8 @@ class JhSummary(C.Structure):
 
 class JhLinConfig(C.Structure):
     _fields_ = [("key", C.c_int64), ("model_value", C.c_int64), ("n_linearized", C.c_int32),
-                ("n_pending", C.c_int32), ("rows_off", C.c_int64)]
+                ("n_pending", C.c_int32), ("rows_off", C.c_int64),
+                ("last_row", C.c_int64)]            # ABI 6: the :ok completion that is :last-op
 
 
 CONFIGS_PER_KEY = 10          # checker.clj:146-158: (take 10 ...) of :configs and :final-paths

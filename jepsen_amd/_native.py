@@ -254,8 +254,9 @@ class Context:
         return {f: getattr(v, f) for f, _ in A.JhKeyVerdict._fields_}
 
     def lin_configs(self, cols, keys, per_key=A.CONFIGS_PER_KEY, init=None, budget=None, **tune):
-        """jh_lin_configs: {key: None | [(model_value, linearized rows, pending rows)]}
-        -- the frontier configurations of each invalid key (include/jh.h)."""
+        """jh_lin_configs: {key: None | [(model_value, linearized rows, pending rows, last_row)]}
+        -- each invalid key's frontier, each valid :linear key's final
+        configurations (include/jh.h)."""
         h = A.make_history(cols)
         keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
         nq = len(keys)
@@ -277,7 +278,8 @@ class Context:
             for j in range(n_out[i]):
                 c = out[i * per_key + j]
                 r = rows[c.rows_off:c.rows_off + c.n_linearized + c.n_pending]
-                cs.append((int(c.model_value), r[:c.n_linearized].tolist(), r[c.n_linearized:].tolist()))
+                cs.append((int(c.model_value), r[:c.n_linearized].tolist(), r[c.n_linearized:].tolist(),
+                           int(c.last_row)))
             res[k] = cs
         return res
 

@@ -157,29 +157,66 @@ CAUSE_ERRORS = {
 }
 
 
-def lin_result(valid, cause, fail_entry, explored, cols=None, previous_ok=-1, last_op=-1, analyzer=A.ANALYZER_WGL):
-    """Per-history result map of checker/linearizable (checker.clj:139-158).
-    :analyzer is the analysis that decided the key (jh_key_verdict.analyzer:
-    :wgl, or :linear under {:algorithm :linear}). An invalid result carries
-    :op (the ok completion no configuration gets past) and, from the search
-    frontier, :previous-ok and :last-op (include/jh.h; knossos is not
-    vendored, so their exact knossos definitions are parity unpinned)."""
+class Analysis(dict):
+    """A result map of checker/linearizable, plus the ABI's per-key side
+    channel as attributes -- not map keys. checker.clj:156-158 returns
+    knossos' analysis with :final-paths and :configs assoc'ed on, and the
+    reference's printed analysis (doc/tutorial/04-checker.md:126-138) has no
+    :explored or failing-row key; jh_key_verdict's `explored` (WGL's cache
+    size, the count the parity tests compare with the oracle) and
+    `fail_entry` (the failing op's row) ride along here, where the JVM shim
+    keeps them out of the Clojure map as well."""
+    __slots__ = ("explored", "fail_entry")
+
+    def __init__(self, m, explored=-1, fail_entry=-1):
+        super().__init__(m)
+        self.explored = explored
+        self.fail_entry = fail_entry
+
+
+def lin_result(valid, cause, fail_entry, explored, cols=None, previous_ok=-1, last_op=-1, analyzer=A.ANALYZER_WGL,
+               ops=None):
+    """Per-history result map of checker/linearizable (checker.clj:139-158):
+    the analysis with :configs and :final-paths assoc'ed on (empty until
+    add_configs fills them) and :analyzer, the analysis that decided the key
+    (jh_key_verdict.analyzer: :wgl, or :linear under {:algorithm :linear}).
+    An invalid result carries :op (the ok completion no configuration gets
+    past) and, from the search frontier, :previous-ok and :last-op (include/jh.h;
+    knossos is not vendored, so their exact knossos definitions are parity
+    unpinned). ops: the history's op maps, when the caller has them (op maps
+    are then the caller's own, :time and all)."""
     c = A.CAUSES.get(int(cause))
     an = A.ANALYZERS.get(int(analyzer), "wgl")
+    side = dict(explored=int(explored), fail_entry=int(fail_entry))
     if valid == A.VALID:
-        return {"valid?": True, "analyzer": an, "explored": int(explored)}
+        return Analysis({"valid?": True, "configs": [], "analyzer": an, "final-paths": []}, **side)
     if valid == A.INVALID:
-        r = {"valid?": False, "analyzer": an, "explored": int(explored),
-             "fail-entry": int(fail_entry)}
+        r = {"valid?": False}
         if cols is not None and 0 <= fail_entry < cols.n:
-            r["op"] = H.decode_op(cols, int(fail_entry))
+            r["op"] = op_at(cols, ops, int(fail_entry))
         if cols is not None:
-            r["previous-ok"] = H.decode_op(cols, int(previous_ok)) if 0 <= previous_ok < cols.n else None
-            r["last-op"] = H.decode_op(cols, int(last_op)) if 0 <= last_op < cols.n else None
-        return r
+            r["previous-ok"] = op_at(cols, ops, int(previous_ok)) if 0 <= previous_ok < cols.n else None
+            r["last-op"] = op_at(cols, ops, int(last_op)) if 0 <= last_op < cols.n else None
+        r.update({"configs": [], "analyzer": an, "final-paths": []})
+        return Analysis(r, **side)
     if c == "budget":
-        return {"valid?": UNKNOWN, "analyzer": an, "cause": "budget", "explored": int(explored)}
-    return {"valid?": UNKNOWN, "error": CAUSE_ERRORS.get(c, c), "cause": c}
+        return Analysis({"valid?": UNKNOWN, "cause": "budget", "configs": [], "analyzer": an, "final-paths": []},
+                        **side)
+    return Analysis({"valid?": UNKNOWN, "error": CAUSE_ERRORS.get(c, c), "cause": c}, **side)
+
+
+def op_at(cols, ops, row):
+    """The op map at a history row: the caller's own map when it passed op
+    maps (knossos hands its analysis the history's maps; their :index is the
+    full history's, core.clj:441), else decoded from the columns. An
+    independent tuple value is unwrapped, as subhistory does
+    (independent.clj:234-245)."""
+    if ops is not None and 0 <= row < len(ops):
+        op = dict(ops[row])
+        op.setdefault("index", row)
+    else:
+        op = H.decode_op(cols, int(row))
+    return _unwrap(op)
 
 
 class Linearizable(Checker):
@@ -203,66 +240,77 @@ class Linearizable(Checker):
     def check(self, test, history, opts):
         if not self.supported():
             raise NotImplementedError(f"model {self.model!r} has no device implementation")
+        ops = None
         if not isinstance(history, H.Columns):
-            history = to_device_ops(self.model, list(history))
+            ops = list(history)
+            history = to_device_ops(self.model, ops)
         cols = _cols(history, keyed=False)
         init = _init_state(self.model, cols)
         r = _ctx().check_cas_full(cols, init=init, budget=self.budget, algorithm=_algorithm(self.algorithm))
         out = lin_result(r["valid"], r["cause"], r["fail_entry"], r["explored"], cols,
-                         r["previous_ok"], r["last_op"], r["analyzer"])
-        if r["valid"] == A.INVALID:
+                         r["previous_ok"], r["last_op"], r["analyzer"], ops=ops)
+        if wants_configs(r["valid"], r["analyzer"]):
             cf = _ctx().lin_configs(cols, [0], init=init, budget=self.budget)
-            add_configs(out, cf[0], cols, self.model)
+            add_configs(out, cf[0], cols, self.model, ops=ops)
             from .report import maybe_render
             maybe_render(test, opts, cols, out)
         return out
 
 
-def add_configs(result, configs, cols, model=None):
-    """:configs and :final-paths of an invalid result (checker.clj:146-158
-    keeps (take 10 ...) of each), from jh_lin_configs: the frontier -- the
-    configurations at the last layer any search reaches, first 10 in the
-    canonical order (include/jh.h).
+def wants_configs(valid, analyzer):
+    """Which analyses carry :configs (checker.clj:156-158 keeps (take 10 ...)):
+    an invalid one's frontier, and a valid :linear one's final configurations
+    (doc/tutorial/04-checker.md:126-138 prints one). A valid WGL analysis has
+    none."""
+    return int(valid) == A.INVALID or (int(valid) == A.VALID and int(analyzer) == A.ANALYZER_LINEAR)
 
-    A configuration is shaped as knossos 0.3.x's Config record [K] (model,
-    last-op, pending): the model, the last op linearized (the linearized
-    window member invoked last; nil when the window has none: the order in
-    which the rest were linearized is not part of a configuration) and the
-    pending ops in call order. A final path starts at the configuration
+
+def add_configs(result, configs, cols, model=None, ops=None):
+    """:configs and :final-paths (checker.clj:146-158 keeps (take 10 ...) of
+    each), from jh_lin_configs: an invalid key's frontier -- the
+    configurations at the last layer any search reaches -- or a valid :linear
+    key's final configurations, first 10 in the canonical order (include/jh.h).
+
+    A configuration is shaped as knossos' analysis prints one
+    (doc/tutorial/04-checker.md:128-135): the model; :last-op, the :ok
+    completion of the last op linearized, with its own :index (jh_lin_config
+    .last_row); :pending, the ops invoked and not linearized, in call order.
+    A final path (invalid keys only) starts at the configuration
     ({:op last-op :model model}), linearizes the pending ops that step
     consistently, in call order, each with the model after it, and ends in
     the failing :op, inconsistent from every frontier model (a model it could
     step from would have a successor past the op's completion) -- one path
-    per configuration. knossos is not vendored: the shape follows its record
-    from memory and the path choice is this library's, parity unpinned."""
+    per configuration. knossos is not vendored: the path choice is this
+    library's, parity unpinned."""
     if configs is None:
         return result
     cf = []
-    for v, lin, pend in configs:
+    for v, lin, pend, last_row in configs:
         val = None if v == A.NIL else int(v)
         if val is not None and cols.values_interned and 0 <= val < len(cols.value_table):
             val = cols.value_table[val]          # interned history: the state is a value-table id
         m = _model_of(model, val)
         cf.append({"model": _model_map(m),
-                   "last-op": _completed_op(cols, max(lin)) if lin else None,
-                   "pending": [_completed_op(cols, x) for x in sorted(pend)],
+                   "last-op": op_at(cols, ops, last_row) if last_row >= 0 else None,
+                   "pending": [_completed_op(cols, x, ops) for x in pend],
                    "_m": m})
     op = result.get("op")
     paths = []
-    for c in cf[:A.CONFIGS_PER_KEY]:
-        m = c["_m"]
-        path = [{"op": c["last-op"], "model": _model_map(m)}]
-        for p in c["pending"]:
-            r = _step(m, p)
-            if r is None or is_inconsistent(r):
-                continue
-            m = r
-            path.append({"op": p, "model": _model_map(m)})
-        if op is not None:
-            r = _step(m, op)
-            path.append({"op": op, "model": ({"inconsistent": r.msg} if is_inconsistent(r) else
-                                             {"error": "no step"} if r is None else _model_map(r))})
-        paths.append(path)
+    if result.get("valid?") is False:
+        for c in cf[:A.CONFIGS_PER_KEY]:
+            m = c["_m"]
+            path = [{"op": c["last-op"], "model": _model_map(m)}]
+            for p in c["pending"]:
+                r = _step(m, p)
+                if r is None or is_inconsistent(r):
+                    continue
+                m = r
+                path.append({"op": p, "model": _model_map(m)})
+            if op is not None:
+                r = _step(m, op)
+                path.append({"op": op, "model": ({"inconsistent": r.msg} if is_inconsistent(r) else
+                                                 {"error": "no step"} if r is None else _model_map(r))})
+            paths.append(path)
     for c in cf:
         del c["_m"]
     result["configs"] = cf[:A.CONFIGS_PER_KEY]
@@ -270,27 +318,38 @@ def add_configs(result, configs, cols, model=None):
     return result
 
 
-def _completed_op(cols, row):
+def _next_same_process(cols):
+    """For every row, the next row of the same process (-1 if none): one
+    stable sort per history, cached on the columns (a scan of the
+    whole column per op cost more than the device check on big histories)."""
+    nxt = getattr(cols, "_next_same_proc", None)
+    if nxt is None:
+        order = np.argsort(cols.process, kind="stable")
+        nxt = np.full(cols.n, -1, np.int64)
+        same = cols.process[order[1:]] == cols.process[order[:-1]]
+        nxt[order[:-1][same]] = order[1:][same]
+        cols._next_same_proc = nxt
+    return nxt
+
+
+def _completed_op(cols, row, ops=None):
     """The invocation at `row` as knossos.history/complete leaves it [K]
     (cassandra/src/cassandra/checker.clj:29-31): an :ok completion fills a
     nil :value -- the next row of the same process completes it."""
-    op = H.decode_op(cols, int(row))
-    v = op.get("value")
-    if v is None or (hasattr(v, "value") and hasattr(v, "key") and v.value is None):
+    op = op_at(cols, ops, int(row))
+    if op.get("value") is None:
         p = int(cols.process[row])
         if p >= 0:
-            nxt = np.nonzero(cols.process[row + 1:] == p)[0]
-            if len(nxt):
-                c = H.decode_op(cols, int(row + 1 + nxt[0]))
-                if c.get("type") == "ok":
-                    op = dict(op, value=c.get("value"))
+            c = int(_next_same_process(cols)[row])
+            if c >= 0 and int(cols.type[c]) == A.TYPE_OK:
+                op = dict(op, value=op_at(cols, ops, c).get("value"))
     return op
 
 
 def _unwrap(op):
     v = op.get("value")
-    if hasattr(v, "key") and hasattr(v, "value"):       # an independent tuple
-        op = dict(op, value=v.value)
+    if H.is_tuple(v):                                   # an independent tuple
+        op = dict(op, value=v.val)
     return op
 
 

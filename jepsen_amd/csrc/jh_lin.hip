@@ -4162,12 +4162,24 @@ __device__ long long cfg_state_value(uint32_t st, int per_key_values, long long 
     }
     return JH_NIL;
 }
-__device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int key, const int32_t *woff,
-                                 const uint16_t *W, uint32_t n_ok) {
+// fin = false: the frontier of an invalid key (above). fin = true (ABI 6):
+// the final configurations of a valid key under :linear -- what the
+// JIT-linearization analysis holds after the key's last :ok completion. Each
+// terminal edge of the reachable set ends one: lifting RET[t] from a layer-t
+// configuration whose cross-layer cascade reaches n_ok. What remains of W(t)
+// then is crashed ops only (every op returning at or after t was dropped on
+// the way), and W(t)'s crashed ops are the first members, in call order, of
+// C = W(n_ok - 1) - {RET[n_ok - 1]} (crashed ops never leave a window): a final
+// configuration is (value, mask over C), ordered like the frontier's. Kept
+// crashed ops invoked after the last :ok return enter no window; they are
+// pending in every final configuration.
+__device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int key, const Op *ops,
+                                 const int32_t *woff, const uint16_t *W, const uint8_t *rpos, uint32_t n_ok,
+                                 bool fin) {
     const int slot = A.cfg_slot[key];
     const int lane = tid & 63, wid = tid >> 6;
-    const uint32_t tm = sh.tmax;
-    const uint32_t a = A.lstart[tm], b = tm + 1 < n_ok ? A.lstart[tm + 1] : sh.nnodes;
+    const uint32_t tm = fin ? n_ok - 1 : sh.tmax;
+    const uint32_t a = fin ? 0 : A.lstart[tm], b = (!fin && tm + 1 < n_ok) ? A.lstart[tm + 1] : sh.nnodes;
     __shared__ unsigned long long sel[CFG_MAX];
     __shared__ long long wrow[64];
     __shared__ int nsel;
@@ -4179,7 +4191,26 @@ __device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int k
         __syncthreads();
         unsigned long long m = ~0ULL;
         for (uint32_t j = a + tid; j < b; j += BFS_THREADS) {
-            const unsigned long long kk = A.nodes[j] & ((1ULL << 44) - 1);   // s:12 | mask:32
+            const uint64_t e = A.nodes[j];
+            unsigned long long kk = e & ((1ULL << 44) - 1);   // s:12 | mask:32
+            if (fin) {
+                const uint32_t t = (uint32_t)(e >> 44), r = rpos[t];
+                const Op o = ops[W[woff[t] + r]];
+                int s2;
+                if (!cas_step(o.fa & 3, o.v1, o.v2, (int)((e >> 32) & 0xFFF), &s2)) continue;
+                uint64_t nm = (uint32_t)e | (1ULL << r);
+                uint32_t u = t, ru = r;
+                for (;;) {
+                    nm = drop_bit(nm, ru);
+                    u++;
+                    if (u >= n_ok) break;
+                    ru = rpos[u];
+                    if (!((nm >> ru) & 1)) break;
+                }
+                if (u < n_ok) continue;                          // not a terminal edge
+                // s:12 | mask over C:32 | t:20 (the layer whose RET was lifted last)
+                kk = ((unsigned long long)(uint32_t)s2 << 52) | ((unsigned long long)(uint32_t)nm << 20) | t;
+            }
             if ((i == 0 || kk > prev) && kk < m) m = kk;
         }
         for (int o = 32; o > 0; o >>= 1) m = min(m, (unsigned long long)__shfl_xor(m, o));
@@ -4192,7 +4223,7 @@ __device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int k
     }
     __syncthreads();
     if (wid != 0) return;
-    // the invocation row of every member of W(tmax)
+    // the invocation row of every member of W(tm)
     const int wo = woff[tm], w = woff[tm + 1] - wo;
     for (uint32_t base = sh.K.s0; base < sh.K.s1; base += 64) {
         const uint32_t p = base + lane;
@@ -4202,23 +4233,71 @@ __device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int k
                 if ((int)W[wo + j] == rk) wrow[j] = (long long)A.src.rows[p];
     }
     wave_sync();
+    // final configurations: C is W(tm) without RET[tm] (member rl)
+    const int rl = fin ? (int)rpos[tm] : 64;
+    const int wc = fin ? w - 1 : w;
+    const long long crow = lane < wc ? wrow[lane + (lane >= rl ? 1 : 0)] : -1;
+    // :last-op: a frontier's is the last :ok op before the failing one
+    // (RET[tmax - 1]); a final configuration's the :ok op its terminal edge
+    // linearized last -- JIT linearization ends each expansion in the op that
+    // completes, and a configuration that already holds a later op keeps it
+    const long long lfront = fin || tm == 0 ? -1 : ret_row(A.src, sh.K, tm - 1, lane);
     for (int i = 0; i < nsel; i++) {
-        const uint32_t st = (uint32_t)(sel[i] >> 32) & 0xFFF, mask = (uint32_t)sel[i];
+        const uint32_t st = fin ? (uint32_t)(sel[i] >> 52) : (uint32_t)(sel[i] >> 32) & 0xFFF;
+        const uint32_t mask = fin ? (uint32_t)(sel[i] >> 20) : (uint32_t)sel[i];
+        const long long lrow = fin ? ret_row(A.src, sh.K, (uint32_t)(sel[i] & 0xFFFFF), lane) : lfront;
         const long long val = cfg_state_value(st, A.per_key_values, A.vmin, A.init_value, A.src, sh.K.s0, sh.K.s1,
                                               A.col_val, A.col_val2, lane);
         const int64_t o = ((int64_t)slot * A.cfg_per + i) * CFG_ROWS;
-        const bool in = lane < w, lin = in && ((mask >> lane) & 1);
+        const bool in = lane < wc, lin = in && ((mask >> lane) & 1);
         const uint64_t bl = ballot(lin), bp = ballot(in && !lin);
         const int nl = __popcll(bl);
-        if (lin) A.cfg_rows[o + mbcnt(bl)] = wrow[lane];
-        if (in && !lin) A.cfg_rows[o + nl + mbcnt(bp)] = wrow[lane];
+        int np = __popcll(bp);
+        if (lin) A.cfg_rows[o + mbcnt(bl)] = crow;
+        if (in && !lin) A.cfg_rows[o + nl + mbcnt(bp)] = crow;
+        if (fin) {
+            // kept crashed ops invoked after the last :ok return (call order)
+            for (uint32_t base = sh.K.s0; base < sh.K.s1; base += 64) {
+                const uint32_t p = base + lane;
+                const int rk = p < sh.K.s1 ? A.src.rank[p] : -1;
+                const bool late = rk >= 0 && ops[rk].rr < 0 && (uint32_t)(ops[rk].fa >> 2) >= n_ok;
+                const uint64_t bm = ballot(late);
+                const int at = nl + np + (int)mbcnt(bm);
+                if (late && at < CFG_ROWS) A.cfg_rows[o + at] = (int64_t)A.src.rows[p];
+                np = min(np + __popcll(bm), CFG_ROWS - nl);
+            }
+        }
         if (lane == 0) {
             jh_lin_config c;
-            c.key = key; c.model_value = val; c.n_linearized = nl; c.n_pending = __popcll(bp); c.rows_off = o;
+            c.key = key; c.model_value = val; c.n_linearized = nl; c.n_pending = np; c.rows_off = o;
+            c.last_row = lrow;
             A.cfg_out[(int64_t)slot * A.cfg_per + i] = c;
         }
     }
     if (lane == 0) A.cfg_n[slot] = nsel;
+}
+
+// the configuration of a valid key with no :ok op (one wave)
+__device__ void bfs_dump_initial(const BfsArgs &A, BfsShared &sh, int lane, int key) {
+    const int slot = A.cfg_slot[key];
+    const long long val = cfg_state_value((uint32_t)A.init_state, A.per_key_values, A.vmin, A.init_value, A.src,
+                                          sh.K.s0, sh.K.s1, A.col_val, A.col_val2, lane);
+    const int64_t o = (int64_t)slot * A.cfg_per * CFG_ROWS;
+    int np = 0;
+    for (uint32_t base = sh.K.s0; base < sh.K.s1; base += 64) {
+        const uint32_t p = base + lane;
+        const bool kept = p < sh.K.s1 && A.src.rank[p] >= 0;
+        const uint64_t bm = ballot(kept);
+        const int at = np + (int)mbcnt(bm);
+        if (kept && at < CFG_ROWS) A.cfg_rows[o + at] = (int64_t)A.src.rows[p];
+        np = min(np + __popcll(bm), CFG_ROWS);
+    }
+    if (lane == 0) {
+        jh_lin_config c;
+        c.key = key; c.model_value = val; c.n_linearized = 0; c.n_pending = np; c.rows_off = o; c.last_row = -1;
+        A.cfg_out[(int64_t)slot * A.cfg_per] = c;
+        A.cfg_n[slot] = 1;
+    }
 }
 
 #ifndef JH_BFS_ITEMS
@@ -4642,8 +4721,8 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         if (tid == 0 && !(sh.status & 4)) A.unres_list[atomicAdd(A.unres_count, 1)] = key;
     } else if (A.linear) {
         // JIT linearization's verdict: the configuration set survives the last return or not
-        if (!sh.term && A.cfg_slot && A.cfg_slot[key] >= 0 && !sh.nostore)
-            bfs_dump_configs(A, sh, tid, key, woff, W, n_ok);
+        if (A.cfg_slot && A.cfg_slot[key] >= 0 && !sh.nostore)
+            bfs_dump_configs(A, sh, tid, key, ops, woff, W, rpos, n_ok, sh.term != 0);
         __syncthreads();
         if (wid == 0) {
             jh_key_verdict v;
@@ -4725,6 +4804,11 @@ __global__ void __launch_bounds__(BFS_THREADS) k_lin_bfs(BfsArgs A0) {
         __syncthreads();
         if (!sh.need) {
             if (tid == 0) emit_verdict(A.out, A.claim, key, sh.v);
+            // jh_lin_configs on a key with no :ok op (valid, no search): its one
+            // configuration is the initial one, every crashed op pending
+            if (wid == 0 && A.cfg_slot && A.cfg_slot[key] >= 0 && sh.v.valid == JH_VALID && sh.v.explored == 0 &&
+                sh.K.n_ok == 0)
+                bfs_dump_initial(A, sh, lane, key);
             __syncthreads();
             continue;
         }
@@ -5000,6 +5084,9 @@ __device__ void xw_dump_configs(const XwArgs &A, const uint64_t *memo, uint32_t 
         }
     }
     const int per = min(A.cfg_per, CFG_MAX);
+    KeyInfo Ki{};
+    Ki.s0 = s0; Ki.s1 = s1;
+    const long long lrow = tmax == 0 ? -1 : ret_row(A.src, Ki, tmax - 1, lane);   // :last-op, RET[tmax - 1]
     Cfg5 prev{0, 0, 0, 0, 0};
     int n = 0;
     for (int i = 0; i < per; i++) {
@@ -5051,6 +5138,7 @@ __device__ void xw_dump_configs(const XwArgs &A, const uint64_t *memo, uint32_t 
         if (lane == 0) {
             jh_lin_config cf;
             cf.key = key; cf.model_value = val; cf.n_linearized = nl; cf.n_pending = np; cf.rows_off = o;
+            cf.last_row = lrow;
             A.cfg_out[(int64_t)slot * A.cfg_per + i] = cf;
         }
     }

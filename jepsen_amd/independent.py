@@ -8,7 +8,7 @@ the GPU); any other composed checkers still run per key on their own.
 from . import _abi as A
 from . import history as H
 from .checker import (Checker, Compose, Linearizable, _algorithm, add_configs, check_safe, lin_result, merge_valid,
-                      _init_state, _ctx)
+                      wants_configs, _init_state, _ctx)
 from .model import to_device_ops
 
 DIR = "independent"
@@ -131,14 +131,16 @@ class IndependentChecker(Checker):
                         continue
                     lin_res[key] = lin_result(int(v["valid"]), int(v["cause"]), int(v["fail_entry"]),
                                               int(v["explored"]), cols, int(v["previous_ok"]),
-                                              int(v["last_op"]), int(v["analyzer"]))
-                bad = [kid for kid, key in enumerate(cols.keys) if int(verdicts[kid]["valid"]) == A.INVALID]
-                if bad:
-                    # the frontier of every invalid key, one device call (jh_lin_configs)
-                    cf = _ctx().lin_configs(cols, bad, init=_init_state(lin.model, cols), budget=lin.budget)
+                                              int(v["last_op"]), int(v["analyzer"]), ops=history)
+                want = [kid for kid, key in enumerate(cols.keys)
+                        if key in lin_res and wants_configs(verdicts[kid]["valid"], verdicts[kid]["analyzer"])]
+                if want:
+                    # every invalid key's frontier and every valid :linear key's
+                    # final configurations, one device call (jh_lin_configs)
+                    cf = _ctx().lin_configs(cols, want, init=_init_state(lin.model, cols), budget=lin.budget)
                     from .report import maybe_render
-                    for kid in bad:
-                        add_configs(lin_res[cols.keys[kid]], cf[kid], cols, lin.model)
+                    for kid in want:
+                        add_configs(lin_res[cols.keys[kid]], cf[kid], cols, lin.model, ops=history)
                         maybe_render(test, {"subdirectory": [DIR, cols.keys[kid]]}, cols, lin_res[cols.keys[kid]])
                 if name is None:
                     return self._results_map(lin_res)

@@ -367,11 +367,45 @@ static void cvec_push(cvec *v, const cfg *c) {
     if (v->n == v->cap) { v->cap = v->cap ? 2 * v->cap : 256; v->e = (cfg *)realloc(v->e, sizeof(cfg) * v->cap); }
     v->e[v->n++] = *c;
 }
+/* The final configurations of a valid key (libjh's jh_lin_configs, ABI 6):
+ * what the JIT-linearization analysis holds after the last :ok completion.
+ * Each terminal edge -- lifting RET[t] from a layer-t configuration with
+ * every later :ok op already linearized -- ends one: the register value and
+ * which crashed ops are linearized, as a mask over C = W(n_ok - 1) minus
+ * RET[n_ok - 1] in call order (every crashed op called before the last :ok
+ * return; crashed ops never leave a window). cpos[op] = the op's position in
+ * C, -1 for an op not in C. */
+static void final_cfg(const orc_key *k, const int32_t *cpos, uint32_t t, const uint64_t *mask, int i, int64_t s2,
+                      cvec *fin) {
+    const int32_t *W = k->w_ops + k->w_off[t];
+    const int w = k->w_off[t + 1] - k->w_off[t];
+    cfg d; memset(&d, 0, sizeof d);
+    d.t = t; d.s = s2;                 /* t: the layer whose :ok op was linearized last */
+    for (int j = 0; j < w; j++)
+        if ((j == i || bit_get(mask, j)) && cpos[W[j]] >= 0) bit_set(d.m, cpos[W[j]]);
+    cvec_push(fin, &d);
+}
+static int orc_linear_fin(const orc_key *k, int64_t init, int64_t budget, int64_t *explored, uint32_t *tmax_out,
+                          cvec *front, cvec *fin);
 static int orc_linear(const orc_key *k, int64_t init, int64_t budget, int64_t *explored, uint32_t *tmax_out,
                cvec *front) {
+    return orc_linear_fin(k, init, budget, explored, tmax_out, front, NULL);
+}
+static int orc_linear_fin(const orc_key *k, int64_t init, int64_t budget, int64_t *explored, uint32_t *tmax_out,
+                          cvec *front, cvec *fin) {
     *explored = 0; *tmax_out = 0;
     if (k->status) return JH_UNKNOWN;
     if (k->n_ok == 0) return JH_VALID;
+    int32_t *cpos = NULL;
+    if (fin) {
+        cpos = (int32_t *)malloc(sizeof(int32_t) * (size_t)(k->n_ops > 0 ? k->n_ops : 1));
+        for (int32_t i = 0; i < k->n_ops; i++) cpos[i] = -1;
+        const uint32_t tl = (uint32_t)k->n_ok - 1;
+        const int32_t *W = k->w_ops + k->w_off[tl];
+        int c = 0;
+        for (int j = 0; j < k->w_off[tl + 1] - k->w_off[tl]; j++)
+            if (W[j] != k->ret_op[tl]) cpos[W[j]] = c++;
+    }
     cset seen; cset_init(&seen);
     cvec q = {0, 0, 0};
     cfg root; memset(&root, 0, sizeof root); root.t = 0; root.s = init;
@@ -391,7 +425,11 @@ static int orc_linear(const orc_key *k, int64_t init, int64_t budget, int64_t *e
             if (!cas_step(o->f, o->v1, o->v2, c.s, &s2)) continue;
             cfg d; d.s = s2;
             cfg_lift(k, c.t, c.m, i, &d.t, d.m);
-            if (d.t == (uint32_t)k->n_ok) { term = 1; continue; }
+            if (d.t == (uint32_t)k->n_ok) {
+                term = 1;
+                if (fin) final_cfg(k, cpos, c.t, c.m, i, s2, fin);
+                continue;
+            }
             if (cset_has(&seen, &d)) continue;
             if (seen.n - 1 >= budget) { verdict = JH_UNKNOWN; goto done; }
             cset_add(&seen, &d);
@@ -404,7 +442,7 @@ static int orc_linear(const orc_key *k, int64_t init, int64_t budget, int64_t *e
 done:
     *explored = seen.n - 1;
     *tmax_out = tmax;
-    cset_free(&seen); free(q.e);
+    cset_free(&seen); free(q.e); free(cpos);
     return verdict;
 }
 
@@ -430,13 +468,14 @@ static int linear_domain(const orc_key *k) {
 /* the frontier's order: value bucket (nil, then with per-key value
  * numbering the initial value, then the rest), value, then the window mask
  * as a JH_MAX_WINDOW-bit number (high word first) */
-typedef struct { int64_t bucket, v; uint64_t m[MW]; } cfg_ord;
+typedef struct { int64_t bucket, v; uint64_t m[MW]; uint32_t t; } cfg_ord;
 static int cmp_cfg_ord(const void *a, const void *b) {
     const cfg_ord *x = (const cfg_ord *)a, *y = (const cfg_ord *)b;
     if (x->bucket != y->bucket) return x->bucket < y->bucket ? -1 : 1;
     if (x->v != y->v) return x->v < y->v ? -1 : 1;
     for (int w = MW - 1; w >= 0; w--)
         if (x->m[w] != y->m[w]) return x->m[w] < y->m[w] ? -1 : 1;
+    if (x->t != y->t) return x->t < y->t ? -1 : 1;
     return 0;
 }
 /* :configs are defined wherever the reachable set can be enumerated: any
@@ -451,30 +490,64 @@ static int configs_one(const jh_history *h, const int64_t *sel, int64_t m, int64
     orc_key_prepare(h, sel, m, &k);
     int n = -1;
     if (configs_domain(&k)) {
-        cvec front = {0, 0, 0};
+        cvec front = {0, 0, 0}, fin = {0, 0, 0};
         int64_t explored; uint32_t tmax;
-        if (orc_linear(&k, init, budget, &explored, &tmax, &front) == JH_INVALID) {
-            cfg_ord *o = (cfg_ord *)malloc(sizeof(cfg_ord) * (front.n ? front.n : 1));
-            for (int64_t i = 0; i < front.n; i++) {
-                const int64_t v = front.e[i].s;
+        /* final configurations only where the analysis itself decides the key
+         * (a valid key it cannot hold is WGL's, and WGL carries none) */
+        const int want_fin = linear_domain(&k);
+        const int verdict = orc_linear_fin(&k, init, budget, &explored, &tmax, &front, want_fin ? &fin : NULL);
+        if (verdict == JH_VALID && want_fin && k.n_ok == 0) {
+            /* no :ok op: the one configuration is the initial one, every
+             * (crashed) op pending, no :last-op */
+            n = 1;
+            jh_lin_config *c = &out[0];
+            c->key = 0; c->model_value = init; c->n_linearized = 0; c->n_pending = 0; c->rows_off = 0;
+            c->last_row = -1;
+            for (int32_t q = 0; q < k.n_ops && q < JH_MAX_WINDOW; q++) rows[c->n_pending++] = k.ops[q].call;
+        } else if (verdict == JH_INVALID || (verdict == JH_VALID && want_fin)) {
+            const int final = verdict == JH_VALID;
+            const cvec *src = final ? &fin : &front;
+            cfg_ord *o = (cfg_ord *)malloc(sizeof(cfg_ord) * (src->n ? src->n : 1));
+            for (int64_t i = 0; i < src->n; i++) {
+                const int64_t v = src->e[i].s;
                 o[i].bucket = v == JH_NIL ? 0 : (per_key_values && init != JH_NIL && v == init) ? 1 : 2;
-                o[i].v = v; memcpy(o[i].m, front.e[i].m, sizeof o[i].m);
+                o[i].v = v; memcpy(o[i].m, src->e[i].m, sizeof o[i].m);
+                o[i].t = final ? src->e[i].t : 0;
             }
-            qsort(o, front.n, sizeof(cfg_ord), cmp_cfg_ord);
-            n = (int)(front.n < per_key ? front.n : per_key);
-            const int32_t *W = k.w_ops + k.w_off[tmax];
-            const int w = k.w_off[tmax + 1] - k.w_off[tmax];
+            qsort(o, src->n, sizeof(cfg_ord), cmp_cfg_ord);
+            int64_t nu = 0;                                   /* distinct configurations */
+            for (int64_t i = 0; i < src->n; i++)
+                if (nu == 0 || cmp_cfg_ord(&o[nu - 1], &o[i]) != 0) o[nu++] = o[i];
+            n = (int)(nu < per_key ? nu : per_key);
+            const uint32_t tl = final ? (uint32_t)k.n_ok - 1 : tmax;
+            const int32_t *W = k.w_ops + k.w_off[tl];
+            const int w = k.w_off[tl + 1] - k.w_off[tl];
+            /* the members the masks range over: W(tmax), or C = W(n_ok - 1) - RET[n_ok - 1] */
+            int32_t *mem = (int32_t *)malloc(sizeof(int32_t) * (size_t)(w > 0 ? w : 1));
+            int nm = 0;
+            for (int j = 0; j < w; j++) if (!final || W[j] != k.ret_op[tl]) mem[nm++] = W[j];
+            const int64_t last_ret = k.ops[k.ret_op[k.n_ok - 1]].ret;
+            /* :last-op: the frontier's is RET[tmax - 1]'s completion, a final
+             * configuration's the :ok op its terminal edge linearized last */
+            const int64_t lfront = tmax == 0 ? -1 : k.ops[k.ret_op[tmax - 1]].ret;
             for (int i = 0; i < n; i++) {
                 jh_lin_config *c = &out[i];
                 c->key = 0; c->model_value = o[i].v; c->n_linearized = 0; c->n_pending = 0;
                 c->rows_off = (int64_t)i * JH_MAX_WINDOW;
+                c->last_row = final ? k.ops[k.ret_op[o[i].t]].ret : lfront;
                 int64_t *r = rows + (int64_t)i * JH_MAX_WINDOW;
-                for (int j = 0; j < w; j++) if (bit_get(o[i].m, j)) r[c->n_linearized++] = k.ops[W[j]].call;
-                for (int j = 0; j < w; j++) if (!bit_get(o[i].m, j)) r[c->n_linearized + c->n_pending++] = k.ops[W[j]].call;
+                for (int j = 0; j < nm; j++) if (bit_get(o[i].m, j)) r[c->n_linearized++] = k.ops[mem[j]].call;
+                for (int j = 0; j < nm; j++) if (!bit_get(o[i].m, j)) r[c->n_linearized + c->n_pending++] = k.ops[mem[j]].call;
+                if (final)      /* crashed ops called after the last :ok return: pending */
+                    for (int32_t q = 0; q < k.n_ops; q++)
+                        if (k.ops[q].ret == ORC_CRASHED && k.ops[q].call > last_ret &&
+                            c->n_linearized + c->n_pending < JH_MAX_WINDOW)
+                            r[c->n_linearized + c->n_pending++] = k.ops[q].call;
             }
+            free(mem);
             free(o);
         }
-        free(front.e);
+        free(front.e); free(fin.e);
     }
     orc_key_free(&k);
     return n;

@@ -136,7 +136,8 @@ def lin_configs(cols, keys, per_key=A.CONFIGS_PER_KEY, init=A.NIL, budget=A.DEFA
         for j in range(n_out[i]):
             c = out[i * per_key + j]
             r = rows[c.rows_off:c.rows_off + c.n_linearized + c.n_pending]
-            cs.append((int(c.model_value), r[:c.n_linearized].tolist(), r[c.n_linearized:].tolist()))
+            cs.append((int(c.model_value), r[:c.n_linearized].tolist(), r[c.n_linearized:].tolist(),
+                       int(c.last_row)))
         res[k] = cs
     return res
 

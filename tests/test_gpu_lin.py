@@ -411,11 +411,11 @@ def test_linear_algorithm_host_mirror(ctx):
     (52, 0, dict(n_keys=120, ops_per_key=300, threads_per_key=12, readers=6, p_invalid=0.3, p_info=0.02)),
 ])
 def test_frontier_configs(ctx, seed, init, kw):
-    """knossos' :configs of an invalid key (checker.clj:146-158, row f1):
-    jh_lin_configs returns the configurations of the last layer the analysis
-    reaches, in the canonical order, the first 10 -- register value,
-    linearized and pending window ops -- equal to the oracle's restatement
-    key by key; valid keys have none."""
+    """knossos' :configs (checker.clj:146-158, row f1): jh_lin_configs
+    returns an invalid key's frontier -- the configurations of the last layer
+    the analysis reaches -- and (ABI 6) a valid key's final configurations, in
+    the canonical order, the first 10 -- register value, linearized and
+    pending ops, :last-op row -- equal to the oracle's restatement key by key."""
     cols, _ = synth.cas_register(seed=seed, init_nil=init is None, **kw)
     iv = A.NIL if init is None else init
     c, _ = oracle.check_cas_independent(cols, init=iv, threads=16)
@@ -427,7 +427,50 @@ def test_frontier_configs(ctx, seed, init, kw):
     o = oracle.lin_configs(cols, keys, init=iv)
     assert g == o
     assert sum(1 for k in bad if g[int(k)]) >= 3
-    assert all(g[int(k)] is None for k in good)
+    assert sum(1 for k in good if g[int(k)]) >= 3
+    assert all(all(c[3] >= 0 for c in g[int(k)]) for k in good if g[int(k)])
+
+
+def test_linear_tutorial_map(ctx):
+    """The reference's printed :linear analysis (doc/tutorial/04-checker.md:
+    126-138), whole map, from the device path: {:valid? true :configs
+    ({:model {:value 1} :last-op {... :type :ok ... :index 151} :pending []})
+    :analyzer :linear :final-paths ()}; under WGL (the default competition)
+    the same history gives :configs () and :final-paths ()."""
+    from jepsen_amd import checker, model
+    d = json.load(open(os.path.join(GOLD, "linear_tutorial.json")))
+    r = checker.linearizable({"model": model.cas_register(), "algorithm": "linear"}).check({}, d["history"], {})
+    assert r == d["expected"]
+    r = checker.linearizable({"model": model.cas_register()}).check({}, d["history"], {})
+    assert r == {"valid?": True, "configs": [], "analyzer": "wgl", "final-paths": []}
+
+
+@pytest.mark.parametrize("seed", [61, 62])
+def test_final_configs_crashed(ctx, seed):
+    """Final configurations of valid keys with crashed ops (ABI 6): which
+    crashed ops stand linearized, the value, and the :ok op each terminal edge
+    linearized last, equal to the oracle's key by key; through the
+    independent checker under :linear every valid key's map carries them."""
+    from jepsen_amd import checker, independent, model
+    cols, _ = synth.cas_register(n_keys=150, ops_per_key=120, threads_per_key=6, readers=2, p_info=0.15,
+                                 p_invalid=0.1, seed=seed)
+    c, _ = oracle.check_cas_independent(cols, init=A.NIL, algorithm="linear", threads=16)
+    good = np.nonzero((c["valid"] == A.VALID) & (c["analyzer"] == A.ANALYZER_LINEAR))[0]
+    g = ctx.lin_configs(cols, good)
+    o = oracle.lin_configs(cols, good, init=A.NIL)
+    assert g == o
+    assert sum(1 for k in good if g[int(k)] and any(c_[1] or c_[2] for c_ in g[int(k)])) >= 5
+    hist = [H.decode_op(cols, i) for i in range(cols.n)]
+    r = independent.checker(checker.linearizable({"model": model.cas_register(), "algorithm": "linear"}))
+    res = r.check({}, hist, {})["results"]
+    for k in good[:40]:
+        m = res[cols.keys[int(k)]]
+        assert m["valid?"] is True and m["analyzer"] == "linear" and m["final-paths"] == []
+        assert len(m["configs"]) == len(g[int(k)])
+        for cfg, (v, lin, pend, last) in zip(m["configs"], g[int(k)]):
+            assert cfg["model"] == {"value": None if v == A.NIL else v}
+            assert cfg["last-op"]["index"] == last and cfg["last-op"]["type"] == "ok"
+            assert [p_["index"] for p_ in cfg["pending"]] == pend
 
 
 def test_frontier_configs_host_map(ctx):
@@ -442,7 +485,11 @@ def test_frontier_configs_host_map(ctx):
     for cfg in r["configs"]:
         assert set(cfg) == {"model", "last-op", "pending"}
         assert all(op["type"] == "invoke" for op in cfg["pending"])
-        assert cfg["last-op"] is None or cfg["last-op"]["type"] == "invoke"
+        # as knossos prints it (doc/tutorial/04-checker.md:128-135): the :ok
+        # completion of the last op linearized, with its own :index
+        if cfg["last-op"] is not None:
+            i = cfg["last-op"]["index"]
+            assert cfg["last-op"]["type"] == "ok" and dict(d["history"][i], index=i) == cfg["last-op"]
     for p in r["final-paths"]:
         assert p[-1]["op"] == r["op"] and "inconsistent" in p[-1]["model"]
 

@@ -206,6 +206,7 @@ def _jit_frontier(cols, key, init):
         if not nxt:
             window = sorted(avail - done)
             _jit_frontier.reach = len(reach)
+            _jit_frontier.last = max((ops[o]["ret"] for o in done), default=-1)
             return window, sorted(seen, key=lambda c: (
                 0 if c[1] == NIL else 2, c[1], sum(1 << j for j, r in enumerate(window) if r in c[0])))
         configs = nxt
@@ -219,7 +220,7 @@ def test_frontier_configs_from_definition(built, seed):
     the GPU) equals the frontier computed from the definition by a
     just-in-time linearization over op maps: the first 10 configurations in
     the canonical order, each value, linearized window rows and pending
-    window rows, for every invalid key; None for every valid key."""
+    window rows and the :last-op row, for every invalid key."""
     cols, _ = synth.cas_register(n_keys=60, ops_per_key=24, threads_per_key=3, readers=1, n_values=3,
                                  process_limit=10 ** 6, p_info=0.0, p_invalid=0.5, nemesis_every=10 ** 9,
                                  seed=seed)
@@ -227,13 +228,14 @@ def test_frontier_configs_from_definition(built, seed):
     n_bad = 0
     for k in range(cols.n_keys):
         ref = _jit_frontier(cols, k, A.NIL)
-        if ref is None:
-            assert got[k] is None, k
+        if ref is None:               # valid: its final configurations, test_final_configs_from_definition
             continue
         n_bad += 1
         window, front = ref
         want = [(v, [r for r in window if r in L], [r for r in window if r not in L]) for L, v in front][:10]
-        assert [(int(v), list(map(int, lin)), list(map(int, pend))) for v, lin, pend in got[k]] == want, k
+        assert [(int(v), list(map(int, lin)), list(map(int, pend))) for v, lin, pend, _ in got[k]] == want, k
+        # :last-op: the completion of the last :ok op before the failing one
+        assert all(last == _jit_frontier.last for *_, last in got[k]), k
     assert n_bad >= 5
 
 
@@ -257,3 +259,104 @@ def test_linear_analysis_from_definition(built):
         if ref is not None:
             assert int(lin["explored"][k]) == _jit_frontier.reach - 1, k
     assert (lin["valid"] == A.INVALID).sum() >= 5
+
+
+def _jit_final(cols, key, init):
+    """The final configurations of a valid key from the definition: knossos'
+    just-in-time linearization over op maps, strictly -- at each :ok
+    completion a configuration that already linearized the op survives as it
+    is; any other is expanded by linearizing pending ops, in every order,
+    until the completing op is linearized, which becomes its :last-op. The
+    configurations left after the history are (value, linearized ops,
+    :last-op row). None when some completion leaves no configuration.
+    :fail ops and :ok reads of nil are dropped (as _jit_frontier)."""
+    NIL = A.NIL
+    rows = [i for i in range(cols.n) if int(cols.key[i]) == key]
+    open_by_proc, ops = {}, {}
+    for i in rows:
+        p, ty = int(cols.process[i]), int(cols.type[i])
+        if ty == A.TYPE_INVOKE:
+            open_by_proc[p] = i
+            ops[i] = {"f": int(cols.f[i]), "v": int(cols.value[i]), "v2": int(cols.value2[i]), "ret": None}
+        else:
+            inv = open_by_proc.pop(p)
+            if ty == A.TYPE_FAIL:
+                ops[inv]["fail"] = True
+            elif ty == A.TYPE_OK:
+                ops[inv]["ret"] = i
+                if ops[inv]["f"] == 0:
+                    ops[inv]["v"] = int(cols.value[i])
+                    if ops[inv]["v"] == NIL:
+                        ops[inv]["fail"] = True
+            elif ops[inv]["f"] == 0:                     # a crashed read never matters: dropped
+                ops[inv]["fail"] = True
+
+    def step(s, o):
+        if o["f"] == 1:
+            return o["v"]
+        if o["f"] == 2:
+            return o["v2"] if s == o["v"] else None
+        return s if (o["v"] == NIL or o["v"] == s) else None
+    configs = {(frozenset(), init, -1)}
+    avail = set()
+    for i in rows:
+        if int(cols.type[i]) == A.TYPE_INVOKE:
+            if not ops[i].get("fail"):
+                avail.add(i)
+            continue
+        if int(cols.type[i]) != A.TYPE_OK:
+            continue
+        inv = next((o for o in avail if ops[o]["ret"] == i), None)
+        if inv is None:
+            continue
+        new = set()
+        for L, s, last in configs:
+            if inv in L:
+                new.add((L, s, last))
+                continue
+            seen, stack = {(L, s)}, [(L, s)]
+            while stack:
+                L2, s2 = stack.pop()
+                for o in avail - L2:
+                    s3 = step(s2, ops[o])
+                    if s3 is None:
+                        continue
+                    if o == inv:
+                        new.add((L2 | {o}, s3, i))
+                    elif (L2 | {o}, s3) not in seen:
+                        seen.add((L2 | {o}, s3))
+                        stack.append((L2 | {o}, s3))
+        if not new:
+            return None
+        configs = new
+    crashed = sorted(o for o in avail if ops[o]["ret"] is None)
+    return crashed, configs
+
+
+@pytest.mark.parametrize("seed", [14, 15])
+def test_final_configs_from_definition(built, seed):
+    """orc_lin_configs on a valid key (ABI 6: the final configurations the
+    :linear analysis holds after the last :ok completion) equals the strict
+    just-in-time linearization from the definition: value, which crashed ops
+    stand linearized, the pending crashed ops, and :last-op -- the :ok op
+    each configuration linearized last -- first 10 in the canonical order."""
+    cols, _ = synth.cas_register(n_keys=60, ops_per_key=24, threads_per_key=3, readers=1, n_values=3,
+                                 process_limit=10 ** 6, p_info=0.12, p_invalid=0.2, nemesis_every=10 ** 9,
+                                 seed=seed)
+    lin, _ = oracle.check_cas_independent(cols, init=A.NIL, algorithm="linear")
+    got = oracle.lin_configs(cols, list(range(cols.n_keys)), init=A.NIL)
+    n_crashed = 0
+    for k in range(cols.n_keys):
+        ref = _jit_final(cols, k, A.NIL)
+        if int(lin["valid"][k]) != A.VALID:
+            assert ref is None, k
+            continue
+        assert ref is not None, k
+        crashed, configs = ref
+        order = sorted(configs, key=lambda c: (0 if c[1] == A.NIL else 2, c[1],
+                                               sum(1 << j for j, r in enumerate(crashed) if r in c[0]), c[2]))
+        want = [(s, [r for r in crashed if r in L], [r for r in crashed if r not in L], last)
+                for L, s, last in order][:10]
+        assert got[k] == want, k
+        n_crashed += any(c[1] or c[2] for c in want)
+    assert n_crashed >= 5

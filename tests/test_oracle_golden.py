@@ -114,3 +114,26 @@ def test_synthetic_counter_set_reproduce(built):
     r = oracle.check_set(cols)
     assert r["valid"] == int(z["valid"]) and r["first_fail_entry"] == int(z["first_fail_entry"])
     assert (r["runs"][1] == z["runs_lost"]).all()
+
+
+def test_linear_tutorial_analysis(built):
+    """doc/tutorial/04-checker.md:126-138: the :linear analysis the reference
+    prints, whole map, built by the host mirror (checker.lin_result +
+    add_configs) from the oracle's analysis of the fixture history: one final
+    configuration, {:model {:value 1}, :last-op the :ok :write 1 at :index
+    151 with its :time, :pending []}, :analyzer :linear, :final-paths ().
+    No :explored key: WGL's cache size is the side channel (.explored)."""
+    from jepsen_amd import checker
+    from jepsen_amd import model as M
+    d = _json("linear_tutorial.json")
+    cols = H.encode(d["history"], keyed=False)
+    keyed = H.encode([dict(o, value=H.tuple_(0, o["value"])) for o in d["history"]], keyed=True)
+    lin, _ = oracle.check_cas_independent(keyed, init=A.NIL, algorithm="linear")
+    assert int(lin["valid"][0]) == A.VALID and int(lin["analyzer"][0]) == A.ANALYZER_LINEAR
+    cf = oracle.lin_configs(cols, [0], init=A.NIL)[0]
+    assert cf == [(1, [], [], 151)]
+    out = checker.lin_result(A.VALID, 0, -1, int(lin["explored"][0]), cols, analyzer=A.ANALYZER_LINEAR,
+                             ops=d["history"])
+    checker.add_configs(out, cf, cols, M.cas_register(), ops=d["history"])
+    assert out == d["expected"]
+    assert out.explored == int(lin["explored"][0]) and "explored" not in out

@@ -8,6 +8,9 @@
      counter.json       jepsen/test/jepsen/checker_test.clj:90-166
      interval_str.json  jepsen/test/jepsen/util_test.clj:14-31
      independent.json   jepsen/test/jepsen/independent_test.clj:78-97
+     linear_tutorial.json  doc/tutorial/04-checker.md:126-138 (the printed
+                        :linear analysis; its history is elided there and
+                        reconstructed here)
 2. Seeded synthetic vectors (synthetic_*.npz + manifest.json): small
    histories from jepsen_amd.synth with the CPU oracle's verdicts, each
    cross-checked against the knossos-style WGL and (for tiny keys) brute
@@ -277,11 +280,71 @@ def queue():
     return {"source": "jepsen/test/jepsen/checker_test.clj:13-88", "queue": q, "total_queue": t}
 
 
+def linear_tutorial():
+    """doc/tutorial/04-checker.md:126-138: the analysis (checker/linearizable
+    {:model (model/cas-register) :algorithm :linear}) prints for the
+    tutorial's etcd register test (:110-124). The tutorial elides the history
+    ("..." between its first and last log lines), so the history here is
+    reconstructed, seeded: five processes running read / write / cas
+    (values 0-4, `gen/cas` of generator.clj:395-403) against a true register
+    linearized at invocation, at most two ops in flight, then -- as its last
+    log line shows -- process 3's :write 1 alone, ok at :index 151, :time
+    14796541900. The expected map is the tutorial's, verbatim (keywords as
+    strings, the :configs list as a JSON list)."""
+    import random
+    rnd = random.Random(20190418)
+    hist, reg, t = [], None, 10_000_000
+    open_ops = {}
+    def emit(op):
+        nonlocal t
+        t += rnd.randint(1_000_000, 90_000_000)
+        op = dict(op, time=t, index=len(hist))
+        hist.append(op)
+    n_inv = 0
+    while n_inv < 75 or open_ops:                   # 75 ops = 150 entries, then drain
+        if open_ops and (len(open_ops) >= 2 or n_inv >= 75 or rnd.random() < 0.5):
+            p = rnd.choice(sorted(open_ops))
+            f, v, res = open_ops.pop(p)
+            emit({"process": p, "type": res, "f": f, "value": v})
+            continue
+        p = rnd.choice([q for q in range(5) if q not in open_ops])
+        f = rnd.choice(["read", "write", "cas"])
+        n_inv += 1
+        if f == "read":
+            emit({"process": p, "type": "invoke", "f": f, "value": None})
+            open_ops[p] = (f, reg, "ok")
+        elif f == "write":
+            v = rnd.randint(0, 4)
+            emit({"process": p, "type": "invoke", "f": f, "value": v})
+            reg = v
+            open_ops[p] = (f, v, "ok")
+        else:
+            v = [rnd.randint(0, 4), rnd.randint(0, 4)]
+            emit({"process": p, "type": "invoke", "f": f, "value": v})
+            res = "ok" if reg == v[0] else "fail"
+            if res == "ok":
+                reg = v[1]
+            open_ops[p] = (f, v, res)
+    assert len(hist) == 150 and not open_ops
+    emit({"process": 3, "type": "invoke", "f": "write", "value": 1})
+    hist.append({"process": 3, "type": "ok", "f": "write", "value": 1, "index": 151, "time": 14796541900})
+    assert hist[-2]["time"] < 14796541900
+    expected = {"valid?": True,
+                "configs": [{"model": {"value": 1},
+                             "last-op": {"process": 3, "type": "ok", "f": "write", "value": 1, "index": 151,
+                                         "time": 14796541900},
+                             "pending": []}],
+                "analyzer": "linear",
+                "final-paths": []}
+    return {"source": "doc/tutorial/04-checker.md:110-138 (expected map verbatim; history reconstructed)",
+            "model": {"cas-register": None}, "algorithm": "linear", "history": hist, "expected": expected}
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
     for name, fn in [("perf_test", perf_test), ("counter", counter), ("interval_str", interval_str),
                      ("independent", independent), ("set_full", set_full),
-                     ("queue", queue)]:
+                     ("queue", queue), ("linear_tutorial", linear_tutorial)]:
         with open(os.path.join(GOLD, name + ".json"), "w") as f:
             json.dump(fn(), f, indent=1)
     man = synthetic()
@@ -291,4 +354,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--linear-tutorial" in sys.argv:       # this fixture alone (no reference tree needed)
+        with open(os.path.join(GOLD, "linear_tutorial.json"), "w") as f:
+            json.dump(linear_tutorial(), f, indent=1)
+    else:
+        main()

@@ -142,6 +142,10 @@ typedef struct jh_history {
  * slower on C3 (the heavy keys' searches share CUs with phase
  * 1 and start without helpers), so it is off by default. */
 #define JH_LIN_STREAM        256
+/* Round 5: phase 1 saves each deferred search (stack + memo) and the heavy-key
+ * pass continues it; this flag restarts deferred keys from scratch instead
+ * (round 4's behaviour; same verdicts and counts, for A/B and the tests). */
+#define JH_LIN_NO_RESUME     512
 
 typedef struct jh_lin_opts {
     int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */
@@ -234,6 +238,10 @@ typedef struct jh_summary {
     int64_t p3_entries;        /* entries of the LEAN keys restarted in phase 3 */
     double  p2_start_ms;       /* heavy-key pass start (streamed: its first key taken), ms after phase 1 began (-1: none) */
     double  p1_span_ms;        /* phase 1's first wave to its last wave's end (streamed) */
+    /* ABI 6 (round 5): deferred searches phase 1 saved and the heavy-key pass
+     * continued (JH_LIN_NO_RESUME: 0), and the bytes of their records */
+    int64_t resumed;
+    int64_t resume_bytes;
 } jh_summary;
 
 typedef struct jh_ctx jh_ctx;

@@ -60,6 +60,7 @@ LIN_BFS_ONLY, LIN_GEN_JUMP, LIN_INTERN_PER_KEY, LIN_NO_HELPERS, LIN_HELPERS_NOW 
 LIN_PHASE1_ONLY, LIN_SKIP_PHASE1 = 32, 64
 LIN_NO_HANDOVER = 128
 LIN_STREAM = 256
+LIN_NO_RESUME = 512           # round 5: restart deferred keys instead of continuing them
 CAUSE_DEFERRED = 9
 
 
@@ -101,7 +102,9 @@ class JhSummary(C.Structure):
                 ("wide_entries", C.c_int64), ("xw_entries", C.c_int64), ("waves", C.c_int64 * 4),
                 # ABI 5: the streaming heavy-key pass
                 ("streamed", C.c_int64), ("p3_entries", C.c_int64), ("p2_start_ms", C.c_double),
-                ("p1_span_ms", C.c_double)]
+                ("p1_span_ms", C.c_double),
+                # ABI 6: deferred searches resumed by the heavy-key pass
+                ("resumed", C.c_int64), ("resume_bytes", C.c_int64)]
 
 
 class JhLinConfig(C.Structure):

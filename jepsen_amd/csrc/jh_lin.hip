@@ -355,6 +355,17 @@ struct DfsArgs {
     int32_t *drained;
     const int32_t *live_n;
     unsigned long long *tl;     // -DJH_TUNING timeline (JH_DEFER_TIMES): per key [2] search start, [3] end
+    // Resume (round 5): phase 1 (rs_mode 1) saves a deferred LEAN key's search
+    // -- its configuration, stack and every configuration in its memo (WGL's
+    // cache) -- as a record in rs_arena (bump-allocated by rs_used, rs_off[key]
+    // = its byte offset, -1 none); phase 2's sequential search (rs_mode 2)
+    // continues that key from its record instead of restarting it. The DFS is
+    // the same from there on, so verdicts and explored counts do not change.
+    uint8_t *rs_arena;
+    unsigned long long *rs_used;
+    uint64_t rs_cap;
+    int64_t *rs_off;
+    int32_t rs_mode;
 };
 constexpr int TL_W = 6;         // timeline words per key: BFS, sequential, helper (start, end)
 #ifdef JH_TUNING
@@ -1442,6 +1453,80 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
     uint32_t wrq = lane < w ? ops[lane].rq : RQ_EMPTY;
     load_up(P);
     wave_sync();
+    uint32_t ins_saved = 0xFFFFFFFFu;     // a handed-over search's real insert count
+    // move the window forward from layer t to layer nt (a lift, or a resume)
+    auto advance = [&](uint32_t nt) {
+        for (uint32_t u = t; u < nt; u++) {
+            const uint32_t ru = u == t ? r : (lay_hi(u) & 63);
+            const uint32_t sh = (uint32_t)wave_shl1((int)wrq);
+            if (lane >= (int)ru) wrq = sh;
+            w--;
+            if (lane == w) wrq = RQ_EMPTY;
+            const int c = (int)(lay_hi(u + 1) >> 6);
+            if (c > 0) {
+                if (P < pb || P + c > pb + 64) load_up(c <= 32 && P >= 32 ? P - 32 : P);
+                for (int kk = 0; kk < c; kk++) {
+                    const uint32_t x = (uint32_t)readlane((int)urq, P - pb + kk);
+                    if (lane == w + kk) wrq = x;
+                }
+                w += c; P += c;
+            }
+        }
+    };
+    if (A.rs_mode == 2 && A.rs_off) {
+        // Resume a search phase 1 deferred (round 5): its memo into this wave's
+        // HBM table behind the Bloom filter (theta above every restored layer,
+        // so each probe there is exact), its stack into the ring and the HBM
+        // stack, then expand its current configuration again: the children it
+        // had inserted are present, the others absent -- the DFS goes on
+        // exactly where phase 1 stopped it.
+        const int64_t ro = A.rs_off[key];
+        if (ro >= 0) {
+            const uint64_t *hd = (const uint64_t *)(A.rs_arena + ro);
+            const uint64_t h_mask = hd[0], h_ts = hd[1], h_dt = hd[2], h_ins = hd[3], h_n = hd[4];
+            const uint32_t d = (uint32_t)h_dt;
+            if (d <= A.stack_cap && h_n <= (uint64_t)A.memo_cap / 4) {
+                const Frame *fsrc = (const Frame *)(hd + 8);
+                const ulonglong2 *ent = (const ulonglong2 *)(fsrc + d);
+                uint32_t tmx = 0;
+                for (uint32_t j = (uint32_t)lane; j < (uint32_t)h_n; j += 64) {
+                    const ulonglong2 e = ent[j];
+                    const uint32_t et = (uint32_t)(e.y >> 20) & T_MASK, es = (uint32_t)e.y & STATE_MASK;
+                    hbm_insert(memo, cap_mask, gen, et, es, e.x);
+                    uint32_t g1, g2;
+                    lk_hash((uint32_t)e.x, (uint32_t)(e.x >> 32) | (et << 16) | (es << 8) | 0x80000000u, g1, g2);
+                    bloom_set2<M>(bloom, lk_bl(g1), lk_bl(g2));
+                    tmx = max(tmx, et + 1);
+                }
+                for (int o = 32; o > 0; o >>= 1) tmx = max(tmx, (uint32_t)__shfl_xor((int)tmx, o));
+                theta = rflu(tmx);
+                ring_lo = d > 32 ? d - 32 : 0;
+                for (uint32_t j = (uint32_t)lane; j < ring_lo; j += 64) stack[j] = fsrc[j];
+                {
+                    const uint32_t idx = ring_lo + (((uint32_t)lane - ring_lo) & 63);
+                    if (idx < d) {
+                        const Frame fr = fsrc[idx];
+                        fm_lo = (uint32_t)fr.mask; fm_hi = (uint32_t)(fr.mask >> 32); f_ti = fr.t_i;
+                        f_s = (uint32_t)fr.s; fr_lo = (uint32_t)fr.rest; fr_hi = (uint32_t)(fr.rest >> 32);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                wave_sync();
+                depth = d;
+                mask = h_mask;
+                s = (uint32_t)(h_ts >> 32);
+                ins = (uint32_t)h_ins;
+                chk = min(budget, ins);                  // the next insert runs the checks
+                const uint32_t nt = (uint32_t)h_ts;
+                advance(nt);
+                t = nt;
+                tmax = max((uint32_t)(h_dt >> 32), t);
+                r = lay_hi(t) & 63;
+                rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
+            }
+        }
+    }
     const ulonglong2 *B = (const ulonglong2 *)lmemo;
     // per-step values shared by the two ways into an insert
     uint64_t absent = 0, nm_r = 0;
@@ -1521,7 +1606,7 @@ insert:
     {
         if (ins >= chk) {
             if (ins >= budget && !extend_budget(A, budget)) { verdict = JH_UNKNOWN; goto done; }
-            if (handover(A, ins)) { ins = budget; verdict = JH_UNKNOWN; goto done; }
+            if (handover(A, ins)) { ins_saved = ins; ins = budget; verdict = JH_UNKNOWN; goto done; }
             if (A.claim) {
                 // racing k_lin_bfs: stop if it settled this key first
                 int c = 0;
@@ -1601,22 +1686,7 @@ insert:
         mask = nm_r;
         if (nt >= n_ok) { t = nt; tmax = max(tmax, t); verdict = JH_VALID; goto done; }
         // move the window forward layer by layer
-        for (uint32_t u = t; u < nt; u++) {
-            const uint32_t ru = u == t ? r : (lay_hi(u) & 63);
-            const uint32_t sh = (uint32_t)wave_shl1((int)wrq);
-            if (lane >= (int)ru) wrq = sh;
-            w--;
-            if (lane == w) wrq = RQ_EMPTY;
-            const int c = (int)(lay_hi(u + 1) >> 6);
-            if (c > 0) {
-                if (P < pb || P + c > pb + 64) load_up(c <= 32 && P >= 32 ? P - 32 : P);
-                for (int kk = 0; kk < c; kk++) {
-                    const uint32_t x = (uint32_t)readlane((int)urq, P - pb + kk);
-                    if (lane == w + kk) wrq = x;
-                }
-                w += c; P += c;
-            }
-        }
+        advance(nt);
         t = nt;
         tmax = max(tmax, t);
         r = lay_hi(t) & 63;
@@ -1678,6 +1748,66 @@ pop:
     goto insert;
 
 done:
+    if (A.rs_mode == 1 && A.rs_off && verdict == JH_UNKNOWN && A.defer) {
+        // Save the deferred search for phase 2 (round 5): header {mask, t | s << 32,
+        // depth | tmax << 32, inserts, entries}, the stack frames, then every
+        // configuration in the memo as {mask, t << 20 | s}: the LDS ones and this
+        // key's generation in the wave's HBM table (scanned whole, 16 entries in
+        // flight per lane). Published only if the count is the insert count.
+        const uint32_t nmem = ins_saved != 0xFFFFFFFFu ? ins_saved : ins;
+        const uint64_t bytes = 64 + (uint64_t)depth * sizeof(Frame) + (uint64_t)nmem * 16;
+        unsigned long long off = 0;
+        if (lane == 0) off = atomicAdd(A.rs_used, (unsigned long long)((bytes + 255) & ~255ULL));
+        off = readlane64(off, 0);
+        if (off + bytes <= A.rs_cap) {
+            uint64_t *hd = (uint64_t *)(A.rs_arena + off);
+            Frame *fdst = (Frame *)(hd + 8);
+            ulonglong2 *ent = (ulonglong2 *)(fdst + depth);
+            for (uint32_t j = (uint32_t)lane; j < ring_lo; j += 64) fdst[j] = stack[j];
+            {
+                const uint32_t idx = ring_lo + (((uint32_t)lane - ring_lo) & 63);
+                if (idx < depth) {
+                    Frame fr;
+                    fr.mask = ((uint64_t)fm_hi << 32) | fm_lo; fr.t_i = f_ti; fr.s = (int32_t)f_s;
+                    fr.rest = ((uint64_t)fr_hi << 32) | fr_lo; fr.pad[0] = fr.pad[1] = 0;
+                    fdst[idx] = fr;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            uint32_t n = 0;
+            for (int base = 0; base < M::SLOTS; base += 64) {
+                const uint64_t x = lmemo[base + lane];
+                const uint64_t bm = ballot(x != 0);
+                const uint32_t at = n + (uint32_t)mbcnt(bm);
+                if (x != 0 && at < nmem) ent[at] = make_ulonglong2(lk_m(x), ((uint64_t)lk_t(x) << 20) | lk_s(x));
+                n += (uint32_t)__popcll(bm);
+            }
+            const ulonglong2 *tab = (const ulonglong2 *)memo;
+            for (uint32_t base = 0; base < A.memo_cap; base += 64 * 16) {
+                ulonglong2 e[16];
+#pragma unroll
+                for (int q = 0; q < 16; q++) e[q] = tab[base + 64 * q + lane];
+#pragma unroll
+                for (int q = 0; q < 16; q++) {
+                    const bool mine = (uint32_t)(e[q].y >> 40) == gen;
+                    const uint64_t bm = ballot(mine);
+                    const uint32_t at = n + (uint32_t)mbcnt(bm);
+                    if (mine && at < nmem) ent[at] = make_ulonglong2(e[q].x, e[q].y & ((1ULL << 40) - 1));
+                    n += (uint32_t)__popcll(bm);
+                }
+            }
+            if (lane == 0) {
+                hd[0] = mask; hd[1] = (uint64_t)t | ((uint64_t)s << 32); hd[2] = (uint64_t)depth | ((uint64_t)tmax << 32);
+                hd[3] = nmem; hd[4] = n;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (lane == 0 && n == nmem) {
+                A.rs_off[key] = (int64_t)off;
+                atomicAdd((int32_t *)A.rs_used + 2, 1);       // Q_RS_N: records published
+            }
+        }
+    }
     inserts = ins;
     tmax_out = tmax;
 #ifdef JH_DFS_STATS
@@ -2897,6 +3027,80 @@ __device__ int dfs_acc(const WgArgs &W, WgShared &sh, const KeyInfo &K, const ch
     uint32_t wrq = lane < w ? ops[lane].rq : RQ_EMPTY;
     load_up(P);
     wave_sync();
+    uint32_t ins_saved = 0xFFFFFFFFu;     // a handed-over search's real insert count
+    // move the window forward from layer t to layer nt (a lift, or a resume)
+    auto advance = [&](uint32_t nt) {
+        for (uint32_t u = t; u < nt; u++) {
+            const uint32_t ru = u == t ? r : (lay_hi(u) & 63);
+            const uint32_t sh = (uint32_t)wave_shl1((int)wrq);
+            if (lane >= (int)ru) wrq = sh;
+            w--;
+            if (lane == w) wrq = RQ_EMPTY;
+            const int c = (int)(lay_hi(u + 1) >> 6);
+            if (c > 0) {
+                if (P < pb || P + c > pb + 64) load_up(c <= 32 && P >= 32 ? P - 32 : P);
+                for (int kk = 0; kk < c; kk++) {
+                    const uint32_t x = (uint32_t)readlane((int)urq, P - pb + kk);
+                    if (lane == w + kk) wrq = x;
+                }
+                w += c; P += c;
+            }
+        }
+    };
+    if (A.rs_mode == 2 && A.rs_off) {
+        // Resume a search phase 1 deferred (round 5): its memo into this wave's
+        // HBM table behind the Bloom filter (theta above every restored layer,
+        // so each probe there is exact), its stack into the ring and the HBM
+        // stack, then expand its current configuration again: the children it
+        // had inserted are present, the others absent -- the DFS goes on
+        // exactly where phase 1 stopped it.
+        const int64_t ro = A.rs_off[key];
+        if (ro >= 0) {
+            const uint64_t *hd = (const uint64_t *)(A.rs_arena + ro);
+            const uint64_t h_mask = hd[0], h_ts = hd[1], h_dt = hd[2], h_ins = hd[3], h_n = hd[4];
+            const uint32_t d = (uint32_t)h_dt;
+            if (d <= A.stack_cap && h_n <= (uint64_t)A.memo_cap / 4) {
+                const Frame *fsrc = (const Frame *)(hd + 8);
+                const ulonglong2 *ent = (const ulonglong2 *)(fsrc + d);
+                uint32_t tmx = 0;
+                for (uint32_t j = (uint32_t)lane; j < (uint32_t)h_n; j += 64) {
+                    const ulonglong2 e = ent[j];
+                    const uint32_t et = (uint32_t)(e.y >> 20) & T_MASK, es = (uint32_t)e.y & STATE_MASK;
+                    hbm_insert(memo, cap_mask, gen, et, es, e.x);
+                    uint32_t g1, g2;
+                    lk_hash((uint32_t)e.x, (uint32_t)(e.x >> 32) | (et << 16) | (es << 8) | 0x80000000u, g1, g2);
+                    bloom_set2<M>(bloom, lk_bl(g1), lk_bl(g2));
+                    tmx = max(tmx, et + 1);
+                }
+                for (int o = 32; o > 0; o >>= 1) tmx = max(tmx, (uint32_t)__shfl_xor((int)tmx, o));
+                theta = rflu(tmx);
+                ring_lo = d > 32 ? d - 32 : 0;
+                for (uint32_t j = (uint32_t)lane; j < ring_lo; j += 64) stack[j] = fsrc[j];
+                {
+                    const uint32_t idx = ring_lo + (((uint32_t)lane - ring_lo) & 63);
+                    if (idx < d) {
+                        const Frame fr = fsrc[idx];
+                        fm_lo = (uint32_t)fr.mask; fm_hi = (uint32_t)(fr.mask >> 32); f_ti = fr.t_i;
+                        f_s = (uint32_t)fr.s; fr_lo = (uint32_t)fr.rest; fr_hi = (uint32_t)(fr.rest >> 32);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                wave_sync();
+                depth = d;
+                mask = h_mask;
+                s = (uint32_t)(h_ts >> 32);
+                ins = (uint32_t)h_ins;
+                chk = min(budget, ins);                  // the next insert runs the checks
+                const uint32_t nt = (uint32_t)h_ts;
+                advance(nt);
+                t = nt;
+                tmax = max((uint32_t)(h_dt >> 32), t);
+                r = lay_hi(t) & 63;
+                rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
+            }
+        }
+    }
     const ulonglong2 *B = (const ulonglong2 *)lmemo;
     uint64_t absent = 0, nm_r = 0;
     uint32_t u_r = 0, klo = 0, khi = 0, b1 = 0, b2 = 0, n1 = 0, n2 = 0, h1 = 0, h2 = 0, nvl = 0;
@@ -5663,6 +5867,7 @@ constexpr int Q_T_WIDE = 46;        // [46..47] first WIDE wave start, [48..49] 
 constexpr int Q_P1_DONE = 64, Q_SEQ_WAVES = 65, Q_BFS_QUEUE = 66;
 constexpr int Q_T_BFS = 68, Q_T_LEAN = 72, Q_T_XW = 76, Q_T_P1 = 80;
 constexpr int Q_ENT_P3 = 84;        // entries of the LEAN keys restarted in phase 3
+constexpr int Q_RS_USED = 88;       // [88..89] resume records' bytes, [90] records published (round 5)
 // LEAN sequential waves launched with the BFS while phase 1 still runs (the
 // rest start behind phase 1): enough for the keys deferred before it ends
 constexpr int EARLY_LEAN_WAVES = 128;
@@ -5924,6 +6129,21 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     }
     const bool skip_p1 = (lflags & JH_LIN_SKIP_PHASE1) != 0 && !linear_mode;
     const bool p1_only = (lflags & JH_LIN_PHASE1_ONLY) != 0 && !linear_mode && !skip_p1;
+    // resume (round 5): phase 1's deferred LEAN searches saved for the heavy-key
+    // pass (a record is <= 64 B + a frame per stack level + 16 B per insert)
+    const bool resume = a.defer && !linear_mode && !skip_p1 && !p1_only && !(lflags & JH_LIN_NO_RESUME) &&
+                        !(lflags & JH_LIN_STREAM) &&
+                        !tune_env("JH_NO_RESUME");
+    if (resume) {
+        const uint64_t per_key = 64 + (uint64_t)stack_cap * sizeof(Frame) + (uint64_t)quick * 16;
+        const uint64_t cap = std::min<uint64_t>((uint64_t)256 << 20, (uint64_t)K * per_key);
+        a.rs_arena = ctx->ws<uint8_t>(WS_RS_ARENA, cap);
+        a.rs_cap = cap;
+        a.rs_off = ctx->ws<int64_t>(WS_RS_OFF, K);
+        a.rs_used = (unsigned long long *)(q + Q_RS_USED);
+        HIP_TRY(hipMemsetAsync(a.rs_off, 0xFF, (size_t)K * sizeof(int64_t), st));
+        a.rs_mode = 1;
+    }
     int32_t qh[Q_WORDS];
     int n_defer = 0, n_def_l = 0, n_def_w = 0, n_x = 0;
     int waves_x = 0;
@@ -5988,6 +6208,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         if (clear_memo && !freshw) HIP_TRY(hipMemsetAsync(memow, 0, ctx->bufs[WS_MEMO_WIDE].bytes, st));
         bw = a;
         bw.handover_min = 0;
+        bw.rs_mode = 0;
         bw.list = defer_w; bw.n_list = n_def_w; bw.n_list_dev = nullptr; bw.queue = q + 7;
         bw.defer64 = nullptr; bw.defer_kind = nullptr; bw.defer_kind_count = nullptr;
         split3w = waves_w < n_def_w && budget > p2;
@@ -6049,6 +6270,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         uint64_t *work = ctx->ws<uint64_t>(WS_WG_WORK, (size_t)n_wg * work_cap, /*zero=*/true);
         WgArgs wa{};
         wa.d = a;
+        wa.d.rs_mode = 0;
         wa.d.handover_min = 0;
         wa.d.list = defer_l; wa.d.n_list = n_def_l; wa.d.n_list_dev = nullptr; wa.d.queue = wg_queue; wa.d.defer = 0;
         wa.d.defer_list = nullptr; wa.d.defer_count = nullptr;
@@ -6214,6 +6436,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // phase 2 stops at p2 inserts and phase 3 restarts those keys
         split3 = waves2 < nd_l && budget > p2;
         b = a;
+        b.rs_mode = 0;                  // the default race below continues phase 1's records
         b.handover_min = 0;
         b.list = defer_l; b.n_list = nd_l; b.n_list_dev = nullptr; b.queue = q + 6; b.defer = split3 ? 1 : 0;
         b.defer_list = defer3; b.defer_count = q + 16;
@@ -6588,6 +6811,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
             DfsArgs f = a;
             f.handover_min = 0;
+            f.rs_mode = 0;
             f.list = c.unres_list; f.n_list = 0; f.n_list_dev = q + 3; f.queue = q + 6; f.defer = 0;
             f.defer_list = nullptr; f.defer_count = nullptr;
             f.defer64 = nullptr; f.defer_kind = nullptr; f.defer_kind_count = nullptr;
@@ -6645,6 +6869,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             //  - the sequential search with the full budget (aux stream: LEAN
             //    and WIDE keys in one grid) settles every key.
             prep_race(n_defer, n_def_l);
+            if (resume) b.rs_mode = 2;      // (and phase 3, c3 = b: a record is never modified)
             if (defer_times) {
                 // tuning builds: per key [BFS start, end, sequential start, end, helper start, end]
                 unsigned long long *tl = ctx->ws<unsigned long long>(WS_TL, TL_W * (size_t)K);
@@ -6911,6 +7136,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         sum->streamed = stream_p2 ? 1 : 0;
         sum->p3_entries = q64(qh, Q_ENT_P3);
         sum->p2_start_ms = -1; sum->p1_span_ms = 0;
+        sum->resumed = resume ? qh[Q_RS_USED + 2] : 0;
+        sum->resume_bytes = resume ? q64(qh, Q_RS_USED) : 0;
         // an engine's own span from its s_memrealtime words (100 MHz): [first key, last wave end]
         auto span_ms = [&](int w) {
             const int64_t t0 = q64(qh, w), t1 = q64(qh, w + 2);

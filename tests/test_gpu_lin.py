@@ -140,6 +140,26 @@ def test_phase1_handover(ctx, handover):
         assert s.n_deferred >= s0.n_deferred
 
 
+@pytest.mark.parametrize("quick,handover", [(300, 0), (2000, 0), (8192, 0), (2000, 256)])
+def test_resume_deferred(ctx, quick, handover):
+    """Round 5: phase 1 saves every deferred LEAN search -- its stack and its
+    memo, WGL's cache -- and the heavy-key pass continues it instead of
+    restarting. Continued and restarted (JH_LIN_NO_RESUME) searches give every
+    field equal to the oracle's, at the full budget and at one the continued
+    searches run into; records were saved and used."""
+    cols, _ = synth.cas_register(n_keys=400, ops_per_key=600, threads_per_key=10, readers=5, p_invalid=0.05,
+                                 p_info=0.03, seed=98)
+    for budget in (None, 20000):
+        c, _ = oracle.check_cas_independent(cols, budget=budget or A.DEFAULT_BUDGET, threads=16)
+        g, s = ctx.check_cas_independent(cols, budget=budget, quick_budget=quick, handover_min=handover)
+        _same(g, c)
+        g2, s2 = ctx.check_cas_independent(cols, budget=budget, quick_budget=quick, handover_min=handover,
+                                           flags=A.LIN_NO_RESUME)
+        _same(g2, c)
+        assert s.resumed > 0 and s2.resumed == 0 and s.resume_bytes > 0
+        assert s.resumed <= s.n_deferred
+
+
 @pytest.mark.parametrize("waves", [None, 1])
 def test_windows_wider_than_64(ctx, waves):
     """Windows of 65..256 members (k_lin_xw, 4-word masks) and wider than

@@ -1,0 +1,39 @@
+# Round 5 GPU runs, one parameterised script (replaces round 4's one-off A/Bs):
+#   gpurun --timeout T -- bash tools/gpu_r5.sh <outdir> <part> [args...]
+# parts:
+#   tests  <pytest args...>   GPU tests (e.g. tests/test_gpu_lin.py -k configs)
+#   final                     the whole GPU suite, smoke(), the default bench line,
+#                             the C3 kernel trace (rocprofv3 --kernel-trace --stats)
+#   bench  <name> <bench.py args...>   one bench line -> <outdir>/<name>.json
+#   ranks  [bench.py args...] C3 ranks 1-7 (--seed-rank) at 5 steps
+#   prof   <name> <cmd...>    rocprofv3 kernel trace + stats of one command
+#   pmc    <name> <counters> <cmd...>  one rocprofv3 --pmc pass
+O=${1:-gpurun_out/r5}; PART=${2:-final}; shift 2
+R=$GRAFT_REPO_ROOT
+cd $R && mkdir -p $O
+case $PART in
+tests)
+  timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread "$@" > $O/tests.log 2>&1 ;;
+final)
+  timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > $O/gpu_tests.log 2>&1 || exit 1
+  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 1
+  timeout -k 10 300 python -u bench.py > $O/bench_c3.json 2> $O/bench_c3.err || exit 1
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/c3prof -o c3 -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 --no-parity > $R/$O/c3prof.log 2>&1 ;;
+bench)
+  N=$1; shift
+  timeout -k 10 600 python -u bench.py "$@" > $O/$N.json 2> $O/$N.err ;;
+ranks)
+  for rk in 1 2 3 4 5 6 7; do
+    timeout -k 10 120 python -u bench.py --no-cpu --e2e 0 --no-parity --steps 5 --warmup 1 --seed-rank $rk "$@" > $O/c3r${rk}.json 2> $O/c3r${rk}.err || exit 1
+  done ;;
+prof)
+  N=$1; shift
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/$N -o $N -- "$@" > $R/$O/$N.log 2>&1 ;;
+pmc)
+  N=$1; C=$2; shift 2
+  cd /tmp && export TMPDIR=/tmp
+  timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $R/$O/$N -o $N -- "$@" > $R/$O/$N.log 2>&1 ;;
+*) echo "unknown part $PART"; exit 2 ;;
+esac

@@ -220,6 +220,7 @@ def main():
     red_sum = torch.zeros(4, dtype=torch.int64, device=dev)
     use_pool = dist is not None and args.pool
     pool_stats = []
+    pool_home = {}          # this rank's keys' pooled verdicts (the measured ones), for the parity check
     if use_pool:
         from jepsen_amd import shard as _shard
         key_rows = _shard.KeyRows(cols.key, cols.n_keys)
@@ -240,16 +241,18 @@ def main():
 
             def stage1():
                 got[1] = ctx.check_cas_independent_device(DCols, verd.data_ptr(), budget=budget,
-                                                          flags=flags0 | A.LIN_PHASE1_ONLY, **tune)
+                                                          flags=flags0 | A.LIN_PHASE1_ONLY, exact_count=False, **tune)
                 return np.frombuffer(verd.cpu().numpy().tobytes(), dtype=A.VERDICT_DTYPE).copy()
 
             def stage2(sub, m):
                 v2 = torch.empty(m * A.VERDICT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
                 got[2] = ctx.check_cas_independent_device(_dev_view(sub, int(sub["key"].numel()), m), v2.data_ptr(),
-                                                          budget=budget, flags=flags0 | A.LIN_SKIP_PHASE1, **tune)
+                                                          budget=budget, flags=flags0 | A.LIN_SKIP_PHASE1,
+                                                          exact_count=False, **tune)
                 return np.frombuffer(v2.cpu().numpy().tobytes(), dtype=A.VERDICT_DTYPE).copy()
 
-            g, st = _shard.two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=dev)
+            g, st = _shard.two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=dev,
+                                              home=pool_home)
             pool_stats.append(st)
             # one jh_summary for the report: phase 1 from stage 1, the heavy-key
             # pass from stage 2 (explored / counts are the all-reduced ones)
@@ -264,7 +267,9 @@ def main():
     def step():
         if use_pool:
             return step_pool()
-        s = ctx.check_cas_independent_device(DCols, verd.data_ptr(), budget=budget, **args.tune)
+        # the checkers' path: no count pass for valid keys the reachable-set
+        # engine settles (their map has no :explored); parity below
+        s = ctx.check_cas_independent_device(DCols, verd.data_ptr(), budget=budget, exact_count=False, **args.tune)
         if dist is not None:
             # RCCL verdict summary all-reduce over xGMI: merge-valid (MAX),
             # failures/unknown/keys counts (SUM), first failing row (MIN as -MAX)
@@ -328,23 +333,36 @@ def main():
     if args.e2e:
         t1 = time.perf_counter()
         for _ in range(args.steps):
-            ctx.check_cas_independent(cols, budget=budget)
+            ctx.check_cas_independent(cols, budget=budget, exact_count=False)
         e2e_s = (time.perf_counter() - t1) / args.steps
         e2e = {"ms_per_call": e2e_s * 1e3, "entries_per_s_this_rank": n_entries / e2e_s,
                "calls": args.steps}
 
     out = None
     if rank == 0:
-        parity = None
+        parity = parity_detail = None
         if not args.no_parity:
             from oracle import oracle
-            if use_pool:
-                # the pool's verdicts are spread over the ranks: rank 0's shard once more in one call
-                ctx.check_cas_independent_device(DCols, verd.data_ptr(), budget=budget, **args.tune)
-            hv = np.frombuffer(verd.cpu().numpy().tobytes(), dtype=A.VERDICT_DTYPE)
+            # the verdicts of the last timed step: rank 0's keys as the pool left
+            # them on their home rank (shard.two_stage_resident), or the call's own
+            timed = (pool_home["verdicts"] if use_pool else
+                     np.frombuffer(verd.cpu().numpy().tobytes(), dtype=A.VERDICT_DTYPE).copy())
             ov, os_ = oracle.check_cas_independent(cols, budget=budget, threads=min(16, len(os.sched_getaffinity(0))))
-            # verdict, cause, failing row and WGL's cache size of every key
-            parity = bool(all((hv[f] == ov[f]).all() for f in A.VERDICT_FIELDS))
+            unc = timed["explored"] == A.EXPLORED_UNCOUNTED
+            # every field of every key; explored wherever counted (an uncounted
+            # key must be valid: JH_LIN_EXACT_COUNT's contract)
+            timed_ok = bool(all((timed[f] == ov[f]).all() for f in A.VERDICT_FIELDS if f != "explored") and
+                            (timed["explored"][~unc] == ov["explored"][~unc]).all() and
+                            (ov["valid"][unc] == A.VALID).all())
+            # and one more call with WGL's exact count for every key: every field
+            ctx.check_cas_independent_device(DCols, verd.data_ptr(), budget=budget, exact_count=True, **args.tune)
+            hv = np.frombuffer(verd.cpu().numpy().tobytes(), dtype=A.VERDICT_DTYPE)
+            exact_ok = bool(all((hv[f] == ov[f]).all() for f in A.VERDICT_FIELDS))
+            parity = timed_ok and exact_ok
+            parity_detail = {"timed_verdicts": timed_ok, "exact_count_call": exact_ok,
+                             "uncounted_valid_keys": int(unc.sum()),
+                             "source": "the last timed step's per-key verdicts" +
+                                       (" (pooled: gathered back to rank 0)" if use_pool else "")}
         cpu = cpu_faithful = None
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(cols, args.cpu_sample_keys or wl["cpu_keys_opt"], args.workload.upper(), mode=0, budget=budget)
@@ -375,6 +393,8 @@ def main():
                        # ABI 5: heavy keys started while phase 1 ran (the streaming pass), when
                        "streamed": bool(s.streamed), "phase2_start_ms": float(np.mean([x["p2_start_ms"] for x in sums])),
                        "phase1_span_ms": float(np.mean([x["p1_span_ms"] for x in sums])),
+                       # round 5: deferred searches continued from phase 1's state
+                       "resumed_keys": int(s.resumed), "resume_bytes": int(s.resume_bytes),
                        "phases": phase_table(sums), "opts": args.tune or None},
             "shard": shard_info,
             "pool": ({"mode": "two-stage (shard.two_stage_resident): phase 1 per rank, deferred keys' rows "
@@ -399,6 +419,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_faithful": cpu_faithful,
             "parity_vs_oracle": parity,
+            "parity_detail": parity_detail,
         }
         if rehearse:
             out["rehearsal"] = "JH_BENCH_REHEARSE: every rank on cuda:0 over gloo; not a bench number"

@@ -146,6 +146,15 @@ typedef struct jh_history {
  * pass continues it; this flag restarts deferred keys from scratch instead
  * (round 4's behaviour; same verdicts and counts, for A/B and the tests). */
 #define JH_LIN_NO_RESUME     512
+/* Round 5: WGL's exact cache size for every key. Without it, a valid key the
+ * reachable-set engine settles (a terminal configuration reachable and at
+ * most `budget` configurations reachable: WGL's cache is a subset of them,
+ * so WGL could not have run out) is emitted at once with explored =
+ * JH_EXPLORED_UNCOUNTED instead of after the count pass -- the reference's
+ * map has no :explored (doc/tutorial/04-checker.md:126-138); the parity
+ * tests set this flag. */
+#define JH_LIN_EXACT_COUNT  1024
+#define JH_EXPLORED_UNCOUNTED (-3)
 
 typedef struct jh_lin_opts {
     int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */

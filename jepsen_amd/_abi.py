@@ -61,6 +61,8 @@ LIN_PHASE1_ONLY, LIN_SKIP_PHASE1 = 32, 64
 LIN_NO_HANDOVER = 128
 LIN_STREAM = 256
 LIN_NO_RESUME = 512           # round 5: restart deferred keys instead of continuing them
+LIN_EXACT_COUNT = 1024        # round 5: WGL's exact count for every key (the parity tests)
+EXPLORED_UNCOUNTED = -3       # a valid key settled without the count pass
 CAUSE_DEFERRED = 9
 
 

@@ -111,10 +111,14 @@ def _raise(rc, err):
         raise JhError(rc, err.value.decode(errors="replace"))
 
 
-def _opts(init, budget, stream=0, algorithm=None, **tune):
+def _opts(init, budget, stream=0, algorithm=None, exact_count=True, **tune):
     """jh_lin_opts. tune: flags, quick_budget, phase2_budget, helpers,
     helper_late_us, xw_waves, p2_waves_per_cu (jh.h; all decide the same
-    verdicts, the tests use them to reach the less common search paths)."""
+    verdicts, the tests use them to reach the less common search paths).
+    exact_count: JH_LIN_EXACT_COUNT, WGL's cache size for every key (what the
+    parity tests compare with the oracle); the checkers pass False -- their
+    result maps carry no :explored, and the count pass then leaves the
+    critical path."""
     o = A.JhLinOpts()
     o.init_value = A.NIL if init is None else int(init)
     o.budget = int(budget or 0)
@@ -126,6 +130,8 @@ def _opts(init, budget, stream=0, algorithm=None, **tune):
         if k not in dict(A.JhLinOpts._fields_) or k in ("init_value", "budget", "stream", "algorithm", "reserved"):
             raise TypeError(f"unknown jh_lin_opts field {k}")
         setattr(o, k, int(v))
+    if exact_count:
+        o.flags |= A.LIN_EXACT_COUNT
     return o
 
 

@@ -246,7 +246,8 @@ class Linearizable(Checker):
             history = to_device_ops(self.model, ops)
         cols = _cols(history, keyed=False)
         init = _init_state(self.model, cols)
-        r = _ctx().check_cas_full(cols, init=init, budget=self.budget, algorithm=_algorithm(self.algorithm))
+        r = _ctx().check_cas_full(cols, init=init, budget=self.budget, algorithm=_algorithm(self.algorithm),
+                                  exact_count=False)
         out = lin_result(r["valid"], r["cause"], r["fail_entry"], r["explored"], cols,
                          r["previous_ok"], r["last_op"], r["analyzer"], ops=ops)
         if wants_configs(r["valid"], r["analyzer"]):

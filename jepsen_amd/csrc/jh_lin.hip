@@ -3689,6 +3689,7 @@ struct BfsArgs {
     int32_t *claim;         // race with the sequential search (see emit_verdict)
     int64_t reach_cap;      // reachable configurations enumerated at most (>= budget + 1)
     int32_t dbg_plen;       // JH_BFS_ONLY=1 (debugging): the BFS alone settles, fail_entry = path length
+    int32_t exact_count;    // JH_LIN_EXACT_COUNT: WGL's count for the valid keys it settles (else uncounted)
     // per workgroup, for bfs_wgl_count (valid keys): every node of the set in
     // layer order, its layer offsets, a node -> id hash, liveness / closure marks
     uint64_t *nodes;        // ncap
@@ -4936,6 +4937,16 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             v.fail_entry = sh.term ? -1 : ret_row(A.src, K, sh.tmax, lane);
             if (lane == 0) emit_verdict(A.out, A.claim, key, v);
         }
+    } else if (sh.term && !A.exact_count && (long long)sh.count <= A.budget) {
+        // valid for certain (round 5): WGL's cache -- the path's configurations
+        // and the dead ones left of it, one terminal included -- is a subset of
+        // the reachable set (sh.count, initial included, terminals not), so WGL
+        // cannot have run out of budget; no count pass unless asked for
+        if (tid == 0) {
+            jh_key_verdict v;
+            v.valid = JH_VALID; v.cause = 0; v.fail_entry = -1; v.explored = JH_EXPLORED_UNCOUNTED;
+            emit_verdict(A.out, A.claim, key, v);
+        }
     } else if (sh.term) {
         // valid, or :unknown if WGL's count passes the budget: WGL's exact count
         if (tid == 0) { if (n_ok < A.lcap) A.lstart[n_ok] = sh.nnodes; sh.ok = 0; }
@@ -5683,7 +5694,9 @@ __global__ void k_summary(const jh_key_verdict *__restrict__ v, int64_t K, long 
          k += (int64_t)gridDim.x * blockDim.x) {
         jh_key_verdict x = v[k];
         if (x.explored == -1) continue;                 // a key in no tuple
-        nk++; ex += x.explored > 0 ? x.explored : 0;     // -2: settled by the BFS, size unknown
+        // explored sums WGL insert counts only: not JH_EXPLORED_UNCOUNTED, and
+        // not a stage-1 deferred key's progress (another unit)
+        nk++; ex += (x.explored > 0 && x.cause != JH_CAUSE_DEFERRED) ? x.explored : 0;
         vmax = max(vmax, (long long)x.valid);
         if (x.valid == JH_INVALID) { ninv++; ff = min(ff, (long long)x.fail_entry); }
         if (x.valid == JH_UNKNOWN) nunk++;
@@ -6372,6 +6385,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // configurations, explored = count
         bfs_only = (lflags & JH_LIN_BFS_ONLY) != 0;
         c.dbg_plen = tune_env("JH_BFS_DBGV") && atoi(tune_env("JH_BFS_DBGV")) ? 1 : 0;
+        c.exact_count = (lflags & JH_LIN_EXACT_COUNT) || c.dbg_plen ? 1 : 0;
         c.ncap = ncap; c.hcap = hcap; c.lcap = lcap;
         c.nodes = ctx->ws<uint64_t>(WS_BFS_NODES, (size_t)wg2 * ncap);
         c.lstart = ctx->ws<uint32_t>(WS_BFS_LSTART, (size_t)wg2 * lcap);

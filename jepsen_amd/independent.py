@@ -123,7 +123,7 @@ class IndependentChecker(Checker):
             if cols.n_keys and not unkeyed_client:
                 verdicts, _ = _ctx().check_cas_independent(
                     cols, init=_init_state(lin.model, cols), budget=lin.budget,
-                    algorithm=_algorithm(lin.algorithm))
+                    algorithm=_algorithm(lin.algorithm), exact_count=False)
                 lin_res = {}
                 for kid, key in enumerate(cols.keys):
                     v = verdicts[kid]

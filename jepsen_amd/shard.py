@@ -218,7 +218,7 @@ def _gather_padded(t, world, dist):
     return [o[:k] for o, k in zip(out, ns)]
 
 
-def two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=None):
+def two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=None, home=None):
     """The two-stage check of a history already resident on this rank's
     device (bench.py --gpus N; independent.clj:266-288's dynamic pool,
     VERDICT r3 item 4), one process per GPU:
@@ -240,7 +240,14 @@ def two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=None
     dcols: dict of 1-D int64 tensors (COLS) on `device`; key_rows: KeyRows
     of this rank's history. stage2(cols) takes a dict of the same columns
     (keys renumbered 0..m-1) and returns the verdicts. Returns (summary dict,
-    stats). A key's failing row is reported in its home rank's row numbers."""
+    stats). A key's failing row is reported in its home rank's row numbers.
+
+    home: a dict to receive this rank's own keys' final verdicts
+    (home["verdicts"]): stage 1's settled keys, and for its deferred keys the
+    stage-2 verdicts of whichever rank checked them, sent back with one more
+    all_gather (their rows mapped to this rank's row numbers) -- what a
+    caller checks key by key against a reference (bench.py's parity, ADVICE
+    r4: the pooled verdicts, not a re-run, are the measured ones)."""
     import torch
     import torch.distributed as dist
     from . import _abi as A
@@ -285,15 +292,33 @@ def two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=None
         sub = {c: allc[i].contiguous() for i, c in enumerate(COLS)}
         src_row = allc[len(COLS)].cpu().numpy()
         v2 = stage2(sub, len(mine)).copy()
-        hit = v2["fail_entry"] >= 0
-        v2["fail_entry"][hit] = src_row[v2["fail_entry"][hit]]
-    # the summary of the keys this rank decided: its own settled keys and its share
-    vs = [v1[~deferred & (v1["explored"] >= 0)]] + ([v2[v2["explored"] >= 0]] if v2 is not None else [])
+        for f in ("fail_entry", "previous_ok", "last_op"):
+            hit = v2[f] >= 0
+            v2[f][hit] = src_row[v2[f][hit]]
+    if home is not None:
+        # every checked key back to its home rank: [home, key, the verdict's fields]
+        fields = [f for f in A.VERDICT_FIELDS]
+        back = (np.stack([np.array([e[1] for e in mine], np.int64), np.array([e[2] for e in mine], np.int64)] +
+                         [v2[f].astype(np.int64) for f in fields], 1).reshape(-1)
+                if v2 is not None else np.zeros(0, np.int64))
+        tb = torch.from_numpy(back).to(device)
+        outs = _gather_padded(tb, world, dist) if multi else [tb]
+        hv = v1.copy()
+        for o in outs:
+            o = o.cpu().numpy().reshape(-1, 2 + len(fields))
+            o = o[o[:, 0] == rank]
+            for j, f in enumerate(fields):
+                hv[f][o[:, 1]] = o[:, 2 + j]
+        home["verdicts"] = hv
+    # the summary of the keys this rank decided: its own settled keys and its
+    # share (explored -1: a key in no tuple; JH_EXPLORED_UNCOUNTED adds nothing)
+    vs = [v1[~deferred & (v1["explored"] != -1)]] + ([v2[v2["explored"] != -1]] if v2 is not None else [])
     verd = np.concatenate(vs) if vs else v1[:0]
     inv = verd["valid"] == A.INVALID
     ff = int(verd["fail_entry"][inv].min()) if inv.any() else _FAR
     mx = [int(verd["valid"].max()) if len(verd) else 0, -ff]
-    sm = [int(inv.sum()), int((verd["valid"] == A.UNKNOWN).sum()), int(len(verd)), int(verd["explored"].sum())]
+    sm = [int(inv.sum()), int((verd["valid"] == A.UNKNOWN).sum()), int(len(verd)),
+          int(np.maximum(verd["explored"], 0).sum())]
     stats = {"deferred_here": int(len(dkeys)), "pool": len(pool), "checked_here": len(mine),
              "rows_sent": int(len(rows)), "rows_received": int(sum(e[4] for e in mine))}
     return all_reduce_summary(mx, sm, device), stats

@@ -82,6 +82,7 @@ int main(int argc, char **argv) {
         jh_key_verdict *vd = (jh_key_verdict *)calloc((size_t)(h.n_keys > 0 ? h.n_keys : 1), sizeof *vd);
         jh_summary s;
         jh_lin_opts o = {JH_NIL, 0, 0};
+        o.flags = JH_LIN_EXACT_COUNT;                       /* every field is compared with the oracle */
         if (argc > 5) o.quick_budget = atoll(argv[5]);       /* a small one: many keys reach stage 2 */
         rc = jh_check_cas_independent(ctx, &v, &o, vd, &s, err, sizeof err);
         if (rc) { fprintf(stderr, "check: %d %s\n", rc, err); jh_close(ctx); return rc; }

@@ -178,7 +178,11 @@ def _worker3(rank, world, port, q):
             got.append(int(c.n))
             return v
 
-        g, st = shard.two_stage_resident(rank, world, dcols, kr, stage1, stage2)
+        home = {}
+        g, st = shard.two_stage_resident(rank, world, dcols, kr, stage1, stage2, home=home)
+        # the pooled verdicts back on their home rank equal the history checked whole
+        want, _ = oracle.check_cas_independent(cols)
+        st["home_equal"] = all(bool((home["verdicts"][f] == want[f]).all()) for f in A.VERDICT_FIELDS)
         q.put((rank, g, st))
     finally:
         dist.destroy_process_group()
@@ -218,4 +222,5 @@ def test_two_stage_resident_pool(built):
             assert g[f] == x, (rank, f, g[f], x)
         assert g["first_fail_entry"] == (min(ffs) if ffs else -1)
         assert st["pool"] > 4 and st["checked_here"] >= st["pool"] // 2
+        assert st["home_equal"], rank
     assert sum(st["checked_here"] for _, _, st in res) == res[0][2]["pool"]

@@ -268,7 +268,10 @@ def test_independent_compose(ctx):
     for k in range(cols.n_keys):
         lr = r["results"][k]["linear"]
         exp = {A.VALID: True, A.INVALID: False, A.UNKNOWN: CK.UNKNOWN}[int(c["valid"][k])]
-        assert lr["valid?"] == exp and lr.explored == int(c["explored"][k]), k
+        # the checkers skip the count pass (no :explored in the map): a valid key
+        # the reachable-set engine settled is uncounted, every other count WGL's
+        assert lr["valid?"] == exp, k
+        assert lr.explored == int(c["explored"][k]) or (exp is True and lr.explored == A.EXPLORED_UNCOUNTED), k
         assert "explored" not in lr and "fail-entry" not in lr        # the ABI side channel, not map keys
         if exp is not CK.UNKNOWN:
             assert lr["configs"] == [] or exp is False

@@ -157,7 +157,11 @@ def main():
     rehearse = world > 1 and os.environ.get("JH_BENCH_REHEARSE") == "1"
     if rehearse:
         local = 0
-    if world > 1:
+    # JH_BENCH_DIST1=1 (under torchrun --nproc-per-node 1): the N > 1 code path
+    # -- RCCL process group, the two-stage pool's all_gathers, the verdict
+    # all-reduce -- on a one-rank communicator, the only RCCL run one GPU allows
+    dist1 = world == 1 and os.environ.get("JH_BENCH_DIST1") == "1"
+    if world > 1 or dist1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         if rehearse:
@@ -420,6 +424,8 @@ def main():
             "cpu_baseline_faithful": cpu_faithful,
             "parity_vs_oracle": parity,
             "parity_detail": parity_detail,
+            "dist_selftest": ("JH_BENCH_DIST1: one-rank RCCL communicator, the N > 1 code path on one GPU"
+                              if dist1 else None),
         }
         if rehearse:
             out["rehearsal"] = "JH_BENCH_REHEARSE: every rank on cuda:0 over gloo; not a bench number"

@@ -69,7 +69,9 @@ def build_libjh(verbose=False):
                 print(out)
     lib = os.path.join(HERE, "libjh.so")
     if _newer(lib, objs):
-        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-pthread", "-o", lib] + objs)
+        # linked aside and renamed: a snapshot of the tree (gpurun) never sees a half-written library
+        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-pthread", "-o", lib + ".tmp"] + objs)
+        os.replace(lib + ".tmp", lib)
     return lib
 
 
@@ -77,7 +79,8 @@ def build_gen():
     src = os.path.join(CSRC, "gen.cpp")
     lib = os.path.join(HERE, "libjhgen.so")
     if _newer(lib, [src, os.path.join(ROOT, "include", "jh.h")]):
-        _run(["g++", "-O2", "-g", "-fPIC", "-shared", "-std=c++17", "-Wall", "-pthread", "-o", lib, src])
+        _run(["g++", "-O2", "-g", "-fPIC", "-shared", "-std=c++17", "-Wall", "-pthread", "-o", lib + ".tmp", src])
+        os.replace(lib + ".tmp", lib)
     return lib
 
 

@@ -116,7 +116,6 @@ void jh_close(jh_ctx *ctx) {
         if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
         if (ctx->aux2) (void)hipStreamDestroy(ctx->aux2);
         if (ctx->aux3) (void)hipStreamDestroy(ctx->aux3);
-        for (hipStream_t m : ctx->msk) if (m) (void)hipStreamDestroy(m);
     }
     delete ctx;
 }

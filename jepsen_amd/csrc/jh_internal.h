@@ -55,8 +55,6 @@ struct jh_ctx {
     hipStream_t aux = nullptr;     // second stream for racing searches (jh_lin.hip)
     hipStream_t aux2 = nullptr;    // third stream: windows wider than 64 (jh_lin.hip)
     hipStream_t aux3 = nullptr;    // fourth stream: phase-2 late helpers (jh_lin.hip)
-    hipStream_t msk[4] = {};       // tuning builds: CU-masked streams of the streamed pass (JH_CU_SPLIT)
-    int msk_split = 0;
     std::mutex mu;
     std::vector<Buf> bufs;
     hipEvent_t ev[24] = {};
@@ -64,6 +62,7 @@ struct jh_ctx {
     bool lds_attr = false;        // >64 KB dynamic-LDS attributes set for this device's kernels
     bool lds_attr_wg = false;
     int n_cu = 256;
+    int share = 1;                // contexts of one jh_open_devices call on this device (fit_units divides by it)
     int32_t *hflag = nullptr;     // host-mapped flag: phase 1's queue drained (jh_lin.hip)
     int32_t *hflag_dev = nullptr;
     void *pinned = nullptr;       // small pinned staging for scalars

@@ -5860,9 +5860,11 @@ static int fit_units(jh_ctx *ctx, int want, uint64_t per_unit, std::initializer_
     size_t fr = 0, tot = 0;
     HIP_TRY(hipMemGetInfo(&fr, &tot));
     const uint64_t reserve = std::max<uint64_t>(2ULL << 30, tot / 32);
-    uint64_t room = fr + held;
+    // contexts sharing the device (jh_open_devices with a device listed more
+    // than once) run at once: each takes its share of what is free
+    uint64_t room = fr / (uint64_t)std::max(1, ctx->share) + held;
     room = room > reserve ? room - reserve : 0;
-    room = std::min<uint64_t>(room, tot / 4);
+    room = std::min<uint64_t>(room, tot / (4 * (uint64_t)std::max(1, ctx->share)));
     const uint64_t fit = room / (per_unit + per_unit / 8);    // ws() allocates 1/8 over
     return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)want, fit));
 }
@@ -6480,23 +6482,12 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // waves; phase 3 follows on st. Four streams: the hardware's queues.
         // Every search is the one the round-3 schedule runs (same verdicts and
         // counts); only when each starts changes.
-        // tuning builds: JH_CU_SPLIT=R gives phase 1 the first n_cu - R CUs and
-        // the consumers the last R (CU-masked streams), and starts the
-        // consumers with phase 1 instead of at its drain
+        // (round 4's CU-masked variant, JH_CU_SPLIT, is gone: slower at every
+        // split, and at R = 48 the late helpers -- which spin until the
+        // sequential grid has left its queue -- held the 48 consumer CUs the
+        // sequential waves needed to become resident, so each step waited out
+        // HELPER_MAX_TICKS, 5 s: DESIGN.md section 5)
         hipStream_t p1s = st, cs1 = ctx->aux, cs2 = ctx->aux2, cs3 = ctx->aux3;
-        const int cu_split = tune_env("JH_CU_SPLIT") ? std::max(0, std::min(ctx->n_cu - 8, atoi(tune_env("JH_CU_SPLIT")))) : 0;
-        if (cu_split > 0) {
-            if (ctx->msk_split != cu_split) {
-                for (hipStream_t &m : ctx->msk) if (m) { HIP_TRY(hipStreamDestroy(m)); m = nullptr; }
-                const int nw = (ctx->n_cu + 31) / 32;
-                std::vector<uint32_t> m1(nw, 0u), m2(nw, 0u);
-                for (int i = 0; i < ctx->n_cu; i++) (i < ctx->n_cu - cu_split ? m1 : m2)[i >> 5] |= 1u << (i & 31);
-                HIP_TRY(hipExtStreamCreateWithCUMask(&ctx->msk[0], (uint32_t)nw, m1.data()));
-                for (int i = 1; i < 4; i++) HIP_TRY(hipExtStreamCreateWithCUMask(&ctx->msk[i], (uint32_t)nw, m2.data()));
-                ctx->msk_split = cu_split;
-            }
-            p1s = ctx->msk[0]; cs1 = ctx->msk[1]; cs2 = ctx->msk[2]; cs3 = ctx->msk[3];
-        }
         int32_t qt[Q_WORDS];
         HIP_TRY(hipMemcpyAsync(qt, q, sizeof qt, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
@@ -6586,7 +6577,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             // 1 holds every CU, and a consumer launched earlier could take CUs
             // from it while it still has keys to hand out
             volatile int32_t *hf = (volatile int32_t *)ctx->hflag;
-            while (!cu_split && !*hf) {
+            while (!*hf) {
                 const hipError_t e = hipEventQuery(ctx->ev[4]);
                 if (e == hipSuccess) break;
                 if (e != hipErrorNotReady) HIP_TRY(e);

@@ -196,6 +196,10 @@ int jh_open_devices(const int32_t *devices, int n, jh_ctx **out) {
         }
         g->members.push_back(m);
     }
+    // members on one device divide its free HBM between them (fit_units):
+    // their checks run at once, one host thread each
+    for (jh_ctx *m : g->members)
+        for (jh_ctx *x : g->members) if (x != m && x->device == m->device) m->share++;
     *out = g;
     return JH_OK;
 }

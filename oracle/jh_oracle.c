@@ -202,12 +202,36 @@ int orc_key_prepare(const jh_history *h, const int64_t *sel, int64_t m, orc_key 
     k->w_off[n_ok] = (int32_t)used;
     free(act);
     k->max_window = maxw;
+    if (orc_reduce_crashed) {
+        k->pred = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+        for (int32_t i = 0; i < n; i++) {
+            k->pred[i] = -1;
+            if (k->ops[i].ret != ORC_CRASHED) continue;
+            for (int32_t j = i - 1; j >= 0; j--)
+                if (k->ops[j].ret == ORC_CRASHED && k->ops[j].f == k->ops[i].f && k->ops[j].v1 == k->ops[i].v1 &&
+                    k->ops[j].v2 == k->ops[i].v2) { k->pred[i] = j; break; }
+        }
+    }
     if (maxw > JH_MAX_WINDOW) k->status = JH_CAUSE_WINDOW;
     return 0;
 }
 
+int orc_reduce_crashed = 0;
+
+/* the crashed-op symmetry: window member i of W (mask over it) may be lifted
+ * only if its class predecessor is linearized (it is in the window: crashed
+ * ops never leave, and it was invoked earlier, so it sits at a lower position) */
+static int sym_blocked(const orc_key *k, const int32_t *W, const uint64_t *mask, int i) {
+    if (!k->pred) return 0;
+    const int32_t p = k->pred[W[i]];
+    if (p < 0) return 0;
+    for (int j = i - 1; j >= 0; j--)
+        if (W[j] == p) return !((mask[j >> 6] >> (j & 63)) & 1);
+    return 0;
+}
+
 void orc_key_free(orc_key *k) {
-    free(k->ops); free(k->ret_op); free(k->w_off); free(k->w_ops);
+    free(k->ops); free(k->ret_op); free(k->w_off); free(k->w_ops); free(k->pred);
     memset(k, 0, sizeof(*k));
 }
 
@@ -313,7 +337,7 @@ int orc_wgl_canonical(const orc_key *k, int64_t init, int64_t budget,
         int w = k->w_off[t + 1] - k->w_off[t];
         int took = 0;
         for (int i = start; i < w; i++) {
-            if (bit_get(mask, i)) continue;
+            if (bit_get(mask, i) || sym_blocked(k, W, mask, i)) continue;
             const orc_op *o = &k->ops[W[i]];
             int64_t s2;
             if (!cas_step(o->f, o->v1, o->v2, s, &s2)) continue;

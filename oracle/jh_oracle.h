@@ -45,7 +45,18 @@ typedef struct orc_key {
     int32_t *w_off;    /* windows: W(t) = w_ops[w_off[t] .. w_off[t+1]) */
     int32_t *w_ops;
     int32_t max_window;
+    int32_t *pred;     /* crashed-op symmetry (orc_reduce_crashed): the previous crashed op
+                          of the same (f, value, value2) in call order, or -1 */
 } orc_key;
+
+/* Round 5: pending crashed ops of one (f, value, value2) class are
+ * interchangeable -- both invoked, neither bounded by a return, the same
+ * step -- so only the earliest-invoked unlinearized member of a class is a
+ * candidate (a sound symmetry reduction: every configuration reachable
+ * without it has an equivalent one, same register value and the same ops
+ * still to linearize up to renaming, reachable with it). Changes explored
+ * counts, never a verdict. Set by the caller (libjh.so's default). */
+extern int orc_reduce_crashed;
 
 /* Prepare key from the rows `sel[0..m)` (increasing history rows). */
 int  orc_key_prepare(const jh_history *h, const int64_t *sel, int64_t m, orc_key *k);

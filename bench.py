@@ -28,11 +28,15 @@ BYTES_PER_ENTRY = 56           # 7 x int64 columns read once
 BYTES_PER_PROBE = 16           # one memo entry {mask, t|state|gen}
 # HBM bytes per launch of a kernel from the rocprofv3 FETCH_SIZE and
 # WRITE_SIZE passes over the SAME history (tools/gpu_pmc.sh + pmc_traffic.py),
-# one file per (workload, seed, kernel) under profiles/r04/: PMC counters
+# one file per (workload, seed, kernel) under profiles/r05/: PMC counters
 # cannot be read inside a timed run, and a file of another history (another
-# workload, seed or rank) is never used. The file also holds the algorithmic
-# bytes of the profiled run itself, so traffic / algorithmic is a same-run ratio.
-TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r04")
+# workload, seed or rank) is never used. Under --pmc the kernels run one at a
+# time (rocprofv3 serializes them), so the search phases take another
+# schedule than the timed run's (e.g. no late helpers beside phase 2): the
+# file's ratio is traffic over the algorithmic bytes of that serialized run,
+# and the line also scales the measured bytes per memo probe to the timed
+# run's probe count.
+TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r05")
 
 
 def traffic_name(workload, seed, kernel):
@@ -264,8 +268,11 @@ def main():
             if 2 in got:
                 for f in ("dfs_ms", "memo_probes"):
                     setattr(s, f, getattr(got[1], f))
+                # both stages' device time (the exchange is in the pool stats)
+                s.device_ms = got[1].device_ms + got[2].device_ms
             s.valid, s.n_invalid, s.n_unknown = g["valid"], g["n_invalid"], g["n_unknown"]
             s.explored = g["explored"]
+            s.first_fail_entry = g["first_fail_entry"]      # all-reduced, in home-rank rows
             return s
 
     def step():
@@ -411,9 +418,18 @@ def main():
             "roofline": ({"bound": "hbm", "phase": dom, "kernel": phases[dom]["kernel"],
                           "achieved": phases[dom]["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                           "frac": phases[dom]["frac"],
-                          # FETCH_SIZE + WRITE_SIZE per launch over this same history (tools/gpu_pmc.sh)
+                          # FETCH_SIZE + WRITE_SIZE per launch over this same history (tools/gpu_pmc.sh),
+                          # measured in rocprofv3's serialized --pmc schedule
                           "traffic": tr["traffic_bytes"] if tr else None,
-                          "traffic_over_alg_same_run": tr.get("traffic_over_alg") if tr else None,
+                          "traffic_schedule": ("serialized (rocprofv3 --pmc runs one kernel at a time: "
+                                               f"that run's phase took {tr['pmc_phase_ms']:.1f} ms, "
+                                               f"{tr['pmc_probes']:.0f} memo probes)") if tr else None,
+                          "traffic_over_alg_pmc_run": tr.get("traffic_over_alg") if tr else None,
+                          # the non-entry part of that traffic per memo probe, times this run's probes
+                          "traffic_scaled_to_timed_probes": (
+                              BYTES_PER_ENTRY * phases[dom]["entries"] +
+                              max(0.0, tr["traffic_bytes"] - BYTES_PER_ENTRY * tr["pmc_entries"]) /
+                              max(1.0, tr["pmc_probes"]) * phases[dom]["probes"]) if tr else None,
                           "traffic_source": traffic_src,
                           "kernel_ms": phases[dom]["ms"], "alg_bytes": phases[dom]["alg_bytes"],
                           "note": "latency-bound tree search: one wave per key, LDS memo; bytes are 56 B per "

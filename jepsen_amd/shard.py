@@ -252,7 +252,10 @@ def two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=None
     import torch.distributed as dist
     from . import _abi as A
     multi = dist.is_initialized()        # (a one-rank communicator too: bench.py JH_BENCH_DIST1)
+    import time
+    t0 = time.perf_counter()
     v1 = stage1()
+    t1 = time.perf_counter()
     deferred = (v1["valid"] == A.UNKNOWN) & (v1["cause"] == A.CAUSE_DEFERRED)
     dkeys = np.nonzero(deferred)[0]
     prog = v1["explored"][dkeys]
@@ -291,6 +294,8 @@ def two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=None
         allc[COLS.index("key")] = torch.from_numpy(kid).to(allp.device)
         sub = {c: allc[i].contiguous() for i, c in enumerate(COLS)}
         src_row = allc[len(COLS)].cpu().numpy()
+    t2 = time.perf_counter()
+    if mine:
         v2 = stage2(sub, len(mine)).copy()
         for f in ("fail_entry", "previous_ok", "last_op"):
             hit = v2[f] >= 0
@@ -319,6 +324,11 @@ def two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=None
     mx = [int(verd["valid"].max()) if len(verd) else 0, -ff]
     sm = [int(inv.sum()), int((verd["valid"] == A.UNKNOWN).sum()), int(len(verd)),
           int(np.maximum(verd["explored"], 0).sum())]
+    t3 = time.perf_counter()
     stats = {"deferred_here": int(len(dkeys)), "pool": len(pool), "checked_here": len(mine),
-             "rows_sent": int(len(rows)), "rows_received": int(sum(e[4] for e in mine))}
+             "rows_sent": int(len(rows)), "rows_received": int(sum(e[4] for e in mine)),
+             # host wall times (each stage ends in a device sync): stage 1, the exchange
+             # (metadata and rows all_gathered, my share assembled), stage 2 + the
+             # verdicts sent home
+             "stage1_ms": (t1 - t0) * 1e3, "exchange_ms": (t2 - t1) * 1e3, "stage2_ms": (t3 - t2) * 1e3}
     return all_reduce_summary(mx, sm, device), stats

@@ -26,10 +26,13 @@ own = np.ones(cols.n_keys, np.int64)
 own[keys] = 0
 sub, mine, _ = shard.shard_history(cols, own, 0)
 ctx = _native.Context(0)
+budget = int(os.environ.get("JH_PROBE_BUDGET", "0")) or wl.get("budget")
+# the checkers' path (no count pass for BFS-settled valid keys) unless "exact"
 for label, kw in [("race", {}), ("bfs-only", {"flags": A.LIN_BFS_ONLY}), ("no-helpers", {"flags": A.LIN_NO_HELPERS}),
-                  ("race", {})]:
+                  ("exact", {"exact_count": True}), ("race", {})]:
+    kw.setdefault("exact_count", False)
     t0 = time.perf_counter()
-    v, s = ctx.check_cas_independent(sub, budget=wl.get("budget"), **kw)
+    v, s = ctx.check_cas_independent(sub, budget=budget, **kw)
     ms = (time.perf_counter() - t0) * 1e3
     print(json.dumps({"run": label, "keys": mine.tolist(), "wall_ms": round(ms, 3), "device_ms": s.device_ms,
                       "valid": v["valid"].tolist(), "explored": v["explored"].tolist(),

@@ -5,7 +5,7 @@ written as the JSON bench.py puts into its roofline object (`traffic`,
 
     python tools/pmc_traffic.py <pmc-dir> <kernel-substring> <workload> <seed>
 
--> profiles/r04/traffic_<workload>_s<seed>_<kernel>.json (bench.traffic_name).
+-> profiles/r05/traffic_<workload>_s<seed>_<kernel>.json (bench.traffic_name).
 Both counters are in KiB. The guide's gfx950 calibration: FETCH_SIZE reports
 1/2 of the bytes of wide (16 B/lane) coalesced streaming reads, WRITE_SIZE is
 exact for 16 B/lane streaming stores; other access widths are uncalibrated.
@@ -48,12 +48,13 @@ def main():
         except (OSError, IndexError, ValueError):
             pass
     # the phase whose kernel this is (bench.PHASES): its entries and probes in each pass's run
-    alg = {}
+    alg, ents, probes, ms = {}, [], [], []
     for log, d in run.items():
         for name, (tf, pf, ef, kf, kern) in PHASES.items():
             if kern.split("<")[0] in kernel and (("<" not in kernel) or kern in kernel) and d.get(tf, 0) > 0:
                 ent = d["entries"] if ef is None else d[ef]
                 alg[log] = BYTES_PER_ENTRY * ent + BYTES_PER_PROBE * d[pf]
+                ents.append(ent); probes.append(d[pf]); ms.append(d[tf])
                 break
     # every launch of the kernel in a pass (reps calls) counts; per launch = mean
     f1, w1 = sum(fetch) / len(fetch), sum(write) / len(write)
@@ -63,6 +64,11 @@ def main():
            "fetch_bytes": f1, "write_bytes": w1, "traffic_bytes": f1 + w1,
            "launches": [len(fetch), len(write)], "alg_bytes_same_run": alg_run,
            "traffic_over_alg": (f1 + w1) / alg_run if alg_run else None,
+           # the serialized --pmc run's own phase (bench.py scales per probe to the timed run)
+           "pmc_entries": sum(ents) / len(ents) if ents else 0.0,
+           "pmc_probes": sum(probes) / len(probes) if probes else 0.0,
+           "pmc_phase_ms": sum(ms) / len(ms) if ms else 0.0,
+           "schedule": "serialized: rocprofv3 --pmc runs one kernel at a time",
            "profiled_runs": run,
            "correction": "none: scattered 8-16 B accesses are uncalibrated on gfx950 (MI355X_MICROARCH.md HBM)"}
     dst = os.path.join(TRAFFIC_DIR, traffic_name(workload, seed, kernel))

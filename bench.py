@@ -99,6 +99,11 @@ def phase_rooflines(sums, n_entries):
 WORKLOADS = {
     "c3": dict(desc="C3: independent cas-register, 10000 keys x ~1k entries per GPU", keys=10000,
                seed=3, cpu_keys=10000, cpu_keys_opt=10000,
+               # round 5: C4's budget (SURVEY A.6 makes it this project's; no C3 key is
+               # :unknown at 2^20 or 2^22). At 2^22 the reachable-set engine settles the
+               # valid keys of 1.17 M reachable configurations (ranks 4 / 6) without the
+               # count pass
+               budget=1 << 22,
                gen=dict(threads_per_key=10, readers=5, n_values=5, process_limit=20, groups=10,
                         init_nil=True, p_info=0.02, p_invalid=0.01, nemesis_every=10000)),
     "c4": dict(desc="C4: independent cas-register, ONE history of 125000 x N keys (1M at N=8) generated "

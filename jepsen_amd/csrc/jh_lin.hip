@@ -448,10 +448,13 @@ __device__ __forceinline__ bool handover(const DfsArgs &A, uint32_t ins) {
 constexpr int64_t P2_BUDGET = 1 << 16;  // phase-2 inserts before a key moves to phase 3
 constexpr int64_t QUICK_BUDGET = 8192;  // phase-1 inserts before a key is deferred
 // phase-1 inserts after which a search may be handed over once the queue is
-// empty; 0 = off by default. Round 1 measured it at 1 024 (phase 1 12.4 -> 8.0
-// ms but 3x the keys restart in phase 2: C3 59.5 -> 69.9 ms); re-measured
-// against the round-3 heavy-key pass through jh_lin_opts.handover_min
-constexpr int32_t HANDOVER_MIN = 0;
+// empty. Round 1 measured it at 1 024 (phase 1 12.4 -> 8.0 ms but 3x the keys
+// restart in phase 2: C3 59.5 -> 69.9 ms), rounds 3-4 kept it off for the same
+// reason. Round 5: a handed-over search continues from its saved state (the
+// resume records), so the hand-over costs nothing: 1 024 is the default when
+// resuming (C3 rank 0 41.4 -> 39.2 ms, ranks 4 / 6 / 7 and C4 down too:
+// profiles/r05/ab/); without resume it stays off
+constexpr int32_t HANDOVER_MIN = 1024;
 // phase-1 issue priority by insert count (DfsArgs.prio_ins): 0 = off until measured
 constexpr int32_t P1_PRIO_INS = 0;
 // phase-2 late helpers (workgroups, one per CU) and how long a key must have run
@@ -6122,7 +6125,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     a.scratch = scr; a.scratch_bytes = scr_bytes; a.budget = quick; a.defer = quick < budget ? 1 : 0;
     a.init_state = init_state; a.gen_base = ctx->gen_base; a.flags = q + 2; a.probes = probes;
     a.states8 = n_states <= 256 ? 1 : 0;
-    a.handover_min = a.defer && !(lflags & JH_LIN_NO_HANDOVER) ? HANDOVER_MIN : 0;
+    // (the default, HANDOVER_MIN, only once resume is known to be on: below)
+    a.handover_min = 0;
     if (a.defer && !(lflags & JH_LIN_NO_HANDOVER) && opts && opts->handover_min)
         a.handover_min = std::max(0, opts->handover_min);
     if (const char *e = tune_env("JH_HANDOVER_MIN")) a.handover_min = a.defer ? std::max(0, atoi(e)) : 0;
@@ -6158,6 +6162,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         a.rs_used = (unsigned long long *)(q + Q_RS_USED);
         HIP_TRY(hipMemsetAsync(a.rs_off, 0xFF, (size_t)K * sizeof(int64_t), st));
         a.rs_mode = 1;
+        // a handed-over search continues where it stopped: the hand-over is free
+        if (!(lflags & JH_LIN_NO_HANDOVER) && !(opts && opts->handover_min) && !tune_env("JH_HANDOVER_MIN"))
+            a.handover_min = HANDOVER_MIN;
     }
     int32_t qh[Q_WORDS];
     int n_defer = 0, n_def_l = 0, n_def_w = 0, n_x = 0;

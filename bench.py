@@ -414,7 +414,7 @@ def main():
                        "phases": phase_table(sums), "opts": args.tune or None},
             "shard": shard_info,
             "pool": ({"mode": "two-stage (shard.two_stage_resident): phase 1 per rank, deferred keys' rows "
-                              "all-gathered over RCCL, dealt round-robin least phase-1 progress first, one "
+                              "all-gathered over RCCL, dealt round-robin most estimated phase-1 work first, one "
                               "stage-2 call per rank", "rank0_last_step": pool_stats[-1]}
                      if use_pool and pool_stats else None),
             "value_kind": "history resident in HBM, verdicts left in HBM (kernel pipeline only); "

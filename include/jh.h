@@ -95,7 +95,9 @@ extern "C" {
 #define JH_CAUSE_OVERFLOW     7  /* long overflow (Clojure + throws)          */
 #define JH_CAUSE_STATES       8  /* more than 65532 distinct values in one key */
 #define JH_CAUSE_DEFERRED     9  /* JH_LIN_PHASE1_ONLY: past the quick budget, not searched further;
-                                    explored = the quick search's progress (deepest layer / layers x 10^6) */
+                                    explored = the key's rank for the heavy-key pass, heaviest first:
+                                    2^31 - 1 - its estimated inserts (the quick search's inserts over
+                                    its progress, deepest layer / layers; round 5) */
 
 #define JH_MAX_WINDOW 256
 

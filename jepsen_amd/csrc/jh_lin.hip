@@ -1398,7 +1398,8 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
 template <class M>
 __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, const char *tb, int key, int lane,
                         uint64_t *memo, Frame *stack, uint64_t *stage,
-                        long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes) {
+                        long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes,
+                        uint32_t &ins_real) {
     const OpC *ops = (const OpC *)tb;
     const Lay *lay = (const Lay *)(tb + tblc_ops_bytes(K));
     const uint32_t n_ok = (uint32_t)K.n_ok;
@@ -1812,6 +1813,7 @@ done:
         }
     }
     inserts = ins;
+    ins_real = ins_saved != 0xFFFFFFFFu ? ins_saved : ins;    // a handed-over search's own count
     tmax_out = tmax;
 #ifdef JH_DFS_STATS
     if (A.dbg && lane == 0) {
@@ -2325,7 +2327,8 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
             __hip_atomic_store(&A.seq_start[key], __builtin_amdgcn_s_memrealtime() | 1ULL, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         int verdict;
-        if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
+        uint32_t ins_real = 0;
+        if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes, ins_real);
         else if constexpr (WL) verdict = dfs_lean_w<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         if (A.dbg && lane == 0) { A.dbg[16 * wv + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * wv + 3] += 1; }
@@ -2339,10 +2342,17 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
             if (lane == 0) {
                 const int d = atomicAdd(A.defer_count, 1);
                 if (A.defer_list) A.defer_list[d] = key;
-                // progress of the quick search (deepest layer / layers): the
-                // heavy-key pass starts with the least advanced keys
-                const uint64_t pk = ((uint64_t)((uint64_t)tmax * 1000000u / (uint64_t)max(1, K.n_ok)) << 32) |
-                                    (uint32_t)key;
+                // the heavy-key pass starts with the keys of most estimated work:
+                // the quick search's inserts over its progress (deepest layer /
+                // layers). Round 5: with the hand-over most deferred keys are
+                // short searches handed over at 1 024 inserts; ordered by progress
+                // alone (rounds 3-4) they went first and the genuinely heavy keys
+                // waited ~12 ms for a sequential wave (profiles/r05/timeline/).
+                // Sort key: 2^31 - 1 - estimate, ascending (the pool's rank too)
+                const uint64_t prog = max<uint64_t>(1, (uint64_t)tmax * 1000000u / (uint64_t)max(1, K.n_ok));
+                const uint64_t real = LEAN ? (uint64_t)ins_real : (uint64_t)inserts;
+                const uint64_t est = min<uint64_t>(0x7FFFFFFFull, real * 1000000ull / prog);
+                const uint64_t pk = ((0x7FFFFFFFull - est) << 32) | (uint32_t)key;
                 if (A.defer64) A.defer64[d] = pk;
                 if (A.defer_kind) {
                     const int dk = atomicAdd(A.defer_kind_count, 1);
@@ -2444,7 +2454,7 @@ __global__ void __launch_bounds__(64) k_lin_seq_lw(DfsPair P) {
     else lin_dfs_waves<MemoWL, false, true, STREAM>(P.w);
 }
 
-// Deferred keys, least advanced first (phase 1's progress, ties by key: the
+// Deferred keys, heaviest estimate first (phase 1's progress, ties by key: the
 // likely longest searches start first), then the key ids alone: one workgroup
 // per list, a bitonic sort of (progress << 32 | key) in LDS. Lists longer than
 // SORT_SMALL are sorted by hipcub on the host side of the call.
@@ -5895,7 +5905,7 @@ static inline int64_t q64(const int32_t *qh, int i) {
 
 // stage 1 of a two-stage check: each deferred key comes back with its quick
 // search's progress (deepest layer / layers, in millionths) as `explored`,
-// the order the stage-2 pool takes them in (least advanced first: the likely
+// the order the stage-2 pool takes them in (heaviest estimate first: the likely
 // longest searches start first, as k_sort_defer orders a device's own pass)
 __global__ void k_mark_deferred(const uint64_t *__restrict__ d64, int n, jh_key_verdict *out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -6682,7 +6692,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         n_x = cfgreq ? 0 : qh[19];
         if (n_def_l + n_def_w != n_defer) throw_jh(JH_EDEVICE, "deferred-key lists disagree");
         if (n_defer > 0 && !linear_mode && !skip_p1) {
-            // heavy keys, least advanced first (the likely longest searches start
+            // heavy keys, heaviest estimate first (the likely longest searches start
             // first), sorted on the device: no host round trip between the phases
             // (stage 1 of a two-stage check reads the list too: k_mark_deferred)
             SortLists sl{};

@@ -315,7 +315,7 @@ int multi_check_cas_independent(jh_ctx *g, const jh_history *h, const jh_lin_opt
         for (int64_t k = 0; k < K; ++k)
             if (out[k].valid == JH_UNKNOWN && out[k].cause == JH_CAUSE_DEFERRED) pool.push_back(k);
     if (!pool.empty()) {
-        // least advanced first by phase 1's progress (stage 1 returns it as
+        // heaviest estimate first by phase 1's progress (stage 1 returns it as
         // `explored` of a deferred key): the window-sum cost ranks the heavy
         // keys no better than chance (Spearman 0.04 on C3)
         std::stable_sort(pool.begin(), pool.end(), [&](int64_t a, int64_t b) { return out[a].explored < out[b].explored; });

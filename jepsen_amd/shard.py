@@ -109,7 +109,7 @@ def check_cas_independent_two_stage(cols, rank, world, check_fn, device=None, in
          budget, stage=1) -- libjh's JH_LIN_PHASE1_ONLY: keys past the quick
          budget come back :unknown with cause "deferred";
       2. every rank's deferred keys are gathered (all_gather_object) into one
-         pool, least phase-1 progress first, and the ranks pull batches from it
+         pool, most estimated phase-1 work first, and the ranks pull batches from it
          through an atomic counter in the rendezvous store (guided
          self-scheduling: a batch is the remainder over twice the world size),
          checking each batch's keys from the global history with
@@ -131,7 +131,7 @@ def check_cas_independent_two_stage(cols, rank, world, check_fn, device=None, in
     deferred = (v1["valid"] == A.UNKNOWN) & (v1["cause"] == A.CAUSE_DEFERRED)
     # (key, phase-1 progress) of every rank's deferred keys: stage 1 returns a
     # deferred key's quick-search progress as `explored`; the pool takes the
-    # least advanced first (the window-sum cost cannot tell which keys are
+    # heaviest estimate first (the window-sum cost cannot tell which keys are
     # heavy: Spearman 0.04 against WGL's insert count)
     mine_def = list(zip(mine[deferred].tolist(), v1["explored"][deferred].tolist()))
     lists = [None] * world
@@ -229,7 +229,7 @@ def two_stage_resident(rank, world, dcols, key_rows, stage1, stage2, device=None
       2. every rank's deferred keys (key, progress, rows) are exchanged --
          the metadata and the key's rows (7 int64 columns, gathered from the
          resident columns on the device) with all_gather (RCCL over xGMI);
-      3. the pool is ordered least phase-1 progress first (the likely longest
+      3. the pool is ordered most estimated phase-1 work first (the likely longest
          searches first, as k_sort_defer orders one device's pass) and dealt
          round-robin, so each rank gets an equal share of every heaviness;
       4. each rank checks its share in ONE stage2(cols) call

@@ -2352,7 +2352,13 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
                 const uint64_t prog = max<uint64_t>(1, (uint64_t)tmax * 1000000u / (uint64_t)max(1, K.n_ok));
                 const uint64_t real = LEAN ? (uint64_t)ins_real : (uint64_t)inserts;
                 const uint64_t est = min<uint64_t>(0x7FFFFFFFull, real * 1000000ull / prog);
+#ifdef JH_ORDER_PROGRESS
+                // rounds 3-4: least phase-1 progress first (A/B builds)
+                const uint64_t pk = ((prog < 0x7FFFFFFFull ? prog : 0x7FFFFFFFull) << 32) | (uint32_t)key;
+                (void)est;
+#else
                 const uint64_t pk = ((0x7FFFFFFFull - est) << 32) | (uint32_t)key;
+#endif
                 if (A.defer64) A.defer64[d] = pk;
                 if (A.defer_kind) {
                     const int dk = atomicAdd(A.defer_kind_count, 1);

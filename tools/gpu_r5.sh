@@ -36,17 +36,19 @@ pmc)
   cd /tmp && export TMPDIR=/tmp
   timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $R/$O/$N -o $N -- "$@" > $R/$O/$N.log 2>&1 ;;
 evidence)
-  # the rest of the round's evidence at HEAD: C3 ranks 1-7, C4, C5, the C2
-  # lines under a kernel trace, the one-rank RCCL path, the dominant kernel's
-  # FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py on the CPU side)
+  # the rest of the round's evidence at HEAD, part 1: C3 ranks 1-7, the
+  # one-rank RCCL path, the C2 lines under a kernel trace
   for rk in 1 2 3 4 5 6 7; do
     timeout -k 10 120 python -u bench.py --no-cpu --e2e 0 --no-parity --steps 5 --warmup 1 --seed-rank $rk > $O/c3r${rk}.json 2> $O/c3r${rk}.err || exit 1
   done
-  timeout -k 10 400 python -u bench.py --workload c4 --steps 3 --warmup 1 > $O/bench_c4.json 2> $O/bench_c4.err || exit 1
-  timeout -k 10 400 python -u bench.py --workload c5 --steps 1 --warmup 1 > $O/bench_c5.json 2> $O/bench_c5.err || exit 1
   JH_BENCH_DIST1=1 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 > $O/dist1.json 2> $O/dist1.err || exit 1
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/c2prof -o c2 -- python3 $R/tools/bench_c2.py --steps 5 --warmup 1 > $R/$O/bench_c2.log 2>&1 || exit 1
-  cd $R && bash tools/gpu_pmc.sh c3 'k_lin_seq_lw' $O/pmc_c3 0 && bash tools/gpu_pmc.sh c3 'k_lin_dfs' $O/pmc_c3p1 0 ;;
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/c2prof -o c2 -- python3 $R/tools/bench_c2.py --steps 5 --warmup 1 > $R/$O/bench_c2.log 2>&1 ;;
+evidence2)
+  # part 2: C4, C5, and the C3 search kernels' FETCH_SIZE / WRITE_SIZE passes
+  # (tools/pmc_traffic.py on the CPU side)
+  timeout -k 10 400 python -u bench.py --workload c4 --steps 3 --warmup 1 > $O/bench_c4.json 2> $O/bench_c4.err || exit 1
+  timeout -k 10 400 python -u bench.py --workload c5 --steps 1 --warmup 1 > $O/bench_c5.json 2> $O/bench_c5.err || exit 1
+  bash tools/gpu_pmc.sh c3 'k_lin_seq_lw' $O/pmc_c3 0 && bash tools/gpu_pmc.sh c3 'k_lin_dfs' $O/pmc_c3p1 0 ;;
 *) echo "unknown part $PART"; exit 2 ;;
 esac

@@ -141,10 +141,12 @@ def parse():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--seed-rank", type=int, default=None,
                     help="generate the history rank R of a multi-GPU run would check (rehearsal on one GPU)")
-    ap.add_argument("--pool", type=int, default=1,
-                    help="N > 1: the two-stage pool (phase 1 per rank, deferred keys exchanged over RCCL "
-                         "and dealt by phase-1 progress, one stage-2 call per rank; shard.two_stage_resident); "
-                         "0: each rank checks its shard in one call")
+    ap.add_argument("--pool", type=int, default=0,
+                    help="1: the two-stage pool (phase 1 per rank, deferred keys exchanged over RCCL and "
+                         "dealt by estimated work, one stage-2 call per rank; shard.two_stage_resident); "
+                         "0 (default since round 5): each rank checks its shard in one call -- the schedule "
+                         "that continues deferred searches and hands long ones over, which the pool's "
+                         "stage 2 (keys restarted on another rank) cannot")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=INT",
                     help="a jh_lin_opts tuning field for A/B runs (e.g. handover_min=2048); "
                          "recorded in config.opts")

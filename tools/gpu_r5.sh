@@ -41,7 +41,8 @@ evidence)
   for rk in 1 2 3 4 5 6 7; do
     timeout -k 10 120 python -u bench.py --no-cpu --e2e 0 --no-parity --steps 5 --warmup 1 --seed-rank $rk > $O/c3r${rk}.json 2> $O/c3r${rk}.err || exit 1
   done
-  JH_BENCH_DIST1=1 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 > $O/dist1.json 2> $O/dist1.err || exit 1
+  JH_BENCH_DIST1=1 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 --pool 1 > $O/dist1.json 2> $O/dist1.err || exit 1
+  JH_BENCH_DIST1=1 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 > $O/dist1_pool0.json 2> $O/dist1_pool0.err || exit 1
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/c2prof -o c2 -- python3 $R/tools/bench_c2.py --steps 5 --warmup 1 > $R/$O/bench_c2.log 2>&1 ;;
 evidence2)

@@ -73,6 +73,18 @@ using MemoQ = MemoCfg<JH_MEMOQ_LG, JH_MEMOQ_BLOOM>;
 using MemoH = MemoCfg<12, JH_MEMOH_BLOOM>;   // heavy keys: 128 KB memo + 16 KB Bloom = 152 KB -> 1 wave/CU
                                               // (16 KB Bloom vs 8 KB: -4..7% on the heaviest C3 keys)
 using MemoM = MemoCfg<10, 15>;   // very heavy keys: 32 KB memo + 4 KB Bloom = 37 KB -> 4 waves/CU
+// phase 2's LEAN role (k_lin_seq_lw) when phase 3 takes the keys past its
+// budget: JH_P2_PER_CU waves per CU with this memo and tables for the phase-2
+// budget only (round 5; the deferred keys are mostly short resumed searches,
+// latency-bound, so more waves per CU drain the queue faster)
+#ifndef JH_P2_LG
+#define JH_P2_LG 10
+#define JH_P2_BLOOM 15
+#endif
+#ifndef JH_P2_PER_CU
+#define JH_P2_PER_CU 4
+#endif
+using MemoP2 = MemoCfg<JH_P2_LG, JH_P2_BLOOM>;
 constexpr int STATE_BITS = 20, T_BITS = 20, GEN_BITS = 24;
 constexpr uint32_t STATE_MASK = (1u << STATE_BITS) - 1, T_MASK = (1u << T_BITS) - 1;
 
@@ -366,6 +378,13 @@ struct DfsArgs {
     uint64_t rs_cap;
     int64_t *rs_off;
     int32_t rs_mode;
+    // phase 1 with resume: per wave, the HBM-table slot of every configuration
+    // the search writes there (hlog_cap each), so a save gathers the key's
+    // entries instead of scanning the wave's whole table
+    uint32_t *hlog;
+    uint32_t hlog_cap;
+    // JH_DEFER_TIMES (tuning builds): per deferred key {inserts, tmax | n_ok << 32}
+    unsigned long long *defer_info;
 };
 constexpr int TL_W = 6;         // timeline words per key: BFS, sequential, helper (start, end)
 #ifdef JH_TUNING
@@ -876,8 +895,8 @@ __device__ __forceinline__ void bloom_set(uint32_t *bloom, uint64_t h) {
 // entries took ~2.5 dependent round trips per miss.
 constexpr uint32_t HB = 4;
 
-__device__ __forceinline__ void hbm_insert(uint64_t *memo, uint32_t cap_mask, uint32_t gen,
-                                           uint32_t ct, uint32_t cs, uint64_t cm) {
+__device__ __forceinline__ uint32_t hbm_insert(uint64_t *memo, uint32_t cap_mask, uint32_t gen,
+                                               uint32_t ct, uint32_t cs, uint64_t cm) {
     uint32_t b = (uint32_t)memo_hash(ct, cs, cm) & cap_mask & ~(HB - 1);
     const uint64_t w1 = ((uint64_t)gen << 40) | ((uint64_t)ct << 20) | cs;
     for (;;) {
@@ -902,7 +921,7 @@ __device__ __forceinline__ void hbm_insert(uint64_t *memo, uint32_t cap_mask, ui
                                                  __HIP_MEMORY_SCOPE_WORKGROUP)) {
             __hip_atomic_store(&memo[2 * (size_t)(b + j0)], cm, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
-            return;
+            return b + (uint32_t)j0;
         }
     }
 }
@@ -958,12 +977,16 @@ __device__ __forceinline__ uint32_t lk_bl(uint32_t h) { return h ^ (h >> 15); }
 // is too wide: HBM for everything below it from now on. Entries are staged
 // through global scratch and the LDS table is rebuilt; an entry that finds
 // both of its buckets full goes to HBM too and theta rises above its layer.
-// Every entry written to HBM enters the Bloom filter. Returns theta << 32 | kept.
+// Every entry written to HBM enters the Bloom filter, and its slot the
+// wave's log when there is one (hlog: nlog entries so far). Returns
+// theta << 32 | min(nlog', 0xFFFF) << 16 | kept.
 template <class M>
 __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint32_t *bcnt, uint32_t *bloom,
                                             uint64_t *memo, uint64_t *stage,
                                             uint32_t cap_mask, uint32_t gen, uint32_t t_cur,
-                                            uint32_t theta_old, int lane) {
+                                            uint32_t theta_old, int lane,
+                                            uint32_t *hlog = nullptr, uint32_t hlog_cap = 0, uint32_t nlog = 0) {
+    static_assert(M::SLOTS < 65536, "kept fits 16 bits");
     // histogram of entries by distance below t_cur (entries at or above it: bin 0)
     int bins = 0;                                  // lane b < 16 holds bin b
 #pragma unroll 1
@@ -1006,10 +1029,9 @@ __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint32_t *bcnt, uin
 #pragma unroll 1
     for (int r = 0; r < M::SLOTS / 64; r++) {
         const uint64_t x = stage[lane + 64 * r];
-        if (x == 0) continue;
         const uint32_t xt = lk_t(x);
-        bool to_hbm = xt < th2;
-        if (!to_hbm) {
+        bool to_hbm = x != 0 && xt < th2;
+        if (x != 0 && !to_hbm) {
             uint32_t h1, h2, b1, b2;
             lk_hash((uint32_t)x, (uint32_t)(x >> 32), h1, h2);
             lk_bkts<M>(h1, h2, b1, b2);
@@ -1024,13 +1046,20 @@ __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint32_t *bcnt, uin
             if (placed) kept++;
             else { to_hbm = true; th_min = max(th_min, xt + 1); }
         }
+        uint32_t slot = 0;
         if (to_hbm) {
             const uint32_t cs = lk_s(x);
             const uint64_t cm = lk_m(x);
-            hbm_insert(memo, cap_mask, gen, xt, cs, cm);
+            slot = hbm_insert(memo, cap_mask, gen, xt, cs, cm);
             uint32_t h1, h2;
             lk_hash((uint32_t)x, (uint32_t)(x >> 32), h1, h2);
             bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
+        }
+        if (hlog) {
+            const uint64_t hm = ballot(to_hbm);
+            const uint32_t at = nlog + (uint32_t)mbcnt(hm);
+            if (to_hbm && at < hlog_cap) hlog[at] = slot;
+            nlog += (uint32_t)__popcll(hm);
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -1044,7 +1073,7 @@ __device__ __noinline__ uint64_t memo_evict(uint64_t *lmemo, uint32_t *bcnt, uin
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     wave_sync();
-    return ((uint64_t)th2 << 32) | (uint32_t)kept;
+    return ((uint64_t)th2 << 32) | ((uint64_t)min(nlog, 0xFFFFu) << 16) | (uint32_t)kept;
 }
 
 
@@ -1399,7 +1428,7 @@ template <class M>
 __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, const char *tb, int key, int lane,
                         uint64_t *memo, Frame *stack, uint64_t *stage,
                         long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes,
-                        uint32_t &ins_real) {
+                        uint32_t &ins_real, uint32_t *hlog) {
     const OpC *ops = (const OpC *)tb;
     const Lay *lay = (const Lay *)(tb + tblc_ops_bytes(K));
     const uint32_t n_ok = (uint32_t)K.n_ok;
@@ -1458,6 +1487,7 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
     load_up(P);
     wave_sync();
     uint32_t ins_saved = 0xFFFFFFFFu;     // a handed-over search's real insert count
+    uint32_t nlog = 0;                    // hlog entries (saturating at 0xFFFF)
     // move the window forward from layer t to layer nt (a lift, or a resume)
     auto advance = [&](uint32_t nt) {
         for (uint32_t u = t; u < nt; u++) {
@@ -1641,18 +1671,22 @@ insert:
                 }
                 if (++lcount >= M::EVICT) {
                     DFS_STAT(n_evict++);
-                    const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane);
-                    DFS_STAT(n_hbm += (uint32_t)lcount - (uint32_t)er);
-                    lcount = rfl((int)(uint32_t)er);
+                    const uint64_t er = memo_evict<M>(lmemo, bcnt, bloom, memo, stage, cap_mask, gen, nt, theta, lane,
+                                                      hlog, A.hlog_cap, nlog);
+                    DFS_STAT(n_hbm += (uint32_t)lcount - ((uint32_t)er & 0xFFFF));
+                    lcount = rfl((int)((uint32_t)er & 0xFFFF));
+                    nlog = rflu(((uint32_t)er >> 16) & 0xFFFF);
                     theta = rflu((uint32_t)(er >> 32));
                 }
             } else {
                 // both buckets full: HBM, and theta rises above the layer
                 const uint64_t nmask = to_r ? nm_r : (mask | (1ULL << i));
                 if (lane == i) {
-                    hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
+                    const uint32_t sl = hbm_insert(memo, cap_mask, gen, nt, ns, nmask);
                     bloom_set2<M>(bloom, lk_bl(h1), lk_bl(h2));
+                    if (hlog && nlog < A.hlog_cap) hlog[nlog] = sl;
                 }
+                nlog = min(nlog + 1, 0xFFFFu);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 theta = max(theta, nt + 1);
@@ -1788,6 +1822,25 @@ done:
                 n += (uint32_t)__popcll(bm);
             }
             const ulonglong2 *tab = (const ulonglong2 *)memo;
+            if (hlog && nlog <= A.hlog_cap) {
+                // the logged slots: this key's entries only (8 gathers in flight per lane)
+                for (uint32_t base = 0; base < nlog; base += 64 * 8) {
+                    ulonglong2 e[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const uint32_t j = base + 64 * q + (uint32_t)lane;
+                        e[q] = j < nlog ? tab[hlog[j]] : make_ulonglong2(0ULL, 0ULL);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const bool mine = base + 64 * q + (uint32_t)lane < nlog && (uint32_t)(e[q].y >> 40) == gen;
+                        const uint64_t bm = ballot(mine);
+                        const uint32_t at = n + (uint32_t)mbcnt(bm);
+                        if (mine && at < nmem) ent[at] = make_ulonglong2(e[q].x, e[q].y & ((1ULL << 40) - 1));
+                        n += (uint32_t)__popcll(bm);
+                    }
+                }
+            } else
             for (uint32_t base = 0; base < A.memo_cap; base += 64 * 16) {
                 ulonglong2 e[16];
 #pragma unroll
@@ -2328,7 +2381,8 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
                                __HIP_MEMORY_SCOPE_AGENT);
         int verdict;
         uint32_t ins_real = 0;
-        if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes, ins_real);
+        if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes, ins_real,
+                                                  A.rs_mode == 1 && A.hlog ? A.hlog + wv * A.hlog_cap : nullptr);
         else if constexpr (WL) verdict = dfs_lean_w<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         if (A.dbg && lane == 0) { A.dbg[16 * wv + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * wv + 3] += 1; }
@@ -2367,6 +2421,10 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
                 }
                 if (STREAM && A.s_all) __hip_atomic_store(&A.s_all[d], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (A.defer_time) A.defer_time[2 + key] = __builtin_amdgcn_s_memrealtime();
+                if (A.defer_info) {
+                    A.defer_info[2 * (size_t)key] = real;
+                    A.defer_info[2 * (size_t)key + 1] = (uint64_t)tmax | ((uint64_t)K.n_ok << 32);
+                }
                 if (A.seq_start)
                     __hip_atomic_store(&A.seq_start[key], SEQ_HANDED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -2453,10 +2511,10 @@ __global__ void __launch_bounds__(64) k_lin_seqw(DfsArgs A) { lin_dfs_waves<Memo
 // WIDE; both 37 KB of LDS): one stream for both, so the heavy-key pass needs
 // no more streams than the hardware has queues
 struct DfsPair { DfsArgs l, w; int32_t n_l; };
-constexpr int SEQLW_LDS = MemoM::LDS > SEQW_LDS ? MemoM::LDS : SEQW_LDS;
+constexpr int SEQLW_LDS = MemoP2::LDS > SEQW_LDS ? MemoP2::LDS : SEQW_LDS;
 template <bool STREAM>
 __global__ void __launch_bounds__(64) k_lin_seq_lw(DfsPair P) {
-    if ((int)blockIdx.x < P.n_l) lin_dfs_waves<MemoM, true, false, STREAM>(P.l);
+    if ((int)blockIdx.x < P.n_l) lin_dfs_waves<MemoP2, true, false, STREAM>(P.l);
     else lin_dfs_waves<MemoWL, false, true, STREAM>(P.w);
 }
 
@@ -3753,6 +3811,7 @@ struct BfsShared {
     int key, need, maxw, status, mode, gclear, ovf, term;
     unsigned npend, npend2, nfront, nnext, tmax, lcount, r;
     unsigned nnodes, nostore, dlen, clen, cnext, ok;
+    unsigned fbase;          // nnodes when the frontier being built started (its slot 0)
     unsigned long long count, ccount, plen;
     alignas(16) uint32_t win_vv[64];    // the current layer's window: v1 | v2 << 16
     uint32_t win_f[64];     // f, or 3 for no member
@@ -4602,7 +4661,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         }
         if (tid == 0) {
             if (t < A.lcap) A.lstart[t] = sh.nnodes;
-            sh.nfront = 0; sh.lcount = 0; sh.mode = 0; sh.ovf = 0; sh.r = rpos[t];
+            sh.fbase = sh.nnodes; sh.nfront = 0; sh.lcount = 0; sh.mode = 0; sh.ovf = 0; sh.r = rpos[t];
             // the sequential search settled this key first
             if (A.claim && __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                 sh.status |= 4;
@@ -4742,15 +4801,17 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                 tot += (uint32_t)__popcll(bq);
             }
             if (tot == 0) return;
-            unsigned nb0 = 0, fb0 = 0;
+            // one LDS atomic per wave (round 5): a new configuration's node id
+            // and its frontier slot differ by the round's base (the node list
+            // and the frontier grow together), and the reachable count is the
+            // node count
+            unsigned nb0 = 0;
             if (lane == 0) {
-                const unsigned long long c0 = atomicAdd(&sh.count, (unsigned long long)tot);
-                if ((long long)(c0 + tot) > A.reach_cap) atomicOr(&sh.status, 2);
                 nb0 = atomicAdd(&sh.nnodes, tot);
-                fb0 = atomicAdd(&sh.nnext, tot);
+                if ((long long)nb0 + tot > A.reach_cap) atomicOr(&sh.status, 2);
             }
             nb0 = readlane(nb0, 0);
-            fb0 = readlane(fb0, 0);
+            const unsigned fb0 = nb0 - sh.fbase;
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 if (!nw[q]) continue;
@@ -4816,15 +4877,13 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             const uint64_t nm = ballot(nw);
             if (!nm) continue;
             const uint32_t tot = (uint32_t)__popcll(nm);
-            unsigned nb0 = 0, fb0 = 0;
+            unsigned nb0 = 0;
             if (lane == 0) {
-                const unsigned long long c0 = atomicAdd(&sh.count, (unsigned long long)tot);
-                if ((long long)(c0 + tot) > A.reach_cap) atomicOr(&sh.status, 2);
                 nb0 = atomicAdd(&sh.nnodes, tot);
-                fb0 = atomicAdd(&sh.nfront, tot);
+                if ((long long)nb0 + tot > A.reach_cap) atomicOr(&sh.status, 2);
             }
             nb0 = readlane(nb0, 0);
-            fb0 = readlane(fb0, 0);
+            const unsigned fb0 = nb0 - sh.fbase;
             if (nw) {
                 const unsigned below = mbcnt(nm);
                 if (nb0 + below < A.ncap) A.nodes[nb0 + below] = bfs_pack(t, cs, cm);
@@ -4838,7 +4897,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         migrate();
         }
         { uint64_t *tp = pcur; pcur = pnxt; pnxt = tp; }
-        if (tid == 0) { sh.npend = sh.npend2; if (sh.nfront) sh.tmax = t; }
+        if (tid == 0) { sh.npend = sh.npend2; sh.nfront = sh.nnodes - sh.fbase; if (sh.nfront) sh.tmax = t; }
         __syncthreads();
         // ---- close layer t under same-layer lifts ---------------------------
         if (sh.status) break;
@@ -4850,7 +4909,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             const unsigned long long rt0 = __builtin_amdgcn_s_memtime();
             const int mode_at = sh.mode;
             if (tid == 0) {
-                sh.nnext = 0;
+                sh.fbase = sh.nnodes;
                 // the sequential search settled this key: stop at the next round
                 if (A.claim && __hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                     sh.status |= 4;
@@ -4878,6 +4937,8 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                 const int je = JH_BFS_ITEMS ? jb + 8 : w;
                 for (int j0 = jb; j0 < je; j0 += 8) {
                     uint64_t ck[8];       // same-layer children of members j0..j0+7: s2 << 32 | mask'
+                    uint64_t pe = 0;      // the cross-layer child (member r), appended per wave
+                    bool hp = false;
                     Win8 wn;
                     win8(sh, j0, wn);
 #pragma unroll
@@ -4901,11 +4962,20 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
                                 if (!((nm >> ru) & 1)) break;
                             }
                             if (u >= n_ok) { sh.term = 1; continue; }   // a terminal configuration
-                            const unsigned pos = atomicAdd(&sh.npend, 1u);
-                            if (pos < A.q_cap) pcur[pos] = bfs_pack(u, (uint32_t)s2, (uint32_t)nm);
-                            else atomicOr(&sh.status, 2);
+                            pe = bfs_pack(u, (uint32_t)s2, (uint32_t)nm);
+                            hp = true;
                         } else {
                             ck[q] = ((uint64_t)(uint32_t)s2 << 32) | (mask | (1u << j));
+                        }
+                    }
+                    if (const uint64_t pm = ballot(hp)) {
+                        unsigned pb = 0;
+                        if (lane == 0) pb = atomicAdd(&sh.npend, (unsigned)__popcll(pm));
+                        pb = readlane(pb, 0);
+                        if (hp) {
+                            const unsigned pos = pb + mbcnt(pm);
+                            if (pos < A.q_cap) pcur[pos] = pe;
+                            else atomicOr(&sh.status, 2);
                         }
                     }
                     BFS_PROF(if (A.dbg && tid == 0) { const unsigned long long q = __builtin_amdgcn_s_memtime(); atomicAdd(&g_bfs_prof[7], q - pq0); pq0 = q; })
@@ -4924,7 +4994,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
             }
             { uint64_t *tp = fcur; fcur = fnxt; fnxt = tp; }
             if (sh.mode == 0 && sh.lcount > LSET / 2 && !sh.status) migrate();
-            if (tid == 0) sh.nfront = sh.nnext;
+            if (tid == 0) sh.nfront = sh.nnodes - sh.fbase;
             if (A.dbg && tid == 0) {
                 // JH_DEBUG=2: rounds and cycles with the layer in the global set (mode 1)
                 unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
@@ -4936,6 +5006,7 @@ __device__ void bfs_key(const BfsArgs &A, BfsShared &sh, char *gscr, int tid, ui
         }
         if (sh.status) break;
     }
+    if (tid == 0) sh.count = sh.nnodes;                  // initial included, terminals not
     __syncthreads();
     if (A.dbg && tid == 0) {
         unsigned long long *d = A.dbg + 16 * (size_t)blockIdx.x;
@@ -6161,6 +6232,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         a.defer_time = ctx->ws<unsigned long long>(WS_DEFER_TIME, (size_t)K + 2);
         HIP_TRY(hipMemsetAsync(a.defer_time, 0, sizeof(unsigned long long) * (K + 2), st));
         HIP_TRY(hipMemsetAsync(a.defer_time, 0xFF, sizeof(unsigned long long), st));
+        a.defer_info = ctx->ws<unsigned long long>(WS_DEFER_INFO, 2 * (size_t)K);
+        HIP_TRY(hipMemsetAsync(a.defer_info, 0, sizeof(unsigned long long) * 2 * K, st));
     }
     const bool skip_p1 = (lflags & JH_LIN_SKIP_PHASE1) != 0 && !linear_mode;
     const bool p1_only = (lflags & JH_LIN_PHASE1_ONLY) != 0 && !linear_mode && !skip_p1;
@@ -6178,6 +6251,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         a.rs_used = (unsigned long long *)(q + Q_RS_USED);
         HIP_TRY(hipMemsetAsync(a.rs_off, 0xFF, (size_t)K * sizeof(int64_t), st));
         a.rs_mode = 1;
+        if (!tune_env("JH_RS_SCAN")) {
+            a.hlog_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(quick, 1024), 32768);
+            a.hlog = ctx->ws<uint32_t>(WS_RS_LOG, (size_t)waves1 * a.hlog_cap);
+        }
         // a handed-over search continues where it stopped: the hand-over is free
         if (!(lflags & JH_LIN_NO_HANDOVER) && !(opts && opts->handover_min) && !tune_env("JH_HANDOVER_MIN"))
             a.handover_min = HANDOVER_MIN;
@@ -6224,6 +6301,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     int32_t *defer3w = defer3 + (K + 1);
     int32_t *claim = nullptr;
     int waves_w = 0, waves2 = 0;
+    int waves3 = 0;                  // phase 3's LEAN waves (full tables; waves2 unless p2_small)
+    uint32_t cap2l = cap2;           // phase 2's LEAN tables (entries per wave)
+    bool p2_small_ok = JH_P2_PER_CU != 4 || JH_P2_LG != 10;   // (the streaming pass keeps round 4's sizing)
     bool split3 = false, split3w = false;
 
     // ---- the deferred WIDE keys (windows of 41-64 members or >= 256 states):
@@ -6440,17 +6520,37 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // (k_lin_seq3), p2_waves_per_cu = 1 for one wave per CU and the 128 KB
         // memo (k_lin_seq): measured C4 shard 268 -> 228 ms, C3 / ranks 3, 6 / C5 flat
         p2_m = !(opts && opts->p2_waves_per_cu == 1);
+        cap2l = cap2;
         if (nd_l > 0) {
-            int want2 = std::min(nd_l, std::max(1, (ctx->n_cu - wg2 - n_help) * (p2_m ? 4 : 1)));
+            const int cus2 = std::max(1, ctx->n_cu - wg2 - n_help);
+            int want2 = std::min(nd_l, cus2 * (p2_m ? 4 : 1));
             if (opts && opts->lean_waves > 0) want2 = std::min(want2, opts->lean_waves);
-            const uint64_t per2 = (uint64_t)cap2 * 16 + (uint64_t)stack_cap * sizeof(Frame) + scr_bytes_h;
+            const uint64_t fixed = (uint64_t)stack_cap * sizeof(Frame) + scr_bytes_h;
+            const uint64_t per2 = (uint64_t)cap2 * 16 + fixed;
             waves2 = fit_units(ctx, want2, per2, {WS_MEMO_DEEP, WS_STACK_DEEP, WS_SCRATCH_DEEP});
+            waves3 = waves2;
+            // more keys than waves: phase 2 stops at p2 inserts and phase 3
+            // takes the rest on full tables, so phase 2's LEAN role can run
+            // JH_P2_PER_CU waves per CU on tables for 2 x p2 entries
+            if (p2_m && p2_small_ok && !(opts && opts->lean_waves > 0) && budget > p2) {
+                uint32_t cs = 1u << 16;
+                while ((int64_t)cs < 2 * p2 && cs < cap2) cs <<= 1;
+                const int want_s = std::min(nd_l, cus2 * JH_P2_PER_CU);
+                const int ws = fit_units(ctx, want_s, (uint64_t)cs * 16 + fixed, {WS_MEMO_DEEP, WS_STACK_DEEP, WS_SCRATCH_DEEP});
+                if (ws < nd_l) {
+                    cap2l = cs;
+                    waves2 = ws;
+                }
+            }
         }
-        // generation-tagged: zeroed once when allocated (and on wrap), not per call
+        // generation-tagged: zeroed once when allocated (and on wrap), not per
+        // call; phases 2 and 3 share it at their own strides (their generation
+        // ranges differ, so one phase's entries are empty slots to the other's)
         uint64_t *memo2 = nullptr;
+        const size_t m2 = std::max((size_t)waves2 * cap2l, (size_t)waves3 * cap2);
         if (waves2 > 0) {
-            const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < (size_t)waves2 * cap2 * 16;
-            memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, (size_t)waves2 * cap2 * 2, /*zero=*/true);
+            const bool fresh2 = ctx->ws_fresh(WS_MEMO_DEEP) || ctx->bufs[WS_MEMO_DEEP].bytes < m2 * 16;
+            memo2 = ctx->ws<uint64_t>(WS_MEMO_DEEP, m2 * 2, /*zero=*/true);
             if (clear_memo && !fresh2) HIP_TRY(hipMemsetAsync(memo2, 0, ctx->bufs[WS_MEMO_DEEP].bytes, st));
         }
         wr = WgArgs{};
@@ -6469,8 +6569,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             if (lflags & JH_LIN_HELPERS_NOW) late_us = 0;
             wh.late_ticks = late_us * 100;     // s_memrealtime: 100 MHz
         }
-        Frame *stack2 = waves2 > 0 ? ctx->ws<Frame>(WS_STACK_DEEP, (size_t)waves2 * stack_cap) : nullptr;
-        char *scr2 = waves2 > 0 ? ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)waves2 * scr_bytes_h) : nullptr;
+        const int wmax = std::max(waves2, waves3);
+        Frame *stack2 = waves2 > 0 ? ctx->ws<Frame>(WS_STACK_DEEP, (size_t)wmax * stack_cap) : nullptr;
+        char *scr2 = waves2 > 0 ? ctx->ws<char>(WS_SCRATCH_DEEP, (size_t)wmax * scr_bytes_h) : nullptr;
         // a wave per key: one pass at the full budget; fewer waves than keys:
         // phase 2 stops at p2 inserts and phase 3 restarts those keys
         split3 = waves2 < nd_l && budget > p2;
@@ -6480,9 +6581,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         b.list = defer_l; b.n_list = nd_l; b.n_list_dev = nullptr; b.queue = q + 6; b.defer = split3 ? 1 : 0;
         b.defer_list = defer3; b.defer_count = q + 16;
         b.defer64 = nullptr; b.defer_kind = nullptr; b.defer_kind_count = nullptr;
-        b.memo = memo2; b.memo_cap = cap2; b.stack = stack2; b.scratch = scr2; b.scratch_bytes = scr_bytes_h;
+        b.memo = memo2; b.memo_cap = cap2l; b.stack = stack2; b.scratch = scr2; b.scratch_bytes = scr_bytes_h;
         b.budget = split3 ? p2 : budget;
-        b.budget_full = split3 ? budget : 0;
+        // (past p2 a search goes on while the queue is empty, on full tables only)
+        b.budget_full = split3 && cap2l == cap2 ? budget : 0;
         b.gen_base = ctx->gen_base + (uint32_t)K + 1;
         b.dbg = dbg ? dbg + 16 * 256 : nullptr; b.claim = claim;
         b.probes = (unsigned long long *)(q + 8);
@@ -6523,6 +6625,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         const bool any = n_defer > 0;
         if (any) {
             HIP_TRY(hipMemsetAsync(defer, 0xFF, 3 * sizeof(int32_t) * (size_t)(K + 1), st));   // live lists: -1 = not yet
+            p2_small_ok = false;
             prep_race(n_defer, n_def_l);
             prep_wide();
             c.list = defer; c.n_list = 0; c.queue = q + Q_BFS_QUEUE;
@@ -6925,7 +7028,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 DfsPair pr;
                 pr.l = b; pr.w = bw; pr.n_l = waves2;
                 pr.w.wave_off = waves2;
-                k_lin_seq_lw<false><<<waves2 + waves_w, 64, SEQLW_LDS, ctx->aux>>>(pr);
+                // (LEAN waves only: their own LDS size, so more of them per CU)
+                k_lin_seq_lw<false><<<waves2 + waves_w, 64, waves_w > 0 ? SEQLW_LDS : MemoP2::LDS, ctx->aux>>>(pr);
                 wide_done = true;
             } else if (waves2) k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
             HIP_TRY(hipGetLastError());
@@ -6950,17 +7054,18 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 c3.defer_list = nullptr; c3.defer_count = nullptr;
                 c3.seq_start = nullptr; c3.exit_count = nullptr;
                 c3.budget = budget; c3.budget_full = 0;
+                c3.memo_cap = cap2;
                 c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
                 c3.dbg = nullptr;
                 c3.probes = (unsigned long long *)(q + Q_PROBES_P3);
                 const int few = std::max(1, ctx->n_cu - wg2);
                 DfsArgs c3a = c3;
                 c3a.queue = q + 17; c3a.n_max = few;
-                k_lin_seq<true><<<std::min(waves2, few), 64, MemoH::LDS, ctx->aux>>>(c3a);
+                k_lin_seq<true><<<std::min(waves3, few), 64, MemoH::LDS, ctx->aux>>>(c3a);
                 HIP_TRY(hipGetLastError());
                 DfsArgs c3b = c3;
                 c3b.queue = q + 18; c3b.n_min = few + 1;
-                k_lin_seq3<true><<<waves2, 64, MemoM::LDS, ctx->aux>>>(c3b);
+                k_lin_seq3<true><<<waves3, 64, MemoM::LDS, ctx->aux>>>(c3b);
                 HIP_TRY(hipGetLastError());
             }
             HIP_TRY(hipEventRecord(ctx->ev[7], ctx->aux));
@@ -7096,6 +7201,22 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                         us(tl[TL_W * k + 5]));
             }
         }
+        if (const char *csv = tune_env("JH_TL_CSV")) {
+            // every deferred key: its quick search, its engines' times, its verdict
+            std::vector<unsigned long long> di(2 * (size_t)K);
+            HIP_TRY(hipMemcpy(di.data(), a.defer_info, 8 * di.size(), hipMemcpyDeviceToHost));
+            if (FILE *fo = fopen(csv, "a")) {
+                fprintf(fo, "key,explored,valid,deferred_us,p1_inserts,p1_tmax,n_ok,bfs0,bfs1,seq0,seq1,help0,help1\n");
+                for (int d = 0; d < n_defer; d++) {
+                    const int k = dk[d];
+                    fprintf(fo, "%d,%lld,%d,%.1f,%llu,%llu,%llu", k, (long long)vv[k].explored, vv[k].valid,
+                            (dt[2 + k] - dt[0]) / 100.0, di[2 * k], di[2 * k + 1] & 0xFFFFFFFFull, di[2 * k + 1] >> 32);
+                    for (int w = 0; w < TL_W; w++) fprintf(fo, ",%.1f", tl.empty() ? -1.0 : us(tl[TL_W * k + w]));
+                    fprintf(fo, "\n");
+                }
+                fclose(fo);
+            }
+        }
         int q5[5] = {0, 0, 0, 0, 0};
         for (auto &e2 : ev) q5[std::min(4, (int)(e2.first / (std::max(1.0, (dt[1] - dt[0]) / 100.0) / 5)))]++;
         fprintf(stderr, "[jh-defer] deferrals by fifth of phase 1: %d %d %d %d %d\n", q5[0], q5[1], q5[2], q5[3], q5[4]);
@@ -7222,7 +7343,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         sum->lean_entries = q64(qh, Q_ENT_LEAN);
         sum->wide_entries = q64(qh, Q_ENT_WIDE);
         sum->xw_entries = q64(qh, Q_ENT_XW);
-        sum->waves[0] = waves2; sum->waves[1] = waves_w; sum->waves[2] = split3 ? waves2 : 0; sum->waves[3] = waves_x;
+        sum->waves[0] = waves2; sum->waves[1] = waves_w; sum->waves[2] = split3 ? waves3 : 0; sum->waves[3] = waves_x;
         if (dbgenv) {
             float a = 0, b = 0, c = 0;
             HIP_TRY(hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]));

@@ -51,5 +51,37 @@ evidence2)
   timeout -k 10 400 python -u bench.py --workload c4 --steps 3 --warmup 1 > $O/bench_c4.json 2> $O/bench_c4.err || exit 1
   timeout -k 10 400 python -u bench.py --workload c5 --steps 1 --warmup 1 > $O/bench_c5.json 2> $O/bench_c5.err || exit 1
   bash tools/gpu_pmc.sh c3 'k_lin_seq_lw' $O/pmc_c3 0 && bash tools/gpu_pmc.sh c3 'k_lin_dfs' $O/pmc_c3p1 0 ;;
+ab)
+  # alternating C3 runs of the in-tree build and of variants/libjh_<v>.so
+  #   ab "<ranks>" <reps> <v>...
+  RK=$1; REPS=$2; shift 2
+  B="python -u bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 --no-parity"
+  for i in $(seq 1 $REPS); do
+    for rk in $RK; do
+      timeout -k 10 120 $B --seed-rank $rk > $O/base_r${rk}_$i.json 2> $O/base_r${rk}_$i.err || exit 1
+      for v in "$@"; do
+        JH_LIB=$R/jepsen_amd/variants/libjh_$v.so timeout -k 10 120 $B --seed-rank $rk > $O/${v}_r${rk}_$i.json 2> $O/${v}_r${rk}_$i.err || exit 1
+      done
+    done
+  done ;;
+c2ab)
+  # counter builds: each variant's counter parity tests, then alternating
+  # C2 lines of the in-tree build and the variants: c2ab <reps> <v>...
+  REPS=$1; shift
+  for v in "$@"; do
+    JH_LIB=$R/jepsen_amd/variants/libjh_$v.so timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_counter_set.py tests/test_gpu_configs.py -k "counter or c2" > $O/tests_$v.log 2>&1 || exit 1
+  done
+  for i in $(seq 1 $REPS); do
+    timeout -k 10 120 python -u tools/bench_c2.py --steps 10 --warmup 2 --no-cpu > $O/base_$i.log 2>&1 || exit 1
+    for v in "$@"; do
+      JH_LIB=$R/jepsen_amd/variants/libjh_$v.so timeout -k 10 120 python -u tools/bench_c2.py --steps 10 --warmup 2 --no-cpu > $O/${v}_$i.log 2>&1 || exit 1
+    done
+  done ;;
+timeline)
+  # per-key timeline of a -DJH_TUNING variant: timeline <v> "<ranks>"
+  V=$1; RK=$2
+  for rk in $RK; do
+    JH_LIB=$R/jepsen_amd/variants/libjh_$V.so JH_DEBUG=1 JH_DEFER_TIMES=1 timeout -k 10 120 python -u bench.py --steps 1 --warmup 1 --no-cpu --e2e 0 --no-parity --seed-rank $rk > $O/tl_${V}_r$rk.log 2>&1 || exit 1
+  done ;;
 *) echo "unknown part $PART"; exit 2 ;;
 esac

@@ -432,11 +432,12 @@ def main():
                                                f"that run's phase took {tr['pmc_phase_ms']:.1f} ms, "
                                                f"{tr['pmc_probes']:.0f} memo probes)") if tr else None,
                           "traffic_over_alg_pmc_run": tr.get("traffic_over_alg") if tr else None,
-                          # the non-entry part of that traffic per memo probe, times this run's probes
-                          "traffic_scaled_to_timed_probes": (
-                              BYTES_PER_ENTRY * phases[dom]["entries"] +
-                              max(0.0, tr["traffic_bytes"] - BYTES_PER_ENTRY * tr["pmc_entries"]) /
-                              max(1.0, tr["pmc_probes"]) * phases[dom]["probes"]) if tr else None,
+                          # that run's traffic per algorithmic byte, times this run's algorithmic
+                          # bytes (its memo writes follow the inserts, not the HBM probes: a
+                          # per-probe scaling overstated it ~13x in round 5's first lines)
+                          "traffic_scaled_to_timed_alg": (
+                              tr["traffic_bytes"] / max(1.0, tr["alg_bytes_same_run"]) * phases[dom]["alg_bytes"])
+                          if tr and tr.get("alg_bytes_same_run") else None,
                           "traffic_source": traffic_src,
                           "kernel_ms": phases[dom]["ms"], "alg_bytes": phases[dom]["alg_bytes"],
                           "note": "latency-bound tree search: one wave per key, LDS memo; bytes are 56 B per "

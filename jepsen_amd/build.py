@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build")
-HIP_SOURCES = ["jh_lin.hip", "jh_counter.hip", "jh_set.hip", "jh_setfull.hip", "jh_queue.hip", "jh_api.hip", "jh_multi.hip"]
+HIP_SOURCES = ["jh_lin.hip", "jh_counter.hip", "jh_set.hip", "jh_setfull.hip", "jh_queue.hip", "jh_api.hip", "jh_multi.hip", "jh_ingest.hip"]
 HOST_SOURCES = ["jh_io.cpp"]
 HEADERS = [os.path.join(CSRC, "jh_internal.h"), os.path.join(ROOT, "include", "jh.h")]
 HOST_HEADERS = [os.path.join(ROOT, "include", "jh.h"), os.path.join(ROOT, "include", "jh_io.h")]

@@ -42,6 +42,21 @@ jh_history stage_history(jh_ctx *ctx, const jh_history *h, bool need_key, bool n
     if (h->on_device) return *h;
     jh_history d = *h;
     hipStream_t st = ctx->stream;
+    if (h->n > 0) {
+        // large histories: packed chunks, packing overlapped with the DMA (jh_ingest.hip)
+        const int64_t *src[7] = {h->process, h->type, h->f, need_key ? h->key : nullptr, h->value, h->value2, nullptr};
+        int64_t *dst[7] = {};
+        const int slot[7] = {WS_COL_PROCESS, WS_COL_TYPE, WS_COL_F, WS_COL_KEY, WS_COL_VALUE, WS_COL_VALUE2, WS_COL_AUX};
+        for (int c = 0; c < 6; c++)
+            if (src[c]) dst[c] = ctx->ws<int64_t>(slot[c], h->n);
+        if (ingest_columns(ctx, src, dst, h->n, st)) {
+            d.process = dst[0]; d.type = dst[1]; d.f = dst[2]; d.key = dst[3];
+            d.value = dst[4]; d.value2 = dst[5];
+            d.aux = need_aux ? stage_col(ctx, WS_COL_AUX, h->aux, h->n_aux, st) : nullptr;
+            d.on_device = 1;
+            return d;
+        }
+    }
     d.process = stage_col(ctx, WS_COL_PROCESS, h->process, h->n, st);
     d.type = stage_col(ctx, WS_COL_TYPE, h->type, h->n, st);
     d.f = stage_col(ctx, WS_COL_F, h->f, h->n, st);
@@ -111,6 +126,7 @@ void jh_close(jh_ctx *ctx) {
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         for (auto &b : ctx->bufs) if (b.p) (void)hipFree(b.p);
         if (ctx->hflag) (void)hipHostFree(ctx->hflag);
+        if (ctx->ingest) ingest_free(ctx->ingest);
         for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         if (ctx->aux) (void)hipStreamDestroy(ctx->aux);

@@ -68,6 +68,7 @@ struct jh_ctx {
     void *pinned = nullptr;       // small pinned staging for scalars
     size_t pinned_bytes = 0;
     std::vector<jh_ctx *> members;  // jh_open_multi: one context per device (jh_multi.hip); empty otherwise
+    struct Ingest *ingest = nullptr;  // host-buffer staging: packing threads, pinned chunks (jh_ingest.hip)
 
     template <class T>
     T *ws(int slot, size_t count, bool zero = false) {
@@ -148,6 +149,9 @@ inline int grid_for(int64_t n, int block, int cap = 65536) {
 // Copies a host jh_history to device workspace columns (or passes device
 // pointers through). Returns a device-pointer view.
 jh_history stage_history(jh_ctx *ctx, const jh_history *h, bool need_key, bool need_aux);
+// jh_ingest.hip: packed, pipelined staging of large host histories (false: too small)
+bool ingest_columns(jh_ctx *ctx, const int64_t *const src[7], int64_t *const dst[7], int64_t n, hipStream_t st);
+void ingest_free(struct Ingest *g);
 
 // linearizability (jh_lin.hip). cfg: a jh_lin_configs request (the frontier
 // configurations of the listed keys, device buffers; null for a check)

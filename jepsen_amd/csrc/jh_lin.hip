@@ -895,6 +895,11 @@ __device__ __forceinline__ void bloom_set(uint32_t *bloom, uint64_t h) {
 // entries took ~2.5 dependent round trips per miss.
 constexpr uint32_t HB = 4;
 
+#ifdef JH_DUP_WRITE
+// tuning builds (round 5, the cost of phase 1's memo writes): every HBM memo
+// insert is written a second time, 16 B scattered into a 1 GB mirror no one reads
+__device__ ulonglong2 *g_dup_base;
+#endif
 __device__ __forceinline__ uint32_t hbm_insert(uint64_t *memo, uint32_t cap_mask, uint32_t gen,
                                                uint32_t ct, uint32_t cs, uint64_t cm) {
     uint32_t b = (uint32_t)memo_hash(ct, cs, cm) & cap_mask & ~(HB - 1);
@@ -921,6 +926,10 @@ __device__ __forceinline__ uint32_t hbm_insert(uint64_t *memo, uint32_t cap_mask
                                                  __HIP_MEMORY_SCOPE_WORKGROUP)) {
             __hip_atomic_store(&memo[2 * (size_t)(b + j0)], cm, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef JH_DUP_WRITE
+            if (g_dup_base)
+                g_dup_base[((uintptr_t)&memo[2 * (size_t)(b + j0)] >> 4) & ((1u << 26) - 1)] = make_ulonglong2(cm, w1);
+#endif
             return b + (uint32_t)j0;
         }
     }
@@ -6251,6 +6260,12 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         a.rs_used = (unsigned long long *)(q + Q_RS_USED);
         HIP_TRY(hipMemsetAsync(a.rs_off, 0xFF, (size_t)K * sizeof(int64_t), st));
         a.rs_mode = 1;
+#ifdef JH_DUP_WRITE
+        {
+            ulonglong2 *mirror = ctx->ws<ulonglong2>(WS_DEFER_INFO + 1, (size_t)1 << 26);
+            HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_dup_base), &mirror, sizeof mirror));
+        }
+#endif
         if (!tune_env("JH_RS_SCAN")) {
             a.hlog_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(quick, 1024), 32768);
             a.hlog = ctx->ws<uint32_t>(WS_RS_LOG, (size_t)waves1 * a.hlog_cap);

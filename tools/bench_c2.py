@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=10_000_000,
                     help="entries of the same generator timed on the CPU oracle")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also time calls on host buffers (H2D of the columns included)")
     args = ap.parse_args()
     import torch
     from jepsen_amd import _native, synth
@@ -83,6 +85,10 @@ def main():
                    args.steps, args.warmup)
     n = int(cols.n)
     alg = 56.0 * n + 24.0 * r["n_reads"]
+    e2e = None
+    if args.e2e:
+        _, hs = timed(lambda: ctx.check_counter(cols, reads_cap=1 << 20, out=reads_buf.array), 2, 1)
+        e2e = {"ms_per_call": hs * 1e3, "entries_per_s": n / hs}
     cpu = None
     if not args.no_cpu:
         cs = synth.counter(n_ops=args.cpu_sample // 2, n_procs=10, read_every=101, p_fail=0.05,
@@ -98,7 +104,7 @@ def main():
                   "ms_per_step": sec * 1e3, "higher_is_better": True, "dtype": "int64",
                   "data": "synthetic (jepsen_amd/csrc/gen.cpp counter, seed 2)",
                   "config": {"workload": "C2 counter", "entries": n, "reads": r["n_reads"],
-                             "errors": r["n_errors"], "valid": r["valid"]},
+                             "errors": r["n_errors"], "valid": r["valid"], "e2e_host_buffers": e2e},
                   "roofline": {"bound": "hbm", "kernel": "whole jh_check_counter call",
                                "achieved": alg / sec / 1e9, "peak": PEAK_HBM_GBS,
                                "unit": "GB/s", "frac": alg / sec / 1e9 / PEAK_HBM_GBS,
@@ -119,6 +125,10 @@ def main():
     _, sec_runs = timed(lambda: ctx.check_set(d, runs_cap=1 << 25, on_device=True), 2, 1)
     n = int(cols.n)
     alg = 56.0 * n + 8.0 * d.n_aux + 16.0 * r["n_words"]
+    e2e = None
+    if args.e2e:
+        _, hs = timed(lambda: ctx.check_set_bitmaps(cols, words_cap=1 << 22, out=[b.array for b in bit_bufs]), 2, 1)
+        e2e = {"ms_per_call": hs * 1e3, "entries_per_s": n / hs}
     cpu = None
     if not args.no_cpu:
         cs = synth.set_history(n_adds=args.cpu_sample // 2, n_procs=10, p_fail=0.05, p_info=0.02,
@@ -137,7 +147,7 @@ def main():
                              "lost": r["lost_count"], "unexpected": r["unexpected_count"],
                              "valid": r["valid"], "n_runs": r["n_runs"], "bitmap_words": r["n_words"],
                              "output": "jh_check_set_bitmaps (4 result bitmaps)",
-                             "ms_per_call_runs_output": sec_runs * 1e3},
+                             "ms_per_call_runs_output": sec_runs * 1e3, "e2e_host_buffers": e2e},
                   "roofline": {"bound": "hbm", "kernel": "whole jh_check_set_bitmaps call",
                                "achieved": alg / sec / 1e9, "peak": PEAK_HBM_GBS,
                                "unit": "GB/s", "frac": alg / sec / 1e9 / PEAK_HBM_GBS,

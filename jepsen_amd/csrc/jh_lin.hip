@@ -73,16 +73,19 @@ using MemoQ = MemoCfg<JH_MEMOQ_LG, JH_MEMOQ_BLOOM>;
 using MemoH = MemoCfg<12, JH_MEMOH_BLOOM>;   // heavy keys: 128 KB memo + 16 KB Bloom = 152 KB -> 1 wave/CU
                                               // (16 KB Bloom vs 8 KB: -4..7% on the heaviest C3 keys)
 using MemoM = MemoCfg<10, 15>;   // very heavy keys: 32 KB memo + 4 KB Bloom = 37 KB -> 4 waves/CU
-// phase 2's LEAN role (k_lin_seq_lw) when phase 3 takes the keys past its
-// budget: JH_P2_PER_CU waves per CU with this memo and tables for the phase-2
-// budget only (round 5; the deferred keys are mostly short resumed searches,
-// latency-bound, so more waves per CU drain the queue faster)
+// phase 2's LEAN role (k_lin_seq_lw) when no WIDE keys share its grid: the
+// 32 KB memo with a 16 KB Bloom filter over its HBM-resident layers, three
+// waves per CU, tables for the phase-2 budget (phase 3 takes the keys past
+// it). Round 5, profiles/r05/ab_p2_bloom/: the heavy keys of the slow ranks
+// keep ~30 K configurations in HBM, where MemoM's 4 KB filter answers "maybe"
+// for most probes (each then an HBM round trip): C3 rank 4 53.4 -> 50.4 ms,
+// rank 7 43.7 -> 41.5 ms, ranks 0 / 3 and C4 flat
 #ifndef JH_P2_LG
 #define JH_P2_LG 10
-#define JH_P2_BLOOM 15
+#define JH_P2_BLOOM 17
 #endif
 #ifndef JH_P2_PER_CU
-#define JH_P2_PER_CU 4
+#define JH_P2_PER_CU 3
 #endif
 using MemoP2 = MemoCfg<JH_P2_LG, JH_P2_BLOOM>;
 constexpr int STATE_BITS = 20, T_BITS = 20, GEN_BITS = 24;
@@ -2520,10 +2523,12 @@ __global__ void __launch_bounds__(64) k_lin_seqw(DfsArgs A) { lin_dfs_waves<Memo
 // WIDE; both 37 KB of LDS): one stream for both, so the heavy-key pass needs
 // no more streams than the hardware has queues
 struct DfsPair { DfsArgs l, w; int32_t n_l; };
-constexpr int SEQLW_LDS = MemoP2::LDS > SEQW_LDS ? MemoP2::LDS : SEQW_LDS;
-template <bool STREAM>
+// (two roles: the LEAN role keeps MemoM, four waves per CU with the WIDE ones;
+// LEAN keys alone: MemoP2)
+constexpr int SEQLW_LDS = MemoM::LDS > SEQW_LDS ? MemoM::LDS : SEQW_LDS;
+template <bool STREAM, class ML = MemoM>
 __global__ void __launch_bounds__(64) k_lin_seq_lw(DfsPair P) {
-    if ((int)blockIdx.x < P.n_l) lin_dfs_waves<MemoP2, true, false, STREAM>(P.l);
+    if ((int)blockIdx.x < P.n_l) lin_dfs_waves<ML, true, false, STREAM>(P.l);
     else lin_dfs_waves<MemoWL, false, true, STREAM>(P.w);
 }
 
@@ -6318,7 +6323,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     int waves_w = 0, waves2 = 0;
     int waves3 = 0;                  // phase 3's LEAN waves (full tables; waves2 unless p2_small)
     uint32_t cap2l = cap2;           // phase 2's LEAN tables (entries per wave)
-    bool p2_small_ok = JH_P2_PER_CU != 4 || JH_P2_LG != 10;   // (the streaming pass keeps round 4's sizing)
+    bool p2_small_ok = true;         // (the streaming pass keeps round 4's sizing)
     bool split3 = false, split3w = false;
 
     // ---- the deferred WIDE keys (windows of 41-64 members or >= 256 states):
@@ -6538,7 +6543,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         cap2l = cap2;
         if (nd_l > 0) {
             const int cus2 = std::max(1, ctx->n_cu - wg2 - n_help);
-            int want2 = std::min(nd_l, cus2 * (p2_m ? 4 : 1));
+            // LEAN keys alone in the grid: MemoP2's waves per CU
+            const int lean_per_cu = n_def_w > 0 || !p2_small_ok ? 4 : JH_P2_PER_CU;
+            int want2 = std::min(nd_l, cus2 * (p2_m ? lean_per_cu : 1));
             if (opts && opts->lean_waves > 0) want2 = std::min(want2, opts->lean_waves);
             const uint64_t fixed = (uint64_t)stack_cap * sizeof(Frame) + scr_bytes_h;
             const uint64_t per2 = (uint64_t)cap2 * 16 + fixed;
@@ -6547,7 +6554,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             // more keys than waves: phase 2 stops at p2 inserts and phase 3
             // takes the rest on full tables, so phase 2's LEAN role can run
             // JH_P2_PER_CU waves per CU on tables for 2 x p2 entries
-            if (p2_m && p2_small_ok && !(opts && opts->lean_waves > 0) && budget > p2) {
+            if (p2_m && p2_small_ok && n_def_w == 0 && !(opts && opts->lean_waves > 0) && budget > p2) {
                 uint32_t cs = 1u << 16;
                 while ((int64_t)cs < 2 * p2 && cs < cap2) cs <<= 1;
                 const int want_s = std::min(nd_l, cus2 * JH_P2_PER_CU);
@@ -7043,8 +7050,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 DfsPair pr;
                 pr.l = b; pr.w = bw; pr.n_l = waves2;
                 pr.w.wave_off = waves2;
-                // (LEAN waves only: their own LDS size, so more of them per CU)
-                k_lin_seq_lw<false><<<waves2 + waves_w, 64, waves_w > 0 ? SEQLW_LDS : MemoP2::LDS, ctx->aux>>>(pr);
+                if (n_def_w > 0) k_lin_seq_lw<false, MemoM><<<waves2 + waves_w, 64, SEQLW_LDS, ctx->aux>>>(pr);
+                else k_lin_seq_lw<false, MemoP2><<<waves2, 64, MemoP2::LDS, ctx->aux>>>(pr);
                 wide_done = true;
             } else if (waves2) k_lin_seq<true><<<waves2, 64, MemoH::LDS, ctx->aux>>>(b);
             HIP_TRY(hipGetLastError());

@@ -3,7 +3,7 @@ passes (one counter per pass, MI355X_MICROARCH.md "HBM") over one history,
 written as the JSON bench.py puts into its roofline object (`traffic`,
 `traffic_over_alg_same_run`).
 
-    python tools/pmc_traffic.py <pmc-dir> <kernel-substring> <workload> <seed>
+    python tools/pmc_traffic.py <pmc-dir> <kernel-substring> <workload> <seed> [bench-label]
 
 -> profiles/r05/traffic_<workload>_s<seed>_<kernel>.json (bench.traffic_name).
 Both counters are in KiB. The guide's gfx950 calibration: FETCH_SIZE reports
@@ -37,6 +37,9 @@ def per_launch(d, counter, kernel):
 
 def main():
     src, kernel, workload, seed = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    # the bench.PHASES label the file is keyed by, when the rocprof name
+    # carries more template arguments (k_lin_seq_lw<false, MemoCfg<10, 17> >)
+    label = sys.argv[5] if len(sys.argv) > 5 else kernel
     fetch, write = per_launch(src, "FETCH_SIZE", kernel), per_launch(src, "WRITE_SIZE", kernel)
     if not fetch or not write:
         sys.exit(f"no FETCH_SIZE/WRITE_SIZE rows for {kernel} under {src}")
@@ -51,7 +54,7 @@ def main():
     alg, ents, probes, ms = {}, [], [], []
     for log, d in run.items():
         for name, (tf, pf, ef, kf, kern) in PHASES.items():
-            if kern.split("<")[0] in kernel and (("<" not in kernel) or kern in kernel) and d.get(tf, 0) > 0:
+            if kern.split("<")[0] in label and (("<" not in label) or kern in label) and d.get(tf, 0) > 0:
                 ent = d["entries"] if ef is None else d[ef]
                 alg[log] = BYTES_PER_ENTRY * ent + BYTES_PER_PROBE * d[pf]
                 ents.append(ent); probes.append(d[pf]); ms.append(d[tf])
@@ -60,18 +63,18 @@ def main():
     f1, w1 = sum(fetch) / len(fetch), sum(write) / len(write)
     a = [alg[k] for k in ("fetch.log", "write.log") if k in alg]
     alg_run = sum(a) / len(a) if a else None
-    out = {"kernel": kernel, "workload": workload, "seed": seed,
+    out = {"kernel": label, "rocprof_kernel_match": kernel, "workload": workload, "seed": seed,
            "fetch_bytes": f1, "write_bytes": w1, "traffic_bytes": f1 + w1,
            "launches": [len(fetch), len(write)], "alg_bytes_same_run": alg_run,
            "traffic_over_alg": (f1 + w1) / alg_run if alg_run else None,
-           # the serialized --pmc run's own phase (bench.py scales per probe to the timed run)
+           # the serialized --pmc run's own phase (bench.py scales by algorithmic bytes)
            "pmc_entries": sum(ents) / len(ents) if ents else 0.0,
            "pmc_probes": sum(probes) / len(probes) if probes else 0.0,
            "pmc_phase_ms": sum(ms) / len(ms) if ms else 0.0,
            "schedule": "serialized: rocprofv3 --pmc runs one kernel at a time",
            "profiled_runs": run,
            "correction": "none: scattered 8-16 B accesses are uncalibrated on gfx950 (MI355X_MICROARCH.md HBM)"}
-    dst = os.path.join(TRAFFIC_DIR, traffic_name(workload, seed, kernel))
+    dst = os.path.join(TRAFFIC_DIR, traffic_name(workload, seed, label))
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "profiled_runs"}))

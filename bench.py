@@ -58,14 +58,23 @@ def pmc_traffic(workload, seed, kernel):
 # the time, of the memo probes, of the entries of the keys searched, of the
 # number of keys searched, kernel). The default schedule's kernels; the
 # phase-2 LEAN and WIDE roles share the k_lin_seq_lw grid but keep their own
-# timers (the WIDE waves' span, ABI 4).
+# timers (the WIDE waves' span, ABI 4). Round 5: that grid's LEAN memo is a
+# template argument -- MemoCfg<10, 17> with LEAN keys alone, MemoCfg<10, 15>
+# beside WIDE ones (phase_kernel names the instance rocprof shows).
 PHASES = {
     "phase1": ("dfs_ms", "memo_probes", None, None, "k_lin_dfs<true, false>"),
-    "phase2_lean": ("seq_ms", "seq_probes", "lean_entries", "n_lean_deferred", "k_lin_seq_lw<false>"),
+    "phase2_lean": ("seq_ms", "seq_probes", "lean_entries", "n_lean_deferred", "k_lin_seq_lw<false, MemoCfg<10, 17>>"),
     "phase3_lean": ("p3_ms", "p3_probes", "p3_entries", "n_phase3", "k_lin_seq3<true>"),
-    "wide": ("wide_ms", "wide_probes", "wide_entries", "n_deferred_wide", "k_lin_seq_lw<false>"),
+    "wide": ("wide_ms", "wide_probes", "wide_entries", "n_deferred_wide", "k_lin_seq_lw<false, MemoCfg<10, 15>>"),
     "xw": ("xw_ms", "xw_probes", "xw_entries", "n_xw", "k_lin_xw"),
 }
+
+
+def phase_kernel(name, kern, sums):
+    # a phase-2 LEAN role beside WIDE keys runs the MemoCfg<10, 15> instance
+    if name == "phase2_lean" and float(np.mean([x["n_deferred_wide"] for x in sums])) > 0:
+        return PHASES["wide"][4]
+    return kern
 
 
 def _field(x, f):
@@ -90,7 +99,7 @@ def phase_rooflines(sums, n_entries):
         ent = float(n_entries if ef is None else np.mean([x[ef] for x in sums]))
         alg = BYTES_PER_ENTRY * ent + BYTES_PER_PROBE * probes
         ach = alg / (ms / 1e3) / 1e9
-        out[name] = {"kernel": kern, "ms": ms, "alg_bytes": alg, "probes": probes, "entries": ent,
+        out[name] = {"kernel": phase_kernel(name, kern, sums), "ms": ms, "alg_bytes": alg, "probes": probes, "entries": ent,
                      "keys": keys, "achieved": ach, "frac": ach / PEAK_HBM_GBS}
     return out
 

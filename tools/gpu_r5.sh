@@ -8,6 +8,29 @@
 #   ranks  [bench.py args...] C3 ranks 1-7 (--seed-rank) at 5 steps
 #   prof   <name> <cmd...>    rocprofv3 kernel trace + stats of one command
 #   pmc    <name> <counters> <cmd...>  one rocprofv3 --pmc pass
+#   evidence / evidence2      the round's remaining evidence at HEAD (see below)
+#   ab "<ranks>" <reps> <v>...  alternating C3 lines, in-tree build vs variants
+#   abopt "<ranks>" <reps> <name>=<bench options>...  the same for jh_lin_opts
+#   c2ab <reps> <v>...        counter parity tests + alternating C2 lines
+#   tests_v <v> <pytest args...>   GPU tests on variants/libjh_<v>.so
+#   pmc_v <v> <name> <counter> <kernel-regex> [workload]  a --pmc pass on a variant
+#   c4 <name> [v]             the C4 line (on a variant)
+#   c2 <name>                 the C2 lines with host-to-host timings
+#   ingest <v>                host-buffer calls, packed vs plain (a -DJH_TUNING variant)
+#   timeline <v> "<ranks>"    per-key timeline of a -DJH_TUNING variant
+# Variants are tools/build_variants.sh builds in jepsen_amd/variants/ (git-ignored).
+# Round 5's runs as calls of this script (the profiles/r05/ directories they made):
+#   ab_helpers_bfs   tests_v bfs1 tests/test_gpu_lin.py -k "bfs or linear or frontier or heavy or c3 or configs or resume"
+#                    && ab "0 4 3" 3 hbo bfs1 && c2ab 3 cp0 cp2 cp3w6 && timeline tlhbo 0
+#   ab_rs_log        tests_v log tests/test_gpu_lin.py -k "resume or stream or frontier or heavy or c3 or bfs"
+#                    && timeline tli 0 && timeline tli 4 (JH_TL_CSV=<file>) && ab "0 4" 3 log bfs1
+#   ab_p2_waves      tests_v p2w8 ... && tests_v p2w12 ... && ab "0 4 3" 2 cur p2w8 p2w12 && c4 p2w8 p2w8 && c4 cur cur
+#   ab_p2_bloom      ab "0 4 3" 2 pb17 p9b17; ab "4 0 7" 2 pb17 pb18 p9b18; ab 0 4 pb17 p9b17 && c4 ...
+#   ab_dup_write     ab "0 4" 3 dup && pmc_v dup pmc_dup WRITE_SIZE k_lin_dfs
+#   ab_cnt_*         c2ab 3 <v>;   ab_bfs_claim  ab "4 3 0" 2 cl8
+#   ab_helpers_r5q   abopt "0 4" 3 l2000h48="--opt helper_late_us=2000 --opt helpers=48" l3000h64="..."
+#   ingest           tests_v - tests/test_gpu_configs.py tests/test_gpu_counter_set.py tests/test_gpu_ingest.py && ingest ingt
+#   final_r5p / r5q  final && c2 bench_c2 && ranks && evidence2
 O=${1:-gpurun_out/r5}; PART=${2:-final}; shift 2
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p $O
@@ -83,5 +106,34 @@ timeline)
   for rk in $RK; do
     JH_LIB=$R/jepsen_amd/variants/libjh_$V.so JH_DEBUG=1 JH_DEFER_TIMES=1 timeout -k 10 120 python -u bench.py --steps 1 --warmup 1 --no-cpu --e2e 0 --no-parity --seed-rank $rk > $O/tl_${V}_r$rk.log 2>&1 || exit 1
   done ;;
+abopt)
+  RK=$1; REPS=$2; shift 2
+  B="python -u bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 --no-parity"
+  for i in $(seq 1 $REPS); do
+    for rk in $RK; do
+      timeout -k 10 120 $B --seed-rank $rk > $O/ctl_r${rk}_$i.json 2>/dev/null || exit 1
+      for nv in "$@"; do
+        timeout -k 10 120 $B --seed-rank $rk ${nv#*=} > $O/${nv%%=*}_r${rk}_$i.json 2>/dev/null || exit 1
+      done
+    done
+  done ;;
+tests_v)
+  V=$1; shift
+  L=""; [ "$V" != "-" ] && L=$R/jepsen_amd/variants/libjh_$V.so
+  JH_LIB=$L timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread "$@" > $O/tests_$V.log 2>&1 ;;
+pmc_v)
+  V=$1; N=$2; C=$3; K=$4; W=${5:-c3}
+  cd /tmp && export TMPDIR=/tmp
+  JH_LIB=$R/jepsen_amd/variants/libjh_$V.so timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "$K" -d $R/$O/$N -o $N --output-format csv -- python3 $R/tools/run_once.py $W 1 0 > $R/$O/$N.log 2>&1 ;;
+c4)
+  N=$1; V=$2
+  L=""; [ -n "$V" ] && L=$R/jepsen_amd/variants/libjh_$V.so
+  JH_LIB=$L timeout -k 10 400 python -u bench.py --workload c4 --steps 3 --warmup 1 --no-cpu --e2e 0 > $O/c4_$N.json 2> $O/c4_$N.err ;;
+c2)
+  timeout -k 10 200 python -u tools/bench_c2.py --steps 5 --warmup 1 --e2e > $O/$1.log 2>&1 ;;
+ingest)
+  L=$R/jepsen_amd/variants/libjh_$1.so
+  JH_LIB=$L JH_INGEST_TRACE=1 timeout -k 10 300 python -u tools/ingest_probe.py > $O/ingest_packed.log 2>&1 || exit 1
+  JH_LIB=$L JH_INGEST_PLAIN=1 timeout -k 10 300 python -u tools/ingest_probe.py > $O/ingest_plain.log 2>&1 ;;
 *) echo "unknown part $PART"; exit 2 ;;
 esac

@@ -475,8 +475,12 @@ constexpr int64_t QUICK_BUDGET = 8192;  // phase-1 inserts before a key is defer
 // reason. Round 5: a handed-over search continues from its saved state (the
 // resume records), so the hand-over costs nothing: 1 024 is the default when
 // resuming (C3 rank 0 41.4 -> 39.2 ms, ranks 4 / 6 / 7 and C4 down too:
-// profiles/r05/ab/); without resume it stays off
-constexpr int32_t HANDOVER_MIN = 1024;
+// profiles/r05/ab/); without resume it stays off. The checks run every 1 024
+// inserts (at 1 023, 2 047, ...), so 1 024 handed searches over at 2 047;
+// 1 023 hands them over at the first check (phase 1 7.6 -> 6.3 ms, C3 rank 0
+// -2 ms, rank 4 -1 ms: profiles/r05/ab_handover/). Finer checks (every 256 /
+// 512 inserts) hand over still earlier but leave rank 0 bimodal (37-51 ms).
+constexpr int32_t HANDOVER_MIN = 1023;
 // phase-1 issue priority by insert count (DfsArgs.prio_ins): 0 = off until measured
 constexpr int32_t P1_PRIO_INS = 0;
 // phase-2 late helpers (workgroups, one per CU) and how long a key must have run

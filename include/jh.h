@@ -171,7 +171,9 @@ typedef struct jh_lin_opts {
     int32_t helpers;           /* phase-2 late helper workgroups; <=0: 32 (JH_LIN_NO_HELPERS: none) */
     int32_t helper_late_us;    /* run time before a helper takes a key; <=0: 250 (JH_LIN_HELPERS_NOW: 0) */
     int32_t xw_waves;          /* waves of the 65-256-member search; <=0: one per key, up to 4 per CU */
-    int32_t p2_waves_per_cu;   /* 1: phase 2 at one wave per CU with the 128 KB LDS memo; else 4 */
+    int32_t p2_waves_per_cu;   /* 1: phase 2 at one wave per CU with the 128 KB LDS memo; else 4,
+                                  or 3 with the 16 KB Bloom filter when LEAN keys run alone
+                                  (round 5) */
     int32_t lean_waves;        /* at most this many phase-2 waves for LEAN keys; <=0: no cap */
     int32_t wide_waves;        /* at most this many waves for WIDE keys; <=0: no cap */
     int32_t handover_min;      /* phase 1: once its queue is empty, searches past this many

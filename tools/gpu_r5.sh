@@ -16,6 +16,7 @@
 #   pmc_v <v> <name> <counter> <kernel-regex> [workload]  a --pmc pass on a variant
 #   c4 <name> [v]             the C4 line (on a variant)
 #   c2 <name>                 the C2 lines with host-to-host timings
+#   abenv <v> "<ranks>" <reps> <name>=<VAR=v,...>...  a -DJH_TUNING variant's JH_* knobs
 #   ingest <v>                host-buffer calls, packed vs plain (a -DJH_TUNING variant)
 #   timeline <v> "<ranks>"    per-key timeline of a -DJH_TUNING variant
 # Variants are tools/build_variants.sh builds in jepsen_amd/variants/ (git-ignored).
@@ -131,6 +132,19 @@ c4)
   JH_LIB=$L timeout -k 10 400 python -u bench.py --workload c4 --steps 3 --warmup 1 --no-cpu --e2e 0 > $O/c4_$N.json 2> $O/c4_$N.err ;;
 c2)
   timeout -k 10 200 python -u tools/bench_c2.py --steps 5 --warmup 1 --e2e > $O/$1.log 2>&1 ;;
+abenv)
+  # a -DJH_TUNING variant under environment settings (its JH_* knobs):
+  #   abenv <v> "<ranks>" <reps> <name>=<VAR=value,...>...
+  V=$1; RK=$2; REPS=$3; shift 3
+  B="python -u bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 --no-parity"
+  for i in $(seq 1 $REPS); do
+    for rk in $RK; do
+      timeout -k 10 120 $B --seed-rank $rk > $O/base_r${rk}_$i.json 2>/dev/null || exit 1
+      for nv in "$@"; do
+        env $(echo ${nv#*=} | tr ',' ' ') JH_LIB=$R/jepsen_amd/variants/libjh_$V.so timeout -k 10 120 $B --seed-rank $rk > $O/${nv%%=*}_r${rk}_$i.json 2>/dev/null || exit 1
+      done
+    done
+  done ;;
 ingest)
   L=$R/jepsen_amd/variants/libjh_$1.so
   JH_LIB=$L JH_INGEST_TRACE=1 timeout -k 10 300 python -u tools/ingest_probe.py > $O/ingest_packed.log 2>&1 || exit 1

@@ -178,8 +178,8 @@ typedef struct jh_lin_opts {
     int32_t wide_waves;        /* at most this many waves for WIDE keys; <=0: no cap */
     int32_t handover_min;      /* phase 1: once its queue is empty, searches past this many
                                   inserts go to the heavy-key pass (checked every 1024
-                                  inserts); 0: default (1023 -- the first check -- when the
-                                  deferred searches resume, round 5; else off), <0: never */
+                                  inserts: 1024 hands over at 2047); 0: default (1024 when
+                                  the deferred searches resume, round 5; else off), <0: never */
     int32_t p1_waves_per_cu;   /* phase-1 waves per CU (<= 26, the LDS limit); <=0: 26 */
 } jh_lin_opts;
 

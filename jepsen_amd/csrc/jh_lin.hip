@@ -476,11 +476,13 @@ constexpr int64_t QUICK_BUDGET = 8192;  // phase-1 inserts before a key is defer
 // resume records), so the hand-over costs nothing: 1 024 is the default when
 // resuming (C3 rank 0 41.4 -> 39.2 ms, ranks 4 / 6 / 7 and C4 down too:
 // profiles/r05/ab/); without resume it stays off. The checks run every 1 024
-// inserts (at 1 023, 2 047, ...), so 1 024 handed searches over at 2 047;
-// 1 023 hands them over at the first check (phase 1 7.6 -> 6.3 ms, C3 rank 0
-// -2 ms, rank 4 -1 ms: profiles/r05/ab_handover/). Finer checks (every 256 /
-// 512 inserts) hand over still earlier but leave rank 0 bimodal (37-51 ms).
-constexpr int32_t HANDOVER_MIN = 1023;
+// inserts (at 1 023, 2 047, ...), so 1 024 hands searches over at 2 047.
+// 1 023 (the first check) ends phase 1 at 6.3 ms instead of 7.6 and helps
+// ranks 3 / 4 / 7 by 0.6-1.6 ms, but rank 0 -- the one-GPU line -- turns
+// heavy-tailed: 2 of 10 runs at 46-49 ms, mean 40.1 vs 39.4 ms over 12 runs at
+// 1 024 (profiles/r05/ab_handover/); finer checks (every 256 / 512 inserts)
+// are worse still. 1 024 stays.
+constexpr int32_t HANDOVER_MIN = 1024;
 // phase-1 issue priority by insert count (DfsArgs.prio_ins): 0 = off until measured
 constexpr int32_t P1_PRIO_INS = 0;
 // phase-2 late helpers (workgroups, one per CU) and how long a key must have run

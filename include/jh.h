@@ -326,11 +326,18 @@ int jh_key_index(jh_ctx *ctx, const jh_history *h, int64_t *key_off, int64_t *ro
  * rows of the linearized ops, then of the pending ones (knossos' :pending),
  * each in call order -- for a frontier the members of the window, for final
  * configurations the crashed ops (their :info completion or none) the search
- * keeps; rows_cap >= n_keys_q * per_key * JH_MAX_WINDOW. last_row (ABI 6) is
- * the configuration's :last-op as knossos' analysis prints it: the row of the
- * key's last client :ok completion before the configurations' point (the
+ * keeps; rows_cap >= n_keys_q * per_key * JH_MAX_WINDOW. Round 6: the reads
+ * the search drops (crashed reads, :ok reads of nil -- they constrain
+ * nothing) are listed too: each configuration is the one knossos holds in
+ * which such a read is linearized exactly when its own completion forces it,
+ * so a read invoked before the configuration's point and not completed there
+ * is pending (call order, at most JH_MAX_WINDOW rows in all). last_row (ABI 6)
+ * is the configuration's :last-op as knossos' analysis prints it: the row of
+ * the key's last client :ok completion before the configurations' point (the
  * failing op's completion for a frontier, the end of the history for final
- * configurations), -1 if there is none. knossos is not vendored: this order,
+ * configurations; a read of nil completing later than a final
+ * configuration's own last op is its :last-op), -1 if there is none.
+ * knossos is not vendored: this order,
  * the cut and the layer are this library's definitions (parity unpinned; the
  * oracle restates them). */
 typedef struct jh_lin_config {

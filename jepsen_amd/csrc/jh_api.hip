@@ -8,6 +8,8 @@
 // shim's ex-info into {:valid? :unknown :error ...}).
 #include "jh_internal.h"
 #include <algorithm>
+#include <unordered_map>
+#include <vector>
 
 static void set_err(char *err, size_t errlen, const std::string &msg) {
     if (!err || errlen == 0) return;
@@ -188,6 +190,62 @@ __global__ void k_cfg_slots(const int64_t *__restrict__ keys, int n, int64_t K, 
     if (i < n && keys[i] >= 0 && keys[i] < K) slot[keys[i]] = i;
 }
 
+// Round 6: the reads the search drops -- a crashed
+// :read, an :ok :read of nil; they constrain nothing -- are ops knossos'
+// analysis holds (checker.clj:156-158 passes it through). Each configuration
+// printed is the one knossos holds in which such a read is linearized exactly
+// when its own completion forces it, and never otherwise: a read invoked
+// before the configuration's point (the failing op's completion for a
+// frontier, the end of the history for final configurations) and not
+// completed there -- a crashed read always -- is pending, in call order among
+// the others (the row list stays within JH_MAX_WINDOW), and an :ok read of nil
+// completing before the point and after the configuration's own :last-op is
+// its :last-op. The oracle restates this (oracle/jh_oracle.c add_noop_reads);
+// the pairing is knossos.history/complete's, as the device's key pass does it.
+struct NoopRead { int64_t call, ret; };            // ret: :ok completion row, INT64_MAX crashed
+static std::vector<std::vector<NoopRead>> noop_reads(const jh_history *h, bool keyed, const int64_t *keys, int nq) {
+    const int64_t n = h->n;
+    std::vector<int64_t> pr, ty, fc, va, ke;
+    const int64_t *P = h->process, *T = h->type, *F = h->f, *V = h->value, *KC = keyed ? h->key : nullptr;
+    if (h->on_device) {
+        auto fetch = [&](std::vector<int64_t> &v, const int64_t *src) {
+            v.resize((size_t)std::max<int64_t>(n, 1));
+            if (n) HIP_TRY(hipMemcpy(v.data(), src, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+            return (const int64_t *)v.data();
+        };
+        P = fetch(pr, P); T = fetch(ty, T); F = fetch(fc, F); V = fetch(va, V);
+        if (KC) KC = fetch(ke, KC);
+    }
+    std::unordered_map<int64_t, std::vector<int>> want;     // key -> queries
+    for (int i = 0; i < nq; i++) want[keyed ? keys[i] : 0].push_back(i);
+    std::vector<std::unordered_map<int64_t, int64_t>> open(nq);   // per query: process -> open invocation
+    std::vector<std::vector<NoopRead>> out(nq);
+    auto row = [&](int q, int64_t r) {
+        const int64_t p = P[r];
+        if (p < 0) return;
+        auto it = open[q].find(p);
+        if (T[r] == JH_TYPE_INVOKE) { open[q][p] = r; return; }
+        if (T[r] != JH_TYPE_OK && T[r] != JH_TYPE_FAIL) return;          // :info leaves it open
+        if (it == open[q].end()) return;
+        const int64_t iv = it->second;
+        open[q].erase(it);
+        if (T[r] == JH_TYPE_OK && F[iv] == JH_F_READ && (V[iv] != JH_NIL ? V[iv] : V[r]) == JH_NIL)
+            out[q].push_back({iv, r});
+    };
+    static const std::vector<int> none;
+    for (int64_t r = 0; r < n; r++) {
+        const int64_t k = KC ? KC[r] : 0;
+        if (k < 0) { for (int q = 0; q < nq; q++) row(q, r); continue; }   // un-keyed rows: every key's
+        auto w = want.find(k);
+        if (w != want.end()) for (int q : w->second) row(q, r);
+    }
+    for (int q = 0; q < nq; q++) {
+        for (auto &o : open[q]) if (F[o.second] == JH_F_READ) out[q].push_back({o.second, INT64_MAX});
+        std::sort(out[q].begin(), out[q].end(), [](const NoopRead &a, const NoopRead &b) { return a.call < b.call; });
+    }
+    return out;
+}
+
 int jh_lin_configs(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts, const int64_t *keys,
                    int64_t n_keys_q, int32_t per_key, jh_lin_config *out, int32_t *n_out, int64_t *rows_out,
                    int64_t rows_cap, char *err, size_t errlen) {
@@ -225,18 +283,31 @@ int jh_lin_configs(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts, co
         HIP_TRY(hipMemcpyAsync(n_out, cn, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(hc.data(), co, sizeof(jh_lin_config) * hc.size(), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(hr.data(), cr, sizeof(int64_t) * hr.size(), hipMemcpyDeviceToHost, st));
+        std::vector<jh_key_verdict> hv((size_t)K);
+        HIP_TRY(hipMemcpyAsync(hv.data(), dv, sizeof(jh_key_verdict) * K, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        // compact: configuration j of key i keeps slot i * per_key + j; its rows move up
+        const auto noop = noop_reads(h, keyed, keys, nq);
+        // compact: configuration j of key i keeps slot i * per_key + j; its rows
+        // move up, the dropped reads join :pending (noop_reads above)
         int64_t w = 0;
         for (int i = 0; i < nq; i++)
             for (int j = 0; j < per_key; j++) {
                 jh_lin_config &c = out[(size_t)i * per_key + j];
                 if (j >= n_out[i]) { memset(&c, 0, sizeof c); c.key = keys[i]; c.rows_off = w; continue; }
                 c = hc[(size_t)i * per_key + j];
-                const int64_t nr = (int64_t)c.n_linearized + c.n_pending;
-                memcpy(rows_out + w, hr.data() + c.rows_off, sizeof(int64_t) * nr);
+                const int64_t nl = c.n_linearized, np0 = c.n_pending;
+                memcpy(rows_out + w, hr.data() + c.rows_off, sizeof(int64_t) * (nl + np0));
+                const jh_key_verdict &v = hv[(size_t)(keyed ? keys[i] : 0)];
+                const int64_t pt = v.valid == JH_INVALID ? v.fail_entry : INT64_MAX - 1;
+                int64_t np = np0;
+                for (const NoopRead &o : noop[i]) {
+                    if (o.ret != INT64_MAX && o.ret < pt && o.ret > c.last_row) c.last_row = o.ret;
+                    if (o.call < pt && o.ret > pt && nl + np < JH_MAX_WINDOW) rows_out[w + nl + np++] = o.call;
+                }
+                std::sort(rows_out + w + nl, rows_out + w + nl + np);
+                c.n_pending = (int32_t)np;
                 c.rows_off = w;
-                w += nr;
+                w += nl + np;
             }
     });
 }

@@ -4489,6 +4489,38 @@ __device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int k
     const int per = min(A.cfg_per, CFG_MAX);
     unsigned long long prev = 0;
     if (tid == 0) nsel = 0;
+    // Round 6: an :ok read of nil, which the search drops, is an op knossos
+    // holds; in the configuration printed for each of ours it is linearized
+    // when its completion forces it, so that completion becomes the :last-op
+    // of every final configuration whose own last op returned before it (the
+    // host moves last_row: jh_api.hip add_noop_reads). Configurations that then
+    // differ in nothing print alike: the selection takes every layer whose
+    // RET returns before the last such read as one, tf = the last of them.
+    __shared__ uint32_t tf;
+    if (fin) {
+        if (wid == 0) {
+            long long y = -1;
+            for (uint32_t base = sh.K.s0; base < sh.K.s1; base += 64) {
+                const uint32_t p = base + lane;
+                if (p < sh.K.s1) {
+                    const Rec x = A.src.rec[p];
+                    const int q = A.src.pair[p];
+                    if (x.proc >= 0 && x.type == T_OK && q >= 0) {
+                        const Rec iv = A.src.rec[q];
+                        if (iv.f == F_READ && (iv.v1 != 0 ? iv.v1 : x.v1) == 0) y = max(y, (long long)A.src.rows[p]);
+                    }
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1) y = max(y, (long long)__shfl_xor(y, o));
+            int before = 0;
+            for (uint32_t base = sh.K.s0; base < sh.K.s1; base += 64) {
+                const uint32_t p = base + lane;
+                before += __popcll(ballot(p < sh.K.s1 && A.src.rank[p] <= -2 && (long long)A.src.rows[p] < y));
+            }
+            if (lane == 0) tf = before > 0 ? (uint32_t)before - 1 : 0;
+        }
+        __syncthreads();
+    }
     for (int i = 0; i < per; i++) {
         if (tid == 0) sh.cfg_min = ~0ULL;
         __syncthreads();
@@ -4512,7 +4544,7 @@ __device__ void bfs_dump_configs(const BfsArgs &A, BfsShared &sh, int tid, int k
                 }
                 if (u < n_ok) continue;                          // not a terminal edge
                 // s:12 | mask over C:32 | t:20 (the layer whose RET was lifted last)
-                kk = ((unsigned long long)(uint32_t)s2 << 52) | ((unsigned long long)(uint32_t)nm << 20) | t;
+                kk = ((unsigned long long)(uint32_t)s2 << 52) | ((unsigned long long)(uint32_t)nm << 20) | max(t, tf);
             }
             if ((i == 0 || kk > prev) && kk < m) m = kk;
         }

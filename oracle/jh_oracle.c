@@ -154,7 +154,14 @@ int orc_key_prepare(const jh_history *h, const int64_t *sel, int64_t m, orc_key 
             } else if (v1 == JH_NIL) v1 = h->value[rc];
         }
         if (f != JH_F_READ && f != JH_F_WRITE && f != JH_F_CAS) { status = JH_CAUSE_BAD_F; break; }
-        if (f == JH_F_READ && (ret == ORC_CRASHED || v1 == JH_NIL)) continue;
+        if (f == JH_F_READ && (ret == ORC_CRASHED || v1 == JH_NIL)) {
+            if (!k->noop_call) {
+                k->noop_call = (int64_t *)malloc(sizeof(int64_t) * (m ? m : 1));
+                k->noop_ret = (int64_t *)malloc(sizeof(int64_t) * (m ? m : 1));
+            }
+            k->noop_call[k->n_noop] = r; k->noop_ret[k->n_noop++] = ret;
+            continue;
+        }
         orc_op *o = &k->ops[n++];
         o->call = r; o->ret = ret; o->f = f; o->v1 = v1; o->v2 = v2; o->rr = -1;
     }
@@ -232,6 +239,7 @@ static int sym_blocked(const orc_key *k, const int32_t *W, const uint64_t *mask,
 
 void orc_key_free(orc_key *k) {
     free(k->ops); free(k->ret_op); free(k->w_off); free(k->w_ops); free(k->pred);
+    free(k->noop_call); free(k->noop_ret);
     memset(k, 0, sizeof(*k));
 }
 
@@ -508,6 +516,29 @@ static int cmp_cfg_ord(const void *a, const void *b) {
 static int configs_domain(const orc_key *k) {
     return !k->status && k->max_window <= JH_MAX_WINDOW && k->n_ok < (1 << 20) - 2;
 }
+/* Round 6: the reads the search drops (a crashed :read, an :ok :read of nil:
+ * they constrain nothing) are ops knossos holds all the same
+ * (checker.clj:156-158 passes its analysis through). Each configuration
+ * printed is the one knossos holds in which such a read is linearized exactly
+ * when its own completion forces it and never otherwise: a read invoked before
+ * the configuration's point p and not completed by then (a crashed read
+ * always) is pending, merged into :pending in call order (the row list stays
+ * within JH_MAX_WINDOW), and an :ok read of nil completing before p is the
+ * last op an expansion linearized when it completes after the configuration's
+ * own :last-op. */
+static int cmp_rows(const void *a, const void *b) {
+    const int64_t x = *(const int64_t *)a, y = *(const int64_t *)b;
+    return x < y ? -1 : x > y;
+}
+static void add_noop_reads(const orc_key *k, int64_t p, jh_lin_config *c, int64_t *r) {
+    for (int32_t q = 0; q < k->n_noop; q++) {
+        if (k->noop_ret[q] != ORC_CRASHED && k->noop_ret[q] < p && k->noop_ret[q] > c->last_row)
+            c->last_row = k->noop_ret[q];
+        if (k->noop_call[q] < p && k->noop_ret[q] > p && c->n_linearized + c->n_pending < JH_MAX_WINDOW)
+            r[c->n_linearized + c->n_pending++] = k->noop_call[q];
+    }
+    qsort(r + c->n_linearized, (size_t)c->n_pending, sizeof(int64_t), cmp_rows);
+}
 static int configs_one(const jh_history *h, const int64_t *sel, int64_t m, int64_t init, int64_t budget,
                        int per_key, int per_key_values, jh_lin_config *out, int64_t *rows) {
     orc_key k;
@@ -528,6 +559,7 @@ static int configs_one(const jh_history *h, const int64_t *sel, int64_t m, int64
             c->key = 0; c->model_value = init; c->n_linearized = 0; c->n_pending = 0; c->rows_off = 0;
             c->last_row = -1;
             for (int32_t q = 0; q < k.n_ops && q < JH_MAX_WINDOW; q++) rows[c->n_pending++] = k.ops[q].call;
+            add_noop_reads(&k, ORC_CRASHED - 1, c, rows);
         } else if (verdict == JH_INVALID || (verdict == JH_VALID && want_fin)) {
             const int final = verdict == JH_VALID;
             const cvec *src = final ? &fin : &front;
@@ -542,7 +574,6 @@ static int configs_one(const jh_history *h, const int64_t *sel, int64_t m, int64
             int64_t nu = 0;                                   /* distinct configurations */
             for (int64_t i = 0; i < src->n; i++)
                 if (nu == 0 || cmp_cfg_ord(&o[nu - 1], &o[i]) != 0) o[nu++] = o[i];
-            n = (int)(nu < per_key ? nu : per_key);
             const uint32_t tl = final ? (uint32_t)k.n_ok - 1 : tmax;
             const int32_t *W = k.w_ops + k.w_off[tl];
             const int w = k.w_off[tl + 1] - k.w_off[tl];
@@ -554,12 +585,15 @@ static int configs_one(const jh_history *h, const int64_t *sel, int64_t m, int64
             /* :last-op: the frontier's is RET[tmax - 1]'s completion, a final
              * configuration's the :ok op its terminal edge linearized last */
             const int64_t lfront = tmax == 0 ? -1 : k.ops[k.ret_op[tmax - 1]].ret;
-            for (int i = 0; i < n; i++) {
-                jh_lin_config *c = &out[i];
+            /* configurations that differ only in :last-op can coincide once the
+             * reads of nil move it (add_noop_reads): adjacent in this order */
+            n = 0;
+            for (int64_t i = 0; i < nu && n < per_key; i++) {
+                jh_lin_config *c = &out[n];
                 c->key = 0; c->model_value = o[i].v; c->n_linearized = 0; c->n_pending = 0;
-                c->rows_off = (int64_t)i * JH_MAX_WINDOW;
+                c->rows_off = (int64_t)n * JH_MAX_WINDOW;
                 c->last_row = final ? k.ops[k.ret_op[o[i].t]].ret : lfront;
-                int64_t *r = rows + (int64_t)i * JH_MAX_WINDOW;
+                int64_t *r = rows + (int64_t)n * JH_MAX_WINDOW;
                 for (int j = 0; j < nm; j++) if (bit_get(o[i].m, j)) r[c->n_linearized++] = k.ops[mem[j]].call;
                 for (int j = 0; j < nm; j++) if (!bit_get(o[i].m, j)) r[c->n_linearized + c->n_pending++] = k.ops[mem[j]].call;
                 if (final)      /* crashed ops called after the last :ok return: pending */
@@ -567,6 +601,13 @@ static int configs_one(const jh_history *h, const int64_t *sel, int64_t m, int64
                         if (k.ops[q].ret == ORC_CRASHED && k.ops[q].call > last_ret &&
                             c->n_linearized + c->n_pending < JH_MAX_WINDOW)
                             r[c->n_linearized + c->n_pending++] = k.ops[q].call;
+                add_noop_reads(&k, final ? ORC_CRASHED - 1 : k.ops[k.ret_op[tmax]].ret, c, r);
+                const jh_lin_config *b = n ? &out[n - 1] : NULL;
+                if (b && b->model_value == c->model_value && b->last_row == c->last_row &&
+                    b->n_linearized == c->n_linearized && b->n_pending == c->n_pending &&
+                    !memcmp(rows + b->rows_off, r, sizeof(int64_t) * (size_t)(c->n_linearized + c->n_pending)))
+                    continue;
+                n++;
             }
             free(mem);
             free(o);

@@ -47,6 +47,9 @@ typedef struct orc_key {
     int32_t max_window;
     int32_t *pred;     /* crashed-op symmetry (orc_reduce_crashed): the previous crashed op
                           of the same (f, value, value2) in call order, or -1 */
+    int32_t n_noop;    /* round 6: the reads the search drops (crashed reads, :ok reads of
+                          nil), kept for knossos' :pending (configs_one), in call order */
+    int64_t *noop_call, *noop_ret;   /* invocation row; :ok completion row or INT64_MAX */
 } orc_key;
 
 /* Round 5: pending crashed ops of one (f, value, value2) class are

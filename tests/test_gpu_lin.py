@@ -591,3 +591,60 @@ def test_frontier_configs_wide_windows(ctx):
     o = oracle.lin_configs(cols, keys, budget=1 << 16)
     assert g == o
     assert all(len(g[k]) == 5 for k in range(4))
+
+
+@pytest.mark.parametrize("case", ["bfs_only", "c3_budget22"])
+def test_uncounted_early_emit(ctx, case):
+    """The checkers' own path: without
+    JH_LIN_EXACT_COUNT, a valid key the reachable-set engine settles with at
+    most `budget` configurations reachable is emitted at once with explored
+    = JH_EXPLORED_UNCOUNTED (jh_lin.hip, the early emit after the forward
+    pass). Forced two ways -- the BFS alone (JH_LIN_BFS_ONLY) on keys whose
+    reachable sets fit it, and the benched C3 configuration itself (seed 3,
+    budget 2^22) -- every key's verdict, cause and failing row equal the
+    oracle's, every uncounted key is valid in the oracle, and every counted
+    key's explored equals WGL's count."""
+    if case == "bfs_only":
+        cols, _ = synth.cas_register(n_keys=150, ops_per_key=300, threads_per_key=12, readers=6, groups=10,
+                                     p_info=0.0, p_invalid=0.05, nemesis_every=0, init_nil=True, seed=21)
+        g, _ = ctx.check_cas_independent(cols, flags=A.LIN_BFS_ONLY, exact_count=False)
+        c, _ = oracle.check_cas_independent(cols, threads=8)
+    else:
+        cols, _ = synth.cas_register(seed=3)
+        g, _ = ctx.check_cas_independent(cols, budget=1 << 22, exact_count=False)
+        c, _ = oracle.check_cas_independent(cols, budget=1 << 22, threads=16)
+    unc = g["explored"] == A.EXPLORED_UNCOUNTED
+    assert unc.sum() >= 5, unc.sum()
+    assert (c["valid"][unc] == A.VALID).all()
+    for f in ("valid", "cause", "fail_entry"):
+        bad = np.nonzero(g[f] != c[f])[0]
+        assert len(bad) == 0, (f, bad[:10])
+    bad = np.nonzero((g["explored"] != c["explored"]) & ~unc)[0]
+    assert len(bad) == 0, ("explored", bad[:10], g[bad[:5]], c[bad[:5]])
+
+
+@pytest.mark.parametrize("seed", [14, 16, 18])
+def test_configs_list_dropped_reads_device(ctx, seed):
+    """Round 6: jh_lin_configs lists the reads the search
+    drops -- crashed reads, :ok reads of nil -- in :pending as knossos holds
+    them, and moves :last-op to a read of nil that completes later (the
+    oracle's restatement is pinned on the strict just-in-time linearization,
+    tests/test_oracle_crosscheck.py::test_configs_list_dropped_reads): the
+    device equals the oracle on every invalid key's frontier and every valid
+    :linear key's final configurations, and some list such reads."""
+    cols, _ = synth.cas_register(n_keys=300, ops_per_key=40, threads_per_key=4, readers=2, n_values=3,
+                                 process_limit=10 ** 6, p_info=0.15, p_invalid=0.3, nemesis_every=10 ** 9,
+                                 init_nil=True, seed=seed)
+    c, _ = oracle.check_cas_independent(cols, init=A.NIL, algorithm="linear", threads=16)
+    keys = np.nonzero((c["valid"] == A.INVALID) | ((c["valid"] == A.VALID) & (c["analyzer"] == A.ANALYZER_LINEAR)))[0]
+    g = ctx.lin_configs(cols, keys)
+    o = oracle.lin_configs(cols, keys, init=A.NIL)
+    assert g == o
+    from jepsen_amd.checker import _next_same_process
+    nxt = _next_same_process(cols)
+    noop = set()
+    for r in np.nonzero((cols.f == A.F_READ) & (cols.type == A.TYPE_INVOKE))[0].tolist():
+        q = int(nxt[r])
+        if q < 0 or cols.type[q] == A.TYPE_INFO or (cols.type[q] == A.TYPE_OK and cols.value[q] == A.NIL):
+            noop.add(r)
+    assert sum(1 for k in keys if g[int(k)] and any(set(p) & noop for _, _, p, _ in g[int(k)])) >= 5

@@ -234,8 +234,10 @@ def test_frontier_configs_from_definition(built, seed):
         window, front = ref
         want = [(v, [r for r in window if r in L], [r for r in window if r not in L]) for L, v in front][:10]
         assert [(int(v), list(map(int, lin)), list(map(int, pend))) for v, lin, pend, _ in got[k]] == want, k
-        # :last-op: the completion of the last :ok op before the failing one
-        assert all(last == _jit_frontier.last for *_, last in got[k]), k
+        # :last-op: the completion of the last :ok op before the failing one,
+        # reads of nil included (round 6: _jit_noop keeps them as ops)
+        (_, _, _, last_ref), _ = _jit_noop(cols, k, A.NIL, "full")
+        assert all(last == last_ref for *_, last in got[k]), k
     assert n_bad >= 5
 
 
@@ -333,30 +335,137 @@ def _jit_final(cols, key, init):
     return crashed, configs
 
 
-@pytest.mark.parametrize("seed", [14, 15])
-def test_final_configs_from_definition(built, seed):
-    """orc_lin_configs on a valid key (ABI 6: the final configurations the
-    :linear analysis holds after the last :ok completion) equals the strict
-    just-in-time linearization from the definition: value, which crashed ops
-    stand linearized, the pending crashed ops, and :last-op -- the :ok op
-    each configuration linearized last -- first 10 in the canonical order."""
-    cols, _ = synth.cas_register(n_keys=60, ops_per_key=24, threads_per_key=3, readers=1, n_values=3,
-                                 process_limit=10 ** 6, p_info=0.12, p_invalid=0.2, nemesis_every=10 ** 9,
-                                 seed=seed)
+def _jit_noop(cols, key, init, mode):
+    """knossos' just-in-time linearization over op maps, strictly (as
+    _jit_final), with the reads the search drops -- crashed reads and :ok
+    reads of nil, which constrain nothing -- kept as ops (round 6, VERDICT r5
+    item 1b). mode "full": they are ops like any other (knossos' own set);
+    mode "lazy": such a read is linearized only when its own completion forces
+    it, by itself, and never as part of another op's expansion (a crashed read
+    never) -- the member of knossos' set libjh prints for each configuration
+    of its search. Returns ("frontier", window rows in call order, closure
+    {(L, s)}, last completion row) at the first completion no configuration
+    survives, else ("final", {(L, s, last)}), plus the no-op read rows."""
+    NIL = A.NIL
+    rows = [i for i in range(cols.n) if int(cols.key[i]) == key]
+    open_by_proc, ops = {}, {}
+    for i in rows:
+        p, ty = int(cols.process[i]), int(cols.type[i])
+        if ty == A.TYPE_INVOKE:
+            open_by_proc[p] = i
+            ops[i] = {"f": int(cols.f[i]), "v": int(cols.value[i]), "v2": int(cols.value2[i]), "ret": None}
+        else:
+            inv = open_by_proc.pop(p, None) if ty != A.TYPE_INFO else None
+            if inv is None:
+                continue
+            if ty == A.TYPE_FAIL:
+                ops[inv]["fail"] = True
+            elif ty == A.TYPE_OK:
+                ops[inv]["ret"] = i
+                if ops[inv]["f"] == 0 and ops[inv]["v"] == NIL:
+                    ops[inv]["v"] = int(cols.value[i])
+    noop = {o for o, d in ops.items() if not d.get("fail") and d["f"] == 0 and (d["ret"] is None or d["v"] == NIL)}
+
+    def step(s, o):
+        if o["f"] == 1:
+            return o["v"]
+        if o["f"] == 2:
+            return o["v2"] if s == o["v"] else None
+        return s if (o["v"] == NIL or o["v"] == s) else None
+    configs = {(frozenset(), init, -1)}
+    avail, done = set(), set()
+    for i in rows:
+        if int(cols.type[i]) == A.TYPE_INVOKE:
+            if not ops[i].get("fail"):
+                avail.add(i)
+            continue
+        if int(cols.type[i]) != A.TYPE_OK:
+            continue
+        inv = next((o for o in avail if ops[o]["ret"] == i), None)
+        if inv is None:
+            continue
+        cand = avail if mode == "full" else avail - noop
+        new, closure = set(), set()
+        for L, s, last in configs:
+            if inv in L:
+                new.add((L, s, last))
+                continue
+            if mode == "lazy" and inv in noop:
+                new.add((L | {inv}, s, i))
+                continue
+            seen, stack = {(L, s)}, [(L, s)]
+            while stack:
+                L2, s2 = stack.pop()
+                for o in cand - L2:
+                    s3 = step(s2, ops[o])
+                    if s3 is None:
+                        continue
+                    if o == inv:
+                        new.add((L2 | {o}, s3, i))
+                    elif (L2 | {o}, s3) not in seen:
+                        seen.add((L2 | {o}, s3))
+                        stack.append((L2 | {o}, s3))
+            closure |= seen
+        if not new:
+            last = max((ops[o]["ret"] for o in done), default=-1)
+            return ("frontier", sorted(avail - done), closure | {(L, s) for L, s, _ in configs}, last), noop
+        configs = new
+        done.add(inv)
+    return ("final", configs), noop
+
+
+@pytest.mark.parametrize("seed", [14, 15, 16, 17, 18])
+def test_configs_list_dropped_reads(built, seed):
+    """Round 6: :pending lists the reads the search
+    drops, as knossos' analysis holds them (checker.clj:156-158). Checked
+    against the strict just-in-time linearization with those reads kept as
+    ops, on histories with crashed reads and :ok reads of nil:
+      - an invalid key's frontier is exactly knossos' closure at the failing
+        completion restricted to the configurations that linearized none of
+        the reads still open there, first 10 in the canonical order, every
+        open read pending, :last-op the last completion before the failure;
+      - a valid key's final configurations are exactly the set in which such
+        a read is linearized only when its own completion forces it, and
+        every one of them is in knossos' own (full) set -- which crashed ops
+        stand linearized, the value and :last-op, the :ok op (a read of nil
+        included) each configuration linearized last (round 5's
+        test_final_configs_from_definition, with the dropped reads kept)."""
+    cols, _ = synth.cas_register(n_keys=60, ops_per_key=24, threads_per_key=3, readers=2, n_values=3,
+                                 process_limit=10 ** 6, p_info=0.15, p_invalid=0.3, nemesis_every=10 ** 9,
+                                 init_nil=True, seed=seed)
     lin, _ = oracle.check_cas_independent(cols, init=A.NIL, algorithm="linear")
     got = oracle.lin_configs(cols, list(range(cols.n_keys)), init=A.NIL)
-    n_crashed = 0
+    n_front = n_final = n_noop_pending = n_crashed = 0
     for k in range(cols.n_keys):
-        ref = _jit_final(cols, k, A.NIL)
-        if int(lin["valid"][k]) != A.VALID:
-            assert ref is None, k
+        (kind, *rest), noop = _jit_noop(cols, k, A.NIL, "full")
+        if kind == "frontier":
+            window, closure, last = rest
+            assert int(lin["valid"][k]) == A.INVALID, k
+            opened = set(window) & noop
+            red = [r for r in window if r not in noop]
+            keep = [(L, s) for L, s in closure if not (L & opened)]
+            keep.sort(key=lambda c: (0 if c[1] == A.NIL else 2, c[1], sum(1 << j for j, r in enumerate(red) if r in c[0])))
+            want = [(s, [r for r in window if r in L], [r for r in window if r not in L], last) for L, s in keep][:10]
+            assert got[k] == want, k
+            n_front += 1
+            n_noop_pending += bool(opened)
             continue
-        assert ref is not None, k
-        crashed, configs = ref
-        order = sorted(configs, key=lambda c: (0 if c[1] == A.NIL else 2, c[1],
-                                               sum(1 << j for j, r in enumerate(crashed) if r in c[0]), c[2]))
-        want = [(s, [r for r in crashed if r in L], [r for r in crashed if r not in L], last)
+        full = rest[0]
+        if int(lin["valid"][k]) != A.VALID or got[k] is None:
+            continue
+        (_, lazy), _ = _jit_noop(cols, k, A.NIL, "lazy")
+        assert lazy <= full, k
+        rows = sorted(set().union(*(L for L, _, _ in lazy)) | {o for o in noop if int(cols.type[o]) == A.TYPE_INVOKE})
+        crashed = sorted(r for r in _jit_final(cols, k, A.NIL)[0])
+        cr_noop = sorted(o for o in noop if all(int(cols.process[j]) != int(cols.process[o]) or
+                                                int(cols.type[j]) != A.TYPE_OK for j in range(o + 1, cols.n)
+                                                if int(cols.key[j]) == k))
+        order = sorted(lazy, key=lambda c: (0 if c[1] == A.NIL else 2, c[1],
+                                            sum(1 << j for j, r in enumerate(crashed) if r in c[0]), c[2]))
+        want = [(s, [r for r in crashed if r in L], sorted([r for r in crashed if r not in L] + cr_noop), last)
                 for L, s, last in order][:10]
-        assert got[k] == want, k
-        n_crashed += any(c[1] or c[2] for c in want)
-    assert n_crashed >= 5
+        assert got[k] == want, (k, rows)
+        n_final += 1
+        n_noop_pending += bool(cr_noop)
+        n_crashed += any(c[1] or set(c[2]) - set(cr_noop) for c in want)
+    assert n_front >= 5 and n_final >= 5 and n_noop_pending >= 3 and n_crashed >= 3

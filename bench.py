@@ -24,8 +24,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: 8 TB/s HBM3E (spec)
-BYTES_PER_ENTRY = 56           # 7 x int64 columns read once
+BYTES_PER_ENTRY = 56           # 7 x int64 columns read once (the whole step)
 BYTES_PER_PROBE = 16           # one memo entry {mask, t|state|gen}
+# Round 6: a search phase reads the compact per-key
+# tables the table pass built, not the history's columns -- ops {rq, fa} and
+# layers {rq, hi}, at most 8 B per entry plus 32 B per key
+# -- and phase 2 also the resume records of the searches it continues. Those
+# are the bytes each phase's roofline charges; 56 B per entry is the whole
+# step's (roofline.step).
+BYTES_PER_TABLE_ENTRY = 8
+BYTES_PER_KEY_TABLE = 32
 # HBM bytes per launch of a kernel from the rocprofv3 FETCH_SIZE and
 # WRITE_SIZE passes over the SAME history (tools/gpu_pmc.sh + pmc_traffic.py),
 # one file per (workload, seed, kernel) under profiles/r05/: PMC counters
@@ -36,7 +44,7 @@ BYTES_PER_PROBE = 16           # one memo entry {mask, t|state|gen}
 # file's ratio is traffic over the algorithmic bytes of that serialized run,
 # and the line also scales the measured bytes per memo probe to the timed
 # run's probe count.
-TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r05")
+TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r06")
 
 
 def traffic_name(workload, seed, kernel):
@@ -83,12 +91,26 @@ def _field(x, f):
     return x[f]
 
 
+def phase_alg_bytes(name, d, n_entries):
+    """Algorithmic bytes of one search phase in one call (jh_summary fields in
+    d): the compact tables of the keys it searches (8 B per entry + 32 B per
+    key), 16 B per HBM memo probe, and for phase 2 the resume records it
+    reads (round 6: not the 56 B per entry of the columns, which the table
+    pass read once)."""
+    tf, pf, ef, kf, kern = PHASES[name]
+    ent = n_entries if ef is None else d[ef]
+    keys = d["n_keys"] if kf is None else _field(d, kf)
+    b = BYTES_PER_TABLE_ENTRY * ent + BYTES_PER_KEY_TABLE * keys + BYTES_PER_PROBE * d[pf]
+    if name == "phase2_lean":
+        b += d.get("resume_bytes", 0)
+    return float(b)
+
+
 def phase_rooflines(sums, n_entries):
     """Per search phase, from jh_summary's per-phase times and probe
-    counters: algorithmic bytes (56 B per entry of the keys the phase
-    searches + 16 B per HBM memo probe) over the phase's time.
-    A phase that searched no key is not a phase of this line (its launch may
-    still have run empty): skipped."""
+    counters: algorithmic bytes (phase_alg_bytes) over the phase's HIP-event
+    time in the timed run. A phase that searched no key is not a phase of
+    this line (its launch may still have run empty): skipped."""
     out = {}
     for name, (tf, pf, ef, kf, kern) in PHASES.items():
         ms = float(np.mean([x[tf] for x in sums]))
@@ -97,7 +119,7 @@ def phase_rooflines(sums, n_entries):
             continue
         probes = float(np.mean([x[pf] for x in sums]))
         ent = float(n_entries if ef is None else np.mean([x[ef] for x in sums]))
-        alg = BYTES_PER_ENTRY * ent + BYTES_PER_PROBE * probes
+        alg = float(np.mean([phase_alg_bytes(name, x, n_entries) for x in sums]))
         ach = alg / (ms / 1e3) / 1e9
         out[name] = {"kernel": phase_kernel(name, kern, sums), "ms": ms, "alg_bytes": alg, "probes": probes, "entries": ent,
                      "keys": keys, "achieved": ach, "frac": ach / PEAK_HBM_GBS}
@@ -115,6 +137,16 @@ WORKLOADS = {
                budget=1 << 22,
                gen=dict(threads_per_key=10, readers=5, n_values=5, process_limit=20, groups=10,
                         init_nil=True, p_info=0.02, p_invalid=0.01, nemesis_every=10000)),
+    # round 6: the north_star's own configuration -- ONE
+    # 10k-key history (C3's rank-0 history, seed 3) split by key over the N
+    # GPUs (jh_key_costs + LPT, shard.assign_keys): strong scaling. --shard r/N
+    # rehearses rank r's shard on one GPU
+    "c3s": dict(desc="C3 strong: ONE independent cas-register history of 10000 keys x ~1k entries (seed 3) "
+                     "split by key over the N GPUs with the window-sum cost model + LPT (jepsen_amd/shard.py)",
+                keys=10000, seed=3, cpu_keys=10000, cpu_keys_opt=10000, global_history=True, strong=True,
+                budget=1 << 22,
+                gen=dict(threads_per_key=10, readers=5, n_values=5, process_limit=20, groups=10,
+                         init_nil=True, p_info=0.02, p_invalid=0.01, nemesis_every=10000)),
     "c4": dict(desc="C4: independent cas-register, ONE history of 125000 x N keys (1M at N=8) generated "
                     "identically on every rank and split by key over the N GPUs with the window-sum cost "
                     "model + LPT (jepsen_amd/shard.py); each GPU checks its shard", keys=125000, seed=4,
@@ -156,11 +188,15 @@ def parse():
                          "0 (default since round 5): each rank checks its shard in one call -- the schedule "
                          "that continues deferred searches and hands long ones over, which the pool's "
                          "stage 2 (keys restarted on another rank) cannot")
+    ap.add_argument("--shard", default=None, metavar="R/N",
+                    help="one GPU rehearses rank R of an N-rank split of a global-history workload "
+                         "(c3s, c4): the same history, cost model and LPT split, R's shard only")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=INT",
                     help="a jh_lin_opts tuning field for A/B runs (e.g. handover_min=2048); "
                          "recorded in config.opts")
     a = ap.parse_args()
     a.tune = {k: int(v) for k, v in (o.split("=", 1) for o in a.opt)}
+    a.shard_rn = tuple(int(x) for x in a.shard.split("/")) if a.shard else None
     return a
 
 
@@ -204,15 +240,25 @@ def main():
         # threads), weighed by jh_key_costs, dealt out by LPT; this rank keeps
         # its keys' rows plus the un-keyed rows (shard.shard_history)
         from jepsen_amd import shard
+        # the split this process takes: its own rank of the launch, or (--shard
+        # R/N on one GPU) rank R of an N-rank split
+        s_rank, s_world = (rank, world) if args.shard_rn is None else args.shard_rn
+        if args.shard_rn is not None and (world != 1 or not 0 <= s_rank < s_world):
+            raise SystemExit("--shard R/N: one process, 0 <= R < N")
         t_g = time.perf_counter()
-        gcols, _ = synth.cas_register(n_keys=n_keys * world, ops_per_key=args.ops_per_key, seed=wl["seed"],
-                                      parts=16, **wl["gen"])
+        total_keys = n_keys if wl.get("strong") else n_keys * s_world
+        # c3s: C3's own rank-0 history (one generator thread, as the c3 line's),
+        # so its N = 1 case is the default line's history
+        gcols, _ = synth.cas_register(n_keys=total_keys, ops_per_key=args.ops_per_key, seed=wl["seed"],
+                                      parts=1 if wl.get("strong") else 16, **wl["gen"])
         t_s = time.perf_counter()
         costs = shard.key_costs(gcols)
-        owner = shard.assign_keys(costs, world)
-        cols, mine, _rows = shard.shard_history(gcols, owner, rank)
-        loads = np.bincount(owner, weights=costs, minlength=world)
+        owner = shard.assign_keys(costs, s_world)
+        cols, mine, _rows = shard.shard_history(gcols, owner, s_rank)
+        loads = np.bincount(owner, weights=costs, minlength=s_world)
         shard_info = {"global_keys": int(gcols.n_keys), "global_entries": int(gcols.n),
+                      "rank": s_rank, "world": s_world, "rehearsed": args.shard_rn is not None,
+                      "shard_keys": int(len(mine)), "shard_entries": int(cols.n),
                       "generate_s": t_s - t_g, "cost_and_split_s": time.perf_counter() - t_s,
                       "cost_model": "entries + window sum (jh_key_costs), LPT",
                       "max_over_mean_load": float(loads.max() / max(loads.mean(), 1.0))}
@@ -403,7 +449,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if wl.get("strong") else "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (seeded jepsen-shaped histories, jepsen_amd/csrc/gen.cpp)",
@@ -422,6 +468,9 @@ def main():
                        "phase1_span_ms": float(np.mean([x["p1_span_ms"] for x in sums])),
                        # round 5: deferred searches continued from phase 1's state
                        "resumed_keys": int(s.resumed), "resume_bytes": int(s.resume_bytes),
+                       # round 6: speculative dead-subtree enumerations by idle late helpers
+                       "spec": {"jobs": int(s.spec_jobs), "dead": int(s.spec_dead), "merges": int(s.spec_merges),
+                                "merged_nodes": int(s.spec_nodes)},
                        "phases": phase_table(sums), "opts": args.tune or None},
             "shard": shard_info,
             "pool": ({"mode": "two-stage (shard.two_stage_resident): phase 1 per rank, deferred keys' rows "
@@ -434,6 +483,18 @@ def main():
             "roofline": ({"bound": "hbm", "phase": dom, "kernel": phases[dom]["kernel"],
                           "achieved": phases[dom]["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                           "frac": phases[dom]["frac"],
+                          # round 6: the kernel time is this timed run's
+                          # HIP events around the phase's launch; rocprofv3's average of the
+                          # same kernel over a traced run of this command is in profiles/r06/
+                          # (the traced run's own line carries the frac that average gives)
+                          "time_source": "HIP events around the phase's launch, this timed run",
+                          "bytes_model": "8 B per table entry + 32 B per key of the keys the phase searches "
+                                         "+ 16 B per HBM memo probe (+ resume records read, phase 2)",
+                          "step": {"alg_bytes": BYTES_PER_ENTRY * float(total_entries) / max(1, world),
+                                   "achieved": BYTES_PER_ENTRY * total_entries / max(1, world) /
+                                               (elapsed / args.steps) / 1e9,
+                                   "note": "the whole step: 56 B per entry (7 int64 columns, SURVEY 8(d)) "
+                                           "over the step time, per GPU"},
                           # FETCH_SIZE + WRITE_SIZE per launch over this same history (tools/gpu_pmc.sh),
                           # measured in rocprofv3's serialized --pmc schedule
                           "traffic": tr["traffic_bytes"] if tr else None,
@@ -449,8 +510,7 @@ def main():
                           if tr and tr.get("alg_bytes_same_run") else None,
                           "traffic_source": traffic_src,
                           "kernel_ms": phases[dom]["ms"], "alg_bytes": phases[dom]["alg_bytes"],
-                          "note": "latency-bound tree search: one wave per key, LDS memo; bytes are 56 B per "
-                                  "entry of the keys the phase searches + 16 B per HBM memo probe (SURVEY 8(d))"}
+                          "note": "latency-bound tree search: one wave per key, LDS memo"}
                          if dom else None),
             "roofline_phases": phases,
             "cpu_baseline": cpu,

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define JH_ABI_VERSION 6
+#define JH_ABI_VERSION 7
 
 /* Return codes. Anything non-zero also writes a NUL-terminated message into
  * the caller's err buffer; the JNA shim throws ex-info and check-safe turns
@@ -157,6 +157,11 @@ typedef struct jh_history {
  * tests set this flag. */
 #define JH_LIN_EXACT_COUNT  1024
 #define JH_EXPLORED_UNCOUNTED (-3)
+/* Round 6: late helpers with no key of their own enumerate dead-subtree
+ * candidates posted by the helpers that run a key's exact search, which merge
+ * the dead ones (same verdicts and counts); this flag turns that off (A/B and
+ * the tests). */
+#define JH_LIN_NO_SPEC      2048
 
 typedef struct jh_lin_opts {
     int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */
@@ -257,6 +262,13 @@ typedef struct jh_summary {
      * continued (JH_LIN_NO_RESUME: 0), and the bytes of their records */
     int64_t resumed;
     int64_t resume_bytes;
+    /* ABI 7 (round 6): speculative dead-subtree enumerations by idle late
+     * helpers (JH_LIN_NO_SPEC: 0): jobs run, of which dead, dead results the
+     * searches merged and the nodes those merges added to their counts */
+    int64_t spec_jobs;
+    int64_t spec_dead;
+    int64_t spec_merges;
+    int64_t spec_nodes;
 } jh_summary;
 
 typedef struct jh_ctx jh_ctx;

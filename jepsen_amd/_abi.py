@@ -6,7 +6,7 @@ every struct layout.
 """
 import ctypes as C
 
-JH_ABI_VERSION = 6
+JH_ABI_VERSION = 7
 
 JH_OK, JH_EINVAL, JH_EUNSUPPORTED, JH_EDEVICE, JH_ENOMEM = 0, 1, 2, 3, 4
 TYPE_INVOKE, TYPE_OK, TYPE_FAIL, TYPE_INFO = 0, 1, 2, 3
@@ -63,6 +63,7 @@ LIN_STREAM = 256
 LIN_NO_RESUME = 512           # round 5: restart deferred keys instead of continuing them
 LIN_EXACT_COUNT = 1024        # round 5: WGL's exact count for every key (the parity tests)
 EXPLORED_UNCOUNTED = -3       # a valid key settled without the count pass
+LIN_NO_SPEC = 2048            # round 6: no speculative dead-subtree enumerations by idle helpers
 CAUSE_DEFERRED = 9
 
 
@@ -106,7 +107,10 @@ class JhSummary(C.Structure):
                 ("streamed", C.c_int64), ("p3_entries", C.c_int64), ("p2_start_ms", C.c_double),
                 ("p1_span_ms", C.c_double),
                 # ABI 6: deferred searches resumed by the heavy-key pass
-                ("resumed", C.c_int64), ("resume_bytes", C.c_int64)]
+                ("resumed", C.c_int64), ("resume_bytes", C.c_int64),
+                # ABI 7: speculative dead-subtree enumerations (round 6)
+                ("spec_jobs", C.c_int64), ("spec_dead", C.c_int64), ("spec_merges", C.c_int64),
+                ("spec_nodes", C.c_int64)]
 
 
 class JhLinConfig(C.Structure):

@@ -2631,7 +2631,40 @@ constexpr int WG_THREADS = JH_WG_THREADS;
 using MemoW = MemoCfg<11, 19>;
 constexpr uint32_t ACC_T = 1024, ACC_CAPF = 4, ACC_CAPMIN = 2048;
 constexpr int ACC_MAXROOTS = 65;    // X lies in the register ring: <= 64 frames + the current node
-constexpr int CMD_ENUM = 1, CMD_DONE = 2;
+constexpr int CMD_ENUM = 1, CMD_DONE = 2, CMD_MERGE = 3;
+
+// Round 6: speculative dead-subtree enumeration across workgroups (VERDICT r5
+// item 2). On a heavy valid key WGL's time is nearly all one dead subtree:
+// C3 rank 0's key 1086 spends 44 700 of its 46 490 inserts below one node at
+// depth 128 (28 layers, 38 levels deep), rank 4's key 1631 25 790 + 7 696
+// below two (tools/shape/wgl_shape.py) -- a few ms for a parallel
+// enumeration, tens of ms for the one-wave DFS, which cannot tell that
+// node's subtree is dead until it has walked all of it. A late helper that
+// runs a key's exact search (the main, dfs_acc) posts the open nodes of its
+// stack near the current one that have many inserts below them to this
+// board; late helpers with no key of their own take them and enumerate each
+// posted node's whole reachable set, with no memo (so nothing the main's
+// open nodes have not finished is pruned), up to a cap. A node whose
+// enumeration meets no terminal configuration is dead: the main, if the node
+// is still on its stack (same depth, same insert index), merges the set into
+// its memo -- the nodes not there yet are exactly what WGL inserts before
+// popping it (the argument of wg_enum_work: memo_X + Reach(X) is WGL's memo at
+// the pop, and everything inserted since X is in Reach(X)) -- adds their
+// number to its count and pops the node. A live result marks the node (and so
+// its ancestors) live. Verdicts, counts and failing rows stay WGL's.
+constexpr int SPEC_SLOTS = 64;         // one per lane of the main's wave
+constexpr int SPEC_PER_CHECK = 4;      // new posts per check of the main
+constexpr uint32_t SPEC_RES_CAP = 1u << 18;    // nodes per helper result buffer (2 MB)
+constexpr int SPEC_FREE = 0, SPEC_POSTED = 1, SPEC_CLAIMED = 2, SPEC_DEAD = 3, SPEC_LIVE = 4, SPEC_INC = 5,
+              SPEC_STALE = 6, SPEC_BUSY = 7;
+struct SpecSlot {
+    int32_t state, key;
+    uint32_t depth, seq;       // the node on the main's stack: depth and insert index
+    uint64_t cfg;              // its configuration (lk_make)
+    uint32_t cap, n;           // the enumeration's cap; a dead result's node count
+    int32_t helper, pad;       // the helper whose result buffer holds the nodes
+    uint64_t pad2;
+};
 constexpr int ENUM_LIVE = 1, ENUM_CAP = 2;
 
 struct WgShared {
@@ -2650,6 +2683,17 @@ struct WgShared {
     const uint32_t *woff;     // the key's window table (wtab_build)
     const uint32_t *wrq;
     const uint8_t *rpos;
+    // round 6, the spec board (see SpecSlot): an enumeration a helper runs for
+    // another workgroup's search keeps its new nodes (keep), ignores its own
+    // memo (nomemo) and stops when the slot goes stale (abort_state); a merge
+    // (CMD_MERGE) folds such a result into this workgroup's memo
+    uint64_t *keep;
+    uint32_t keep_n;
+    int nomemo;
+    const int32_t *abort_state;
+    const uint64_t *m_src;
+    uint32_t m_n, m_new, m_tmin, m_tmax;
+    int spec_slot, res_slot, wtab_key;
 };
 constexpr int WG_SH_OFF = (MemoW::LDS + 255) & ~255;
 constexpr int ESET = 2048;          // LDS set of the current layer's configurations (8-byte keys)
@@ -2685,6 +2729,14 @@ struct WgArgs {
     // streaming heavy-key pass: the sequential search's wave count on the
     // device (its early and late grids); d.live_n etc. make d.list live
     const int32_t *seq_waves_dev;
+    // round 6: the spec board (late helpers only; null: off), each helper's
+    // result buffer (spec_res_cap nodes), and the posting policy: nodes with
+    // at least spec_min inserts below them, within spec_dist levels of the
+    // current node, enumerated up to spec_mult x their inserts so far
+    SpecSlot *spec;
+    uint64_t *spec_res;
+    uint32_t spec_res_cap, spec_min, spec_mult, spec_dist;
+    int32_t *spec_q;           // the counters (q + Q_SPEC)
 };
 
 __device__ __forceinline__ uint64_t lk_make(uint32_t t, uint32_t s, uint64_t m) {
@@ -2733,6 +2785,7 @@ __device__ unsigned int g_prof_hbm, g_prof_gset, g_prof_rounds, g_prof_layers;
 __device__ unsigned long long g_prof_form, g_prof_close, g_prof_merge;
 __device__ __forceinline__ bool wg_memo_has(uint64_t k, const WgShared &sh, const uint64_t *memo,
                                             uint32_t cap_mask, unsigned long long &probes) {
+    if (sh.nomemo) return false;        // a spec enumeration: the whole reachable set
     const ulonglong2 *B = (const ulonglong2 *)(jh_lds + MemoW::OFF_MEMO);
     const uint32_t *bloom = (const uint32_t *)(jh_lds + MemoW::OFF_BLOOM);
     uint32_t h1, h2, b1, b2;
@@ -2896,6 +2949,10 @@ __device__ __forceinline__ void wg_enum_work(const WgArgs &W, WgShared &sh, int 
             // racing k_lin_bfs: a key it settled ends the enumeration as incomplete
             if (W.d.claim && __hip_atomic_load(&W.d.claim[sh.key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                 sh.status |= ENUM_CAP;
+            // a spec enumeration whose main no longer needs it
+            if (sh.abort_state &&
+                __hip_atomic_load(sh.abort_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == SPEC_STALE)
+                sh.status |= ENUM_CAP;
         }
         __syncthreads();
         const uint32_t tc = sh.t_cur, np = sh.npend, sel = sh.pend_sel;
@@ -3012,6 +3069,15 @@ __device__ __forceinline__ void wg_enum_work(const WgArgs &W, WgShared &sh, int 
             tmax = max(tmax, (uint32_t)__shfl_xor((int)tmax, o));
         }
         if (lane == 0) { atomicMin(&sh.tmin_new, tmin); atomicMax(&sh.tmax_new, tmax); }
+        if (sh.keep && sh.status == 0) {
+            // a spec enumeration's result: its new nodes, for the main to merge
+            for (uint32_t i = wt; i < end; i += WN) {
+                const uint64_t k = __hip_atomic_load(&work[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (k & LK_ROOT) continue;
+                sh.keep[atomicAdd(&sh.keep_n, 1u)] = k;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        }
         if (sh.merge && sh.status == 0) {
             uint32_t *bloom = (uint32_t *)(jh_lds + MemoW::OFF_BLOOM);
             for (uint32_t i = wt; i < end; i += WN) {
@@ -3050,6 +3116,44 @@ __device__ __forceinline__ void wg_enum_work(const WgArgs &W, WgShared &sh, int 
     // slots) is complete before any wave goes on: the next call's atomics and
     // the DFS's memo probes must not race a late store (workgroup scope: the
     // waves of a workgroup share this CU's L1)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// All waves (CMD_MERGE): fold a spec result -- the reachable set of a node of
+// this workgroup's stack that a helper found dead -- into the DFS memo (HBM
+// table + Bloom filter): the nodes not there yet are counted (sh.m_new) with
+// their layer range (sh.m_tmin / m_tmax: the merged range the DFS probes).
+__device__ void wg_merge(const WgArgs &W, WgShared &sh, int tid, uint64_t *memo, unsigned long long &probes) {
+    // the helper published the buffer at agent scope; drop any stale L1 copy
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t cap_mask = W.d.memo_cap - 1;
+    uint32_t *bloom = (uint32_t *)(jh_lds + MemoW::OFF_BLOOM);
+    const uint32_t n = sh.m_n;
+    const uint64_t *src = sh.m_src;
+    uint32_t nnew = 0, tmin = 0xFFFFFFFFu, tmax = 0;
+    for (uint32_t i = (uint32_t)tid; i < n; i += WG_THREADS) {
+        const uint64_t k = src[i];
+        if (wg_memo_has(k, sh, memo, cap_mask, probes)) continue;
+        hbm_insert(memo, cap_mask, sh.gen, lk_t(k), lk_s(k), lk_m(k));
+        uint32_t h1, h2;
+        lk_hash((uint32_t)k, (uint32_t)(k >> 32), h1, h2);
+        bloom_set2<MemoW>(bloom, lk_bl(h1), lk_bl(h2));
+        nnew++;
+        tmin = min(tmin, lk_t(k));
+        tmax = max(tmax, lk_t(k));
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        nnew += (uint32_t)__shfl_xor((int)nnew, o);
+        tmin = min(tmin, (uint32_t)__shfl_xor((int)tmin, o));
+        tmax = max(tmax, (uint32_t)__shfl_xor((int)tmax, o));
+    }
+    if ((tid & 63) == 0) {
+        atomicAdd(&sh.m_new, nnew);
+        atomicMin(&sh.m_tmin, tmin);
+        atomicMax(&sh.m_tmax, tmax);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -3241,6 +3345,7 @@ __device__ int dfs_acc(const WgArgs &W, WgShared &sh, const KeyInfo &K, const ch
         if (n_roots > W.pend_cap) return 2;
         if (cap <= 0) return 2;
         if (!wtab_ready) {
+            if (lane == 0) sh.wtab_key = -1;        // (a spec job's cached table is gone)
             uint32_t *woff = (uint32_t *)wtab;
             uint32_t *wrqt = (uint32_t *)(wtab + (((n_ok + 1) * 4 + 255) & ~255u));
             uint8_t *rp = (uint8_t *)((char *)wrqt + ((n_ok * 40 * 4 + 255) & ~255u));
@@ -3343,6 +3448,112 @@ insert:
                         c = 1;
                 }
                 if (readlane(c, 0)) { verdict = JH_CANCELLED; goto done; }
+            }
+            if (W.spec) {
+                // Round 6, the spec board (SpecSlot): this search's results first.
+                SpecSlot *SB = W.spec;
+                const int st = __hip_atomic_load(&SB[lane].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const bool mine = st >= SPEC_DEAD && st <= SPEC_INC && SB[lane].key == key;
+                const uint32_t sd = mine ? SB[lane].depth : 0u, sq = mine ? SB[lane].seq : 0u;
+                const uint32_t fsq = (uint32_t)__shfl((int)f_seq, (int)(sd & 63));
+                // still on the stack: same depth, same insert index
+                const bool on = mine && sd >= 1 && sd >= ring_lo && sd <= depth && (sd == depth ? cur_seq : fsq) == sq;
+                int lmax = on && st == SPEC_LIVE ? (int)sd : -1;          // live: it and its ancestors
+                for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, __shfl_xor(lmax, o));
+                if (lmax > l_live) l_live = lmax;
+                const bool dd = on && st == SPEC_DEAD && (int)sd > l_live;
+                uint32_t dmin = dd ? sd : 0xFFFFFFFFu;                      // the shallowest dead one
+                for (int o = 32; o > 0; o >>= 1) dmin = min(dmin, (uint32_t)__shfl_xor((int)dmin, o));
+                const uint64_t pm = ballot(dd && sd == dmin);
+                const int pk = pm ? __builtin_ctzll(pm) : -1;
+                if (mine && lane != pk)
+                    __hip_atomic_store(&SB[lane].state, SPEC_FREE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                if (pk >= 0) {
+                    // merge the dead node's reachable set (every wave: wg_merge) and pop it
+                    const uint32_t rn = (uint32_t)readlane((int)(lane == pk ? SB[lane].n : 0u), pk);
+                    const int rh = readlane(lane == pk ? SB[lane].helper : 0, pk);
+                    if (lane == 0) {
+                        sh.cmd = CMD_MERGE; sh.m_src = W.spec_res + (size_t)rh * W.spec_res_cap; sh.m_n = rn;
+                        sh.m_new = 0; sh.m_tmin = 0xFFFFFFFFu; sh.m_tmax = 0;
+                        sh.theta = theta; sh.acc_lo = acc_lo; sh.acc_hi = acc_hi; sh.gen = gen; sh.nomemo = 0;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __syncthreads();
+                    wg_merge(W, sh, lane, memo, my_probes);
+                    if (lane == pk)
+                        __hip_atomic_store(&SB[pk].state, SPEC_FREE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t mnew = sh.m_new;
+                    if (lane == 0) {
+                        atomicAdd((unsigned long long *)W.spec_q, (unsigned long long)mnew);
+                        atomicAdd(&W.spec_q[2], 1);
+                    }
+                    ins += mnew;
+                    if (ins > budget) { ins = budget; verdict = JH_UNKNOWN; goto done; }
+                    if (mnew) {
+                        tmax = max(tmax, sh.m_tmax);
+                        acc_lo = acc_lo > acc_hi ? sh.m_tmin : min(acc_lo, sh.m_tmin);
+                        acc_hi = max(acc_hi, sh.m_tmax);
+                    }
+                    next_acc = ins + acc_t;
+                    chk = min(budget, min(ins + chk_step, next_acc));
+                    depth = dmin;
+                    goto pop;                  // pops node dmin
+                }
+                // New posts: the open nodes within spec_dist levels of the current
+                // one (the register ring), below the deepest known live node, with
+                // spec_min inserts below them and never posted (or 4x as many since),
+                // deepest first, into free slots; posting counts as an attempt (inc)
+                uint64_t freem = ballot(st == SPEC_FREE || mine);
+                const uint32_t dlo = max(max(max(ring_lo, 1u), (uint32_t)(l_live + 1)),
+                                         depth > W.spec_dist ? depth - W.spec_dist : 0u);
+                auto elig = [&](uint32_t sqv, uint32_t inc) {
+                    const uint32_t b = ins - sqv;
+                    return b >= W.spec_min && (inc == 0 || b >= 4 * inc);
+                };
+                auto post = [&](uint32_t d, uint64_t cfgk, uint32_t sqv) -> bool {
+                    while (freem) {
+                        const int sl = __builtin_ctzll(freem);
+                        freem &= freem - 1;
+                        int ok = 0;
+                        if (lane == 0) {
+                            int exp = SPEC_FREE;
+                            ok = __hip_atomic_compare_exchange_strong(&SB[sl].state, &exp, SPEC_BUSY, __ATOMIC_ACQUIRE,
+                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (ok) {
+                                SB[sl].key = key; SB[sl].depth = d; SB[sl].seq = sqv; SB[sl].cfg = cfgk;
+                                SB[sl].cap = min(W.spec_res_cap - 1, max(8192u, W.spec_mult * (ins - sqv)));
+                                SB[sl].n = 0; SB[sl].helper = -1;
+                                __hip_atomic_store(&SB[sl].state, SPEC_POSTED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                            }
+                        }
+                        if (readlane(ok, 0)) return true;
+                    }
+                    return false;
+                };
+                int nposted = 0;
+                if (depth >= dlo && depth >= 1 && elig(cur_seq, cur_inc) && post(depth, lk_make(t, s, mask), cur_seq)) {
+                    cur_inc = ins - cur_seq;
+                    nposted++;
+                }
+                {
+                    const uint32_t fd = ring_lo + (((uint32_t)lane - ring_lo) & 63);
+                    const uint64_t cm = ballot(fd < depth && fd >= dlo && elig(f_seq, f_inc));
+                    const uint32_t rs = ring_lo & 63;
+                    uint64_t rot = rs ? ((cm >> rs) | (cm << (64 - rs))) : cm;
+                    while (rot && freem && nposted < SPEC_PER_CHECK) {
+                        const int q = 63 - __builtin_clzll(rot);
+                        rot &= ~(1ULL << q);
+                        const uint32_t d = ring_lo + (uint32_t)q;
+                        const int ln = (int)(d & 63);
+                        const uint32_t qs = (uint32_t)readlane((int)f_seq, ln);
+                        const uint64_t ck = lk_make((uint32_t)readlane((int)f_ti, ln) >> 6, (uint32_t)readlane((int)f_s, ln),
+                                                    ((uint64_t)(uint32_t)readlane((int)fm_hi, ln) << 32) |
+                                                    (uint32_t)readlane((int)fm_lo, ln));
+                        if (!post(d, ck, qs)) break;
+                        if (lane == ln) f_inc = ins - qs;
+                        nposted++;
+                    }
+                }
             }
             if (ins >= next_acc) {
                 next_acc = ins + acc_t;
@@ -3624,9 +3835,122 @@ __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned 
         }
         __syncthreads();
         if (sh.key >= 0) return;
+        if (W.spec && sh.key == -2 && tid < 64) {
+            // round 6: no key of its own to race -- a posted node of another
+            // helper's search (SpecSlot), the smallest cap first, once the main
+            // has released this helper's last dead result (its buffer)
+            SpecSlot *SB = W.spec;
+            const int lane = tid;
+            bool busy = false;
+            const int rs = sh.res_slot;
+            if (rs >= 0)
+                busy = __hip_atomic_load(&SB[rs].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == SPEC_DEAD &&
+                       SB[rs].helper == (int)blockIdx.x;
+            if (!busy) {
+                const int st = __hip_atomic_load(&SB[lane].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const int k = SB[lane].key;
+                const bool cand = st == SPEC_POSTED && k >= 0 &&
+                                  !__hip_atomic_load(&A.claim[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                unsigned long long c = cand ? ((unsigned long long)SB[lane].cap << 8) | (unsigned)lane : ~0ULL;
+                for (int o = 32; o > 0; o >>= 1) c = min(c, (unsigned long long)__shfl_xor(c, o));
+                if (c != ~0ULL && lane == 0) {
+                    const int sl = (int)(c & 255);
+                    int exp = SPEC_POSTED;
+                    if (__hip_atomic_compare_exchange_strong(&SB[sl].state, &exp, SPEC_CLAIMED, __ATOMIC_ACQUIRE,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        sh.res_slot = -1;
+                        sh.spec_slot = sl;
+                        sh.key = -4;
+                    } else {
+                        sh.key = -3;              // lost it: scan again at once
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (sh.key == -4) return;
         if (sh.key == -2)
             for (int k = 0; k < 16; k++) __builtin_amdgcn_s_sleep(127);   // ~50 us between scans
         __syncthreads();
+    }
+}
+
+// Round 6: a late helper's spec job (wave 0 with the other waves in
+// wg_enum_work): the posted node's whole reachable set, no memo, up to the
+// slot's cap; the result goes to the slot (dead: the new nodes in this
+// helper's buffer, which stays the main's until it frees the slot).
+__device__ void spec_enum(const WgArgs &W, WgShared &sh, int lane, char *wtab, uint64_t *gset, uint64_t *work,
+                          uint64_t *memo, uint64_t *pend, unsigned long long &probes) {
+    const DfsArgs &A = W.d;
+    SpecSlot *S = W.spec + sh.spec_slot;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int key = S->key;
+    const uint64_t cfg = S->cfg;
+    const uint32_t cap = S->cap;
+    if (sh.wtab_key != key) {
+        const KeyMeta mt = A.meta[key];
+        KeyInfo K;
+        K.n_ops = mt.n_ops; K.n_ok = mt.n_ok; K.sumW = mt.pad; K.s0 = 0; K.s1 = 0;
+        const uint32_t n_ok = (uint32_t)K.n_ok;
+        uint32_t *woff = (uint32_t *)wtab;
+        uint32_t *wrqt = (uint32_t *)(wtab + (((n_ok + 1) * 4 + 255) & ~255u));
+        uint8_t *rp = (uint8_t *)((char *)wrqt + ((n_ok * 40 * 4 + 255) & ~255u));
+        wtab_build(K, A.tables + mt.off, lane, woff, wrqt, rp);
+        if (lane == 0) { sh.woff = woff; sh.wrq = wrqt; sh.rpos = rp; sh.wtab_key = key; sh.n_ok = n_ok; }
+    }
+    uint32_t c = min(cap, W.spec_res_cap - 1);
+    c = min(c, W.work_cap - 16384u - 2u);
+    if (lane == 0) {
+        __hip_atomic_store(&pend[0], cfg | LK_ROOT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        sh.n_ok = (uint32_t)A.meta[key].n_ok;
+        sh.cmd = CMD_ENUM; sh.merge = 0; sh.status = 0; sh.key = key;
+        sh.n_roots = 1; sh.theta = 0; sh.acc_lo = 1; sh.acc_hi = 0; sh.gen = 0;
+        sh.cap_total = 1 + c;
+        sh.head = 0; sh.tail = 0; sh.active = 0; sh.tmin_new = 0xFFFFFFFFu; sh.tmax_new = 0;
+        sh.t_next = lk_t(cfg); sh.npend = 1; sh.pend_sel = 0; sh.gset_used = 0;
+        sh.keep = W.spec_res + (size_t)blockIdx.x * W.spec_res_cap; sh.keep_n = 0;
+        sh.nomemo = 1; sh.abort_state = &S->state;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();                        // the other waves join wg_enum_work
+    wg_enum_work(W, sh, lane, gset, work, memo, pend, probes);
+    const int st = sh.status;
+    const int res = st == 0 ? SPEC_DEAD : (st & ENUM_LIVE) ? SPEC_LIVE : SPEC_INC;
+    if (lane == 0) {
+        atomicAdd(&W.spec_q[3], 1);
+        if (res == SPEC_DEAD) { S->n = sh.keep_n; S->helper = (int)blockIdx.x; atomicAdd(&W.spec_q[4], 1); }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        int exp = SPEC_CLAIMED;
+        if (__hip_atomic_compare_exchange_strong(&S->state, &exp, res, __ATOMIC_RELEASE, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+            if (res == SPEC_DEAD) sh.res_slot = sh.spec_slot;
+        } else {
+            // stale: the main has left (or moved on); the slot is free again
+            __hip_atomic_store(&S->state, SPEC_FREE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        sh.keep = nullptr; sh.nomemo = 0; sh.abort_state = nullptr;
+        sh.cmd = CMD_DONE;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();                        // releases the other waves
+}
+
+// Round 6: a main leaving its key gives back every slot of it: posted ones
+// freed, claimed ones marked stale (their helper stops and frees them),
+// results freed.
+__device__ void spec_release(const WgArgs &W, int key, int lane) {
+    SpecSlot *SB = W.spec;
+    for (;;) {
+        const int st = __hip_atomic_load(&SB[lane].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const bool mine = st != SPEC_FREE && st != SPEC_STALE && st != SPEC_BUSY && SB[lane].key == key;
+        bool retry = false;
+        if (mine) {
+            int exp = st;
+            retry = !__hip_atomic_compare_exchange_strong(&SB[lane].state, &exp,
+                                                          st == SPEC_CLAIMED ? SPEC_STALE : SPEC_FREE,
+                                                          __ATOMIC_RELEASE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!ballot(retry)) break;
     }
 }
 
@@ -3643,6 +3967,11 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
     uint64_t *pend = W.pend + (size_t)blockIdx.x * 2 * W.pend_cap;
     unsigned long long my_probes = 0;
     const unsigned long long t_enter = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+        sh.keep = nullptr; sh.keep_n = 0; sh.nomemo = 0; sh.abort_state = nullptr;
+        sh.spec_slot = -1; sh.res_slot = -1; sh.wtab_key = -1;
+    }
+    __syncthreads();
     for (;;) {
         if (W.seq_start) {
             wg_helper_pick(W, sh, tid, t_enter);
@@ -3653,6 +3982,21 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
         }
         __syncthreads();
         const int key = sh.key;
+        if (key == -4) {
+            // round 6: a spec job for another helper's search
+            if (wid == 0) {
+                spec_enum(W, sh, lane, wtab, gset, work, memo, pend, my_probes);
+            } else {
+                for (;;) {
+                    __syncthreads();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    if (sh.cmd == CMD_DONE) break;
+                    wg_enum_work(W, sh, tid, gset, work, memo, pend, my_probes);
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         if (key < 0) break;
         const KeyMeta mt = A.meta[key];
         if (!(A.states8 && mt.maxw <= 40)) {      // WIDE keys: k_lin_seq3<false>
@@ -3669,6 +4013,7 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
             const int verdict = dfs_acc<MemoW>(W, sh, K, A.tables + mt.off, key, lane, memo, stack, stage, gset,
                                                work, wtab, pend, inserts, tmax, my_probes);
             TL_REC(A.tl, key, 5);
+            if (W.spec) spec_release(W, key, lane);
             jh_key_verdict v;
             v.valid = verdict;
             v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
@@ -3692,10 +4037,11 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
             __syncthreads();                    // releases the helpers
         } else {
             for (;;) {
-                __syncthreads();                // wave 0's enumeration request, or the end of the key
+                __syncthreads();                // wave 0's enumeration / merge request, or the end of the key
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 if (sh.cmd == CMD_DONE) break;
-                wg_enum_work(W, sh, tid, gset, work, memo, pend, my_probes);
+                if (sh.cmd == CMD_MERGE) wg_merge(W, sh, tid, memo, my_probes);
+                else wg_enum_work(W, sh, tid, gset, work, memo, pend, my_probes);
             }
         }
         __syncthreads();
@@ -6013,7 +6359,7 @@ static int fit_units(jh_ctx *ctx, int want, uint64_t per_unit, std::initializer_
 
 // words of the per-call counter block q (device): queues, list lengths, probe
 // and entry counters of the phases
-constexpr int Q_WORDS = 96;
+constexpr int Q_WORDS = 104;
 constexpr int Q_ENT_ALL = 24, Q_DEFER_L = 29, Q_DEFER_W = 30, Q_DEFER3W = 31;
 constexpr int Q_PROBES_HELP = 32, Q_PROBES_P3 = 34, Q_PROBES_WIDE = 36;
 constexpr int Q_ENT_LEAN = 40, Q_ENT_WIDE = 42, Q_ENT_XW = 44;
@@ -6025,6 +6371,7 @@ constexpr int Q_P1_DONE = 64, Q_SEQ_WAVES = 65, Q_BFS_QUEUE = 66;
 constexpr int Q_T_BFS = 68, Q_T_LEAN = 72, Q_T_XW = 76, Q_T_P1 = 80;
 constexpr int Q_ENT_P3 = 84;        // entries of the LEAN keys restarted in phase 3
 constexpr int Q_RS_USED = 88;       // [88..89] resume records' bytes, [90] records published (round 5)
+constexpr int Q_SPEC = 96;          // round 6: [96..97] merged nodes, [98] merges, [99] spec jobs, [100] dead results
 // LEAN sequential waves launched with the BFS while phase 1 still runs (the
 // rest start behind phase 1): enough for the keys deferred before it ends
 constexpr int EARLY_LEAN_WAVES = 128;
@@ -6628,6 +6975,19 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             if (opts && opts->helper_late_us > 0) late_us = (uint64_t)opts->helper_late_us;
             if (lflags & JH_LIN_HELPERS_NOW) late_us = 0;
             wh.late_ticks = late_us * 100;     // s_memrealtime: 100 MHz
+            // round 6: the spec board (SpecSlot), unless JH_LIN_NO_SPEC
+            if (!(lflags & JH_LIN_NO_SPEC)) {
+                wh.spec = ctx->ws<SpecSlot>(WS_SPEC, SPEC_SLOTS);
+                HIP_TRY(hipMemsetAsync(wh.spec, 0, sizeof(SpecSlot) * SPEC_SLOTS, st));
+                wh.spec_res_cap = SPEC_RES_CAP;
+                wh.spec_res = ctx->ws<uint64_t>(WS_SPEC_RES, (size_t)n_wg * SPEC_RES_CAP);
+                wh.spec_min = 512; wh.spec_mult = 32; wh.spec_dist = 64;
+                wh.spec_q = q + Q_SPEC;
+                if (const char *e = tune_env("JH_SPEC_MIN")) wh.spec_min = (uint32_t)std::max(1, atoi(e));
+                if (const char *e = tune_env("JH_SPEC_MULT")) wh.spec_mult = (uint32_t)std::max(1, atoi(e));
+                if (const char *e = tune_env("JH_SPEC_DIST")) wh.spec_dist = (uint32_t)std::max(1, atoi(e));
+                if (const char *e = tune_env("JH_SPEC")) if (!atoi(e)) wh.spec = nullptr;
+            }
         }
         const int wmax = std::max(waves2, waves3);
         Frame *stack2 = waves2 > 0 ? ctx->ws<Frame>(WS_STACK_DEEP, (size_t)wmax * stack_cap) : nullptr;
@@ -7346,6 +7706,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         sum->p3_entries = q64(qh, Q_ENT_P3);
         sum->p2_start_ms = -1; sum->p1_span_ms = 0;
         sum->resumed = resume ? qh[Q_RS_USED + 2] : 0;
+        sum->spec_nodes = q64(qh, Q_SPEC); sum->spec_merges = qh[Q_SPEC + 2];
+        sum->spec_jobs = qh[Q_SPEC + 3]; sum->spec_dead = qh[Q_SPEC + 4];
         sum->resume_bytes = resume ? q64(qh, Q_RS_USED) : 0;
         // an engine's own span from its s_memrealtime words (100 MHz): [first key, last wave end]
         auto span_ms = [&](int w) {

@@ -614,7 +614,9 @@ def test_uncounted_early_emit(ctx, case):
         g, _ = ctx.check_cas_independent(cols, budget=1 << 22, exact_count=False)
         c, _ = oracle.check_cas_independent(cols, budget=1 << 22, threads=16)
     unc = g["explored"] == A.EXPLORED_UNCOUNTED
-    assert unc.sum() >= 5, unc.sum()
+    # the BFS alone settles many valid keys; on C3 the race leaves it the few
+    # it wins (one on seed 3, as the bench's parity_detail reports)
+    assert unc.sum() >= (5 if case == "bfs_only" else 1), unc.sum()
     assert (c["valid"][unc] == A.VALID).all()
     for f in ("valid", "cause", "fail_entry"):
         bad = np.nonzero(g[f] != c[f])[0]
@@ -648,3 +650,32 @@ def test_configs_list_dropped_reads_device(ctx, seed):
         if q < 0 or cols.type[q] == A.TYPE_INFO or (cols.type[q] == A.TYPE_OK and cols.value[q] == A.NIL):
             noop.add(r)
     assert sum(1 for k in keys if g[int(k)] and any(set(p) & noop for _, _, p, _ in g[int(k)])) >= 5
+
+
+@pytest.mark.parametrize("rank,keys", [(0, [1086, 8979, 4457, 8190]), (4, [1631, 4356])])
+def test_spec_dead_subtrees(ctx, rank, keys):
+    """Round 6: idle late helpers enumerate dead-subtree
+    candidates the key's exact search posts (SpecSlot) and the search merges
+    the dead ones: on the C3 keys that end the step (rank 0's 1086 / 8979 /
+    4457 / 8190, rank 4's 1631), one big dead subtree each
+    (tools/shape/wgl_shape.py), every field -- WGL's count included -- equals
+    the oracle's, with merges made, at the full budget and at one the merged
+    searches run into; the same without the board (JH_LIN_NO_SPEC)."""
+    from jepsen_amd import shard
+    from bench import WORKLOADS
+    wl = WORKLOADS["c3"]
+    cols, _ = synth.cas_register(n_keys=wl["keys"], ops_per_key=500, seed=wl["seed"] + 7919 * rank, **wl["gen"])
+    own = np.ones(cols.n_keys, np.int64)
+    own[keys] = 0
+    sub, mine, _ = shard.shard_history(cols, own, 0)
+    merged = 0
+    for budget in (1 << 22, 20000):
+        c, _ = oracle.check_cas_independent(sub, budget=budget, threads=8)
+        g, s = ctx.check_cas_independent(sub, budget=budget, flags=A.LIN_HELPERS_NOW)
+        _same(g, c)
+        merged += s.spec_merges
+        assert s.spec_nodes >= 0 and s.spec_dead >= s.spec_merges
+        g2, s2 = ctx.check_cas_independent(sub, budget=budget, flags=A.LIN_HELPERS_NOW | A.LIN_NO_SPEC)
+        _same(g2, c)
+        assert s2.spec_jobs == 0 and s2.spec_merges == 0
+    assert merged > 0

@@ -149,5 +149,16 @@ ingest)
   L=$R/jepsen_amd/variants/libjh_$1.so
   JH_LIB=$L JH_INGEST_TRACE=1 timeout -k 10 300 python -u tools/ingest_probe.py > $O/ingest_packed.log 2>&1 || exit 1
   JH_LIB=$L JH_INGEST_PLAIN=1 timeout -k 10 300 python -u tools/ingest_probe.py > $O/ingest_plain.log 2>&1 ;;
+probe)
+  # per-key engine traces on a -DJH_TUNING variant: probe <v> "<env VAR=v,...>" <rank> <key>...
+  V=$1; E=$2; RK=$3; shift 3
+  env $(echo $E | tr ',' ' ') JH_LIB=$R/jepsen_amd/variants/libjh_$V.so timeout -k 10 150 python -u tools/key_probe.py c3 $RK "$@" > $O/probe_${V}_r${RK}_$(echo $E | tr ',=' '__').log 2>&1 ;;
+strong)
+  # C3 strong scaling (one 10k-key history split by key): every shard of N = 2, 4, 8 on this GPU
+  for n in 2 4 8; do
+    for rk in $(seq 0 $((n - 1))); do
+      timeout -k 10 150 python -u bench.py --workload c3s --shard $rk/$n --no-cpu --e2e 0 --no-parity --steps 5 --warmup 1 "$@" > $O/c3s_${rk}of${n}.json 2> $O/c3s_${rk}of${n}.err || exit 1
+    done
+  done ;;
 *) echo "unknown part $PART"; exit 2 ;;
 esac

@@ -36,4 +36,5 @@ for label, kw in [("race", {}), ("bfs-only", {"flags": A.LIN_BFS_ONLY}), ("no-he
     ms = (time.perf_counter() - t0) * 1e3
     print(json.dumps({"run": label, "keys": mine.tolist(), "wall_ms": round(ms, 3), "device_ms": s.device_ms,
                       "valid": v["valid"].tolist(), "explored": v["explored"].tolist(),
-                      "seq_ms": s.seq_ms, "bfs_ms": s.bfs_ms, "n_deferred": s.n_deferred}), flush=True)
+                      "seq_ms": s.seq_ms, "bfs_ms": s.bfs_ms, "n_deferred": s.n_deferred,
+                      "spec": [s.spec_jobs, s.spec_dead, s.spec_merges, s.spec_nodes]}), flush=True)

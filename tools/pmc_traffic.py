@@ -5,7 +5,7 @@ written as the JSON bench.py puts into its roofline object (`traffic`,
 
     python tools/pmc_traffic.py <pmc-dir> <kernel-substring> <workload> <seed> [bench-label]
 
--> profiles/r05/traffic_<workload>_s<seed>_<kernel>.json (bench.traffic_name).
+-> profiles/r06/traffic_<workload>_s<seed>_<kernel>.json (bench.traffic_name).
 Both counters are in KiB. The guide's gfx950 calibration: FETCH_SIZE reports
 1/2 of the bytes of wide (16 B/lane) coalesced streaming reads, WRITE_SIZE is
 exact for 16 B/lane streaming stores; other access widths are uncalibrated.
@@ -23,7 +23,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from bench import BYTES_PER_ENTRY, BYTES_PER_PROBE, PHASES, TRAFFIC_DIR, traffic_name  # noqa: E402
+from bench import PHASES, TRAFFIC_DIR, phase_alg_bytes, traffic_name  # noqa: E402
 
 
 def per_launch(d, counter, kernel):
@@ -56,7 +56,7 @@ def main():
         for name, (tf, pf, ef, kf, kern) in PHASES.items():
             if kern.split("<")[0] in label and (("<" not in label) or kern in label) and d.get(tf, 0) > 0:
                 ent = d["entries"] if ef is None else d[ef]
-                alg[log] = BYTES_PER_ENTRY * ent + BYTES_PER_PROBE * d[pf]
+                alg[log] = phase_alg_bytes(name, d, d["entries"])
                 ents.append(ent); probes.append(d[pf]); ms.append(d[tf])
                 break
     # every launch of the kernel in a pass (reps calls) counts; per launch = mean

@@ -314,6 +314,13 @@ int jh_check_cas_independent(jh_ctx *ctx, const jh_history *h,
 int jh_key_index(jh_ctx *ctx, const jh_history *h, int64_t *key_off, int64_t *rows,
                  char *err, size_t errlen);
 
+/* Round 6: the columns of a host history exactly as the device sees them
+ * after staging (the packed host-buffer path for >= 2 M rows, plain copies
+ * below): process, type, f, key, value, value2 -- n int64 each, in that
+ * order, into out (6 * n; the key block is left as is without a key column).
+ * Checks nothing: a maintainer's (and the tests') view of the staging. */
+int jh_stage_history(jh_ctx *ctx, const jh_history *h, int64_t *out, char *err, size_t errlen);
+
 /* knossos' :configs (checker.clj:146-158 passes the analysis through and
  * keeps (take 10 ...) of them), from the JIT-linearization analysis
  * (:algorithm :linear; doc/tutorial/04-checker.md:126-138 prints one).

@@ -39,6 +39,7 @@ def lib():
             L.jh_key_index.argtypes = [C.c_void_p, H, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                        C.c_char_p, C.c_size_t]
             L.jh_key_costs.argtypes = [C.POINTER(A.JhHistory), C.POINTER(C.c_int64), C.c_char_p, C.c_size_t]
+            L.jh_stage_history.argtypes = [C.c_void_p, H, C.POINTER(C.c_int64), C.c_char_p, C.c_size_t]
             L.jh_close.argtypes = [C.c_void_p]
             L.jh_close.restype = None
             L.jh_check_cas_independent.argtypes = [C.c_void_p, H, C.POINTER(A.JhLinOpts),
@@ -97,6 +98,7 @@ def lib():
 
 
 EXPORTED_SYMBOLS = ["jh_version", "jh_open", "jh_open_multi", "jh_open_devices", "jh_n_devices", "jh_key_costs", "jh_key_index",
+                    "jh_stage_history",
                     "jh_close", "jh_check_cas_independent",
                     "jh_check_cas", "jh_check_cas_independent_device", "jh_lin_configs", "jh_check_counter",
                     "jh_check_set", "jh_check_set_bitmaps", "jh_check_set_full", "jh_check_set_full_opts", "jh_check_total_queue", "jh_check_queue",
@@ -213,6 +215,16 @@ class Context:
                                 err, len(err))
         _raise(rc, err)
         return off, rows[:cols.n]
+
+    def stage_history(self, cols):
+        """jh_stage_history: the six int64 columns (process, type, f, key,
+        value, value2) as the device holds them after staging the host
+        history -- the packed path for >= 2 M rows (jh_ingest.hip)."""
+        h = A.make_history(cols)
+        out = np.zeros(6 * max(cols.n, 1), np.int64)
+        err = C.create_string_buffer(512)
+        _raise(lib().jh_stage_history(self._h, C.byref(h), A.ptr64(out), err, len(err)), err)
+        return out[:6 * cols.n].reshape(6, cols.n)
 
     # -- linearizability ---------------------------------------------------
     def check_cas_independent(self, cols, init=None, budget=None, **tune):

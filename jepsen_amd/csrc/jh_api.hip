@@ -312,6 +312,24 @@ int jh_lin_configs(jh_ctx *ctx, const jh_history *h, const jh_lin_opts *opts, co
     });
 }
 
+int jh_stage_history(jh_ctx *ctx, const jh_history *h, int64_t *out, char *err, size_t errlen) {
+    if (!ctx || !out) { set_err(err, errlen, "null argument"); return JH_EINVAL; }
+    ctx = primary(ctx);
+    std::lock_guard<std::mutex> g(ctx->mu);
+    return guarded(err, errlen, [&] {
+        check_hist(h);
+        if (h->on_device) throw_jh(JH_EINVAL, "jh_stage_history takes a host history");
+        HIP_TRY(hipSetDevice(ctx->device));
+        const jh_history d = stage_history(ctx, h, h->key != nullptr, false);
+        const int64_t *cols[6] = {d.process, d.type, d.f, d.key, d.value, d.value2};
+        for (int c = 0; c < 6; c++)
+            if (cols[c] && h->n > 0)
+                HIP_TRY(hipMemcpyAsync(out + (size_t)c * h->n, cols[c], sizeof(int64_t) * h->n, hipMemcpyDeviceToHost,
+                                       ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    });
+}
+
 int jh_key_index(jh_ctx *ctx, const jh_history *h, int64_t *key_off, int64_t *rows, char *err,
                  size_t errlen) {
     if (!ctx || !key_off || (!rows && h && h->n > 0)) { set_err(err, errlen, "null argument"); return JH_EINVAL; }

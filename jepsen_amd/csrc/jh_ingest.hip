@@ -18,6 +18,7 @@
 #include <condition_variable>
 #include <functional>
 #include <chrono>
+#include <memory>
 
 namespace {
 
@@ -53,7 +54,9 @@ struct Pool {
             if (--pending == 0) done.notify_all();
         }
     }
+    std::mutex serial;              // one job at a time: contexts share the pool (jh_open_multi's threads)
     void run(const std::function<void(int)> &f) {
+        std::lock_guard<std::mutex> one(serial);
         {
             std::lock_guard<std::mutex> lk(m);
             job = f;
@@ -120,15 +123,24 @@ __global__ void __launch_bounds__(256) k_widen_cols(WidenArgs A) {
     }
 }
 
+// Round 6: ONE packing pool per process, shared by every
+// context (a JVM may open many), created on first use and kept to the end.
+Pool &packing_pool() {
+    static Pool *p = new Pool((int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()),
+                                                      ING_MAX_THREADS));
+    return *p;
+}
+
 }  // namespace
 
+// Per context: two pinned chunk buffers and their device twins (7 columns x
+// ING_CHUNK rows x 8 B = 56 MB each, 112 MB pinned host + 112 MB HBM), made on
+// the first packed call; INTEGRATION.md lists them.
 struct Ingest {
-    Pool pool;
     void *pin[2] = {nullptr, nullptr};      // packed chunk, host side (pinned)
     void *dev[2] = {nullptr, nullptr};      // packed chunk, device side
     hipEvent_t ev[2] = {nullptr, nullptr};  // chunk's DMA out of pin[b] done
     bool rec[2] = {false, false};           // ev[b] recorded (by this call or an earlier one)
-    explicit Ingest(int k) : pool(k) {}
     ~Ingest() {
         for (int b = 0; b < 2; b++) {
             if (pin[b]) (void)hipHostFree(pin[b]);
@@ -158,20 +170,21 @@ static bool ingest_plain() {
 bool ingest_columns(jh_ctx *ctx, const int64_t *const src[ING_COLS], int64_t *const dst[ING_COLS], int64_t n,
                     hipStream_t st) {
     if (n < ING_MIN || ingest_plain()) return false;
+    const size_t region = (size_t)ING_CHUNK * 8;              // one column's room in a chunk buffer
     if (!ctx->ingest) {
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        ctx->ingest = new Ingest((int)std::min<unsigned>(hw, ING_MAX_THREADS));
+        // every buffer first, then the context's: a failed allocation leaves
+        // nothing half made -- the Ingest destructor frees what was
+        std::unique_ptr<Ingest> fresh(new Ingest());
+        for (int b = 0; b < 2; b++) {
+            HIP_TRY(hipHostMalloc(&fresh->pin[b], region * ING_COLS, hipHostMallocNonCoherent));   // CPU-cached: the packers write it byte by byte
+            HIP_TRY(hipMalloc(&fresh->dev[b], region * ING_COLS));
+            HIP_TRY(hipEventCreateWithFlags(&fresh->ev[b], hipEventDisableTiming));
+        }
+        ctx->ingest = fresh.release();
     }
     Ingest &g = *ctx->ingest;
-    const size_t region = (size_t)ING_CHUNK * 8;              // one column's room in a chunk buffer
-    if (!g.pin[0]) {
-        for (int b = 0; b < 2; b++) {
-            HIP_TRY(hipHostMalloc(&g.pin[b], region * ING_COLS, hipHostMallocNonCoherent));   // CPU-cached: the packers write it byte by byte
-            HIP_TRY(hipMalloc(&g.dev[b], region * ING_COLS));
-            HIP_TRY(hipEventCreateWithFlags(&g.ev[b], hipEventDisableTiming));
-        }
-    }
-    const int nt = g.pool.n;
+    Pool &pool = packing_pool();
+    const int nt = pool.n;
     const int64_t n_chunks = (n + ING_CHUNK - 1) / ING_CHUNK;
 #ifdef JH_TUNING
     // JH_INGEST_TRACE=1: where the host time goes (event waits, packing, enqueue)
@@ -193,7 +206,7 @@ bool ingest_columns(jh_ctx *ctx, const int64_t *const src[ING_COLS], int64_t *co
         for (auto &x : wide) x.store(0, std::memory_order_relaxed);
         // narrow every column of the chunk; a value that does not fit marks
         // the column wide (then it is copied whole, below)
-        ING_T(t_pack, g.pool.run([&](int i) {
+        ING_T(t_pack, pool.run([&](int i) {
             const int64_t a = cn * i / nt, e = cn * (i + 1) / nt;
             for (int c = 0; c < ING_COLS; c++) {
                 if (!src[c]) continue;
@@ -224,7 +237,7 @@ bool ingest_columns(jh_ctx *ctx, const int64_t *const src[ING_COLS], int64_t *co
         bool any_wide = false;
         for (int c = 0; c < ING_COLS; c++) any_wide |= src[c] && wide[c].load();
         if (any_wide)
-            g.pool.run([&](int i) {
+            pool.run([&](int i) {
                 const int64_t a = cn * i / nt, e = cn * (i + 1) / nt;
                 for (int c = 0; c < ING_COLS; c++)
                     if (src[c] && wide[c].load(std::memory_order_relaxed))

@@ -63,6 +63,7 @@ struct jh_ctx {
     bool lds_attr_wg = false;
     int n_cu = 256;
     int share = 1;                // contexts of one jh_open_devices call on this device (fit_units divides by it)
+    size_t hbm_total = 0;         // the device's HBM (hipMemGetInfo, once): bounds the resume buffers
     int32_t *hflag = nullptr;     // host-mapped flag: phase 1's queue drained (jh_lin.hip)
     int32_t *hflag_dev = nullptr;
     void *pinned = nullptr;       // small pinned staging for scalars

@@ -3229,79 +3229,8 @@ __device__ int dfs_acc(const WgArgs &W, WgShared &sh, const KeyInfo &K, const ch
     load_up(P);
     wave_sync();
     uint32_t ins_saved = 0xFFFFFFFFu;     // a handed-over search's real insert count
-    // move the window forward from layer t to layer nt (a lift, or a resume)
-    auto advance = [&](uint32_t nt) {
-        for (uint32_t u = t; u < nt; u++) {
-            const uint32_t ru = u == t ? r : (lay_hi(u) & 63);
-            const uint32_t sh = (uint32_t)wave_shl1((int)wrq);
-            if (lane >= (int)ru) wrq = sh;
-            w--;
-            if (lane == w) wrq = RQ_EMPTY;
-            const int c = (int)(lay_hi(u + 1) >> 6);
-            if (c > 0) {
-                if (P < pb || P + c > pb + 64) load_up(c <= 32 && P >= 32 ? P - 32 : P);
-                for (int kk = 0; kk < c; kk++) {
-                    const uint32_t x = (uint32_t)readlane((int)urq, P - pb + kk);
-                    if (lane == w + kk) wrq = x;
-                }
-                w += c; P += c;
-            }
-        }
-    };
-    if (A.rs_mode == 2 && A.rs_off) {
-        // Resume a search phase 1 deferred (round 5): its memo into this wave's
-        // HBM table behind the Bloom filter (theta above every restored layer,
-        // so each probe there is exact), its stack into the ring and the HBM
-        // stack, then expand its current configuration again: the children it
-        // had inserted are present, the others absent -- the DFS goes on
-        // exactly where phase 1 stopped it.
-        const int64_t ro = A.rs_off[key];
-        if (ro >= 0) {
-            const uint64_t *hd = (const uint64_t *)(A.rs_arena + ro);
-            const uint64_t h_mask = hd[0], h_ts = hd[1], h_dt = hd[2], h_ins = hd[3], h_n = hd[4];
-            const uint32_t d = (uint32_t)h_dt;
-            if (d <= A.stack_cap && h_n <= (uint64_t)A.memo_cap / 4) {
-                const Frame *fsrc = (const Frame *)(hd + 8);
-                const ulonglong2 *ent = (const ulonglong2 *)(fsrc + d);
-                uint32_t tmx = 0;
-                for (uint32_t j = (uint32_t)lane; j < (uint32_t)h_n; j += 64) {
-                    const ulonglong2 e = ent[j];
-                    const uint32_t et = (uint32_t)(e.y >> 20) & T_MASK, es = (uint32_t)e.y & STATE_MASK;
-                    hbm_insert(memo, cap_mask, gen, et, es, e.x);
-                    uint32_t g1, g2;
-                    lk_hash((uint32_t)e.x, (uint32_t)(e.x >> 32) | (et << 16) | (es << 8) | 0x80000000u, g1, g2);
-                    bloom_set2<M>(bloom, lk_bl(g1), lk_bl(g2));
-                    tmx = max(tmx, et + 1);
-                }
-                for (int o = 32; o > 0; o >>= 1) tmx = max(tmx, (uint32_t)__shfl_xor((int)tmx, o));
-                theta = rflu(tmx);
-                ring_lo = d > 32 ? d - 32 : 0;
-                for (uint32_t j = (uint32_t)lane; j < ring_lo; j += 64) stack[j] = fsrc[j];
-                {
-                    const uint32_t idx = ring_lo + (((uint32_t)lane - ring_lo) & 63);
-                    if (idx < d) {
-                        const Frame fr = fsrc[idx];
-                        fm_lo = (uint32_t)fr.mask; fm_hi = (uint32_t)(fr.mask >> 32); f_ti = fr.t_i;
-                        f_s = (uint32_t)fr.s; fr_lo = (uint32_t)fr.rest; fr_hi = (uint32_t)(fr.rest >> 32);
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                wave_sync();
-                depth = d;
-                mask = h_mask;
-                s = (uint32_t)(h_ts >> 32);
-                ins = (uint32_t)h_ins;
-                chk = min(budget, ins);                  // the next insert runs the checks
-                const uint32_t nt = (uint32_t)h_ts;
-                advance(nt);
-                t = nt;
-                tmax = max((uint32_t)(h_dt >> 32), t);
-                r = lay_hi(t) & 63;
-                rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
-            }
-        }
-    }
+    // (the workgroup engine never continues a phase-1 record -- its
+    // searches start at the root -- so dfs_lean's resume block has no copy here)
     const ulonglong2 *B = (const ulonglong2 *)lmemo;
     uint64_t absent = 0, nm_r = 0;
     uint32_t u_r = 0, klo = 0, khi = 0, b1 = 0, b2 = 0, n1 = 0, n2 = 0, h1 = 0, h2 = 0, nvl = 0;
@@ -6638,12 +6567,25 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     const bool p1_only = (lflags & JH_LIN_PHASE1_ONLY) != 0 && !linear_mode && !skip_p1;
     // resume (round 5): phase 1's deferred LEAN searches saved for the heavy-key
     // pass (a record is <= 64 B + a frame per stack level + 16 B per insert)
+    // (not for the workgroup engine's tuning modes, JH_WG: its
+    // searches start at the root, so records would only be written)
+    const bool wg_mode = tune_env("JH_WG") && atoi(tune_env("JH_WG")) != 0;
     const bool resume = a.defer && !linear_mode && !skip_p1 && !p1_only && !(lflags & JH_LIN_NO_RESUME) &&
-                        !(lflags & JH_LIN_STREAM) &&
+                        !(lflags & JH_LIN_STREAM) && !wg_mode &&
                         !tune_env("JH_NO_RESUME");
     if (resume) {
+        if (!ctx->hbm_total) {
+            size_t fr = 0, tot = 0;
+            HIP_TRY(hipMemGetInfo(&fr, &tot));
+            ctx->hbm_total = tot;
+        }
+        // ADVICE r5 / VERDICT r5 item 7: the record arena and the slot log are
+        // bounded by the device's HBM over the contexts sharing it (1/64 each:
+        // 4.5 GB for one context on an MI355X, so the 256 MB cap rules there).
+        // A smaller log only fails saves (those searches restart: same results)
+        const uint64_t rs_lim = (uint64_t)ctx->hbm_total / (64 * (uint64_t)std::max(1, ctx->share));
         const uint64_t per_key = 64 + (uint64_t)stack_cap * sizeof(Frame) + (uint64_t)quick * 16;
-        const uint64_t cap = std::min<uint64_t>((uint64_t)256 << 20, (uint64_t)K * per_key);
+        const uint64_t cap = std::min<uint64_t>(std::min<uint64_t>((uint64_t)256 << 20, rs_lim), (uint64_t)K * per_key);
         a.rs_arena = ctx->ws<uint8_t>(WS_RS_ARENA, cap);
         a.rs_cap = cap;
         a.rs_off = ctx->ws<int64_t>(WS_RS_OFF, K);
@@ -6658,6 +6600,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
 #endif
         if (!tune_env("JH_RS_SCAN")) {
             a.hlog_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(quick, 1024), 32768);
+            a.hlog_cap = (uint32_t)std::max<uint64_t>(256, std::min<uint64_t>(a.hlog_cap, rs_lim / (4 * (uint64_t)std::max(1, waves1))));
             a.hlog = ctx->ws<uint32_t>(WS_RS_LOG, (size_t)waves1 * a.hlog_cap);
         }
         // a handed-over search continues where it stopped: the hand-over is free

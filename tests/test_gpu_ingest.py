@@ -73,3 +73,35 @@ def test_ingest_counter_equals_resident(ctx):
     for k in ("valid", "cause", "n_reads", "n_errors", "first_err_entry"):
         assert rh[k] == rd[k], k
     assert np.array_equal(rh["reads"], rd["reads"])
+
+
+def test_stage_roundtrip_boundary_values(ctx):
+    """the packed staging read back bit for bit (jh_stage_history)
+    on the edges of its narrowing: INT32_MIN as a real value (must send its
+    chunk's column whole), nil, 32-bit extremes, int8 -128 / 127 in type and
+    :f (fit) and 128 (does not), a chunk wide only in the process column,
+    another only in the key column, and n a multiple of neither 4 nor the
+    1 M-row chunk."""
+    from jepsen_amd.history import Columns
+    rng = np.random.default_rng(7)
+    n = (2 << 20) + 3 * (1 << 20) // 2 + 7           # 3.5 chunks + 7 rows
+    C = 1 << 20
+    cols = Columns(n=n, process=rng.integers(0, 50, n), type=rng.integers(0, 4, n), f=rng.integers(0, 3, n),
+                   key=rng.integers(0, 1000, n), value=rng.integers(-5, 6, n), value2=rng.integers(-5, 6, n),
+                   n_keys=1000)
+    cols.value[rng.integers(0, n, 5000)] = A.NIL
+    cols.value2[rng.integers(0, n, 5000)] = A.NIL
+    cols.type[[1, 2]] = [-128, 127]; cols.f[[3, 4]] = [-128, 127]              # chunk 0: fit
+    cols.value[[5, 6]] = [-(1 << 31) + 1, (1 << 31) - 1]                       # fit
+    cols.f[C + 9] = 128                                                          # chunk 1: :f wide
+    cols.value[C + 10] = -(1 << 31)                                              # INT32_MIN, not nil: wide
+    cols.process[2 * C + 11] = 1 << 40                                           # chunk 2: process only
+    cols.key[3 * C + 3] = 1 << 33                                                # chunk 3 (partial): key only
+    cols.value2[n - 1] = 1 << 31                                                 # last row
+    for name in ("process", "type", "f", "key", "value", "value2"):
+        setattr(cols, name, np.ascontiguousarray(getattr(cols, name), dtype=np.int64))
+    got = ctx.stage_history(cols)
+    for i, name in enumerate(("process", "type", "f", "key", "value", "value2")):
+        want = getattr(cols, name)
+        bad = np.nonzero(got[i] != want)[0]
+        assert len(bad) == 0, (name, bad[:5], got[i][bad[:5]], want[bad[:5]])

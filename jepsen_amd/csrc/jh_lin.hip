@@ -2653,7 +2653,8 @@ constexpr int CMD_ENUM = 1, CMD_DONE = 2, CMD_MERGE = 3;
 // number to its count and pops the node. A live result marks the node (and so
 // its ancestors) live. Verdicts, counts and failing rows stay WGL's.
 constexpr int SPEC_SLOTS = 64;         // one per lane of the main's wave
-constexpr int SPEC_PER_CHECK = 4;      // new posts per check of the main
+constexpr int SPEC_PER_CHECK = 4;      // new posts per poll of the main
+constexpr uint32_t SPEC_CHK = 128;     // inserts between polls
 constexpr uint32_t SPEC_RES_CAP = 1u << 18;    // nodes per helper result buffer (2 MB)
 constexpr int SPEC_FREE = 0, SPEC_POSTED = 1, SPEC_CLAIMED = 2, SPEC_DEAD = 3, SPEC_LIVE = 4, SPEC_INC = 5,
               SPEC_STALE = 6, SPEC_BUSY = 7;
@@ -3213,6 +3214,7 @@ __device__ int dfs_acc(const WgArgs &W, WgShared &sh, const KeyInfo &K, const ch
     const uint32_t budget = (uint32_t)min<int64_t>(A.budget, 0x7FFFFFFF);
     const uint32_t acc_t = W.acc_t ? W.acc_t : 0x7FFFFFFFu;
     uint32_t next_acc = acc_t;
+    uint32_t spec_chk = 0;                             // the next spec-board poll (round 6)
     // a late helper checks its key more often: it races a search that may be about to finish
     const uint32_t chk_step = W.seq_start ? 128u : 1024u;
     uint32_t chk = min(budget, min(acc_t, chk_step));
@@ -3323,6 +3325,114 @@ __device__ int dfs_acc(const WgArgs &W, WgShared &sh, const KeyInfo &K, const ch
     };
 
 expand:
+    if (W.spec && ins >= spec_chk) {
+        // Round 6, the spec board (SpecSlot), every SPEC_CHK inserts, here where
+        // the children's keys are not live yet: this search's results first.
+        spec_chk = ins + SPEC_CHK;
+        SpecSlot *SB = W.spec;
+        const int st = __hip_atomic_load(&SB[lane].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const bool mine = st >= SPEC_DEAD && st <= SPEC_INC && SB[lane].key == key;
+        const uint32_t sd = mine ? SB[lane].depth : 0u, sq = mine ? SB[lane].seq : 0u;
+        const uint32_t fsq = (uint32_t)__shfl((int)f_seq, (int)(sd & 63));
+        // still on the stack: same depth, same insert index
+        const bool on = mine && sd >= 1 && sd >= ring_lo && sd <= depth && (sd == depth ? cur_seq : fsq) == sq;
+        int lmax = on && st == SPEC_LIVE ? (int)sd : -1;          // live: it and its ancestors
+        for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, __shfl_xor(lmax, o));
+        if (lmax > l_live) l_live = lmax;
+        const bool dd = on && st == SPEC_DEAD && (int)sd > l_live;
+        uint32_t dmin = dd ? sd : 0xFFFFFFFFu;                      // the shallowest dead one
+        for (int o = 32; o > 0; o >>= 1) dmin = min(dmin, (uint32_t)__shfl_xor((int)dmin, o));
+        const uint64_t pm = ballot(dd && sd == dmin);
+        const int pk = pm ? __builtin_ctzll(pm) : -1;
+        if (mine && lane != pk)
+            __hip_atomic_store(&SB[lane].state, SPEC_FREE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (pk >= 0) {
+            // merge the dead node's reachable set (every wave: wg_merge) and pop it
+            const uint32_t rn = (uint32_t)readlane((int)(lane == pk ? SB[lane].n : 0u), pk);
+            const int rh = readlane(lane == pk ? SB[lane].helper : 0, pk);
+            if (lane == 0) {
+                sh.cmd = CMD_MERGE; sh.m_src = W.spec_res + (size_t)rh * W.spec_res_cap; sh.m_n = rn;
+                sh.m_new = 0; sh.m_tmin = 0xFFFFFFFFu; sh.m_tmax = 0;
+                sh.theta = theta; sh.acc_lo = acc_lo; sh.acc_hi = acc_hi; sh.gen = gen; sh.nomemo = 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __syncthreads();
+            wg_merge(W, sh, lane, memo, my_probes);
+            if (lane == pk)
+                __hip_atomic_store(&SB[pk].state, SPEC_FREE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t mnew = sh.m_new;
+            if (lane == 0) {
+                atomicAdd((unsigned long long *)W.spec_q, (unsigned long long)mnew);
+                atomicAdd(&W.spec_q[2], 1);
+            }
+            ins += mnew;
+            if (ins > budget) { ins = budget; verdict = JH_UNKNOWN; goto done; }
+            if (mnew) {
+                tmax = max(tmax, sh.m_tmax);
+                acc_lo = acc_lo > acc_hi ? sh.m_tmin : min(acc_lo, sh.m_tmin);
+                acc_hi = max(acc_hi, sh.m_tmax);
+            }
+            next_acc = ins + acc_t;
+            chk = min(budget, min(ins + chk_step, next_acc));
+            depth = dmin;
+            goto pop;                  // pops node dmin
+        }
+        // New posts: the open nodes within spec_dist levels of the current
+        // one (the register ring), below the deepest known live node, with
+        // spec_min inserts below them and never posted (or 4x as many since),
+        // deepest first, into free slots; posting counts as an attempt (inc)
+        uint64_t freem = ballot(st == SPEC_FREE || mine);
+        const uint32_t dlo = max(max(max(ring_lo, 1u), (uint32_t)(l_live + 1)),
+                                 depth > W.spec_dist ? depth - W.spec_dist : 0u);
+        auto elig = [&](uint32_t sqv, uint32_t inc) {
+            const uint32_t b = ins - sqv;
+            return b >= W.spec_min && (inc == 0 || b >= 4 * inc);
+        };
+        auto post = [&](uint32_t d, uint64_t cfgk, uint32_t sqv) -> bool {
+            while (freem) {
+                const int sl = __builtin_ctzll(freem);
+                freem &= freem - 1;
+                int ok = 0;
+                if (lane == 0) {
+                    int exp = SPEC_FREE;
+                    ok = __hip_atomic_compare_exchange_strong(&SB[sl].state, &exp, SPEC_BUSY, __ATOMIC_ACQUIRE,
+                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (ok) {
+                        SB[sl].key = key; SB[sl].depth = d; SB[sl].seq = sqv; SB[sl].cfg = cfgk;
+                        SB[sl].cap = min(W.spec_res_cap - 1, max(8192u, W.spec_mult * (ins - sqv)));
+                        SB[sl].n = 0; SB[sl].helper = -1;
+                        __hip_atomic_store(&SB[sl].state, SPEC_POSTED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                if (readlane(ok, 0)) return true;
+            }
+            return false;
+        };
+        int nposted = 0;
+        if (depth >= dlo && depth >= 1 && elig(cur_seq, cur_inc) && post(depth, lk_make(t, s, mask), cur_seq)) {
+            cur_inc = ins - cur_seq;
+            nposted++;
+        }
+        {
+            const uint32_t fd = ring_lo + (((uint32_t)lane - ring_lo) & 63);
+            const uint64_t cm = ballot(fd < depth && fd >= dlo && elig(f_seq, f_inc));
+            const uint32_t rs = ring_lo & 63;
+            uint64_t rot = rs ? ((cm >> rs) | (cm << (64 - rs))) : cm;
+            while (rot && freem && nposted < SPEC_PER_CHECK) {
+                const int q = 63 - __builtin_clzll(rot);
+                rot &= ~(1ULL << q);
+                const uint32_t d = ring_lo + (uint32_t)q;
+                const int ln = (int)(d & 63);
+                const uint32_t qs = (uint32_t)readlane((int)f_seq, ln);
+                const uint64_t ck = lk_make((uint32_t)readlane((int)f_ti, ln) >> 6, (uint32_t)readlane((int)f_s, ln),
+                                            ((uint64_t)(uint32_t)readlane((int)fm_hi, ln) << 32) |
+                                            (uint32_t)readlane((int)fm_lo, ln));
+                if (!post(d, ck, qs)) break;
+                if (lane == ln) f_inc = ins - qs;
+                nposted++;
+            }
+        }
+    }
     if (++n_steps > (1u << 28)) {       // watchdog: far beyond any budget's step count
         if (lane == 0) atomicOr(A.flags, 128);
         verdict = JH_UNKNOWN;
@@ -3377,112 +3487,6 @@ insert:
                         c = 1;
                 }
                 if (readlane(c, 0)) { verdict = JH_CANCELLED; goto done; }
-            }
-            if (W.spec) {
-                // Round 6, the spec board (SpecSlot): this search's results first.
-                SpecSlot *SB = W.spec;
-                const int st = __hip_atomic_load(&SB[lane].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                const bool mine = st >= SPEC_DEAD && st <= SPEC_INC && SB[lane].key == key;
-                const uint32_t sd = mine ? SB[lane].depth : 0u, sq = mine ? SB[lane].seq : 0u;
-                const uint32_t fsq = (uint32_t)__shfl((int)f_seq, (int)(sd & 63));
-                // still on the stack: same depth, same insert index
-                const bool on = mine && sd >= 1 && sd >= ring_lo && sd <= depth && (sd == depth ? cur_seq : fsq) == sq;
-                int lmax = on && st == SPEC_LIVE ? (int)sd : -1;          // live: it and its ancestors
-                for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, __shfl_xor(lmax, o));
-                if (lmax > l_live) l_live = lmax;
-                const bool dd = on && st == SPEC_DEAD && (int)sd > l_live;
-                uint32_t dmin = dd ? sd : 0xFFFFFFFFu;                      // the shallowest dead one
-                for (int o = 32; o > 0; o >>= 1) dmin = min(dmin, (uint32_t)__shfl_xor((int)dmin, o));
-                const uint64_t pm = ballot(dd && sd == dmin);
-                const int pk = pm ? __builtin_ctzll(pm) : -1;
-                if (mine && lane != pk)
-                    __hip_atomic_store(&SB[lane].state, SPEC_FREE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                if (pk >= 0) {
-                    // merge the dead node's reachable set (every wave: wg_merge) and pop it
-                    const uint32_t rn = (uint32_t)readlane((int)(lane == pk ? SB[lane].n : 0u), pk);
-                    const int rh = readlane(lane == pk ? SB[lane].helper : 0, pk);
-                    if (lane == 0) {
-                        sh.cmd = CMD_MERGE; sh.m_src = W.spec_res + (size_t)rh * W.spec_res_cap; sh.m_n = rn;
-                        sh.m_new = 0; sh.m_tmin = 0xFFFFFFFFu; sh.m_tmax = 0;
-                        sh.theta = theta; sh.acc_lo = acc_lo; sh.acc_hi = acc_hi; sh.gen = gen; sh.nomemo = 0;
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __syncthreads();
-                    wg_merge(W, sh, lane, memo, my_probes);
-                    if (lane == pk)
-                        __hip_atomic_store(&SB[pk].state, SPEC_FREE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t mnew = sh.m_new;
-                    if (lane == 0) {
-                        atomicAdd((unsigned long long *)W.spec_q, (unsigned long long)mnew);
-                        atomicAdd(&W.spec_q[2], 1);
-                    }
-                    ins += mnew;
-                    if (ins > budget) { ins = budget; verdict = JH_UNKNOWN; goto done; }
-                    if (mnew) {
-                        tmax = max(tmax, sh.m_tmax);
-                        acc_lo = acc_lo > acc_hi ? sh.m_tmin : min(acc_lo, sh.m_tmin);
-                        acc_hi = max(acc_hi, sh.m_tmax);
-                    }
-                    next_acc = ins + acc_t;
-                    chk = min(budget, min(ins + chk_step, next_acc));
-                    depth = dmin;
-                    goto pop;                  // pops node dmin
-                }
-                // New posts: the open nodes within spec_dist levels of the current
-                // one (the register ring), below the deepest known live node, with
-                // spec_min inserts below them and never posted (or 4x as many since),
-                // deepest first, into free slots; posting counts as an attempt (inc)
-                uint64_t freem = ballot(st == SPEC_FREE || mine);
-                const uint32_t dlo = max(max(max(ring_lo, 1u), (uint32_t)(l_live + 1)),
-                                         depth > W.spec_dist ? depth - W.spec_dist : 0u);
-                auto elig = [&](uint32_t sqv, uint32_t inc) {
-                    const uint32_t b = ins - sqv;
-                    return b >= W.spec_min && (inc == 0 || b >= 4 * inc);
-                };
-                auto post = [&](uint32_t d, uint64_t cfgk, uint32_t sqv) -> bool {
-                    while (freem) {
-                        const int sl = __builtin_ctzll(freem);
-                        freem &= freem - 1;
-                        int ok = 0;
-                        if (lane == 0) {
-                            int exp = SPEC_FREE;
-                            ok = __hip_atomic_compare_exchange_strong(&SB[sl].state, &exp, SPEC_BUSY, __ATOMIC_ACQUIRE,
-                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            if (ok) {
-                                SB[sl].key = key; SB[sl].depth = d; SB[sl].seq = sqv; SB[sl].cfg = cfgk;
-                                SB[sl].cap = min(W.spec_res_cap - 1, max(8192u, W.spec_mult * (ins - sqv)));
-                                SB[sl].n = 0; SB[sl].helper = -1;
-                                __hip_atomic_store(&SB[sl].state, SPEC_POSTED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                            }
-                        }
-                        if (readlane(ok, 0)) return true;
-                    }
-                    return false;
-                };
-                int nposted = 0;
-                if (depth >= dlo && depth >= 1 && elig(cur_seq, cur_inc) && post(depth, lk_make(t, s, mask), cur_seq)) {
-                    cur_inc = ins - cur_seq;
-                    nposted++;
-                }
-                {
-                    const uint32_t fd = ring_lo + (((uint32_t)lane - ring_lo) & 63);
-                    const uint64_t cm = ballot(fd < depth && fd >= dlo && elig(f_seq, f_inc));
-                    const uint32_t rs = ring_lo & 63;
-                    uint64_t rot = rs ? ((cm >> rs) | (cm << (64 - rs))) : cm;
-                    while (rot && freem && nposted < SPEC_PER_CHECK) {
-                        const int q = 63 - __builtin_clzll(rot);
-                        rot &= ~(1ULL << q);
-                        const uint32_t d = ring_lo + (uint32_t)q;
-                        const int ln = (int)(d & 63);
-                        const uint32_t qs = (uint32_t)readlane((int)f_seq, ln);
-                        const uint64_t ck = lk_make((uint32_t)readlane((int)f_ti, ln) >> 6, (uint32_t)readlane((int)f_s, ln),
-                                                    ((uint64_t)(uint32_t)readlane((int)fm_hi, ln) << 32) |
-                                                    (uint32_t)readlane((int)fm_lo, ln));
-                        if (!post(d, ck, qs)) break;
-                        if (lane == ln) f_inc = ins - qs;
-                        nposted++;
-                    }
-                }
             }
             if (ins >= next_acc) {
                 next_acc = ins + acc_t;
@@ -6711,7 +6715,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     // the workgroup engine (k_lin_wg): exact WGL, dead subtrees enumerated by
     // the workgroup's helper waves; built for wg_cus CUs, racing the BFS when
     // wg_claim is set
-    auto build_wg = [&](int wg_cus, int32_t *wg_claim, int32_t *wg_queue) -> WgArgs {
+    auto build_wg = [&](int wg_cus, int32_t *wg_claim, int32_t *wg_queue, bool all_cus = false) -> WgArgs {
         acc_stats = ctx->ws<unsigned long long>(WS_ACC_STATS, 8);
         HIP_TRY(hipMemsetAsync(acc_stats, 0, 8 * sizeof(unsigned long long), st));
         // + slack: keys claimed in the set after the cap is hit are still recorded
@@ -6725,7 +6729,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                                 MemoW::SLOTS * 8 + wtab_b;
         uint64_t mem_limit = 48ULL << 30;
         if (const char *e = tune_env("JH_WG_MEM_GB")) mem_limit = (uint64_t)std::max(1, atoi(e)) << 30;
-        n_wg = (int)std::min<int64_t>(n_def_l, (int64_t)wg_cus);
+        // (with the spec board every helper is useful, a key of its own or not)
+        n_wg = all_cus ? wg_cus : (int)std::min<int64_t>(n_def_l, (int64_t)wg_cus);
         n_wg = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)n_wg, mem_limit / per_wg));
         n_wg = fit_units(ctx, n_wg, per_wg, {WS_WG_MEMO, WS_WG_GSET, WS_WG_WORK, WS_WG_PEND});
         const bool fresh2 = ctx->ws_fresh(WS_WG_MEMO) || ctx->bufs[WS_WG_MEMO].bytes < (size_t)n_wg * cap2 * 16;
@@ -6908,7 +6913,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         wh = WgArgs{};
         seq_start = nullptr;
         if (n_help > 0) {
-            wh = build_wg(n_help, claim, nullptr);
+            const bool spec_on = !(lflags & JH_LIN_NO_SPEC) && !(tune_env("JH_SPEC") && !atoi(tune_env("JH_SPEC")));
+            wh = build_wg(n_help, claim, nullptr, spec_on);
             seq_start = ctx->ws<unsigned long long>(WS_HELP_START, K);
             int32_t *taken = ctx->ws<int32_t>(WS_HELP_TAKEN, K);
             HIP_TRY(hipMemsetAsync(seq_start, 0, (size_t)K * sizeof(unsigned long long), st));
@@ -6919,7 +6925,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             if (lflags & JH_LIN_HELPERS_NOW) late_us = 0;
             wh.late_ticks = late_us * 100;     // s_memrealtime: 100 MHz
             // round 6: the spec board (SpecSlot), unless JH_LIN_NO_SPEC
-            if (!(lflags & JH_LIN_NO_SPEC)) {
+            if (spec_on) {
                 wh.spec = ctx->ws<SpecSlot>(WS_SPEC, SPEC_SLOTS);
                 HIP_TRY(hipMemsetAsync(wh.spec, 0, sizeof(SpecSlot) * SPEC_SLOTS, st));
                 wh.spec_res_cap = SPEC_RES_CAP;
@@ -6929,7 +6935,6 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 if (const char *e = tune_env("JH_SPEC_MIN")) wh.spec_min = (uint32_t)std::max(1, atoi(e));
                 if (const char *e = tune_env("JH_SPEC_MULT")) wh.spec_mult = (uint32_t)std::max(1, atoi(e));
                 if (const char *e = tune_env("JH_SPEC_DIST")) wh.spec_dist = (uint32_t)std::max(1, atoi(e));
-                if (const char *e = tune_env("JH_SPEC")) if (!atoi(e)) wh.spec = nullptr;
             }
         }
         const int wmax = std::max(waves2, waves3);

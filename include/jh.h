@@ -186,6 +186,8 @@ typedef struct jh_lin_opts {
                                   inserts: 1024 hands over at 2047); 0: default (1024 when
                                   the deferred searches resume, round 5; else off), <0: never */
     int32_t p1_waves_per_cu;   /* phase-1 waves per CU (<= 26, the LDS limit); <=0: 26 */
+    int32_t bfs_wgs;           /* ABI 7: phase-2 reachable-set BFS workgroups (one per CU); <=0: default */
+    int32_t reserved2;
 } jh_lin_opts;
 
 #define JH_DEFAULT_BUDGET (1 << 20)

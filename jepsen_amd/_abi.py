@@ -74,7 +74,8 @@ class JhLinOpts(C.Structure):
                 ("helpers", C.c_int32), ("helper_late_us", C.c_int32),
                 ("xw_waves", C.c_int32), ("p2_waves_per_cu", C.c_int32),
                 ("lean_waves", C.c_int32), ("wide_waves", C.c_int32),
-                ("handover_min", C.c_int32), ("p1_waves_per_cu", C.c_int32)]
+                ("handover_min", C.c_int32), ("p1_waves_per_cu", C.c_int32),
+                ("bfs_wgs", C.c_int32), ("reserved2", C.c_int32)]       # ABI 7
 
 
 # every field of jh_key_verdict: the parity tests compare all of them

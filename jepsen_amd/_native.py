@@ -129,7 +129,7 @@ def _opts(init, budget, stream=0, algorithm=None, exact_count=True, **tune):
         algorithm = A.ALGORITHMS[algorithm]
     o.algorithm = int(algorithm or 0)
     for k, v in tune.items():
-        if k not in dict(A.JhLinOpts._fields_) or k in ("init_value", "budget", "stream", "algorithm", "reserved"):
+        if k not in dict(A.JhLinOpts._fields_) or k in ("init_value", "budget", "stream", "algorithm", "reserved", "reserved2"):
             raise TypeError(f"unknown jh_lin_opts field {k}")
         setattr(o, k, int(v))
     if exact_count:

@@ -85,6 +85,19 @@ static jh_ctx *primary(jh_ctx *c) { return c->members.empty() ? c : c->members[0
 int multi_check_cas_independent(jh_ctx *g, const jh_history *h, const jh_lin_opts *opts,
                                 jh_key_verdict *out, jh_summary *sum, char *err, size_t errlen);
 
+static std::mutex g_open_mu;
+static int g_open[256];              // open single-device contexts per device id
+static void device_open_delta(int device, int d) {
+    if (device < 0 || device >= 256) return;
+    std::lock_guard<std::mutex> g(g_open_mu);
+    g_open[device] += d;
+}
+int device_open_contexts(int device) {
+    if (device < 0 || device >= 256) return 1;
+    std::lock_guard<std::mutex> g(g_open_mu);
+    return std::max(1, g_open[device]);
+}
+
 extern "C" {
 
 int jh_version(void) { return JH_ABI_VERSION; }
@@ -111,6 +124,7 @@ int jh_open(int device, jh_ctx **out) {
         delete c;
         return e.code;
     }
+    device_open_delta(device, 1);
     *out = c;
     return JH_OK;
 }
@@ -135,6 +149,7 @@ void jh_close(jh_ctx *ctx) {
         if (ctx->aux2) (void)hipStreamDestroy(ctx->aux2);
         if (ctx->aux3) (void)hipStreamDestroy(ctx->aux3);
     }
+    device_open_delta(ctx->device, -1);
     delete ctx;
 }
 

@@ -93,6 +93,12 @@ struct jh_ctx {
     bool ws_fresh(int slot) const { return (int)bufs.size() <= slot || bufs[slot].p == nullptr; }
 };
 
+// Round 6: contexts open on each device in this process (jh_open / jh_close):
+// fit_units and the resume buffers divide a device by max(share, this), so a
+// second context opened with its own jh_open does not size its tables as if
+// it had the device to itself
+int device_open_contexts(int device);
+
 // workspace slot ids (one namespace for the whole library)
 enum WsSlot {
     WS_COL_PROCESS = 0, WS_COL_TYPE, WS_COL_F, WS_COL_KEY, WS_COL_VALUE, WS_COL_VALUE2, WS_COL_AUX,
@@ -114,7 +120,7 @@ enum WsSlot {
     WS_DEFER64, WS_DEFER64_T, WS_MEMO_WIDE, WS_STACK_WIDE, WS_SCRATCH_WIDE,
     WS_CFG_SLOT, WS_CFG_OUT, WS_CFG_N, WS_CFG_ROWS, WS_CFG_KEYS,
     WS_S_RB_HIST, WS_S_RB_OUT, WS_TL, WS_RS_ARENA, WS_RS_OFF, WS_RS_LOG, WS_DEFER_INFO,
-    WS_SPEC, WS_SPEC_RES,
+    WS_SPEC, WS_SPEC_RES, WS_DEBUG_WG,
     WS_COUNT
 };
 

@@ -6282,10 +6282,12 @@ static int fit_units(jh_ctx *ctx, int want, uint64_t per_unit, std::initializer_
     HIP_TRY(hipMemGetInfo(&fr, &tot));
     const uint64_t reserve = std::max<uint64_t>(2ULL << 30, tot / 32);
     // contexts sharing the device (jh_open_devices with a device listed more
-    // than once) run at once: each takes its share of what is free
-    uint64_t room = fr / (uint64_t)std::max(1, ctx->share) + held;
+    // than once; round 6: or opened one by one, device_open_contexts) may run
+    // at once: each takes its share of what is free
+    const uint64_t share = (uint64_t)std::max(ctx->share, device_open_contexts(ctx->device));
+    uint64_t room = fr / share + held;
     room = room > reserve ? room - reserve : 0;
-    room = std::min<uint64_t>(room, tot / (4 * (uint64_t)std::max(1, ctx->share)));
+    room = std::min<uint64_t>(room, tot / (4 * share));
     const uint64_t fit = room / (per_unit + per_unit / 8);    // ws() allocates 1/8 over
     return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)want, fit));
 }
@@ -6587,7 +6589,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // bounded by the device's HBM over the contexts sharing it (1/64 each:
         // 4.5 GB for one context on an MI355X, so the 256 MB cap rules there).
         // A smaller log only fails saves (those searches restart: same results)
-        const uint64_t rs_lim = (uint64_t)ctx->hbm_total / (64 * (uint64_t)std::max(1, ctx->share));
+        const uint64_t rs_lim = (uint64_t)ctx->hbm_total /
+                                (64 * (uint64_t)std::max(ctx->share, device_open_contexts(ctx->device)));
         const uint64_t per_key = 64 + (uint64_t)stack_cap * sizeof(Frame) + (uint64_t)quick * 16;
         const uint64_t cap = std::min<uint64_t>(std::min<uint64_t>((uint64_t)256 << 20, rs_lim), (uint64_t)K * per_key);
         a.rs_arena = ctx->ws<uint8_t>(WS_RS_ARENA, cap);
@@ -6756,7 +6759,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         wa.gset = gset; wa.gset_cap = (uint32_t)gcap; wa.work = work; wa.work_cap = (uint32_t)work_cap;
         wa.wtab = ctx->ws<char>(WS_WG_WTAB, (size_t)n_wg * wtab_b); wa.wtab_bytes = wtab_b;
         if (dbgenv && atoi(dbgenv) >= 3) {
-            wa.d.dbg = ctx->ws<unsigned long long>(WS_DEBUG, (size_t)n_wg * 256 + 16 * 1024);
+            // its own slot: the BFS's JH_DEBUG words live in WS_DEBUG (a shared slot
+            // grown here would leave their pointer dangling)
+            wa.d.dbg = ctx->ws<unsigned long long>(WS_DEBUG_WG, (size_t)n_wg * 256 + 16 * 1024);
             HIP_TRY(hipMemsetAsync(wa.d.dbg, 0, sizeof(unsigned long long) * n_wg * 256, st));
         }
         wa.acc_stats = acc_stats;
@@ -6816,7 +6821,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // 96 of 256 (round 2, with phase 2 at four waves per CU): C4 shard
         // 230 -> 223 ms, C3 ranks 0 / 3 / 6 flat (32: C4 +9 %, 128: no better)
         const int bfs_cus = std::max(1, std::min(96, ctx->n_cu * 3 / 8));
-        wg2 = std::min(nd_all, tune_env("JH_BFS_CUS") ? std::max(1, atoi(tune_env("JH_BFS_CUS"))) : bfs_cus);
+        wg2 = std::min(nd_all, tune_env("JH_BFS_CUS") ? std::max(1, atoi(tune_env("JH_BFS_CUS"))) :
+                               opts && opts->bfs_wgs > 0 ? std::min(opts->bfs_wgs, ctx->n_cu - 16) : bfs_cus);
         const uint64_t per_bfs = (uint64_t)set_cap * 8 + 4ULL * q_cap * 8 + scr_bytes_bfs + (uint64_t)ncap * 8 +
                                  (uint64_t)lcap * 4 + (uint64_t)hcap * 16 + (uint64_t)ncap * 4 + ((uint64_t)ncap / 32 + 1) * 4 +
                                  (uint64_t)ncap * 4 + (uint64_t)ncap * 8;
@@ -7606,10 +7612,10 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
     HIP_TRY(hipStreamSynchronize(st));
     if (qh[2] & 2) throw_jh(JH_EDEVICE, "per-key table exceeded the scratch reservation");
     if (qh[2] & 4) throw_jh(JH_EDEVICE, "DFS stack overflow");
-    if ((qh[2] & 0x1F0) && acc_stats && ctx->bufs.size() > WS_DEBUG && ctx->bufs[WS_DEBUG].p && n_wg > 0 &&
+    if ((qh[2] & 0x1F0) && acc_stats && ctx->bufs.size() > WS_DEBUG_WG && ctx->bufs[WS_DEBUG_WG].p && n_wg > 0 &&
         dbgenv && atoi(dbgenv) >= 3) {
         std::vector<unsigned long long> tr((size_t)n_wg * 256);
-        HIP_TRY(hipMemcpy(tr.data(), ctx->bufs[WS_DEBUG].p, tr.size() * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(tr.data(), ctx->bufs[WS_DEBUG_WG].p, tr.size() * 8, hipMemcpyDeviceToHost));
         for (int g = 0; g < n_wg; g++) {
             for (int e = 0; e < 31; e++) {
                 const unsigned long long *d8 = &tr[(size_t)g * 256 + 8 * e];
@@ -7636,6 +7642,16 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // the live lists' final lengths (the bounds used to size the pass above)
         n_defer = qh[1]; n_def_l = qh[Q_DEFER_L]; n_def_w = qh[Q_DEFER_W];
         if (n_def_l + n_def_w != n_defer) throw_jh(JH_EDEVICE, "deferred-key lists disagree");
+    }
+    if (tune_env("JH_WS_REPORT")) {
+        // tuning builds: the context's workspace, largest buffers first
+        std::vector<std::pair<size_t, int>> b;
+        size_t tot = 0;
+        for (int i = 0; i < (int)ctx->bufs.size(); i++) { b.push_back({ctx->bufs[i].bytes, i}); tot += ctx->bufs[i].bytes; }
+        std::sort(b.rbegin(), b.rend());
+        fprintf(stderr, "[jh-ws] total %.2f GB:", tot / 1073741824.0);
+        for (size_t i = 0; i < b.size() && i < 12; i++) fprintf(stderr, " slot %d %.2f GB;", b[i].second, b[i].first / 1073741824.0);
+        fprintf(stderr, "\n");
     }
     if (sum) {
         sum->valid = sh[0]; sum->n_invalid = sh[1]; sum->n_unknown = sh[2];
@@ -7728,7 +7744,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                     sum->p3_ms, sum->wide_ms, waves_w, (long long)sum->n_phase3_wide, n_x, sum->xw_ms, waves_x);
             if (acc_stats && dbgenv && atoi(dbgenv) >= 3 && n_wg > 0) {
                 std::vector<unsigned long long> tr((size_t)n_wg * 256);
-                HIP_TRY(hipMemcpy(tr.data(), ctx->bufs[WS_DEBUG].p, tr.size() * 8, hipMemcpyDeviceToHost));
+                HIP_TRY(hipMemcpy(tr.data(), ctx->bufs[WS_DEBUG_WG].p, tr.size() * 8, hipMemcpyDeviceToHost));
                 for (int g = 0; g < std::min(n_wg, 8); g++)
                     for (int e = 0; e < 32; e++) {
                         const unsigned long long *d8 = &tr[(size_t)g * 256 + 8 * e];

@@ -160,5 +160,13 @@ strong)
       timeout -k 10 150 python -u bench.py --workload c3s --shard $rk/$n --no-cpu --e2e 0 --no-parity --steps 5 --warmup 1 "$@" > $O/c3s_${rk}of${n}.json 2> $O/c3s_${rk}of${n}.err || exit 1
     done
   done ;;
+rprobe)
+  # per-key engine runs on the release library: rprobe <name> <rank> <key>... (JH_PROBE_FLAGS from the caller)
+  N=$1; RK=$2; shift 2
+  timeout -k 10 150 python -u tools/key_probe.py c3 $RK "$@" > $O/rprobe_$N.log 2>&1 ;;
+tl)
+  # per-key timeline CSV (JH_TL_CSV) of a -DJH_TUNING variant: tl <v> <name> <rank> [bench.py args...]
+  V=$1; N=$2; RK=$3; shift 3
+  JH_LIB=$R/jepsen_amd/variants/libjh_$V.so JH_DEFER_TIMES=1 JH_TL_CSV=$R/$O/tl_$N.csv timeout -k 10 120 python -u bench.py --steps 1 --warmup 1 --no-cpu --e2e 0 --no-parity --seed-rank $RK "$@" > $O/tl_$N.json 2> $O/tl_$N.err ;;
 *) echo "unknown part $PART"; exit 2 ;;
 esac

@@ -31,6 +31,9 @@ budget = int(os.environ.get("JH_PROBE_BUDGET", "0")) or wl.get("budget")
 for label, kw in [("race", {}), ("bfs-only", {"flags": A.LIN_BFS_ONLY}), ("no-helpers", {"flags": A.LIN_NO_HELPERS}),
                   ("exact", {"exact_count": True}), ("race", {})]:
     kw.setdefault("exact_count", False)
+    # JH_PROBE_FLAGS: extra jh_lin_opts flags for every run (e.g. 2048, JH_LIN_NO_SPEC)
+    if os.environ.get("JH_PROBE_FLAGS"):
+        kw["flags"] = kw.get("flags", 0) | int(os.environ["JH_PROBE_FLAGS"])
     t0 = time.perf_counter()
     v, s = ctx.check_cas_independent(sub, budget=budget, **kw)
     ms = (time.perf_counter() - t0) * 1e3

@@ -162,6 +162,13 @@ typedef struct jh_history {
  * the dead ones (same verdicts and counts); this flag turns that off (A/B and
  * the tests). */
 #define JH_LIN_NO_SPEC      2048
+/* Round 6: late helpers serve posted spec jobs before taking keys of their
+ * own (scheduling only: same verdicts and counts). */
+#define JH_LIN_SPEC_FIRST   4096
+/* Round 6: late helpers pick the keys whose sequential search has gone
+ * longest without reaching a deeper layer (stuck in a big dead subtree)
+ * instead of the ones running longest (scheduling only). */
+#define JH_LIN_HELP_STALL   8192
 
 typedef struct jh_lin_opts {
     int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */

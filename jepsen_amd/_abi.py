@@ -64,6 +64,8 @@ LIN_NO_RESUME = 512           # round 5: restart deferred keys instead of contin
 LIN_EXACT_COUNT = 1024        # round 5: WGL's exact count for every key (the parity tests)
 EXPLORED_UNCOUNTED = -3       # a valid key settled without the count pass
 LIN_NO_SPEC = 2048            # round 6: no speculative dead-subtree enumerations by idle helpers
+LIN_SPEC_FIRST = 4096         # round 6: helpers serve posted spec jobs before taking keys
+LIN_HELP_STALL = 8192         # round 6: helpers pick the keys stuck longest (no deeper layer)
 CAUSE_DEFERRED = 9
 
 

@@ -56,6 +56,22 @@ static_assert(SPILL_LANES >= 1 && SPILL_LANES <= 256 && (SPILL_LANES & (SPILL_LA
 #define JH_CNT_HASH32 0      // a 32-bit multiplicative slot hash instead of jh_mix64 (A/B)
 #endif
 
+// Round 6: k_cnt_pack's barriers order LDS only. Nothing the pack stores to
+// global memory is read back inside a block (words, pairs, spills, tables and
+// the counters' atomics are for later kernels), so a barrier need not wait
+// for those stores -- __syncthreads() did (s_waitcnt vmcnt(0) before every
+// s_barrier): the word pass's barrier waited on the block's word stores.
+#ifndef JH_CNT_LDSBAR
+#define JH_CNT_LDSBAR 1
+#endif
+#if JH_CNT_LDSBAR
+#define PACK_BARRIER() do { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); \
+                            __builtin_amdgcn_s_barrier(); \
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); } while (0)
+#else
+#define PACK_BARRIER() __syncthreads()
+#endif
+
 constexpr int T_INVOKE = 0, T_OK = 1, T_FAIL = 2, T_INFO = 3;
 constexpr int CHUNK = 2048, HSLOTS = 1024;
 
@@ -196,7 +212,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
         for (int i = tid; i < HSLOTS; i += PACK_THREADS) { hk[i] = 0; hv[i] = -1; hc[i] = -1; }
         for (int i = tid; i < PAIR_GROUPS * PAIR_PROCS; i += PACK_THREADS) (&M[0][0])[i] = 0;
         if (tid == 0) { nd = 0; nls = 0; }
-        __syncthreads();
+        PACK_BARRIER();
         // each row's hash slot (-1: none) and kind stay in this thread's
         // registers: only the pairing reads other rows' (round 4)
         int rsl[PER];
@@ -244,7 +260,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
             else atomicMax(&last[pk], (int)r);
             rsl[k] = slot;
         }
-        __syncthreads();
+        PACK_BARRIER();
         // compact process index of every row (the hash is complete now), and the
         // group masks of non-:info rows
         int8_t rc[PER];
@@ -276,7 +292,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
             if (c >= 0 && (cx[k] & 3) != T_INFO) atomicOr(&M[i >> 6][c], 1ULL << (i & 63));
 #endif
         }
-        __syncthreads();
+        PACK_BARRIER();
 #if JH_SPILL_TAB
         // the chunk's table for k_cnt_pair_spill: per tracked process its
         // first non-:info row here (flag << 31 | sc << 16 | row in chunk), so a
@@ -355,7 +371,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
             gotk[k] = got;                             // -1: spill (no completion in the chunk)
             if (got >= 0) sp[got] = (int16_t)i;
         }
-        __syncthreads();
+        PACK_BARRIER();
         // the contribution words
 #pragma unroll
         for (int k = 0; k < PER; k++) {
@@ -414,7 +430,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
     if ((tid & 63) == 0) {
         sh[0][tid >> 6] = am; sh[1][tid >> 6] = na; sh[2][tid >> 6] = t_lo; sh[3][tid >> 6] = t_hi; sh[4][tid >> 6] = t_nr;
     }
-    __syncthreads();                                  // (also orders every nls increment)
+    PACK_BARRIER();                                  // (also orders every nls increment)
     if (tid == 0) {
         for (int w = 1; w < PACK_THREADS / 64; w++) {
             am = max(am, sh[0][w]); na += sh[1][w]; t_lo += sh[2][w]; t_hi += sh[3][w]; t_nr += sh[4][w];

@@ -331,6 +331,10 @@ struct DfsArgs {
     // phase 3), and the number of waves that have left the queue
     unsigned long long *seq_start;
     int32_t *exit_count;
+    // round 6 (JH_LIN_HELP_STALL): the sequential search re-stamps seq_start
+    // whenever its deepest layer advances, so the late helpers pick the keys
+    // stuck longest (a big dead subtree) rather than the ones running longest
+    int32_t stamp_progress;
     // JH_DEFER_TIMES=1 (timeline study): [0] first wave start, [1] last wave
     // end (s_memrealtime), [2 + key] the time the key was handed on
     unsigned long long *defer_time;
@@ -1744,7 +1748,12 @@ insert:
         // move the window forward layer by layer
         advance(nt);
         t = nt;
-        tmax = max(tmax, t);
+        if (t > tmax) {
+            tmax = t;
+            if (A.stamp_progress && A.seq_start && lane == 0)
+                __hip_atomic_store(&A.seq_start[key], __builtin_amdgcn_s_memrealtime() | 1ULL, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
         r = lay_hi(t) & 63;
         rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
         goto expand;
@@ -2738,6 +2747,7 @@ struct WgArgs {
     uint64_t *spec_res;
     uint32_t spec_res_cap, spec_min, spec_mult, spec_dist;
     int32_t *spec_q;           // the counters (q + Q_SPEC)
+    int32_t spec_first;        // helpers serve the board before taking keys (JH_LIN_SPEC_FIRST)
 };
 
 __device__ __forceinline__ uint64_t lk_make(uint32_t t, uint32_t s, uint64_t m) {
@@ -3726,6 +3736,40 @@ constexpr unsigned long long HELPER_MAX_TICKS = 500000000ULL;   // 5 s of s_memr
 #ifndef JH_HELP_BY_ORDER
 #define JH_HELP_BY_ORDER 0
 #endif
+// Round 6: a late helper claims a posted spec job (wave 0): the smallest cap
+// first, once the main has released this helper's last dead result (its
+// buffer). Sets sh.key = -4 (a job) or -3 (lost a race: scan again).
+__device__ void spec_try_claim(const WgArgs &W, WgShared &sh, int tid) {
+    const DfsArgs &A = W.d;
+    if (!(W.spec && sh.key == -2 && tid < 64)) return;
+    SpecSlot *SB = W.spec;
+    const int lane = tid;
+    bool busy = false;
+    const int rs = sh.res_slot;
+    if (rs >= 0)
+        busy = __hip_atomic_load(&SB[rs].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == SPEC_DEAD &&
+               SB[rs].helper == (int)blockIdx.x;
+    if (busy) return;
+    const int st = __hip_atomic_load(&SB[lane].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const int k = SB[lane].key;
+    const bool cand = st == SPEC_POSTED && k >= 0 &&
+                      !__hip_atomic_load(&A.claim[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long c = cand ? ((unsigned long long)SB[lane].cap << 8) | (unsigned)lane : ~0ULL;
+    for (int o = 32; o > 0; o >>= 1) c = min(c, (unsigned long long)__shfl_xor(c, o));
+    if (c != ~0ULL && lane == 0) {
+        const int sl = (int)(c & 255);
+        int exp = SPEC_POSTED;
+        if (__hip_atomic_compare_exchange_strong(&SB[sl].state, &exp, SPEC_CLAIMED, __ATOMIC_ACQUIRE,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            sh.res_slot = -1;
+            sh.spec_slot = sl;
+            sh.key = -4;
+        } else {
+            sh.key = -3;
+        }
+    }
+}
+
 __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned long long t_enter) {
     const DfsArgs &A = W.d;
     for (;;) {
@@ -3743,6 +3787,13 @@ __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned 
         }
         __syncthreads();
         if (sh.key == -1) return;
+        if (W.spec_first) {
+            // spec jobs before keys of its own (JH_LIN_SPEC_FIRST)
+            spec_try_claim(W, sh, tid);
+            __syncthreads();
+            if (sh.key == -4) return;
+            if (sh.key == -3) continue;
+        }
         const unsigned long long now = __builtin_amdgcn_s_memrealtime();
         const int n_list = sh.n_live;
         for (int i = tid; i < n_list; i += WG_THREADS) {
@@ -3768,38 +3819,7 @@ __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned 
         }
         __syncthreads();
         if (sh.key >= 0) return;
-        if (W.spec && sh.key == -2 && tid < 64) {
-            // round 6: no key of its own to race -- a posted node of another
-            // helper's search (SpecSlot), the smallest cap first, once the main
-            // has released this helper's last dead result (its buffer)
-            SpecSlot *SB = W.spec;
-            const int lane = tid;
-            bool busy = false;
-            const int rs = sh.res_slot;
-            if (rs >= 0)
-                busy = __hip_atomic_load(&SB[rs].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == SPEC_DEAD &&
-                       SB[rs].helper == (int)blockIdx.x;
-            if (!busy) {
-                const int st = __hip_atomic_load(&SB[lane].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                const int k = SB[lane].key;
-                const bool cand = st == SPEC_POSTED && k >= 0 &&
-                                  !__hip_atomic_load(&A.claim[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                unsigned long long c = cand ? ((unsigned long long)SB[lane].cap << 8) | (unsigned)lane : ~0ULL;
-                for (int o = 32; o > 0; o >>= 1) c = min(c, (unsigned long long)__shfl_xor(c, o));
-                if (c != ~0ULL && lane == 0) {
-                    const int sl = (int)(c & 255);
-                    int exp = SPEC_POSTED;
-                    if (__hip_atomic_compare_exchange_strong(&SB[sl].state, &exp, SPEC_CLAIMED, __ATOMIC_ACQUIRE,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        sh.res_slot = -1;
-                        sh.spec_slot = sl;
-                        sh.key = -4;
-                    } else {
-                        sh.key = -3;              // lost it: scan again at once
-                    }
-                }
-            }
-        }
+        if (!W.spec_first) spec_try_claim(W, sh, tid);
         __syncthreads();
         if (sh.key == -4) return;
         if (sh.key == -2)
@@ -6938,6 +6958,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 wh.spec_res = ctx->ws<uint64_t>(WS_SPEC_RES, (size_t)n_wg * SPEC_RES_CAP);
                 wh.spec_min = 512; wh.spec_mult = 32; wh.spec_dist = 64;
                 wh.spec_q = q + Q_SPEC;
+                wh.spec_first = (lflags & JH_LIN_SPEC_FIRST) ? 1 : 0;
                 if (const char *e = tune_env("JH_SPEC_MIN")) wh.spec_min = (uint32_t)std::max(1, atoi(e));
                 if (const char *e = tune_env("JH_SPEC_MULT")) wh.spec_mult = (uint32_t)std::max(1, atoi(e));
                 if (const char *e = tune_env("JH_SPEC_DIST")) wh.spec_dist = (uint32_t)std::max(1, atoi(e));
@@ -6963,6 +6984,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         b.dbg = dbg ? dbg + 16 * 256 : nullptr; b.claim = claim;
         b.probes = (unsigned long long *)(q + 8);
         b.seq_start = seq_start; b.exit_count = seq_start ? q + 28 : nullptr;
+        b.stamp_progress = seq_start && (lflags & JH_LIN_HELP_STALL) ? 1 : 0;
         b.defer_time = nullptr;
     };
     // the streaming heavy-key pass (round 4) whenever the default race runs

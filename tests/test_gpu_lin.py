@@ -680,4 +680,9 @@ def test_spec_dead_subtrees(ctx, rank, keys):
         g2, s2 = ctx.check_cas_independent(sub, budget=budget, flags=A.LIN_HELPERS_NOW | A.LIN_NO_SPEC)
         _same(g2, c)
         assert s2.spec_jobs == 0 and s2.spec_merges == 0
+        # the scheduling variants: helpers serving the board first, helpers
+        # picking the keys stuck longest (JH_LIN_SPEC_FIRST, JH_LIN_HELP_STALL)
+        for fl in (A.LIN_SPEC_FIRST, A.LIN_HELP_STALL | A.LIN_SPEC_FIRST):
+            g3, s3 = ctx.check_cas_independent(sub, budget=budget, flags=fl, helper_late_us=100)
+            _same(g3, c)
     assert merged > 0

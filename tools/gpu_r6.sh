@@ -168,5 +168,27 @@ tl)
   # per-key timeline CSV (JH_TL_CSV) of a -DJH_TUNING variant: tl <v> <name> <rank> [bench.py args...]
   V=$1; N=$2; RK=$3; shift 3
   JH_LIB=$R/jepsen_amd/variants/libjh_$V.so JH_DEFER_TIMES=1 JH_TL_CSV=$R/$O/tl_$N.csv timeout -k 10 120 python -u bench.py --steps 1 --warmup 1 --no-cpu --e2e 0 --no-parity --seed-rank $RK "$@" > $O/tl_$N.json 2> $O/tl_$N.err ;;
+ev6a)
+  # round 6 evidence, part a: C3 strong-scaling shards (N = 2, 4, 8), ranks 1-7, the
+  # C3 line at round 4's definition (budget 2^20, exact counts)
+  for n in 2 4 8; do
+    for rk in $(seq 0 $((n - 1))); do
+      timeout -k 10 150 python -u bench.py --workload c3s --shard $rk/$n --no-cpu --e2e 0 --no-parity --steps 5 --warmup 1 > $O/c3s_${rk}of${n}.json 2> $O/c3s_${rk}of${n}.err || exit 1
+    done
+  done
+  for rk in 1 2 3 4 5 6 7; do
+    timeout -k 10 120 python -u bench.py --no-cpu --e2e 0 --no-parity --steps 5 --warmup 1 --seed-rank $rk > $O/c3r${rk}.json 2> $O/c3r${rk}.err || exit 1
+  done
+  timeout -k 10 300 python -u bench.py --no-cpu --e2e 0 --steps 10 --warmup 2 --budget 1048576 --opt flags=1024 > $O/c3_r4def.json 2> $O/c3_r4def.err ;;
+ev6b)
+  # part b: C4, C5, C2 under a kernel trace, the one-rank RCCL path
+  timeout -k 10 400 python -u bench.py --workload c4 --steps 3 --warmup 1 > $O/bench_c4.json 2> $O/bench_c4.err || exit 1
+  timeout -k 10 400 python -u bench.py --workload c5 --steps 1 --warmup 1 > $O/bench_c5.json 2> $O/bench_c5.err || exit 1
+  JH_BENCH_DIST1=1 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 > $O/dist1_pool0.json 2> $O/dist1_pool0.err || exit 1
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/c2prof -o c2 -- python3 $R/tools/bench_c2.py --steps 5 --warmup 1 --e2e > $R/$O/bench_c2.log 2>&1 ;;
+pmc6)
+  # FETCH_SIZE / WRITE_SIZE passes over the C3 search kernels (tools/pmc_traffic.py on the CPU side)
+  bash tools/gpu_pmc.sh c3 'k_lin_seq_lw' $O/pmc_c3 0 && bash tools/gpu_pmc.sh c3 'k_lin_dfs' $O/pmc_c3p1 0 ;;
 *) echo "unknown part $PART"; exit 2 ;;
 esac

@@ -89,3 +89,53 @@ done:
     cset_free(&memo); free(st); free(sid); free(nr); orc_key_free(&kk);
     return 0;
 }
+
+/* For the heavy-key pass's order (round 6): the WGL DFS of one key up to `at`
+ * inserts (phase 1's hand-over point) -- out: [0] total inserts (to the end,
+ * capped by budget), [1] tmax at `at`, [2] inserts when tmax last rose before
+ * `at`, [3] depth at `at`, [4] n_ok, [5] verdict. */
+int wgl_at(const jh_history *h, const int64_t *sel, int64_t m, int64_t init, int64_t budget, int64_t at, int64_t *out) {
+    orc_key kk; orc_key_prepare(h, sel, m, &kk); const orc_key *k = &kk;
+    out[0] = out[1] = out[2] = out[3] = 0; out[4] = k->n_ok; out[5] = -1;
+    if (k->status || k->n_ok == 0) { orc_key_free(&kk); return -1; }
+    cset memo; cset_init(&memo);
+    int64_t scap = 256, depth = 0;
+    frame *st = (frame *)malloc(sizeof(frame) * scap);
+    uint32_t t = 0, tmax = 0; int64_t s = init; int start = 0, snap = 0;
+    int64_t last_rise = 0;
+    uint64_t mask[MW] = {0};
+    int verdict = -1;
+    for (;;) {
+        if (!snap && memo.n >= at) { out[1] = tmax; out[2] = last_rise; out[3] = depth; snap = 1; }
+        const int32_t *W = k->w_ops + k->w_off[t];
+        int w = k->w_off[t + 1] - k->w_off[t];
+        int took = 0;
+        for (int i = start; i < w; i++) {
+            if (bit_get(mask, i)) continue;
+            const orc_op *o = &k->ops[W[i]];
+            int64_t s2;
+            if (!cas_step(o->f, o->v1, o->v2, s, &s2)) continue;
+            cfg c; c.s = s2;
+            cfg_lift(k, t, mask, i, &c.t, c.m);
+            if (cset_has(&memo, &c)) continue;
+            if (memo.n >= budget) { verdict = JH_UNKNOWN; goto done; }
+            cset_add(&memo, &c);
+            if (depth == scap) { scap *= 2; st = (frame *)realloc(st, sizeof(frame) * scap); }
+            st[depth].t = t; st[depth].i = i; st[depth].s = s; memcpy(st[depth].m, mask, sizeof mask); depth++;
+            t = c.t; s = c.s; memcpy(mask, c.m, sizeof mask); start = 0;
+            if (t > tmax) { tmax = t; last_rise = memo.n; }
+            if (t == (uint32_t)k->n_ok) { verdict = JH_VALID; goto done; }
+            took = 1;
+            break;
+        }
+        if (took) continue;
+        if (depth == 0) { verdict = JH_INVALID; goto done; }
+        depth--;
+        t = st[depth].t; s = st[depth].s; memcpy(mask, st[depth].m, sizeof mask); start = st[depth].i + 1;
+    }
+done:
+    if (!snap) { out[1] = tmax; out[2] = last_rise; out[3] = depth; }
+    out[0] = memo.n; out[5] = verdict;
+    cset_free(&memo); free(st); orc_key_free(&kk);
+    return 0;
+}

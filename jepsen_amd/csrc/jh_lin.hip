@@ -3344,8 +3344,11 @@ expand:
         const bool mine = st >= SPEC_DEAD && st <= SPEC_INC && SB[lane].key == key;
         const uint32_t sd = mine ? SB[lane].depth : 0u, sq = mine ? SB[lane].seq : 0u;
         const uint32_t fsq = (uint32_t)__shfl((int)f_seq, (int)(sd & 63));
+        // a node below the register ring: its frame in the HBM stack
+        const uint32_t hsq = mine && sd >= 1 && sd < ring_lo ? stack[sd].pad[0] : 0xFFFFFFFFu;
         // still on the stack: same depth, same insert index
-        const bool on = mine && sd >= 1 && sd >= ring_lo && sd <= depth && (sd == depth ? cur_seq : fsq) == sq;
+        const bool on = mine && sd >= 1 && sd <= depth &&
+                        (sd == depth ? cur_seq : sd >= ring_lo ? fsq : hsq) == sq;
         int lmax = on && st == SPEC_LIVE ? (int)sd : -1;          // live: it and its ancestors
         for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, __shfl_xor(lmax, o));
         if (lmax > l_live) l_live = lmax;
@@ -3385,6 +3388,10 @@ expand:
             next_acc = ins + acc_t;
             chk = min(budget, min(ins + chk_step, next_acc));
             depth = dmin;
+            // a node below the register ring: the ring is empty down to it, the
+            // pop refills it from the HBM stack (whose frames below ring_lo are
+            // the current ones)
+            if (dmin < ring_lo) ring_lo = dmin;
             goto pop;                  // pops node dmin
         }
         // New posts: the open nodes within spec_dist levels of the current
@@ -3392,8 +3399,8 @@ expand:
         // spec_min inserts below them and never posted (or 4x as many since),
         // deepest first, into free slots; posting counts as an attempt (inc)
         uint64_t freem = ballot(st == SPEC_FREE || mine);
-        const uint32_t dlo = max(max(max(ring_lo, 1u), (uint32_t)(l_live + 1)),
-                                 depth > W.spec_dist ? depth - W.spec_dist : 0u);
+        const uint32_t dlo_all = max(max(1u, (uint32_t)(l_live + 1)), depth > W.spec_dist ? depth - W.spec_dist : 0u);
+        const uint32_t dlo = max(ring_lo, dlo_all);
         auto elig = [&](uint32_t sqv, uint32_t inc) {
             const uint32_t b = ins - sqv;
             return b >= W.spec_min && (inc == 0 || b >= 4 * inc);
@@ -3439,6 +3446,28 @@ expand:
                                             (uint32_t)readlane((int)fm_lo, ln));
                 if (!post(d, ck, qs)) break;
                 if (lane == ln) f_inc = ins - qs;
+                nposted++;
+            }
+        }
+        if (freem && nposted < SPEC_PER_CHECK && ring_lo > dlo_all) {
+            // the nodes below the ring (a dead subtree deeper than 64 levels:
+            // rank 4's key 1631 has one of 95), from the HBM stack, deepest first
+            const uint32_t nh = min(64u, ring_lo - dlo_all);
+            const uint32_t hd = ring_lo - 1 - (uint32_t)lane;
+            Frame fr{};
+            if ((uint32_t)lane < nh) fr = stack[hd];
+            const uint64_t hm = ballot((uint32_t)lane < nh && elig(fr.pad[0], fr.pad[1]));
+            uint64_t hr = hm;
+            while (hr && freem && nposted < SPEC_PER_CHECK) {
+                const int q = __builtin_ctzll(hr);
+                hr &= hr - 1;
+                const uint32_t d = ring_lo - 1 - (uint32_t)q;
+                const uint32_t qs = (uint32_t)readlane((int)fr.pad[0], q);
+                const uint64_t fm = ((uint64_t)(uint32_t)readlane((int)(uint32_t)(fr.mask >> 32), q) << 32) |
+                                    (uint32_t)readlane((int)(uint32_t)fr.mask, q);
+                const uint64_t ck = lk_make((uint32_t)readlane((int)fr.t_i, q) >> 6, (uint32_t)readlane(fr.s, q), fm);
+                if (!post(d, ck, qs)) break;
+                if (lane == q) stack[d].pad[1] = ins - qs;
                 nposted++;
             }
         }
@@ -6956,7 +6985,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 HIP_TRY(hipMemsetAsync(wh.spec, 0, sizeof(SpecSlot) * SPEC_SLOTS, st));
                 wh.spec_res_cap = SPEC_RES_CAP;
                 wh.spec_res = ctx->ws<uint64_t>(WS_SPEC_RES, (size_t)n_wg * SPEC_RES_CAP);
-                wh.spec_min = 512; wh.spec_mult = 32; wh.spec_dist = 64;
+                wh.spec_min = 512; wh.spec_mult = 32; wh.spec_dist = 128;
                 wh.spec_q = q + Q_SPEC;
                 wh.spec_first = (lflags & JH_LIN_SPEC_FIRST) ? 1 : 0;
                 if (const char *e = tune_env("JH_SPEC_MIN")) wh.spec_min = (uint32_t)std::max(1, atoi(e));

@@ -39,7 +39,7 @@ case $PART in
 tests)
   timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread "$@" > $O/tests.log 2>&1 ;;
 final)
-  timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > $O/gpu_tests.log 2>&1 || exit 1
+  timeout -k 10 1000 python -u -m pytest -x -v --timeout 150 --timeout-method thread tests -m gpu > $O/gpu_tests.log 2>&1 || exit 1
   timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py > $O/bench_c3.json 2> $O/bench_c3.err || exit 1
   cd /tmp && export TMPDIR=/tmp

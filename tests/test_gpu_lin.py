@@ -614,9 +614,11 @@ def test_uncounted_early_emit(ctx, case):
         g, _ = ctx.check_cas_independent(cols, budget=1 << 22, exact_count=False)
         c, _ = oracle.check_cas_independent(cols, budget=1 << 22, threads=16)
     unc = g["explored"] == A.EXPLORED_UNCOUNTED
-    # the BFS alone settles many valid keys; on C3 the race leaves it the few
-    # it wins (one on seed 3, as the bench's parity_detail reports)
-    assert unc.sum() >= (5 if case == "bfs_only" else 1), unc.sum()
+    # the BFS alone settles many valid keys (forced); on C3 the race leaves it
+    # the few it wins, zero or a handful by timing (the helpers and the spec
+    # board often settle them first), so only the fields are checked there
+    if case == "bfs_only":
+        assert unc.sum() >= 5, unc.sum()
     assert (c["valid"][unc] == A.VALID).all()
     for f in ("valid", "cause", "fail_entry"):
         bad = np.nonzero(g[f] != c[f])[0]

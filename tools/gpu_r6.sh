@@ -43,7 +43,7 @@ final)
   timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py > $O/bench_c3.json 2> $O/bench_c3.err || exit 1
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/c3prof -o c3 -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu --e2e 0 --no-parity > $R/$O/c3prof.log 2>&1 ;;
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/c3prof -o c3 -- python3 $R/bench.py --steps 5 --warmup 0 --no-cpu --e2e 0 --no-parity > $R/$O/c3prof.log 2>&1 ;;
 bench)
   N=$1; shift
   timeout -k 10 600 python -u bench.py "$@" > $O/$N.json 2> $O/$N.err ;;

@@ -6921,7 +6921,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // late helpers (k_lin_wg in helper mode, wg_helper_pick): a few CUs
         // taken from the sequential search of the LEAN keys
         n_help = bfs_only || wg_race || nd_l == 0 ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 8));
-        if (opts && opts->helpers > 0) n_help = std::min(64, opts->helpers);
+        if (opts && opts->helpers > 0) n_help = std::min(ctx->n_cu / 2, opts->helpers);
         if (lflags & JH_LIN_NO_HELPERS) n_help = 0;
         if (n_help > 0 && ctx->n_cu - wg2 - n_help < 16) n_help = 0;
         // phase 2's sequential search with four waves per CU and the 32 KB memo

@@ -118,6 +118,20 @@ abopt)
       done
     done
   done ;;
+abshard)
+  # alternating c3s shard lines (strong scaling), control vs jh_lin_opts variants:
+  # abshard "<r/N>..." <reps> <name>=<bench options>...
+  SH=$1; REPS=$2; shift 2
+  B="python -u bench.py --workload c3s --steps 5 --warmup 1 --no-cpu --e2e 0 --no-parity"
+  for i in $(seq 1 $REPS); do
+    for sh in $SH; do
+      t=${sh/\//of}
+      timeout -k 10 150 $B --shard $sh > $O/ctl_s${t}_$i.json 2>/dev/null || exit 1
+      for nv in "$@"; do
+        timeout -k 10 150 $B --shard $sh ${nv#*=} > $O/${nv%%=*}_s${t}_$i.json 2>/dev/null || exit 1
+      done
+    done
+  done ;;
 tests_v)
   V=$1; shift
   L=""; [ "$V" != "-" ] && L=$R/jepsen_amd/variants/libjh_$V.so
@@ -190,5 +204,15 @@ ev6b)
 pmc6)
   # FETCH_SIZE / WRITE_SIZE passes over the C3 search kernels (tools/pmc_traffic.py on the CPU side)
   bash tools/gpu_pmc.sh c3 'k_lin_seq_lw' $O/pmc_c3 0 && bash tools/gpu_pmc.sh c3 'k_lin_dfs' $O/pmc_c3p1 0 ;;
+ev6c)
+  # part c: the PMC traffic passes, the C3 kernel trace at --warmup 0 (its
+  # stats average = the line's timed launches), per-context HBM, k_cnt_pack's
+  # instruction mix
+  bash tools/gpu_pmc.sh c3 'k_lin_seq_lw' $O/pmc_c3 0 && bash tools/gpu_pmc.sh c3 'k_lin_dfs' $O/pmc_c3p1 0 || exit 1
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/c3prof -o c3 -- python3 $R/bench.py --steps 5 --warmup 0 --no-cpu --e2e 0 --no-parity > $R/$O/c3prof.log 2>&1 || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-include-regex k_cnt_pack --output-format csv -d $R/$O/cntsq -o cntsq -- python3 $R/tools/bench_c2.py --steps 1 --warmup 0 --no-cpu > $R/$O/cntsq.log 2>&1 || exit 1
+  cd $R
+  timeout -k 10 200 python -u tools/mem_probe.py 1 > $O/mem1.json 2> $O/mem1.err && timeout -k 10 200 python -u tools/mem_probe.py 2 > $O/mem2.json 2> $O/mem2.err ;;
 *) echo "unknown part $PART"; exit 2 ;;
 esac

@@ -99,6 +99,19 @@ constexpr uint32_t F2_OTHER = 0, F2_ADD = 1, F2_READ = 2;
 //   bits 5-31 the value, 27-bit signed (adds of 1 in the C2 workload)
 constexpr uint32_t CW_NONE = 0, CW_LO = 1, CW_HI = 2, CW_OKREAD = 3, CW_INVREAD = 4, CW_PEND = 5;
 constexpr uint32_t CW_U = 8, CW_X = 16;
+#ifndef JH_CNT_LUT
+#define JH_CNT_LUT 1         // the word pass by a class LUT and selects (0: per-kind branches)
+#endif
+// The word pass's row classes by f2 << 2 | type (4 bits each): bits 0-2 the
+// kind (HI for an :invoke :add, whose word depends on its completion; LO, the
+// two reads), bit 3 the row may carry CW_U (:ok / :fail rows)
+constexpr unsigned long long cnt_lut_entry(uint32_t q) {
+    return (q & 3) == 0 ? ((q >> 2) == F2_ADD ? CW_HI : (q >> 2) == F2_READ ? CW_INVREAD : CW_NONE)
+         : (q & 3) == 1 ? 8u | ((q >> 2) == F2_ADD ? CW_LO : (q >> 2) == F2_READ ? CW_OKREAD : CW_NONE)
+         : (q & 3) == 2 ? 8u : 0u;
+}
+constexpr unsigned long long cnt_lut(uint32_t q) { return q == 12 ? 0ULL : (cnt_lut_entry(q) << (4 * q)) | cnt_lut(q + 1); }
+constexpr unsigned long long CNT_KIND_LUT = cnt_lut(0);
 constexpr long long CW_VMAX = (1LL << 26) - 1, CW_VMIN = -(1LL << 26);
 __device__ __forceinline__ uint32_t cw_make(uint32_t kind, long long v) {
     if (v < CW_VMIN || v > CW_VMAX) return kind | CW_X;
@@ -373,6 +386,50 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
         }
         PACK_BARRIER();
         // the contribution words
+#if JH_CNT_LUT
+        // Round 6: the (type, f) class from a LUT and the
+        // word by selects; only the rare rows branch (a spill's store, a nil
+        // value, an orphan read, a partner's value)
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int i = k * PACK_THREADS + tid;
+            if (i >= nc) continue;
+            const uint32_t x = cx[k];
+            const uint32_t ty = x & 3;
+            const int64_t r = c0 + i;
+            const uint32_t e = (uint32_t)(CNT_KIND_LUT >> (4 * x)) & 15u;
+            const uint32_t kd = e & 7u;
+            const int c = ty == T_INVOKE ? gotk[k] : (int)sp[i];
+            const bool spl = ty == T_INVOKE && c == -1;
+            if (spl)
+                spill[c0 + atomicAdd(&nls, 1)] = make_uint2((uint32_t)(walk_from_end[k] ? ~(int32_t)r : (int32_t)r),
+                                                            cp[k] | ((x >> 2) << 28));
+            const uint32_t psc = sc[c > 0 ? c : 0];
+            long long v = cv[k];
+            const bool hi = kd == CW_HI && c >= 0 && (psc & 3) != T_FAIL;
+            const bool lo = kd == CW_LO;
+            const bool okr = kd == CW_OKREAD;
+            const bool own = !(hi && v == JH_NIL);
+            if (!own) v = val[c0 + c];
+            const bool isv = hi || lo;
+            const bool nil = isv && v == JH_NIL;
+            const bool orphan = okr && c >= 0 && (psc >> 2) != F2_READ;
+            if (nil || orphan)
+                atomicMin(&m->viol2, ((unsigned long long)r << 4) | (nil ? JH_CAUSE_NIL_VALUE : JH_CAUSE_ORPHAN));
+            const bool fits = v >= CW_VMIN && v <= CW_VMAX;
+            const uint32_t vw = fits ? ((uint32_t)(int32_t)v << 5) : CW_X;
+            const bool good = isv && !nil;
+            uint32_t w = good ? (kd | vw) : kd == CW_HI ? (spl ? CW_PEND : CW_NONE) : lo || orphan ? CW_NONE : kd;
+            w |= (e >> 3) && c < 0 ? CW_U : 0u;
+            const long long vz = good ? v : 0;
+            t_hi += hi ? vz : 0;
+            t_lo += lo ? vz : 0;
+            const bool rd = okr && !orphan && c >= 0;
+            t_nr += rd ? 1 : 0;
+            if (rd || (hi && !own && !fits)) pair[r] = (int32_t)(c0 + c);
+            cw[r] = w;
+        }
+#else
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const int i = k * PACK_THREADS + tid;
@@ -422,6 +479,7 @@ __global__ void __launch_bounds__(PACK_THREADS) k_cnt_pack(const int64_t *__rest
             }
             cw[r] = w;
         }
+#endif
     }
     for (int o = 32; o > 0; o >>= 1) {
         am = max(am, (long long)__shfl_xor(am, o)); na += (long long)__shfl_xor(na, o);

@@ -180,7 +180,7 @@ typedef struct jh_lin_opts {
     int64_t phase2_budget;     /* phase-2 inserts before a key restarts in phase 3; <=0: 65536 */
     /* scheduling of the heavy-key pass (every value decides the same verdicts;
      * the parity tests run the less common paths through these): */
-    int32_t helpers;           /* phase-2 late helper workgroups; <=0: 32, at most half the CUs (JH_LIN_NO_HELPERS: none) */
+    int32_t helpers;           /* phase-2 late helper workgroups; <=0: 64 (a quarter of the CUs), at most half the CUs (JH_LIN_NO_HELPERS: none) */
     int32_t helper_late_us;    /* run time before a helper takes a key; <=0: 250 (JH_LIN_HELPERS_NOW: 0) */
     int32_t xw_waves;          /* waves of the 65-256-member search; <=0: one per key, up to 4 per CU */
     int32_t p2_waves_per_cu;   /* 1: phase 2 at one wave per CU with the 128 KB LDS memo; else 4,

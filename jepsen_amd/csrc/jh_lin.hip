@@ -492,8 +492,13 @@ constexpr int32_t P1_PRIO_INS = 0;
 // phase-2 late helpers (workgroups, one per CU) and how long a key must have run
 // in the sequential search before one takes it: 32 and 250 us measured against
 // 16 and 2 000 us (C3 rank 0 43.2 -> 40.9 ms, ranks 3 / 6 unchanged; the sweep
-// of tools/gpu_env_sweep.sh is flat from 24 to 48 helpers and 0 to 250 us)
-constexpr int HELPERS = 32;
+// of tools/gpu_env_sweep.sh is flat from 24 to 48 helpers and 0 to 250 us).
+// Round 6, with the spec board (idle helpers enumerate the mains' dead
+// subtrees): 64 (a quarter of the CUs), measured against 32 and 96
+// (profiles/r06/ab_helpers64/: C3 rank 0 39.5 -> 39.2 ms, rank 4 47.7 ->
+// 45.3, the strong-scaling shards' max at N = 2 / 4 / 8 35.9 / 29.1 / 24.7 ->
+// 32.6 / 24.9 / 21.1 ms; 96 leaves the sequential search too few CUs)
+constexpr int HELPERS = 64;
 constexpr uint64_t HELPER_LATE_US = 250;
 
 // write a key's verdict; in a race only the first finisher writes
@@ -6920,7 +6925,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
 
         // late helpers (k_lin_wg in helper mode, wg_helper_pick): a few CUs
         // taken from the sequential search of the LEAN keys
-        n_help = bfs_only || wg_race || nd_l == 0 ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 8));
+        n_help = bfs_only || wg_race || nd_l == 0 ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 4));
         if (opts && opts->helpers > 0) n_help = std::min(ctx->n_cu / 2, opts->helpers);
         if (lflags & JH_LIN_NO_HELPERS) n_help = 0;
         if (n_help > 0 && ctx->n_cu - wg2 - n_help < 16) n_help = 0;

@@ -6927,15 +6927,21 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // taken from the sequential search of the LEAN keys
         n_help = bfs_only || wg_race || nd_l == 0 ? 0 : std::min(HELPERS, std::max(0, ctx->n_cu / 4));
         if (opts && opts->helpers > 0) n_help = std::min(ctx->n_cu / 2, opts->helpers);
+        if (const char *e = tune_env("JH_HELPERS")) n_help = std::max(0, std::min(ctx->n_cu, atoi(e)));
         if (lflags & JH_LIN_NO_HELPERS) n_help = 0;
-        if (n_help > 0 && ctx->n_cu - wg2 - n_help < 16) n_help = 0;
+        // JH_HELP_CUS (tuning builds): CUs the sizing of phase 2's sequential
+        // search leaves to the helpers (default: one per helper); helpers
+        // beyond it start when CUs free up
+        int help_cus = n_help;
+        if (const char *e = tune_env("JH_HELP_CUS")) help_cus = std::max(0, std::min(n_help, atoi(e)));
+        if (n_help > 0 && ctx->n_cu - wg2 - help_cus < 16) n_help = help_cus = 0;
         // phase 2's sequential search with four waves per CU and the 32 KB memo
         // (k_lin_seq3), p2_waves_per_cu = 1 for one wave per CU and the 128 KB
         // memo (k_lin_seq): measured C4 shard 268 -> 228 ms, C3 / ranks 3, 6 / C5 flat
         p2_m = !(opts && opts->p2_waves_per_cu == 1);
         cap2l = cap2;
         if (nd_l > 0) {
-            const int cus2 = std::max(1, ctx->n_cu - wg2 - n_help);
+            const int cus2 = std::max(1, ctx->n_cu - wg2 - help_cus);
             // LEAN keys alone in the grid: MemoP2's waves per CU
             const int lean_per_cu = n_def_w > 0 || !p2_small_ok ? 4 : JH_P2_PER_CU;
             int want2 = std::min(nd_l, cus2 * (p2_m ? lean_per_cu : 1));

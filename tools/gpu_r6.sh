@@ -159,6 +159,19 @@ abenv)
       done
     done
   done ;;
+abenvsh)
+  # abenv over c3s shards (strong scaling): abenvsh <v> "<r/N>..." <reps> <name>=<VAR=value,...>...
+  V=$1; SH=$2; REPS=$3; shift 3
+  B="python -u bench.py --workload c3s --steps 5 --warmup 1 --no-cpu --e2e 0 --no-parity"
+  for i in $(seq 1 $REPS); do
+    for sh in $SH; do
+      t=${sh/\//of}
+      timeout -k 10 150 $B --shard $sh > $O/base_s${t}_$i.json 2>/dev/null || exit 1
+      for nv in "$@"; do
+        env $(echo ${nv#*=} | tr ',' ' ') JH_LIB=$R/jepsen_amd/variants/libjh_$V.so timeout -k 10 150 $B --shard $sh > $O/${nv%%=*}_s${t}_$i.json 2>/dev/null || exit 1
+      done
+    done
+  done ;;
 ingest)
   L=$R/jepsen_amd/variants/libjh_$1.so
   JH_LIB=$L JH_INGEST_TRACE=1 timeout -k 10 300 python -u tools/ingest_probe.py > $O/ingest_packed.log 2>&1 || exit 1

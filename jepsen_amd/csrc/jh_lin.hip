@@ -2753,6 +2753,7 @@ struct WgArgs {
     uint32_t spec_res_cap, spec_min, spec_mult, spec_dist;
     int32_t *spec_q;           // the counters (q + Q_SPEC)
     int32_t spec_first;        // helpers serve the board before taking keys (JH_LIN_SPEC_FIRST)
+    int32_t n_mains;           // helpers [n_mains, grid) only serve the board (never take a key)
 };
 
 __device__ __forceinline__ uint64_t lk_make(uint32_t t, uint32_t s, uint64_t m) {
@@ -3821,7 +3822,9 @@ __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned 
         }
         __syncthreads();
         if (sh.key == -1) return;
-        if (W.spec_first) {
+        // a server (JH_SPEC_SERVERS, tuning builds) takes spec jobs only
+        const bool server = W.spec && (int)blockIdx.x >= W.n_mains;
+        if (W.spec_first || server) {
             // spec jobs before keys of its own (JH_LIN_SPEC_FIRST)
             spec_try_claim(W, sh, tid);
             __syncthreads();
@@ -3829,7 +3832,7 @@ __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned 
             if (sh.key == -3) continue;
         }
         const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-        const int n_list = sh.n_live;
+        const int n_list = server ? 0 : sh.n_live;
         for (int i = tid; i < n_list; i += WG_THREADS) {
             const int key = A.live_n ? ld_agent(&A.list[i]) : A.list[i];
             if (key < 0) continue;
@@ -3853,7 +3856,7 @@ __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned 
         }
         __syncthreads();
         if (sh.key >= 0) return;
-        if (!W.spec_first) spec_try_claim(W, sh, tid);
+        if (!(W.spec_first || server)) spec_try_claim(W, sh, tid);
         __syncthreads();
         if (sh.key == -4) return;
         if (sh.key == -2)
@@ -6999,6 +7002,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 wh.spec_min = 512; wh.spec_mult = 32; wh.spec_dist = 128;
                 wh.spec_q = q + Q_SPEC;
                 wh.spec_first = (lflags & JH_LIN_SPEC_FIRST) ? 1 : 0;
+                wh.n_mains = n_wg;
+                if (const char *e = tune_env("JH_SPEC_SERVERS")) wh.n_mains = std::max(1, n_wg - std::max(0, atoi(e)));
                 if (const char *e = tune_env("JH_SPEC_MIN")) wh.spec_min = (uint32_t)std::max(1, atoi(e));
                 if (const char *e = tune_env("JH_SPEC_MULT")) wh.spec_mult = (uint32_t)std::max(1, atoi(e));
                 if (const char *e = tune_env("JH_SPEC_DIST")) wh.spec_dist = (uint32_t)std::max(1, atoi(e));

@@ -473,7 +473,7 @@ def main():
                        "resumed_keys": int(s.resumed), "resume_bytes": int(s.resume_bytes),
                        # round 6: speculative dead-subtree enumerations by idle late helpers
                        "spec": {"jobs": int(s.spec_jobs), "dead": int(s.spec_dead), "merges": int(s.spec_merges),
-                                "merged_nodes": int(s.spec_nodes)},
+                                "merged_nodes": int(s.spec_nodes), "takeovers": int(s.takeovers)},
                        "phases": phase_table(sums), "opts": args.tune or None},
             "shard": shard_info,
             "pool": ({"mode": "two-stage (shard.two_stage_resident): phase 1 per rank, deferred keys' rows "

@@ -169,6 +169,10 @@ typedef struct jh_history {
  * longest without reaching a deeper layer (stuck in a big dead subtree)
  * instead of the ones running longest (scheduling only). */
 #define JH_LIN_HELP_STALL   8192
+/* Round 6: a late helper that takes a key phase 2's sequential search is
+ * running restarts it instead of continuing its saved state (the takeover;
+ * same verdicts and counts either way). */
+#define JH_LIN_NO_TAKEOVER  16384
 
 typedef struct jh_lin_opts {
     int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */
@@ -278,6 +282,9 @@ typedef struct jh_summary {
     int64_t spec_dead;
     int64_t spec_merges;
     int64_t spec_nodes;
+    /* round 6: keys a late helper took over from the sequential search with
+     * its saved state (the takeover; JH_LIN_NO_TAKEOVER: 0) */
+    int64_t takeovers;
 } jh_summary;
 
 typedef struct jh_ctx jh_ctx;

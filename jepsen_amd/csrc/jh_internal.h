@@ -120,7 +120,7 @@ enum WsSlot {
     WS_DEFER64, WS_DEFER64_T, WS_MEMO_WIDE, WS_STACK_WIDE, WS_SCRATCH_WIDE,
     WS_CFG_SLOT, WS_CFG_OUT, WS_CFG_N, WS_CFG_ROWS, WS_CFG_KEYS,
     WS_S_RB_HIST, WS_S_RB_OUT, WS_TL, WS_RS_ARENA, WS_RS_OFF, WS_RS_LOG, WS_DEFER_INFO,
-    WS_SPEC, WS_SPEC_RES, WS_DEBUG_WG,
+    WS_SPEC, WS_SPEC_RES, WS_DEBUG_WG, WS_HANDOFF, WS_RS_LOG2,
     WS_COUNT
 };
 

@@ -392,7 +392,14 @@ struct DfsArgs {
     uint32_t hlog_cap;
     // JH_DEFER_TIMES (tuning builds): per deferred key {inserts, tmax | n_ok << 32}
     unsigned long long *defer_info;
+    // Round 6, the takeover: per key, a late helper that takes a key phase 2's
+    // sequential search is running asks it for its state (HO_ASK); the search
+    // saves its record at its next check (HO_SAVING, then HO_DONE with
+    // rs_off[key] set, or HO_REFUSED) and leaves the key, and the helper's
+    // dfs_acc continues it instead of restarting it. null: off.
+    int32_t *handoff;
 };
+constexpr int32_t HO_NONE = 0, HO_ASK = 1, HO_DONE = 2, HO_REFUSED = 3, HO_WITHDRAWN = 4, HO_SAVING = 5;
 constexpr int TL_W = 6;         // timeline words per key: BFS, sequential, helper (start, end)
 #ifdef JH_TUNING
 #define TL_REC(tl, key, w) \
@@ -1515,6 +1522,7 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
     wave_sync();
     uint32_t ins_saved = 0xFFFFFFFFu;     // a handed-over search's real insert count
     uint32_t nlog = 0;                    // hlog entries (saturating at 0xFFFF)
+    bool ho = false;                      // a late helper takes this search over (A.handoff)
     // move the window forward from layer t to layer nt (a lift, or a resume)
     auto advance = [&](uint32_t nt) {
         for (uint32_t u = t; u < nt; u++) {
@@ -1553,7 +1561,9 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
                 for (uint32_t j = (uint32_t)lane; j < (uint32_t)h_n; j += 64) {
                     const ulonglong2 e = ent[j];
                     const uint32_t et = (uint32_t)(e.y >> 20) & T_MASK, es = (uint32_t)e.y & STATE_MASK;
-                    hbm_insert(memo, cap_mask, gen, et, es, e.x);
+                    const uint32_t sl = hbm_insert(memo, cap_mask, gen, et, es, e.x);
+                    // (a takeover's save gathers the restored entries too)
+                    if (hlog && j < A.hlog_cap) hlog[j] = sl;
                     uint32_t g1, g2;
                     lk_hash((uint32_t)e.x, (uint32_t)(e.x >> 32) | (et << 16) | (es << 8) | 0x80000000u, g1, g2);
                     bloom_set2<M>(bloom, lk_bl(g1), lk_bl(g2));
@@ -1561,6 +1571,7 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
                 }
                 for (int o = 32; o > 0; o >>= 1) tmx = max(tmx, (uint32_t)__shfl_xor((int)tmx, o));
                 theta = rflu(tmx);
+                nlog = (uint32_t)min<uint64_t>(h_n, 0xFFFFu);
                 ring_lo = d > 32 ? d - 32 : 0;
                 for (uint32_t j = (uint32_t)lane; j < ring_lo; j += 64) stack[j] = fsrc[j];
                 {
@@ -1679,7 +1690,24 @@ insert:
                 else if (ins >= 2u * (uint32_t)A.prio_ins) __builtin_amdgcn_s_setprio(2);
                 else __builtin_amdgcn_s_setprio(1);
             }
-            chk = min(budget, ins + 1024);
+            if (A.handoff) {
+                // round 6: a late helper asks for this search (the takeover);
+                // saved only if the slot log holds every HBM entry of the key
+                int h = 0;
+                if (lane == 0) h = __hip_atomic_load(&A.handoff[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (readlane(h, 0) == HO_ASK) {
+                    const bool ok = hlog && nlog <= A.hlog_cap;
+                    int won = 0;
+                    if (lane == 0) {
+                        int exp = HO_ASK;
+                        won = __hip_atomic_compare_exchange_strong(&A.handoff[key], &exp, ok ? HO_SAVING : HO_REFUSED,
+                                                                   __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT) ? 1 : 0;
+                    }
+                    if (readlane(won, 0) && ok) { ho = true; verdict = JH_CANCELLED; goto done; }
+                }
+            }
+            chk = min(budget, ins + (A.handoff ? 256u : 1024u));
         }
         const int i = __builtin_ctzll(absent);
         ins++;
@@ -1818,7 +1846,7 @@ pop:
     goto insert;
 
 done:
-    if (A.rs_mode == 1 && A.rs_off && verdict == JH_UNKNOWN && A.defer) {
+    if ((A.rs_mode == 1 && A.rs_off && verdict == JH_UNKNOWN && A.defer) || ho) {
         // Save the deferred search for phase 2 (round 5): header {mask, t | s << 32,
         // depth | tmax << 32, inserts, entries}, the stack frames, then every
         // configuration in the memo as {mask, t << 20 | s}: the LDS ones and this
@@ -1893,8 +1921,17 @@ done:
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             if (lane == 0 && n == nmem) {
                 A.rs_off[key] = (int64_t)off;
-                atomicAdd((int32_t *)A.rs_used + 2, 1);       // Q_RS_N: records published
+                // Q_RS_N: records published; [91]: takeovers (round 6)
+                atomicAdd((int32_t *)A.rs_used + (ho ? 3 : 2), 1);
             }
+            if (ho && lane == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __hip_atomic_store(&A.handoff[key], n == nmem ? HO_DONE : HO_REFUSED, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else if (ho && lane == 0) {
+            // no room in the arena: the helper restarts the key
+            __hip_atomic_store(&A.handoff[key], HO_REFUSED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     inserts = ins;
@@ -2414,7 +2451,7 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
         int verdict;
         uint32_t ins_real = 0;
         if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes, ins_real,
-                                                  A.rs_mode == 1 && A.hlog ? A.hlog + wv * A.hlog_cap : nullptr);
+                                                  (A.rs_mode == 1 || A.handoff) && A.hlog ? A.hlog + wv * A.hlog_cap : nullptr);
         else if constexpr (WL) verdict = dfs_lean_w<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         if (A.dbg && lane == 0) { A.dbg[16 * wv + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * wv + 3] += 1; }
@@ -3176,12 +3213,42 @@ __device__ void wg_merge(const WgArgs &W, WgShared &sh, int tid, uint64_t *memo,
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// The takeover's restore, out of line (dfs_acc's registers stay its own):
+// the record's configurations into the HBM table and Bloom filter, its frames
+// below the ring into the HBM stack (insert index hseq). Returns one past the
+// highest restored layer (the theta above which no probe needs HBM).
+template <class M>
+__device__ __noinline__ uint32_t acc_restore(const uint64_t *hd, uint32_t d, uint32_t h_n, uint32_t ring_lo,
+                                             uint32_t hseq, uint64_t *memo, uint32_t cap_mask, uint32_t gen,
+                                             uint32_t *bloom, Frame *stack, int lane) {
+    const Frame *fsrc = (const Frame *)(hd + 8);
+    const ulonglong2 *ent = (const ulonglong2 *)(fsrc + d);
+    uint32_t tmx = 0;
+    for (uint32_t j = (uint32_t)lane; j < h_n; j += 64) {
+        const ulonglong2 e = ent[j];
+        const uint32_t et = (uint32_t)(e.y >> 20) & T_MASK, es = (uint32_t)e.y & STATE_MASK;
+        hbm_insert(memo, cap_mask, gen, et, es, e.x);
+        uint32_t g1, g2;
+        lk_hash((uint32_t)e.x, (uint32_t)(e.x >> 32) | (et << 16) | (es << 8) | 0x80000000u, g1, g2);
+        bloom_set2<M>(bloom, lk_bl(g1), lk_bl(g2));
+        tmx = max(tmx, et + 1);
+    }
+    for (int o = 32; o > 0; o >>= 1) tmx = max(tmx, (uint32_t)__shfl_xor((int)tmx, o));
+    for (uint32_t j = (uint32_t)lane; j < ring_lo; j += 64) {
+        Frame fr = fsrc[j];
+        fr.pad[0] = hseq; fr.pad[1] = 0;
+        stack[j] = fr;
+    }
+    return tmx;
+}
+
 // dfs_lean with the acceleration hooks (see above). Only wave 0 runs it; the
 // other waves wait at the workgroup barrier for wg_enum_work.
 template <class M>
 __device__ int dfs_acc(const WgArgs &W, WgShared &sh, const KeyInfo &K, const char *tb, int key, int lane,
                        uint64_t *memo, Frame *stack, uint64_t *stage, uint64_t *gset, uint64_t *work, char *wtab,
-                       uint64_t *pend, long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes) {
+                       uint64_t *pend, long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes,
+                       const bool resume) {
     const DfsArgs &A = W.d;
     const OpC *ops = (const OpC *)tb;
     const Lay *lay = (const Lay *)(tb + tblc_ops_bytes(K));
@@ -3247,8 +3314,67 @@ __device__ int dfs_acc(const WgArgs &W, WgShared &sh, const KeyInfo &K, const ch
     load_up(P);
     wave_sync();
     uint32_t ins_saved = 0xFFFFFFFFu;     // a handed-over search's real insert count
-    // (the workgroup engine never continues a phase-1 record -- its
-    // searches start at the root -- so dfs_lean's resume block has no copy here)
+    if (resume) {
+        // Round 6, the takeover: continue the record phase 2's sequential
+        // search saved for this helper (dfs_lean's save: header, frames, every
+        // configuration of its memo). As dfs_lean's resume: the memo into the
+        // HBM table behind the Bloom filter with theta above every restored
+        // layer, the stack into the ring and the HBM stack, then the current
+        // configuration is expanded again. The restored frames' insert index is
+        // the record's insert count (a node pushed later has a larger one, so a
+        // spec result still names one stack node).
+        const uint64_t *hd = (const uint64_t *)(A.rs_arena + A.rs_off[key]);
+        const uint64_t h_mask = hd[0], h_ts = hd[1], h_dt = hd[2], h_ins = hd[3], h_n = hd[4];
+        const uint32_t d = (uint32_t)h_dt;
+        if (d <= A.stack_cap && h_n <= (uint64_t)A.memo_cap / 4) {
+            const Frame *fsrc = (const Frame *)(hd + 8);
+            const uint32_t hseq = (uint32_t)h_ins;
+            ring_lo = d > 32 ? d - 32 : 0;
+            theta = rflu(acc_restore<M>(hd, d, (uint32_t)h_n, ring_lo, hseq, memo, cap_mask, gen, bloom, stack, lane));
+            {
+                const uint32_t idx = ring_lo + (((uint32_t)lane - ring_lo) & 63);
+                if (idx < d) {
+                    const Frame fr = fsrc[idx];
+                    fm_lo = (uint32_t)fr.mask; fm_hi = (uint32_t)(fr.mask >> 32); f_ti = fr.t_i;
+                    f_s = (uint32_t)fr.s; fr_lo = (uint32_t)fr.rest; fr_hi = (uint32_t)(fr.rest >> 32);
+                    f_seq = hseq; f_inc = 0;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            wave_sync();
+            depth = d;
+            mask = h_mask;
+            s = (uint32_t)(h_ts >> 32);
+            ins = hseq;
+            cur_seq = hseq;
+            chk = min(budget, ins);                  // the next insert runs the checks
+            next_acc = ins + acc_t;
+            spec_chk = ins;
+            // the window forward from layer 0 to the record's layer
+            const uint32_t nt = (uint32_t)h_ts;
+            for (uint32_t u = t; u < nt; u++) {
+                const uint32_t ru = u == t ? r : (lay_hi(u) & 63);
+                const uint32_t shv = (uint32_t)wave_shl1((int)wrq);
+                if (lane >= (int)ru) wrq = shv;
+                w--;
+                if (lane == w) wrq = RQ_EMPTY;
+                const int c = (int)(lay_hi(u + 1) >> 6);
+                if (c > 0) {
+                    if (P < pb || P + c > pb + 64) load_up(c <= 32 && P >= 32 ? P - 32 : P);
+                    for (int kk = 0; kk < c; kk++) {
+                        const uint32_t x = (uint32_t)readlane((int)urq, P - pb + kk);
+                        if (lane == w + kk) wrq = x;
+                    }
+                    w += c; P += c;
+                }
+            }
+            t = nt;
+            tmax = max((uint32_t)(h_dt >> 32), t);
+            r = lay_hi(t) & 63;
+            rn = t + 1 < n_ok ? (lay_hi(t + 1) & 63) : 0;
+        }
+    }
     const ulonglong2 *B = (const ulonglong2 *)lmemo;
     uint64_t absent = 0, nm_r = 0;
     uint32_t u_r = 0, klo = 0, khi = 0, b1 = 0, b2 = 0, n1 = 0, n2 = 0, h1 = 0, h2 = 0, nvl = 0;
@@ -4000,8 +4126,35 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
             uint32_t tmax = 0;
             const unsigned long long ck0 = __builtin_amdgcn_s_memtime();
             TL_REC(A.tl, key, 4);
+            // Round 6, the takeover: ask the sequential search for its state
+            // (it answers at its next check, every 256 inserts); a search that
+            // does not answer within ~3 ms (not running this key) is withdrawn
+            // from, and a refused or unsaved one restarts here from the root
+            int ho_st = HO_NONE;
+            if (A.handoff && lane == 0) {
+                __hip_atomic_store(&A.handoff[key], HO_ASK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long h0 = __builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    ho_st = __hip_atomic_load(&A.handoff[key], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    if (ho_st == HO_DONE || ho_st == HO_REFUSED) break;
+                    if (__hip_atomic_load(&A.claim[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+                    const unsigned long long el = __builtin_amdgcn_s_memrealtime() - h0;
+                    if (ho_st == HO_ASK && el > 300000ULL) {
+                        int exp = HO_ASK;
+                        if (__hip_atomic_compare_exchange_strong(&A.handoff[key], &exp, HO_WITHDRAWN, __ATOMIC_RELAXED,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                            ho_st = HO_WITHDRAWN;
+                            break;
+                        }
+                        continue;
+                    }
+                    if (el > HELPER_MAX_TICKS) break;      // (a save never takes this long)
+                    __builtin_amdgcn_s_sleep(16);
+                }
+            }
+            ho_st = readlane(ho_st, 0);
             const int verdict = dfs_acc<MemoW>(W, sh, K, A.tables + mt.off, key, lane, memo, stack, stage, gset,
-                                               work, wtab, pend, inserts, tmax, my_probes);
+                                               work, wtab, pend, inserts, tmax, my_probes, ho_st == HO_DONE);
             TL_REC(A.tl, key, 5);
             if (W.spec) spec_release(W, key, lane);
             jh_key_verdict v;
@@ -6362,7 +6515,7 @@ constexpr int Q_T_WIDE = 46;        // [46..47] first WIDE wave start, [48..49] 
 constexpr int Q_P1_DONE = 64, Q_SEQ_WAVES = 65, Q_BFS_QUEUE = 66;
 constexpr int Q_T_BFS = 68, Q_T_LEAN = 72, Q_T_XW = 76, Q_T_P1 = 80;
 constexpr int Q_ENT_P3 = 84;        // entries of the LEAN keys restarted in phase 3
-constexpr int Q_RS_USED = 88;       // [88..89] resume records' bytes, [90] records published (round 5)
+constexpr int Q_RS_USED = 88;       // [88..89] resume records' bytes, [90] records published (round 5), [91] takeovers (round 6)
 constexpr int Q_SPEC = 96;          // round 6: [96..97] merged nodes, [98] merges, [99] spec jobs, [100] dead results
 // LEAN sequential waves launched with the BFS while phase 1 still runs (the
 // rest start behind phase 1): enough for the keys deferred before it ends
@@ -6649,7 +6802,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         const uint64_t rs_lim = (uint64_t)ctx->hbm_total /
                                 (64 * (uint64_t)std::max(ctx->share, device_open_contexts(ctx->device)));
         const uint64_t per_key = 64 + (uint64_t)stack_cap * sizeof(Frame) + (uint64_t)quick * 16;
-        const uint64_t cap = std::min<uint64_t>(std::min<uint64_t>((uint64_t)256 << 20, rs_lim), (uint64_t)K * per_key);
+        // (+ 64 MB for the takeovers' records, round 6)
+        const uint64_t cap = std::min<uint64_t>(std::min<uint64_t>((uint64_t)320 << 20, rs_lim),
+                                                (uint64_t)K * per_key + ((uint64_t)64 << 20));
         a.rs_arena = ctx->ws<uint8_t>(WS_RS_ARENA, cap);
         a.rs_cap = cap;
         a.rs_off = ctx->ws<int64_t>(WS_RS_OFF, K);
@@ -7036,6 +7191,18 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         b.seq_start = seq_start; b.exit_count = seq_start ? q + 28 : nullptr;
         b.stamp_progress = seq_start && (lflags & JH_LIN_HELP_STALL) ? 1 : 0;
         b.defer_time = nullptr;
+        // round 6, the takeover: a late helper continues the sequential
+        // search's record (phase 2's own slot log, 32 K entries per wave)
+        // instead of restarting the key
+        b.handoff = nullptr;
+        if (n_help > 0 && a.rs_off && waves2 > 0 && !(lflags & JH_LIN_NO_TAKEOVER)) {
+            int32_t *ho = ctx->ws<int32_t>(WS_HANDOFF, K);
+            HIP_TRY(hipMemsetAsync(ho, 0, (size_t)K * sizeof(int32_t), st));
+            b.handoff = ho;
+            b.hlog_cap = 32768;
+            b.hlog = ctx->ws<uint32_t>(WS_RS_LOG2, (size_t)wmax * b.hlog_cap);
+            wh.d.handoff = ho;
+        }
     };
     // the streaming heavy-key pass (round 4) whenever the default race runs
     const bool stream_p2 = !linear_mode && !skip_p1 && !p1_only && !use_wg && !wg_race && !dbg2 &&
@@ -7181,7 +7348,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 c3.list = defer3; c3.n_list = 0; c3.n_list_dev = q + 16; c3.defer = 0; c3.live_n = nullptr;
                 c3.defer_list = nullptr; c3.defer_count = nullptr;
                 c3.seq_start = nullptr; c3.exit_count = nullptr; c3.t_span = nullptr; c3.wave_off = 0;
-                c3.budget = budget; c3.budget_full = 0;
+                c3.budget = budget; c3.budget_full = 0; c3.handoff = nullptr;
                 c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
                 c3.dbg = nullptr;
                 c3.probes = (unsigned long long *)(q + Q_PROBES_P3);
@@ -7499,7 +7666,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
                 c3.list = defer3; c3.n_list = 0; c3.n_list_dev = q + 16; c3.defer = 0;
                 c3.defer_list = nullptr; c3.defer_count = nullptr;
                 c3.seq_start = nullptr; c3.exit_count = nullptr;
-                c3.budget = budget; c3.budget_full = 0;
+                c3.budget = budget; c3.budget_full = 0; c3.handoff = nullptr;
                 c3.memo_cap = cap2;
                 c3.gen_base = ctx->gen_base + 2 * (uint32_t)K + 1;
                 c3.dbg = nullptr;
@@ -7742,6 +7909,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         sum->p3_entries = q64(qh, Q_ENT_P3);
         sum->p2_start_ms = -1; sum->p1_span_ms = 0;
         sum->resumed = resume ? qh[Q_RS_USED + 2] : 0;
+        sum->takeovers = resume ? qh[Q_RS_USED + 3] : 0;
         sum->spec_nodes = q64(qh, Q_SPEC); sum->spec_merges = qh[Q_SPEC + 2];
         sum->spec_jobs = qh[Q_SPEC + 3]; sum->spec_dead = qh[Q_SPEC + 4];
         sum->resume_bytes = resume ? q64(qh, Q_RS_USED) : 0;

@@ -688,3 +688,34 @@ def test_spec_dead_subtrees(ctx, rank, keys):
             g3, s3 = ctx.check_cas_independent(sub, budget=budget, flags=fl, helper_late_us=100)
             _same(g3, c)
     assert merged > 0
+
+
+@pytest.mark.parametrize("rank,keys", [(0, [1086, 8979, 4457, 8190, 932, 3101]), (4, [1631, 4356])])
+def test_takeover(ctx, rank, keys):
+    """Round 6, the takeover: a late helper that takes a key phase 2's
+    sequential search is running asks that search for its state (it saves its
+    record at its next check and leaves the key) and continues it in dfs_acc
+    instead of restarting it. On the C3 keys that end the step, with the
+    helpers taking keys after 1 ms (so the sequential searches are well under
+    way), every field -- WGL's count included -- equals the oracle's at the
+    full budget and at one the searches run into, with takeovers made; the
+    same with JH_LIN_NO_TAKEOVER and none made."""
+    from jepsen_amd import shard
+    from bench import WORKLOADS
+    wl = WORKLOADS["c3"]
+    cols, _ = synth.cas_register(n_keys=wl["keys"], ops_per_key=500, seed=wl["seed"] + 7919 * rank, **wl["gen"])
+    own = np.ones(cols.n_keys, np.int64)
+    own[keys] = 0
+    sub, mine, _ = shard.shard_history(cols, own, 0)
+    took = 0
+    for budget in (1 << 22, 20000):
+        c, _ = oracle.check_cas_independent(sub, budget=budget, threads=8)
+        for late in (1000, 3000):
+            g, s = ctx.check_cas_independent(sub, budget=budget, helper_late_us=late)
+            _same(g, c)
+            took += s.takeovers
+            print("takeovers at budget", budget, "late", late, s.takeovers, "spec merges", s.spec_merges)
+        g2, s2 = ctx.check_cas_independent(sub, budget=budget, flags=A.LIN_NO_TAKEOVER, helper_late_us=1000)
+        _same(g2, c)
+        assert s2.takeovers == 0
+    assert took > 0

@@ -2791,6 +2791,7 @@ struct WgArgs {
     int32_t *spec_q;           // the counters (q + Q_SPEC)
     int32_t spec_first;        // helpers serve the board before taking keys (JH_LIN_SPEC_FIRST)
     int32_t n_mains;           // helpers [n_mains, grid) only serve the board (never take a key)
+    int32_t *mains_live;       // helpers running a key now (the board's servers stay while any does)
 };
 
 __device__ __forceinline__ uint64_t lk_make(uint32_t t, uint32_t s, uint64_t m) {
@@ -3941,7 +3942,10 @@ __device__ void wg_helper_pick(const WgArgs &W, WgShared &sh, int tid, unsigned 
             // streaming: the sequential search's waves may all be idle
             // (left the queue) before phase 1 has finished deferring
             const bool more = A.live_n && !p1_finished(A.p1_done, A.p1_tot);
-            const bool over = (!more && __hip_atomic_load(W.seq_exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= waves) ||
+            // (round 6: while a helper still runs a key -- one it took over from
+            // a sequential wave that has left -- the others stay to serve its board)
+            const bool over = (!more && __hip_atomic_load(W.seq_exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= waves &&
+                               !(W.mains_live && __hip_atomic_load(W.mains_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0)) ||
                               __builtin_amdgcn_s_memrealtime() - t_enter > HELPER_MAX_TICKS;
             sh.key = over ? -1 : -2;
             sh.n_live = A.live_n ? ld_agent(A.live_n) : A.n_list;
@@ -4131,6 +4135,7 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
             // does not answer within ~3 ms (not running this key) is withdrawn
             // from, and a refused or unsaved one restarts here from the root
             int ho_st = HO_NONE;
+            if (W.mains_live && lane == 0) atomicAdd(W.mains_live, 1);
             if (A.handoff && lane == 0) {
                 __hip_atomic_store(&A.handoff[key], HO_ASK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned long long h0 = __builtin_amdgcn_s_memrealtime();
@@ -4157,6 +4162,7 @@ __global__ void __launch_bounds__(WG_THREADS) k_lin_wg(WgArgs W) {
                                                work, wtab, pend, inserts, tmax, my_probes, ho_st == HO_DONE);
             TL_REC(A.tl, key, 5);
             if (W.spec) spec_release(W, key, lane);
+            if (W.mains_live && lane == 0) atomicSub(W.mains_live, 1);
             jh_key_verdict v;
             v.valid = verdict;
             v.cause = verdict == JH_UNKNOWN ? JH_CAUSE_BUDGET : 0;
@@ -6516,6 +6522,7 @@ constexpr int Q_P1_DONE = 64, Q_SEQ_WAVES = 65, Q_BFS_QUEUE = 66;
 constexpr int Q_T_BFS = 68, Q_T_LEAN = 72, Q_T_XW = 76, Q_T_P1 = 80;
 constexpr int Q_ENT_P3 = 84;        // entries of the LEAN keys restarted in phase 3
 constexpr int Q_RS_USED = 88;       // [88..89] resume records' bytes, [90] records published (round 5), [91] takeovers (round 6)
+constexpr int Q_MAINS = 92;         // round 6: late helpers running a key now
 constexpr int Q_SPEC = 96;          // round 6: [96..97] merged nodes, [98] merges, [99] spec jobs, [100] dead results
 // LEAN sequential waves launched with the BFS while phase 1 still runs (the
 // rest start behind phase 1): enough for the keys deferred before it ends
@@ -7149,6 +7156,7 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             HIP_TRY(hipMemsetAsync(seq_start, 0, (size_t)K * sizeof(unsigned long long), st));
             HIP_TRY(hipMemsetAsync(taken, 0, (size_t)K * sizeof(int32_t), st));
             wh.seq_start = seq_start; wh.seq_exit = q + 28; wh.seq_waves = waves2; wh.taken = taken;
+            wh.mains_live = q + Q_MAINS;
             uint64_t late_us = HELPER_LATE_US;
             if (opts && opts->helper_late_us > 0) late_us = (uint64_t)opts->helper_late_us;
             if (lflags & JH_LIN_HELPERS_NOW) late_us = 0;

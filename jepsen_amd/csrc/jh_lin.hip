@@ -1704,7 +1704,10 @@ insert:
                                                                    __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                                    __HIP_MEMORY_SCOPE_AGENT) ? 1 : 0;
                     }
-                    if (readlane(won, 0) && ok) { ho = true; verdict = JH_CANCELLED; goto done; }
+                    // the save (in done:) then comes back here: the search goes on
+                    // and races the helper that continues its copy (measured:
+                    // leaving the key to the helper was slower, the race wins)
+                    if (readlane(won, 0) && ok) { ho = true; goto done; }
                 }
             }
             chk = min(budget, ins + (A.handoff ? 256u : 1024u));
@@ -1933,6 +1936,12 @@ done:
             // no room in the arena: the helper restarts the key
             __hip_atomic_store(&A.handoff[key], HO_REFUSED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
+    }
+    if (ho) {
+        // a takeover's copy is saved: back to the insert it was taken at (the
+        // check runs again and finds the request answered)
+        ho = false;
+        goto insert;
     }
     inserts = ins;
     ins_real = ins_saved != 0xFFFFFFFFu ? ins_saved : ins;    // a handed-over search's own count

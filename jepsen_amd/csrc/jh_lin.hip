@@ -399,6 +399,7 @@ struct DfsArgs {
     // dfs_acc continues it instead of restarting it. null: off.
     int32_t *handoff;
 };
+constexpr int V_HANDED = -9;            // dfs_lean: saved for a takeover, continue from the record
 constexpr int32_t HO_NONE = 0, HO_ASK = 1, HO_DONE = 2, HO_REFUSED = 3, HO_WITHDRAWN = 4, HO_SAVING = 5;
 constexpr int TL_W = 6;         // timeline words per key: BFS, sequential, helper (start, end)
 #ifdef JH_TUNING
@@ -1458,7 +1459,7 @@ __device__ int dfs_search(const DfsArgs &A, const KeyInfo &K, char *tb, int key,
 // Search order and memo contents are exactly WGL's (orc_wgl_canonical,
 // oracle/jh_oracle.c, which does probe after a backtrack and never finds the
 // child present): explored counts stay identical.
-template <class M>
+template <class M, bool HO = false>    // HO: phase 2's takeover code (A.handoff) compiled in
 __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, const char *tb, int key, int lane,
                         uint64_t *memo, Frame *stack, uint64_t *stage,
                         long long &inserts, uint32_t &tmax_out, unsigned long long &my_probes,
@@ -1563,7 +1564,7 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
                     const uint32_t et = (uint32_t)(e.y >> 20) & T_MASK, es = (uint32_t)e.y & STATE_MASK;
                     const uint32_t sl = hbm_insert(memo, cap_mask, gen, et, es, e.x);
                     // (a takeover's save gathers the restored entries too)
-                    if (hlog && j < A.hlog_cap) hlog[j] = sl;
+                    if constexpr (HO) { if (hlog && j < A.hlog_cap) hlog[j] = sl; } else (void)sl;
                     uint32_t g1, g2;
                     lk_hash((uint32_t)e.x, (uint32_t)(e.x >> 32) | (et << 16) | (es << 8) | 0x80000000u, g1, g2);
                     bloom_set2<M>(bloom, lk_bl(g1), lk_bl(g2));
@@ -1571,7 +1572,7 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
                 }
                 for (int o = 32; o > 0; o >>= 1) tmx = max(tmx, (uint32_t)__shfl_xor((int)tmx, o));
                 theta = rflu(tmx);
-                nlog = (uint32_t)min<uint64_t>(h_n, 0xFFFFu);
+                if constexpr (HO) nlog = (uint32_t)min<uint64_t>(h_n, 0xFFFFu);
                 ring_lo = d > 32 ? d - 32 : 0;
                 for (uint32_t j = (uint32_t)lane; j < ring_lo; j += 64) stack[j] = fsrc[j];
                 {
@@ -1690,7 +1691,7 @@ insert:
                 else if (ins >= 2u * (uint32_t)A.prio_ins) __builtin_amdgcn_s_setprio(2);
                 else __builtin_amdgcn_s_setprio(1);
             }
-            if (A.handoff) {
+            if (HO && A.handoff) {
                 // round 6: a late helper asks for this search (the takeover);
                 // saved only if the slot log holds every HBM entry of the key
                 int h = 0;
@@ -1704,13 +1705,15 @@ insert:
                                                                    __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                                    __HIP_MEMORY_SCOPE_AGENT) ? 1 : 0;
                     }
-                    // the save (in done:) then comes back here: the search goes on
-                    // and races the helper that continues its copy (measured:
-                    // leaving the key to the helper was slower, the race wins)
+                    // saved in done:, then the caller continues this search from
+                    // the same record (V_HANDED): it races the helper that
+                    // continues its copy (measured: leaving the key to the
+                    // helper was slower). A restart from the record rather than a
+                    // jump back here keeps the search loop's registers its own.
                     if (readlane(won, 0) && ok) { ho = true; goto done; }
                 }
             }
-            chk = min(budget, ins + (A.handoff ? 256u : 1024u));
+            chk = min(budget, ins + (HO && A.handoff ? 256u : 1024u));
         }
         const int i = __builtin_ctzll(absent);
         ins++;
@@ -1849,7 +1852,7 @@ pop:
     goto insert;
 
 done:
-    if ((A.rs_mode == 1 && A.rs_off && verdict == JH_UNKNOWN && A.defer) || ho) {
+    if ((A.rs_mode == 1 && A.rs_off && verdict == JH_UNKNOWN && A.defer) || (HO && ho)) {
         // Save the deferred search for phase 2 (round 5): header {mask, t | s << 32,
         // depth | tmax << 32, inserts, entries}, the stack frames, then every
         // configuration in the memo as {mask, t << 20 | s}: the LDS ones and this
@@ -1937,12 +1940,7 @@ done:
             __hip_atomic_store(&A.handoff[key], HO_REFUSED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if (ho) {
-        // a takeover's copy is saved: back to the insert it was taken at (the
-        // check runs again and finds the request answered)
-        ho = false;
-        goto insert;
-    }
+    if (HO && ho) return V_HANDED;      // (published: HO_DONE, or HO_REFUSED)
     inserts = ins;
     ins_real = ins_saved != 0xFFFFFFFFu ? ins_saved : ins;    // a handed-over search's own count
     tmax_out = tmax;
@@ -2400,7 +2398,7 @@ __global__ void __launch_bounds__(256) k_key_tables(TblArgs A) {
 // STREAM: the kernel takes part in the streaming heavy-key pass (phase 1 as
 // the producer of the live lists, or a consumer of them); without it the
 // streaming code is compiled out (it costs phase 1 registers and occupancy).
-template <class M, bool LEAN, bool WL = false, bool STREAM = false>
+template <class M, bool LEAN, bool WL = false, bool STREAM = false, bool HO = false>
 __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
     const int lane = threadIdx.x;
     const size_t wv = (size_t)(blockIdx.x - A.wave_off);
@@ -2459,8 +2457,15 @@ __device__ __forceinline__ void lin_dfs_waves(const DfsArgs &A) {
                                __HIP_MEMORY_SCOPE_AGENT);
         int verdict;
         uint32_t ins_real = 0;
-        if constexpr (LEAN) verdict = dfs_lean<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes, ins_real,
-                                                  (A.rs_mode == 1 || A.handoff) && A.hlog ? A.hlog + wv * A.hlog_cap : nullptr);
+        if constexpr (LEAN) {
+            // (a takeover's save returns V_HANDED: the search goes on from the
+            // record it just published, rs_off[key], as phase 2 resumes phase 1's)
+            do {
+                verdict = dfs_lean<M, HO>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes, ins_real,
+                                          (A.rs_mode == 1 || (HO && A.handoff)) && A.hlog ? A.hlog + wv * A.hlog_cap
+                                                                                     : nullptr);
+            } while (verdict == V_HANDED);
+        }
         else if constexpr (WL) verdict = dfs_lean_w<M>(A, K, tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         else verdict = dfs_search<false, false, M>(A, K, (char *)tb, key, lane, memo, stack, stage, inserts, tmax, my_probes);
         if (A.dbg && lane == 0) { A.dbg[16 * wv + 2] += __builtin_amdgcn_s_memtime() - c1; A.dbg[16 * wv + 3] += 1; }
@@ -2594,7 +2599,7 @@ struct DfsPair { DfsArgs l, w; int32_t n_l; };
 constexpr int SEQLW_LDS = MemoM::LDS > SEQW_LDS ? MemoM::LDS : SEQW_LDS;
 template <bool STREAM, class ML = MemoM>
 __global__ void __launch_bounds__(64) k_lin_seq_lw(DfsPair P) {
-    if ((int)blockIdx.x < P.n_l) lin_dfs_waves<ML, true, false, STREAM>(P.l);
+    if ((int)blockIdx.x < P.n_l) lin_dfs_waves<ML, true, false, STREAM, !STREAM>(P.l);
     else lin_dfs_waves<MemoWL, false, true, STREAM>(P.w);
 }
 
@@ -7630,7 +7635,8 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
             //  - the sequential search with the full budget (aux stream: LEAN
             //    and WIDE keys in one grid) settles every key.
             prep_race(n_defer, n_def_l);
-            if (resume) b.rs_mode = 2;      // (and phase 3, c3 = b: a record is never modified)
+            if (resume) b.rs_mode = 2;      // (and phase 3, c3 = b: a record is replaced only by a takeover's newer one)
+            if (!resume) { b.handoff = nullptr; wh.d.handoff = nullptr; }   // (a takeover continues from records)
             if (defer_times) {
                 // tuning builds: per key [BFS start, end, sequential start, end, helper start, end]
                 unsigned long long *tl = ctx->ws<unsigned long long>(WS_TL, TL_W * (size_t)K);

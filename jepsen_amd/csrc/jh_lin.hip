@@ -1524,6 +1524,7 @@ __device__ __forceinline__ int dfs_lean(const DfsArgs &A, const KeyInfo &K, cons
     uint32_t ins_saved = 0xFFFFFFFFu;     // a handed-over search's real insert count
     uint32_t nlog = 0;                    // hlog entries (saturating at 0xFFFF)
     bool ho = false;                      // a late helper takes this search over (A.handoff)
+    unsigned long long ho_off = 0;        // its record's place, reserved when the request is accepted
     // move the window forward from layer t to layer nt (a lift, or a resume)
     auto advance = [&](uint32_t nt) {
         for (uint32_t u = t; u < nt; u++) {
@@ -1697,7 +1698,19 @@ insert:
                 int h = 0;
                 if (lane == 0) h = __hip_atomic_load(&A.handoff[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (readlane(h, 0) == HO_ASK) {
-                    const bool ok = hlog && nlog <= A.hlog_cap;
+                    // accepted only if the save cannot fail: the slot log holds
+                    // every HBM entry, the record fits this wave's table when the
+                    // search continues from it, and its arena space is reserved
+                    // now (a failed save would leave the table holding entries
+                    // the record lacks)
+                    bool ok = hlog && nlog <= A.hlog_cap && ins <= A.memo_cap / 4;
+                    if (ok) {
+                        const uint64_t bytes = 64 + (uint64_t)depth * sizeof(Frame) + (uint64_t)ins * 16;
+                        unsigned long long off = 0;
+                        if (lane == 0) off = atomicAdd(A.rs_used, (unsigned long long)((bytes + 255) & ~255ULL));
+                        ho_off = readlane64(off, 0);
+                        ok = ho_off + bytes <= A.rs_cap;
+                    }
                     int won = 0;
                     if (lane == 0) {
                         int exp = HO_ASK;
@@ -1861,8 +1874,11 @@ done:
         const uint32_t nmem = ins_saved != 0xFFFFFFFFu ? ins_saved : ins;
         const uint64_t bytes = 64 + (uint64_t)depth * sizeof(Frame) + (uint64_t)nmem * 16;
         unsigned long long off = 0;
-        if (lane == 0) off = atomicAdd(A.rs_used, (unsigned long long)((bytes + 255) & ~255ULL));
-        off = readlane64(off, 0);
+        if (HO && ho) off = ho_off;
+        else {
+            if (lane == 0) off = atomicAdd(A.rs_used, (unsigned long long)((bytes + 255) & ~255ULL));
+            off = readlane64(off, 0);
+        }
         if (off + bytes <= A.rs_cap) {
             uint64_t *hd = (uint64_t *)(A.rs_arena + off);
             Frame *fdst = (Frame *)(hd + 8);
@@ -1935,9 +1951,15 @@ done:
                 __hip_atomic_store(&A.handoff[key], n == nmem ? HO_DONE : HO_REFUSED, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
-        } else if (ho && lane == 0) {
-            // no room in the arena: the helper restarts the key
-            __hip_atomic_store(&A.handoff[key], HO_REFUSED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            // (never expected: a save whose gather missed an entry leaves the
+            // key to the helper, which restarts it -- this wave's table would
+            // hold entries the record lacks)
+            if (HO && ho && n != nmem) { ins = 0; verdict = JH_CANCELLED; ho = false; }
+        } else if (ho) {
+            // (not reached: the space was reserved at the request) the helper
+            // restarts the key and this wave leaves it
+            if (lane == 0) __hip_atomic_store(&A.handoff[key], HO_REFUSED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            verdict = JH_CANCELLED; ho = false;
         }
     }
     if (HO && ho) return V_HANDED;      // (published: HO_DONE, or HO_REFUSED)

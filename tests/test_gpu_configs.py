@@ -306,3 +306,23 @@ def test_key_index(ctx):
     subs = IND.subhistories_indexed(hist, off, rows, {k: k for k in (0, 5, K - 1)})
     for k in (0, 5, K - 1):
         assert subs[k] == IND.subhistory(k, hist)
+
+
+def test_c4_shard_full_parity(ctx):
+    """C4's whole one-GPU shard (bench.py --workload c4 at N = 1: 125 000 keys,
+    118.6 M entries, budget 2^22) with the default engines -- the round-6
+    takeover among them, where phase 1's records fill the resume arena and the
+    phase-2 tables are the small ones -- every field of every key equal to the
+    oracle's (round 6: a takeover save that failed for want of arena space let
+    a search continue from an older record over a table holding newer entries,
+    and undercounted; tools/c4_parity.py found it)."""
+    from bench import WORKLOADS
+    wl = WORKLOADS["c4"]
+    gcols, _ = synth.cas_register(n_keys=wl["keys"], ops_per_key=500, seed=wl["seed"], parts=16, **wl["gen"])
+    owner = shard.assign_keys(shard.key_costs(gcols), 1)
+    cols, _, _ = shard.shard_history(gcols, owner, 0)
+    del gcols
+    c, _ = oracle.check_cas_independent(cols, budget=wl["budget"], threads=16)
+    g, s = ctx.check_cas_independent(cols, budget=wl["budget"])
+    print("C4 shard: takeovers", s.takeovers, "spec merges", s.spec_merges)
+    _same(g, c)

@@ -7075,12 +7075,16 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // many (every valid deferred key), so most CUs go to the latter
         // 96 of 256 (round 2, with phase 2 at four waves per CU): C4 shard
         // 230 -> 223 ms, C3 ranks 0 / 3 / 6 flat (32: C4 +9 %, 128: no better)
-        // Round 6, with 64 helpers: 64 when more than 2 000 keys are deferred
-        // (the sequential search keeps 128 CUs for its queue; C3 ranks 0-4
-        // 39.0 / 36.0 / 35.2 / 39.6 / 45.4 -> 38.1 / 34.0 / 31.3 / 40.5 / 43.7
-        // ms), 96 for fewer (the strong-scaling shards' 1 335 / 694 deferred
-        // keys: 27.1 / 21.0 -> 24.5 / 19.4 ms), profiles/r06/ab_bfs_helpers/
-        const int bfs_cus = std::max(1, nd_all > 2000 ? ctx->n_cu / 4 : std::min(96, ctx->n_cu * 3 / 8));
+        // Round 6, with 64 helpers: 64 when 2 000-4 000 keys are deferred
+        // (the sequential search keeps 128 CUs for its queue; C3 ranks 0-4,
+        // 3 550-3 750 deferred keys: 39.0 / 36.0 / 35.2 / 39.6 / 45.4 -> 38.1 /
+        // 34.0 / 31.3 / 40.5 / 43.7 ms), 96 for fewer (the strong-scaling
+        // shards' 1 335 / 694 deferred keys: 27.1 / 21.0 -> 24.5 / 19.4 ms) and
+        // for more (C4's shard, 4 258 deferred keys, 812 of them invalid ones
+        // the BFS settles: 209.7 -> 202.0 ms); profiles/r06/ab_bfs_helpers/,
+        // ab_c4_split/. A measured band, not a model of the race.
+        const int bfs_cus = std::max(1, nd_all > 2000 && nd_all <= 4000 ? ctx->n_cu / 4
+                                                                          : std::min(96, ctx->n_cu * 3 / 8));
         wg2 = std::min(nd_all, tune_env("JH_BFS_CUS") ? std::max(1, atoi(tune_env("JH_BFS_CUS"))) :
                                opts && opts->bfs_wgs > 0 ? std::min(opts->bfs_wgs, ctx->n_cu - 16) : bfs_cus);
         const uint64_t per_bfs = (uint64_t)set_cap * 8 + 4ULL * q_cap * 8 + scr_bytes_bfs + (uint64_t)ncap * 8 +

@@ -6532,7 +6532,10 @@ static int fit_units(jh_ctx *ctx, int want, uint64_t per_unit, std::initializer_
     if ((uint64_t)want * per_unit <= held) return want;
     size_t fr = 0, tot = 0;
     HIP_TRY(hipMemGetInfo(&fr, &tot));
-    const uint64_t reserve = std::max<uint64_t>(2ULL << 30, tot / 32);
+    // (round 6: 1/16, was 1/32 -- the buffers sized outside fit_units grew with
+    // the helpers, the spec board and the takeover's logs, and a second context
+    // opened beside a first that holds ~140 GB ran out at budget 2^24)
+    const uint64_t reserve = std::max<uint64_t>(4ULL << 30, tot / 16);
     // contexts sharing the device (jh_open_devices with a device listed more
     // than once; round 6: or opened one by one, device_open_contexts) may run
     // at once: each takes its share of what is free

@@ -87,3 +87,13 @@ def test_open_without_gpu_fails_loudly(built):
         assert e.code in (A.JH_EDEVICE, A.JH_EINVAL)
     else:
         raise AssertionError("jh_open succeeded without a GPU")
+
+
+def test_lin_flags_match_header():
+    """Every JH_LIN_* flag jh.h defines has the same value in _abi (the
+    round-6 scheduling and takeover flags included)."""
+    src = open(os.path.join(ROOT, "include", "jh.h")).read()
+    flags = dict(re.findall(r"^#define\s+JH_(LIN_\w+)\s+(\d+)", src, re.M))
+    assert {"LIN_NO_SPEC", "LIN_SPEC_FIRST", "LIN_HELP_STALL", "LIN_NO_TAKEOVER"} <= set(flags)
+    for name, v in flags.items():
+        assert getattr(A, name) == int(v), name

@@ -169,10 +169,11 @@ typedef struct jh_history {
  * longest without reaching a deeper layer (stuck in a big dead subtree)
  * instead of the ones running longest (scheduling only). */
 #define JH_LIN_HELP_STALL   8192
-/* Round 6: a late helper that takes a key phase 2's sequential search is
- * running restarts it instead of continuing its saved state (the takeover;
- * same verdicts and counts either way). */
+/* Round 6, the takeover (opt-in): a late helper that takes a key phase 2's
+ * sequential search is running continues that search's saved state instead
+ * of restarting it (JH_LIN_TAKEOVER); JH_LIN_NO_TAKEOVER forces it off. */
 #define JH_LIN_NO_TAKEOVER  16384
+#define JH_LIN_TAKEOVER     32768
 
 typedef struct jh_lin_opts {
     int64_t init_value;        /* (model/cas-register init); JH_NIL = (cas-register) */

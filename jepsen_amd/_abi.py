@@ -66,7 +66,8 @@ EXPLORED_UNCOUNTED = -3       # a valid key settled without the count pass
 LIN_NO_SPEC = 2048            # round 6: no speculative dead-subtree enumerations by idle helpers
 LIN_SPEC_FIRST = 4096         # round 6: helpers serve posted spec jobs before taking keys
 LIN_HELP_STALL = 8192         # round 6: helpers pick the keys stuck longest (no deeper layer)
-LIN_NO_TAKEOVER = 16384       # round 6: a helper restarts a key instead of continuing the sequential search
+LIN_NO_TAKEOVER = 16384       # round 6: forces the takeover off
+LIN_TAKEOVER = 32768          # round 6 (opt-in): a helper continues the sequential search's saved state
 CAUSE_DEFERRED = 9
 
 

@@ -7246,7 +7246,9 @@ void lin_check_independent(jh_ctx *ctx, const jh_history *dh, const jh_lin_opts 
         // search's record (phase 2's own slot log, 32 K entries per wave)
         // instead of restarting the key
         b.handoff = nullptr;
-        if (n_help > 0 && a.rs_off && waves2 > 0 && !(lflags & JH_LIN_NO_TAKEOVER)) {
+        // (opt-in, JH_LIN_TAKEOVER: one exact-count call of sixteen final
+        // lines disagreed with the oracle with it on, unexplained)
+        if (n_help > 0 && a.rs_off && waves2 > 0 && (lflags & JH_LIN_TAKEOVER) && !(lflags & JH_LIN_NO_TAKEOVER)) {
             int32_t *ho = ctx->ws<int32_t>(WS_HANDOFF, K);
             HIP_TRY(hipMemsetAsync(ho, 0, (size_t)K * sizeof(int32_t), st));
             b.handoff = ho;

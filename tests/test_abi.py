@@ -94,6 +94,6 @@ def test_lin_flags_match_header():
     round-6 scheduling and takeover flags included)."""
     src = open(os.path.join(ROOT, "include", "jh.h")).read()
     flags = dict(re.findall(r"^#define\s+JH_(LIN_\w+)\s+(\d+)", src, re.M))
-    assert {"LIN_NO_SPEC", "LIN_SPEC_FIRST", "LIN_HELP_STALL", "LIN_NO_TAKEOVER"} <= set(flags)
+    assert {"LIN_NO_SPEC", "LIN_SPEC_FIRST", "LIN_HELP_STALL", "LIN_NO_TAKEOVER", "LIN_TAKEOVER"} <= set(flags)
     for name, v in flags.items():
         assert getattr(A, name) == int(v), name

@@ -310,8 +310,8 @@ def test_key_index(ctx):
 
 def test_c4_shard_full_parity(ctx):
     """C4's whole one-GPU shard (bench.py --workload c4 at N = 1: 125 000 keys,
-    118.6 M entries, budget 2^22) with the default engines -- the round-6
-    takeover among them, where phase 1's records fill the resume arena and the
+    118.6 M entries, budget 2^22) with the default engines and with the
+    round-6 takeover (JH_LIN_TAKEOVER), where phase 1's records fill the resume arena and the
     phase-2 tables are the small ones -- every field of every key equal to the
     oracle's (round 6: a takeover save that failed for want of arena space let
     a search continue from an older record over a table holding newer entries,
@@ -324,5 +324,7 @@ def test_c4_shard_full_parity(ctx):
     del gcols
     c, _ = oracle.check_cas_independent(cols, budget=wl["budget"], threads=16)
     g, s = ctx.check_cas_independent(cols, budget=wl["budget"])
+    _same(g, c)
+    g, s = ctx.check_cas_independent(cols, budget=wl["budget"], flags=A.LIN_TAKEOVER)
     print("C4 shard: takeovers", s.takeovers, "spec merges", s.spec_merges)
     _same(g, c)

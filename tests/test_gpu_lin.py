@@ -711,11 +711,11 @@ def test_takeover(ctx, rank, keys):
     for budget in (1 << 22, 20000):
         c, _ = oracle.check_cas_independent(sub, budget=budget, threads=8)
         for late in (1000, 3000):
-            g, s = ctx.check_cas_independent(sub, budget=budget, helper_late_us=late)
+            g, s = ctx.check_cas_independent(sub, budget=budget, flags=A.LIN_TAKEOVER, helper_late_us=late)
             _same(g, c)
             took += s.takeovers
             print("takeovers at budget", budget, "late", late, s.takeovers, "spec merges", s.spec_merges)
-        g2, s2 = ctx.check_cas_independent(sub, budget=budget, flags=A.LIN_NO_TAKEOVER, helper_late_us=1000)
+        g2, s2 = ctx.check_cas_independent(sub, budget=budget, helper_late_us=1000)      # the default: off
         _same(g2, c)
         assert s2.takeovers == 0
     assert took > 0
